@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Benchmark of the north-star path: device-resident Reed-Solomon Encode.
+
+BASELINE.json metric: "Encode GiB/s device-resident ((k+m)*vec/cost),
+10+4 @1MiB, 1/2/4/8 GPU; %HBM peak".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step = one launch of the HIP encode over one batch of S synthetic stripes
+(default S=256 stripes of 10+4 x 1 MiB = 3.5 GiB per GPU, far beyond the
+256 MiB Infinity Cache) that are already resident in HBM.  Stripes are
+independent, so N GPUs each encode their own S stripes with no collective on
+the data path (weak scaling); the only collectives are the timing barrier and
+the max-over-ranks of the elapsed time.
+
+Rank 0 prints ONE JSON line.  `value` = (k+m)*vec*S*N*K / max-rank time in
+GiB/s.  `roofline` prices the encode kernel itself: algorithmic bytes per
+launch / mean launch time from HIP events on the launch stream, against
+8 TB/s HBM3E.  `cpu_baseline` times the oracle's AVX2 restatement of the
+reference's split-nibble path on one host core over a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), GB/s
+CONFIGS = {
+    # name: (k, m, vector bytes, stripes per GPU)
+    "10+4@1MiB": (10, 4, 1 << 20, 256),
+    "12+4@1MiB": (12, 4, 1 << 20, 256),
+    "10+4@8KiB": (10, 4, 8 << 10, 32768),
+}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="10+4@1MiB", choices=sorted(CONFIGS))
+    ap.add_argument("--stripes", type=int, default=0, help="stripes per GPU (default: per config)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--verify", type=int, default=1, help="check one stripe per rank against the oracle")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------- distributed plumbing
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def stripe_range(rank: int, stripes_per_rank: int):
+    """Global ids of the stripes a rank owns (weak scaling: fixed per rank)."""
+    return rank * stripes_per_rank, (rank + 1) * stripes_per_rank
+
+
+def timed_region(step_fn, steps: int, barrier, sync, max_over_ranks):
+    """barrier + sync, time exactly `steps` steps, sync + barrier; max over ranks."""
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step_fn(i)
+    sync()
+    t1 = time.perf_counter()
+    barrier()
+    return max_over_ranks(t1 - t0)
+
+
+# ---------------------------------------------------------------- CPU baseline
+
+def cpu_baseline(k, m, vec, seconds):
+    """The oracle's AVX2 restatement of the reference's encode path
+    (gmu_amd64.s split-nibble + rs.go:141-203 chunking), one core."""
+    import numpy as np
+
+    from oracle import oracle
+
+    oracle.build()
+    rng = np.random.default_rng(0x5EED)
+    nstripes = 4
+    stripes = [[rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] +
+               [np.zeros(vec, np.uint8) for _ in range(m)] for _ in range(nstripes)]
+    used_avx2 = oracle.has_avx2()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        oracle.encode_avx2(k, m, stripes[n % nstripes])
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gibs = n * (k + m) * vec / el / 2 ** 30
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"{n} encodes of {k}+{m} x {vec} B stripes (4 distinct, host memory) in {el:.1f} s, "
+                  f"{'AVX2 split-nibble' if used_avx2 else 'scalar table'} restatement of gmu_amd64.s, "
+                  f"1 thread on {cpu}",
+    }
+
+
+def load_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        data = json.load(open(path))
+        return data.get(config, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+# ---------------------------------------------------------------- main
+
+def main(argv=None):
+    args = parse_args(argv)
+    world, rank, local = dist_env()
+    if world != args.gpus and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    n_gpus = world
+
+    import torch
+
+    import reedsolomon_amd as rs
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist
+
+    k, m, vec, S = CONFIGS[args.config]
+    if args.stripes:
+        S = args.stripes
+    lo, hi = stripe_range(rank, S)
+
+    codec = rs.New(k, m, device=local)
+    stream = torch.cuda.current_stream(dev)
+
+    # Synthetic stripes: uniform random data seeded per (seed, rank); parity
+    # pre-filled with 0xA5 so an encode that skipped a byte would show.
+    g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
+    buf = torch.empty((S, k + m, vec), dtype=torch.uint8, device=dev)
+    for s0 in range(0, S, 32):
+        s1 = min(S, s0 + 32)
+        buf[s0:s1, :k].random_(0, 256, generator=g)
+    buf[:, k:].fill_(0xA5)
+    torch.cuda.synchronize(dev)
+
+    def step(_i):
+        codec.encode_batch(buf, stream=stream)
+
+    for _ in range(args.warmup):
+        step(0)
+    torch.cuda.synchronize(dev)
+
+    if args.verify:
+        from oracle import oracle
+
+        oracle.build()
+        host = buf[S // 2].cpu().numpy()
+        v = [host[i].copy() for i in range(k)] + [host[k + j].copy() * 0 for j in range(m)]
+        oracle.encode(k, m, v)
+        for j in range(m):
+            if not (v[k + j] == host[k + j]).all():
+                raise SystemExit(f"rank {rank}: parity mismatch vs oracle (stripe {lo + S // 2}, row {j})")
+
+    # Kernel time: HIP events on the launch stream around every timed launch.
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def timed_step(i):
+        ev[i][0].record(stream)
+        step(i)
+        ev[i][1].record(stream)
+
+    if pg is not None:
+        def barrier():
+            pg.barrier()
+
+        def max_over(x):
+            t = torch.tensor([x], dtype=torch.float64, device=dev)
+            pg.all_reduce(t, op=pg.ReduceOp.MAX)
+            return float(t.item())
+    else:
+        def barrier():
+            pass
+
+        def max_over(x):
+            return x
+
+    elapsed = timed_region(timed_step, args.steps, barrier, lambda: torch.cuda.synchronize(dev), max_over)
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_mean_s = sum(kern_ms) / len(kern_ms) / 1e3
+    kern_mean_s = max_over(kern_mean_s)
+
+    bytes_per_step_rank = S * (k + m) * vec
+    total_bytes = bytes_per_step_rank * n_gpus * args.steps
+    value = total_bytes / elapsed / 2 ** 30
+    achieved = bytes_per_step_rank / kern_mean_s / 1e9
+
+    result = None
+    if rank == 0:
+        traffic = load_traffic(args.config)
+        result = {
+            "metric": "Encode GiB/s device-resident ((k+m)*vec/cost), 10+4 @1MiB, 1/2/4/8 GPU; %HBM peak",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (uniform random bytes, seeded per rank; parity pre-filled 0xA5)",
+            "config": {
+                "workload": f"RS encode {k}+{m}, {vec} B vectors, {S} stripes per GPU, device-resident",
+                "k": k, "m": m, "vector_bytes": vec, "stripes_per_gpu": S,
+                "parallelism": f"stripes partitioned over {n_gpus} GPU(s), no collective",
+                "kernel": _kernel_name(k, m),
+            },
+            "pct_hbm_peak": round(bytes_per_step_rank * n_gpus * args.steps / elapsed / 1e9 / n_gpus
+                                  / HBM_PEAK_GBS * 100, 2),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_per_step_rank,
+                "kernel_ms_mean": round(kern_mean_s * 1e3, 4),
+            },
+        }
+        if n_gpus == 1 and args.cpu_seconds > 0:
+            result["cpu_baseline"] = cpu_baseline(k, m, vec, args.cpu_seconds)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if pg is not None:
+        pg.barrier()
+        pg.destroy_process_group()
+    return result
+
+
+def _kernel_name(k, m):
+    return f"gf_matmul_vec<{k},true,4,false,1>" if (k, m) in ((10, 4), (12, 4)) else "gf_matmul_vec"
+
+
+if __name__ == "__main__":
+    main()

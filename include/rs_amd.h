@@ -1,0 +1,213 @@
+/*
+ * rs_amd.h — C ABI of the MI355X-native Reed-Solomon engine (librsamd.so).
+ *
+ * This is the drop-in boundary for templexxx/reedsolomon's public Go API
+ * (reference: /root/reference/rs.go).  Every entry point below names the
+ * reference function it replaces.  A Go caller binds these through cgo
+ * (see INTEGRATION.md); Python binds them through ctypes
+ * (reedsolomon_amd/_lib.py).  No torch or HIP C++ types appear in the
+ * signatures: device memory is passed as plain pointers and streams as
+ * `void*` (a hipStream_t, NULL = the legacy default stream).
+ *
+ * Conventions (same as the reference, rs.go:101-111, 205-237, 422-529):
+ *   - The caller owns every buffer; outputs are written in place.
+ *   - A vector is (pointer, length).  Lengths are passed per vector so that
+ *     the reference's size checks (ErrZeroVectSize, ErrMismatchVectSize) are
+ *     reproduced exactly.
+ *   - Host-memory entry points (rs_encode, rs_reconst, rs_update, rs_replace)
+ *     are synchronous, like the Go methods.
+ *   - Device entry points (*_dev, *_batch) are asynchronous on `stream`.
+ *   - An rs_t handle is safe for concurrent use from several threads, like
+ *     *RS (its only mutable state, the inverse-matrix cache, is locked).
+ *   - Return value: RS_OK (0) or one of the RS_ERR_* codes; codes 1..12 map
+ *     1:1 to the reference's sentinel errors (rs_strerror gives the exact Go
+ *     error text, so a cgo wrapper can return errors that compare equal).
+ */
+#ifndef RS_AMD_H
+#define RS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define RS_API __attribute__((visibility("default")))
+#else
+#define RS_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes: rs.go:44,113-117,239-242,451-454,531-534; matrix.go:81-82 ---- */
+enum {
+    RS_OK = 0,
+    RS_ERR_ILLEGAL_VECTS = 1,       /* ErrIllegalVects      rs.go:44  */
+    RS_ERR_MISMATCH_VECTS = 2,      /* ErrMismatchVects     rs.go:114 */
+    RS_ERR_ZERO_VECT_SIZE = 3,      /* ErrZeroVectSize      rs.go:115 */
+    RS_ERR_MISMATCH_VECT_SIZE = 4,  /* ErrMismatchVectSize  rs.go:116 */
+    RS_ERR_NO_NEED_RECONST = 5,     /* ErrNoNeedReconst     rs.go:240 (swallowed by Reconst) */
+    RS_ERR_TOO_MANY_LOST = 6,       /* ErrTooManyLost       rs.go:241 */
+    RS_ERR_MISMATCH_PARITY_NUM = 7, /* ErrMismatchParityNum rs.go:452 */
+    RS_ERR_ILLEGAL_VECT_INDEX = 8,  /* ErrIllegalVectIndex  rs.go:453 */
+    RS_ERR_TOO_MANY_REPLACE = 9,    /* ErrTooManyReplace    rs.go:532 */
+    RS_ERR_MISMATCH_REPLACE = 10,   /* ErrMismatchReplace   rs.go:533 */
+    RS_ERR_NOT_SQUARE = 11,         /* ErrNotSquare         matrix.go:81 */
+    RS_ERR_SINGULAR_MATRIX = 12,    /* ErrSingularMatrix    matrix.go:82 */
+    /* Misuse the reference does not return an error for but panics on
+     * (index out of range: Replace with empty data rs.go:549, Reconst with
+     * fewer than d+p vectors rs.go:343,346,366,369). */
+    RS_ERR_INVAL = 13,
+    RS_ERR_DEVICE = 14,             /* a HIP runtime call failed (no GPU, OOM, ...) */
+    RS_ERR_NOMEM = 15               /* host allocation failed */
+};
+
+typedef struct rs_codec rs_t;
+
+/* Text of the reference's error for `code` ("" for RS_OK). */
+RS_API const char* rs_strerror(int code);
+
+/* Library / device information. */
+RS_API int rs_version(void);                /* 100*major + minor */
+RS_API int rs_device_count(void);           /* number of visible HIP devices, <0 on error */
+
+/* ------------------------------------------------------------------------
+ * Codec lifetime.  Replaces New(dataNum, parityNum) rs.go:54-85.
+ * Validates d>0, p>0, d+p<=256 (RS_ERR_ILLEGAL_VECTS), builds the
+ * identity+Cauchy encoding matrix (matrix.go:37-54), sets GenMatrix = rows
+ * d..d+p-1, and enables the inverse-matrix cache when d+p<=64
+ * (rs.go:70-74).  `device` selects the HIP device the handle launches on
+ * (-1 = the calling thread's current device at first use).  No device work
+ * happens here: the handle can be created on a host without a GPU.
+ * ------------------------------------------------------------------------ */
+RS_API int  rs_new(int data_num, int parity_num, int device, rs_t** out);
+RS_API void rs_free(rs_t* rs);
+RS_API int  rs_data_num(const rs_t* rs);                 /* RS.DataNum   rs.go:24 */
+RS_API int  rs_parity_num(const rs_t* rs);               /* RS.ParityNum rs.go:25 */
+/* Copies GenMatrix (p x d, row-major, G[j*d+i]) into out[p*d]. rs.go:31,65-68 */
+RS_API int  rs_gen_matrix(const rs_t* rs, uint8_t* out);
+/* Copies the (d+p) x d encoding matrix into out[(d+p)*d]. rs.go:30 */
+RS_API int  rs_enc_matrix(const rs_t* rs, uint8_t* out);
+
+/* ------------------------------------------------------------------------
+ * Host-memory operations (synchronous; the drop-in for the Go methods).
+ * vects[i] is a host pointer of length lens[i].
+ * ------------------------------------------------------------------------ */
+
+/* (*RS).Encode rs.go:104-111: vects[d..d+p) = GenMatrix * vects[0..d). */
+RS_API int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n);
+
+/* (*RS).Reconst rs.go:221-237 with checkReconst rs.go:264-325.  survived /
+ * need are index lists (ns / nn entries; ns==0 means "all survived").  The
+ * reconstructed vectors are written into vects[need...] (and, when any
+ * parity is rebuilt, every data vector that is neither survived nor needed,
+ * exactly like the reference rs.go:297-303). Returns RS_OK when nn==0. */
+RS_API int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n,
+               const int* survived, int ns, const int* need, int nn);
+
+/* (*RS).Update rs.go:424-449: parity[j] ^= G[j][row] * (old ^ new). */
+RS_API int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len,
+              const uint8_t* new_data, size_t new_len, int row,
+              uint8_t* const* parity, const size_t* parity_lens, int np);
+
+/* (*RS).Replace rs.go:492-529: parity[j] ^= sum_k G[j][rows[k]] * data[k]. */
+RS_API int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd,
+               const int* replace_rows, int nr,
+               uint8_t* const* parity, const size_t* parity_lens, int np);
+
+/* ------------------------------------------------------------------------
+ * Device-memory operations, one stripe, asynchronous on `stream`.
+ * Same semantics and checks as the host versions; pointers are device
+ * pointers (hipMalloc / torch CUDA tensors) on the handle's device.
+ * ------------------------------------------------------------------------ */
+RS_API int rs_encode_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, void* stream);
+RS_API int rs_reconst_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n,
+                   const int* survived, int ns, const int* need, int nn, void* stream);
+RS_API int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len,
+                  const uint8_t* new_data, size_t new_len, int row,
+                  uint8_t* const* parity, const size_t* parity_lens, int np, void* stream);
+RS_API int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd,
+                   const int* replace_rows, int nr,
+                   uint8_t* const* parity, const size_t* parity_lens, int np, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Batched device-resident operations over `nstripes` independent stripes
+ * laid out with fixed strides: vector v of stripe s lives at
+ *     base + s*stripe_stride + v*vect_stride       (bytes)
+ * with v in [0, d+p), each vector `len` bytes.  This is the layout the
+ * benchmark uses (one [S][d+p][len] allocation) and the unit the multi-GPU
+ * path partitions (stripes are independent: no collective).
+ * ------------------------------------------------------------------------ */
+
+/* Encode every stripe (the north-star hot path). */
+RS_API int rs_encode_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                    int nstripes, size_t len, void* stream);
+
+/* Reconst every stripe with the same survived/need pattern
+ * (one host plan + one cached matrix, then at most two device passes). */
+RS_API int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                     int nstripes, size_t len, const int* survived, int ns,
+                     const int* need, int nn, void* stream);
+
+/* Update: old/new vectors of stripe s at old_base + s*old_stride and
+ * new_base + s*new_stride; parity vectors are vectors d..d+p of the stripe
+ * layout above. */
+RS_API int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride,
+                    const uint8_t* new_base, int64_t new_stride, int row,
+                    uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                    int nstripes, size_t len, void* stream);
+
+/* Replace: replacement data vector r of stripe s at
+ * data_base + s*data_stripe_stride + r*data_vect_stride; parity as above. */
+RS_API int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_stripe_stride,
+                     int64_t data_vect_stride, const int* replace_rows, int nr,
+                     uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                     int nstripes, size_t len, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Generic GF(2^8) matrix product over device vectors — the primitive all of
+ * the above reduce to (rs.go:175-203 encodePart, gmu.go:4-9):
+ *   out[r] (=|^=) sum_c mat[r*cols+c] (x) in[c]        byte-wise, for every stripe
+ * in/out vector c of stripe s at in_base + s*in_stripe_stride + in_map[c]*in_vect_stride
+ * (same for out).  accumulate=0 overwrites, 1 XORs into out (updateOnly).
+ * ------------------------------------------------------------------------ */
+RS_API int rs_gf_matmul_batch(rs_t* rs, const uint8_t* mat, int rows, int cols,
+                       const uint8_t* in_base, int64_t in_stripe_stride, int64_t in_vect_stride,
+                       const int* in_map,
+                       uint8_t* out_base, int64_t out_stripe_stride, int64_t out_vect_stride,
+                       const int* out_map,
+                       int nstripes, size_t len, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Host-side planning helpers (no device work; exported for tests and for
+ * callers that batch many erasure patterns themselves).
+ * ------------------------------------------------------------------------ */
+
+/* checkReconst rs.go:264-325.  Writes sorted survived indexes (vs, up to
+ * d+p), indexes to rebuild (nr, data first; up to d+p) and the count of data
+ * indexes among them.  Returns RS_OK, RS_ERR_NO_NEED_RECONST,
+ * RS_ERR_ILLEGAL_VECTS or RS_ERR_TOO_MANY_LOST. */
+RS_API int rs_plan_reconst(const rs_t* rs, const int* survived, int ns, const int* need, int nn,
+                    int* vs, int* nvs, int* nr, int* nnr, int* dn);
+
+/* getReconstMatrix rs.go:382-412 (through the inverse cache when enabled):
+ * rows `need` (data indexes) of inv(encMatrix rows survived[0..d)).
+ * out has nn*d bytes. */
+RS_API int rs_reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out);
+
+/* invert matrix.go:85-147: n x n inverse over GF(2^8); m has m_len bytes. */
+RS_API int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out);
+
+/* makeInverseCacheKey rs.go:414-420 */
+RS_API uint64_t rs_inverse_cache_key(const int* survived, int ns);
+
+/* Number of inverse matrices currently cached (rs.go:33-39). */
+RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
+
+/* GF(2^8) multiply (gmu.go:26-28) — for tests. */
+RS_API uint8_t rs_gf_mul(uint8_t a, uint8_t b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS_AMD_H */

@@ -1,0 +1,60 @@
+"""Builds librsamd.so (the HIP/CDNA4 engine + C ABI) in-tree for gfx950.
+
+    python -m reedsolomon_amd.build          # or __graft_entry__.build()
+
+The library is written to reedsolomon_amd/_lib/librsamd.so; it is
+git-ignored but travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIB_DIR, "librsamd.so")
+SOURCES = [os.path.join(CSRC, "codec.cpp"), os.path.join(CSRC, "kernels.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("gf256.hpp", "kernels.hpp")] + [
+    os.path.join(ROOT, "include", "rs_amd.h")
+]
+ARCH = os.environ.get("RSAMD_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: librsamd.so cannot be built")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [
+        hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}",
+        "-fvisibility=hidden", "-Wall", "-Wno-unused-result",
+        "-I", os.path.join(ROOT, "include"),
+        *SOURCES, "-o", tmp,
+    ]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,859 @@
+// codec.cpp — host side of librsamd: the reference's codec driver
+// (rs.go, matrix.go) re-expressed around a device GF(2^8) matrix product.
+//
+// What runs here (small, per call or per erasure pattern):
+//   * argument checks in the reference's exact order and error codes
+//     (checkEncode rs.go:119-134, checkReconst :264-325, checkUpdate
+//     :456-477, checkReplace :536-570);
+//   * encoding-matrix construction (matrix.go:37-54), Gauss-Jordan inverse
+//     (matrix.go:85-147) and the survivor-bitmap inverse cache (rs.go:33-39,
+//     70-74, 382-420);
+//   * conversion of a small coefficient matrix into per-coefficient device
+//     perm tables, uploaded once per distinct matrix (registry below).
+// What runs on the GPU: every byte of every vector (kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rs_amd.h"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+using namespace rsamd;
+
+namespace {
+
+constexpr int kMaxVects = 256;                              // rs.go:47
+constexpr uint64_t kMaxInverseCacheBytes = 16ull << 20;     // rs.go:50
+constexpr size_t kMaxRegistryEntries = 1 << 14;
+
+// ---------------------------------------------------------------- matrix.go
+
+// makeEncodeMatrix matrix.go:37-54: identity over a Cauchy block 1/(i^j).
+std::vector<uint8_t> make_encode_matrix(int d, int p) {
+    std::vector<uint8_t> m(static_cast<size_t>(d + p) * d, 0);
+    for (int i = 0; i < d; ++i) m[i * d + i] = 1;
+    size_t off = static_cast<size_t>(d) * d;
+    for (int i = d; i < d + p; ++i)
+        for (int j = 0; j < d; ++j) m[off++] = gf_inv(static_cast<uint8_t>(i ^ j));
+    return m;
+}
+
+// invert matrix.go:85-147 (Gauss-Jordan; a zero pivot swaps with the first
+// lower row that has a non-zero entry in the pivot column; the result is
+// bit-identical to the reference's).
+int invert(const uint8_t* src, size_t len, int n, uint8_t* out) {
+    if (static_cast<size_t>(n) * n != len) return RS_ERR_NOT_SQUARE;
+    std::vector<uint8_t> left(src, src + len), inv(len, 0);
+    for (int i = 0; i < n; ++i) inv[i * n + i] = 1;
+    auto swap_rows = [n](std::vector<uint8_t>& m, int a, int b) {
+        std::swap_ranges(m.begin() + a * n, m.begin() + (a + 1) * n, m.begin() + b * n);
+    };
+    const auto& T = gf();
+    for (int i = 0; i < n; ++i) {
+        if (left[i * n + i] == 0) {
+            int j = i + 1;
+            while (j < n && left[j * n + i] == 0) ++j;
+            if (j == n) return RS_ERR_SINGULAR_MATRIX;
+            swap_rows(left, i, j);
+            swap_rows(inv, i, j);
+        }
+        const uint8_t piv = left[i * n + i];
+        if (piv != 1) {
+            const uint8_t v = T.inv[piv];
+            for (int j = 0; j < n; ++j) {
+                left[i * n + j] = T.mul[left[i * n + j]][v];
+                inv[i * n + j] = T.mul[inv[i * n + j]][v];
+            }
+        }
+        for (int j = 0; j < n; ++j) {
+            if (j == i) continue;
+            const uint8_t v = left[j * n + i];
+            if (!v) continue;
+            const uint8_t* mv = T.mul[v];
+            for (int k = 0; k < n; ++k) {
+                left[j * n + k] ^= mv[left[i * n + k]];
+                inv[j * n + k] ^= mv[inv[i * n + k]];
+            }
+        }
+    }
+    std::memcpy(out, inv.data(), len);
+    return RS_OK;
+}
+
+uint64_t cache_key(const int* survived, int ns) {  // makeInverseCacheKey rs.go:414-420
+    uint64_t key = 0;
+    for (int k = 0; k < ns; ++k) {
+        const unsigned s = static_cast<uint8_t>(survived[k]);  // Go: 1 << uint8(i)
+        key += s < 64 ? (uint64_t{1} << s) : 0;
+    }
+    return key;
+}
+
+// ---------------------------------------------------------------- device helpers
+
+struct DeviceGuard {  // switch to the handle's device, restore the caller's on exit
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) return;
+        ok = (prev == dev) || hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (ok && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline uint64_t rup(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+// ---------------------------------------------------------------- the handle
+
+struct rs_codec {
+    int d = 0, p = 0;
+    std::vector<uint8_t> enc;  // (d+p) x d; GenMatrix = enc[d*d:]   rs.go:30-31,65-68
+
+    // inverse cache rs.go:33-39,70-74
+    bool cache_enabled = false;
+    uint64_t cache_max = 0;
+    std::atomic<uint64_t> cache_n{0};
+    std::mutex cache_mu;
+    std::unordered_map<uint64_t, std::vector<uint8_t>> cache;
+
+    // device state (created lazily; the handle works on a GPU-less host)
+    std::mutex dev_mu;
+    int device = -1;
+    bool device_ready = false;
+
+    std::mutex tab_mu;  // coefficient-table registry: matrix bytes -> device perm tables
+    std::map<std::string, uint32_t*> tables;
+
+    std::mutex stage_mu;  // staging for the host-memory entry points
+    uint8_t* stage = nullptr;
+    size_t stage_bytes = 0;
+    hipStream_t stream = nullptr;
+
+    const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
+
+    ~rs_codec() {
+        if (!device_ready) return;
+        DeviceGuard g(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        (void)hipDeviceSynchronize();
+        for (auto& kv : tables) (void)hipFree(kv.second);
+        if (stage) (void)hipFree(stage);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+int ensure_device(rs_t* rs) {
+    std::lock_guard<std::mutex> lk(rs->dev_mu);
+    if (rs->device_ready) return RS_OK;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RS_ERR_DEVICE;
+    if (rs->device < 0) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return RS_ERR_DEVICE;
+        rs->device = cur;
+    }
+    if (rs->device >= count) return RS_ERR_DEVICE;
+    rs->device_ready = true;
+    return RS_OK;
+}
+
+// Perm tables for a rows x cols coefficient matrix, laid out
+// [col][rows_pad][5] dwords (rows padded to a multiple of 8 so that every
+// kernel row group reads inside the allocation).  Uploaded once per distinct
+// matrix and reused by every later launch.
+int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t** out, int* rows_pad_out) {
+    const int rows_pad = static_cast<int>(rup(rows, 8));
+    std::string key(reinterpret_cast<const char*>(&rows), sizeof rows);
+    key.append(reinterpret_cast<const char*>(&cols), sizeof cols);
+    key.append(reinterpret_cast<const char*>(mat), static_cast<size_t>(rows) * cols);
+    std::lock_guard<std::mutex> lk(rs->tab_mu);
+    auto it = rs->tables.find(key);
+    if (it != rs->tables.end()) {
+        *out = it->second;
+        *rows_pad_out = rows_pad;
+        return RS_OK;
+    }
+    if (rs->tables.size() >= kMaxRegistryEntries) {
+        // Bounded registry: drain the device before recycling table memory.
+        if (hipDeviceSynchronize() != hipSuccess) return RS_ERR_DEVICE;
+        for (auto& kv : rs->tables) (void)hipFree(kv.second);
+        rs->tables.clear();
+    }
+    std::vector<uint32_t> host(static_cast<size_t>(cols) * rows_pad * 5, 0);
+    for (int c = 0; c < cols; ++c)
+        for (int r = 0; r < rows; ++r)
+            perm_table(mat[static_cast<size_t>(r) * cols + c], &host[(static_cast<size_t>(c) * rows_pad + r) * 5]);
+    uint32_t* dptr = nullptr;
+    if (hipMalloc(&dptr, host.size() * 4) != hipSuccess) return RS_ERR_DEVICE;
+    if (hipMemcpy(dptr, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(dptr);
+        return RS_ERR_DEVICE;
+    }
+    rs->tables.emplace(std::move(key), dptr);
+    *out = dptr;
+    *rows_pad_out = rows_pad;
+    return RS_OK;
+}
+
+// One launch of the product: out[r] (=|^=) sum_c mat[r][c] * in[c] on every
+// stripe.  in_ptrs/out_ptrs are stripe-0 addresses; stripe s adds s*ss.
+int matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs, int64_t in_ss,
+           uint8_t* const* out_ptrs, int64_t out_ss, int nstripes, uint64_t len, bool accumulate,
+           hipStream_t stream) {
+    if (rows <= 0 || cols <= 0 || nstripes <= 0 || len == 0) return RS_OK;
+    if (rows + cols > kMaxPtrs) return RS_ERR_INVAL;
+    MatmulArgs a;
+    std::memset(&a, 0, sizeof a);
+    int rc = get_tables(rs, mat, rows, cols, &a.tables, &a.rows_pad);
+    if (rc) return rc;
+    a.rows = rows;
+    a.cols = cols;
+    a.nstripes = nstripes;
+    a.accumulate = accumulate ? 1 : 0;
+    a.len = len;
+    a.in_ss = in_ss;
+    a.out_ss = out_ss;
+    for (int c = 0; c < cols; ++c) a.ptr[c] = reinterpret_cast<uint64_t>(in_ptrs[c]);
+    for (int r = 0; r < rows; ++r) a.ptr[cols + r] = reinterpret_cast<uint64_t>(out_ptrs[r]);
+    return launch_gf_matmul(a, stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+
+// ---------------------------------------------------------------- reference checks
+
+int check_encode(const rs_t* rs, const size_t* lens, int n) {  // checkEncode rs.go:119-134
+    if (rs->d + rs->p != n) return RS_ERR_MISMATCH_VECTS;
+    const size_t size = lens[0];
+    if (size == 0) return RS_ERR_ZERO_VECT_SIZE;
+    for (int i = 1; i < n; ++i)
+        if (lens[i] != size) return RS_ERR_MISMATCH_VECT_SIZE;
+    return RS_OK;
+}
+
+// checkEncode of the temporary RS built by reconst rs.go:375-380 over the
+// vectors idx[0..cnt).
+int check_encode_idx(const size_t* lens, const int* idx, int cnt) {
+    const size_t size = lens[idx[0]];
+    if (size == 0) return RS_ERR_ZERO_VECT_SIZE;
+    for (int i = 1; i < cnt; ++i)
+        if (lens[idx[i]] != size) return RS_ERR_MISMATCH_VECT_SIZE;
+    return RS_OK;
+}
+
+int check_vect_idx(const int* idx, int cnt, int n) {  // checkVectIdx rs.go:250-258
+    for (int k = 0; k < cnt; ++k)
+        if (idx[k] < 0 || idx[k] >= n) return RS_ERR_ILLEGAL_VECTS;
+    return RS_OK;
+}
+
+// checkReconst rs.go:264-325
+int plan_reconst(const rs_t* rs, const int* survived, int ns, const int* need, int nn, int* vs, int* nvs,
+                 int* nr, int* nnr, int* dn) {
+    const int d = rs->d, p = rs->p;
+    *nvs = *nnr = *dn = 0;
+    if (nn <= 0) return RS_ERR_NO_NEED_RECONST;
+    if (ns < 0) return RS_ERR_INVAL;
+    int rc = check_vect_idx(survived, ns, d + p);
+    if (rc) return rc;
+    rc = check_vect_idx(need, nn, d + p);
+    if (rc) return rc;
+    enum : uint8_t { kUnknown = 0, kSurvived = 1, kNeed = 2 };
+    uint8_t status[kMaxVects];
+    std::memset(status, ns == 0 ? kSurvived : kUnknown, sizeof status);
+    for (int k = 0; k < ns; ++k) status[survived[k]] = kSurvived;
+    bool full_data = false;
+    for (int k = 0; k < nn; ++k) {
+        status[need[k]] = kNeed;  // need overrides survived
+        if (need[k] >= d) full_data = true;
+    }
+    if (full_data)  // rebuilding parity needs every data vector
+        for (int i = 0; i < d; ++i)
+            if (status[i] == kUnknown) status[i] = kNeed;
+    for (int i = 0; i < d + p; ++i) {
+        if (status[i] == kSurvived) vs[(*nvs)++] = i;
+        else if (status[i] == kNeed) {
+            if (i < d) ++*dn;
+            nr[(*nnr)++] = i;
+        }
+    }
+    if (*nvs < d || *nnr > p) return RS_ERR_TOO_MANY_LOST;
+    return RS_OK;
+}
+
+// getReconstMatrix rs.go:382-412 + makeEncMatrixForReconst matrix.go:68-79 +
+// makeReconstMatrix matrix.go:56-64.  survived_d: the first d survivors.
+int reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out) {
+    const int d = rs->d;
+    std::vector<uint8_t> inv;
+    const uint64_t key = cache_key(survived_d, d);
+    bool hit = false;
+    if (rs->cache_enabled) {
+        std::lock_guard<std::mutex> lk(rs->cache_mu);
+        auto it = rs->cache.find(key);
+        if (it != rs->cache.end()) {
+            inv = it->second;
+            hit = true;
+        }
+    }
+    if (!hit) {
+        std::vector<uint8_t> sub(static_cast<size_t>(d) * d);
+        for (int i = 0; i < d; ++i)
+            std::memcpy(&sub[static_cast<size_t>(i) * d], &rs->enc[static_cast<size_t>(survived_d[i]) * d], d);
+        inv.resize(sub.size());
+        int rc = invert(sub.data(), sub.size(), d, inv.data());
+        if (rc) return rc;
+        if (rs->cache_enabled && rs->cache_n.fetch_add(1) + 1 <= rs->cache_max) {
+            std::lock_guard<std::mutex> lk(rs->cache_mu);
+            rs->cache.emplace(key, inv);
+        }
+    }
+    for (int i = 0; i < nn; ++i)
+        std::memcpy(out + static_cast<size_t>(i) * d, &inv[static_cast<size_t>(need[i]) * d], d);
+    return RS_OK;
+}
+
+int check_update(const rs_t* rs, size_t old_len, size_t new_len, int row, const size_t* plens, int np) {
+    if (np != rs->p) return RS_ERR_MISMATCH_PARITY_NUM;  // checkUpdate rs.go:456-477
+    const size_t size = new_len;
+    if (size == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (size != old_len) return RS_ERR_MISMATCH_VECT_SIZE;
+    for (int i = 0; i < np; ++i)
+        if (plens[i] != size) return RS_ERR_MISMATCH_VECT_SIZE;
+    if (row >= rs->d || row < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
+    return RS_OK;
+}
+
+int check_replace(const rs_t* rs, const size_t* dlens, int nd, const int* rows, int nr, const size_t* plens,
+                  int np) {
+    if (nd > rs->d) return RS_ERR_TOO_MANY_REPLACE;  // checkReplace rs.go:536-570
+    if (nr != nd) return RS_ERR_MISMATCH_REPLACE;
+    if (np != rs->p) return RS_ERR_MISMATCH_PARITY_NUM;
+    if (nd <= 0) return RS_ERR_INVAL;  // reference indexes data[0] and panics
+    const size_t size = dlens[0];
+    if (size == 0) return RS_ERR_ZERO_VECT_SIZE;
+    for (int i = 0; i < nd; ++i)
+        if (dlens[i] != size) return RS_ERR_MISMATCH_VECT_SIZE;
+    for (int i = 0; i < np; ++i)
+        if (plens[i] != size) return RS_ERR_MISMATCH_VECT_SIZE;
+    for (int i = 0; i < nr; ++i)
+        if (rows[i] >= rs->d || rows[i] < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
+    return RS_OK;
+}
+
+// Update's matrix: p x 2, both columns G[j][row] (g*old ^ g*new == g*(old^new),
+// so xorsimd's step rs.go:432-433 folds into the product).
+std::vector<uint8_t> update_matrix(const rs_t* rs, int row) {
+    std::vector<uint8_t> m(static_cast<size_t>(rs->p) * 2);
+    for (int j = 0; j < rs->p; ++j) m[2 * j] = m[2 * j + 1] = rs->gen()[static_cast<size_t>(j) * rs->d + row];
+    return m;
+}
+
+std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr) {  // rs.go:506-514
+    std::vector<uint8_t> m(static_cast<size_t>(rs->p) * nr);
+    for (int i = 0; i < rs->p; ++i)
+        for (int j = 0; j < nr; ++j) m[static_cast<size_t>(i) * nr + j] = rs->gen()[static_cast<size_t>(i) * rs->d + rows[j]];
+    return m;
+}
+
+std::vector<uint8_t> enc_rows(const rs_t* rs, const int* rows, int nrows) {  // reconstParity rs.go:359-362
+    std::vector<uint8_t> m(static_cast<size_t>(nrows) * rs->d);
+    for (int i = 0; i < nrows; ++i)
+        std::memcpy(&m[static_cast<size_t>(i) * rs->d], &rs->enc[static_cast<size_t>(rows[i]) * rs->d], rs->d);
+    return m;
+}
+
+// ---------------------------------------------------------------- host staging
+
+// Staging area for the host-memory entry points: `slots` vectors of `pitch`
+// bytes (pitch 256-aligned so every slot takes the vector kernel).  Caller
+// holds stage_mu.
+int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
+    *pitch = rup(size, 256);
+    const size_t need = *pitch * static_cast<size_t>(slots);
+    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+        return RS_ERR_DEVICE;
+    if (need > rs->stage_bytes) {
+        if (rs->stage) {
+            (void)hipStreamSynchronize(rs->stream);
+            (void)hipFree(rs->stage);
+            rs->stage = nullptr;
+            rs->stage_bytes = 0;
+        }
+        if (hipMalloc(&rs->stage, need) != hipSuccess) return RS_ERR_DEVICE;
+        rs->stage_bytes = need;
+    }
+    return RS_OK;
+}
+
+int h2d(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
+    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
+    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE; }
+
+#define RS_TRY(x)                 \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
+    } while (0)
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Reconst on one stripe whose vectors are addressed by `ptr` (host staging
+// slots or caller device pointers).  Shared by rs_reconst / rs_reconst_dev /
+// rs_reconst_batch.  `before_parity` lets the host path copy the rebuilt data
+// back before the parity check runs (the reference returns the parity-pass
+// error with the data already rebuilt).
+struct ReconstPlan {
+    int vs[kMaxVects], nr[kMaxVects];
+    int nvs = 0, nnr = 0, dn = 0;
+};
+
+}  // namespace
+
+// ======================================================================
+// C ABI
+// ======================================================================
+extern "C" {
+
+const char* rs_strerror(int code) {
+    switch (code) {
+        case RS_OK: return "";
+        case RS_ERR_ILLEGAL_VECTS: return "illegal data/parity number: <= 0 or data+parity > 256";
+        case RS_ERR_MISMATCH_VECTS: return "too few/many vectors given";
+        case RS_ERR_ZERO_VECT_SIZE: return "vector size is 0";
+        case RS_ERR_MISMATCH_VECT_SIZE: return "vectors size mismatched";
+        case RS_ERR_NO_NEED_RECONST: return "no need reconst";
+        case RS_ERR_TOO_MANY_LOST: return "too many lost";
+        case RS_ERR_MISMATCH_PARITY_NUM: return "parity number mismatched";
+        case RS_ERR_ILLEGAL_VECT_INDEX: return "illegal vect index";
+        case RS_ERR_TOO_MANY_REPLACE: return "too many data for replacing";
+        case RS_ERR_MISMATCH_REPLACE: return "number of replaceRows and data mismatch";
+        case RS_ERR_NOT_SQUARE: return "not a square matrix";
+        case RS_ERR_SINGULAR_MATRIX: return "matrix is singular";
+        case RS_ERR_INVAL: return "invalid argument (the reference panics on this input)";
+        case RS_ERR_DEVICE: return "HIP device error";
+        case RS_ERR_NOMEM: return "out of host memory";
+        default: return "unknown error";
+    }
+}
+
+int rs_version(void) { return 100; }
+
+int rs_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : -1;
+}
+
+int rs_new(int data_num, int parity_num, int device, rs_t** out) {
+    if (!out) return RS_ERR_INVAL;
+    *out = nullptr;
+    const int d = data_num, p = parity_num;
+    if (d <= 0 || p <= 0 || d + p > kMaxVects) return RS_ERR_ILLEGAL_VECTS;  // rs.go:61-63
+    rs_t* rs = new (std::nothrow) rs_codec();
+    if (!rs) return RS_ERR_NOMEM;
+    rs->d = d;
+    rs->p = p;
+    rs->enc = make_encode_matrix(d, p);
+    if (d + p <= 64) {  // rs.go:70-74 (the cache key is a 64-bit bitmap)
+        rs->cache_enabled = true;
+        rs->cache_max = kMaxInverseCacheBytes / static_cast<uint64_t>(d) / static_cast<uint64_t>(d);
+    }
+    rs->device = device;
+    *out = rs;
+    return RS_OK;
+}
+
+void rs_free(rs_t* rs) { delete rs; }
+
+int rs_data_num(const rs_t* rs) { return rs ? rs->d : 0; }
+int rs_parity_num(const rs_t* rs) { return rs ? rs->p : 0; }
+
+int rs_gen_matrix(const rs_t* rs, uint8_t* out) {
+    if (!rs || !out) return RS_ERR_INVAL;
+    std::memcpy(out, rs->gen(), static_cast<size_t>(rs->p) * rs->d);
+    return RS_OK;
+}
+
+int rs_enc_matrix(const rs_t* rs, uint8_t* out) {
+    if (!rs || !out) return RS_ERR_INVAL;
+    std::memcpy(out, rs->enc.data(), rs->enc.size());
+    return RS_OK;
+}
+
+uint8_t rs_gf_mul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
+
+int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out) {
+    if (n < 0 || (!m && m_len) || !out) return RS_ERR_INVAL;
+    return invert(m, m_len, n, out);
+}
+
+uint64_t rs_inverse_cache_key(const int* survived, int ns) { return cache_key(survived, ns); }
+
+int64_t rs_inverse_cache_size(const rs_t* rs) {
+    if (!rs) return -1;
+    std::lock_guard<std::mutex> lk(const_cast<rs_t*>(rs)->cache_mu);
+    return static_cast<int64_t>(rs->cache.size());
+}
+
+int rs_plan_reconst(const rs_t* rs, const int* survived, int ns, const int* need, int nn, int* vs, int* nvs,
+                    int* nr, int* nnr, int* dn) {
+    if (!rs || !vs || !nvs || !nr || !nnr || !dn) return RS_ERR_INVAL;
+    return plan_reconst(rs, survived, ns, need, nn, vs, nvs, nr, nnr, dn);
+}
+
+int rs_reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out) {
+    if (!rs || !survived_d || (nn && (!need || !out))) return RS_ERR_INVAL;
+    RS_TRY(check_vect_idx(survived_d, rs->d, rs->d + rs->p));
+    for (int i = 0; i < nn; ++i)
+        if (need[i] < 0 || need[i] >= rs->d) return RS_ERR_INVAL;
+    return reconst_matrix(rs, survived_d, need, nn, out);
+}
+
+// ---------------------------------------------------------------- Encode
+
+int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
+    if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
+    RS_TRY(check_encode(rs, lens, n));
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const int d = rs->d, p = rs->p;
+    const size_t size = lens[0];
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    size_t pitch = 0;
+    RS_TRY(ensure_stage(rs, d + p, size, &pitch));
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    for (int i = 0; i < d; ++i) {
+        RS_TRY(h2d(rs, rs->stage + i * pitch, vects[i], size));
+        in[i] = rs->stage + i * pitch;
+    }
+    for (int j = 0; j < p; ++j) out[j] = rs->stage + (d + j) * pitch;
+    RS_TRY(matmul(rs, rs->gen(), p, d, in, 0, out, 0, 1, size, false, rs->stream));
+    for (int j = 0; j < p; ++j) RS_TRY(d2h(rs, vects[d + j], out[j], size));
+    return sync(rs);
+}
+
+int rs_encode_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, void* stream) {
+    if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
+    RS_TRY(check_encode(rs, lens, n));
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    return matmul(rs, rs->gen(), rs->p, rs->d, vects, 0, vects + rs->d, 0, 1, lens[0], false, as_stream(stream));
+}
+
+int rs_encode_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
+                    void* stream) {
+    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (nstripes == 0) return RS_OK;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    for (int i = 0; i < rs->d; ++i) in[i] = base + i * vect_stride;
+    for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
+    return matmul(rs, rs->gen(), rs->p, rs->d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
+                  as_stream(stream));
+}
+
+// ---------------------------------------------------------------- Reconst
+
+int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
+               const int* need, int nn) {
+    if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+    ReconstPlan pl;
+    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;  // rs.go:225-228
+    if (rc) return rc;
+    const int d = rs->d, pn = pl.nnr - pl.dn;
+    if (!vects || !lens) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    size_t pitch = 0;
+    bool staged_data = false;
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    auto slot = [&](int v) { return rs->stage + static_cast<size_t>(v) * pitch; };
+
+    if (pl.dn > 0) {  // reconstData rs.go:327-349
+        int idx[2 * kMaxVects];
+        for (int i = 0; i < d; ++i) idx[i] = pl.vs[i];
+        for (int i = 0; i < pl.dn; ++i) idx[d + i] = pl.nr[i];
+        for (int i = 0; i < d + pl.dn; ++i)
+            if (idx[i] >= n) return RS_ERR_INVAL;
+        RS_TRY(check_encode_idx(lens, idx, d + pl.dn));
+        const size_t size = lens[idx[0]];
+        std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
+        RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
+        RS_TRY(ensure_stage(rs, rs->d + rs->p, size, &pitch));
+        for (int i = 0; i < d; ++i) {
+            RS_TRY(h2d(rs, slot(pl.vs[i]), vects[pl.vs[i]], size));
+            in[i] = slot(pl.vs[i]);
+        }
+        for (int i = 0; i < pl.dn; ++i) out[i] = slot(pl.nr[i]);
+        RS_TRY(matmul(rs, gm.data(), pl.dn, d, in, 0, out, 0, 1, size, false, rs->stream));
+        for (int i = 0; i < pl.dn; ++i) RS_TRY(d2h(rs, vects[pl.nr[i]], out[i], size));
+        RS_TRY(sync(rs));
+        staged_data = true;
+    }
+    if (pn > 0) {  // reconstParity rs.go:351-373
+        int idx[2 * kMaxVects];
+        for (int i = 0; i < d; ++i) idx[i] = i;
+        for (int i = 0; i < pn; ++i) idx[d + i] = pl.nr[pl.dn + i];
+        for (int i = 0; i < d + pn; ++i)
+            if (idx[i] >= n) return RS_ERR_INVAL;
+        RS_TRY(check_encode_idx(lens, idx, d + pn));
+        const size_t size = lens[0];
+        std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
+        if (!staged_data || rup(size, 256) != pitch) {
+            RS_TRY(ensure_stage(rs, rs->d + rs->p, size, &pitch));
+            for (int i = 0; i < d; ++i) RS_TRY(h2d(rs, slot(i), vects[i], size));
+        }
+        for (int i = 0; i < d; ++i) in[i] = slot(i);
+        for (int i = 0; i < pn; ++i) out[i] = slot(pl.nr[pl.dn + i]);
+        RS_TRY(matmul(rs, gm.data(), pn, d, in, 0, out, 0, 1, size, false, rs->stream));
+        for (int i = 0; i < pn; ++i) RS_TRY(d2h(rs, vects[pl.nr[pl.dn + i]], out[i], size));
+        RS_TRY(sync(rs));
+    }
+    return RS_OK;
+}
+
+int rs_reconst_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
+                   const int* need, int nn, void* stream) {
+    if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+    ReconstPlan pl;
+    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
+    if (rc) return rc;
+    if (!vects || !lens) return RS_ERR_INVAL;
+    const int d = rs->d, pn = pl.nnr - pl.dn;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    if (pl.dn > 0) {
+        int idx[2 * kMaxVects];
+        for (int i = 0; i < d; ++i) idx[i] = pl.vs[i];
+        for (int i = 0; i < pl.dn; ++i) idx[d + i] = pl.nr[i];
+        for (int i = 0; i < d + pl.dn; ++i)
+            if (idx[i] >= n) return RS_ERR_INVAL;
+        RS_TRY(check_encode_idx(lens, idx, d + pl.dn));
+        std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
+        RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
+        for (int i = 0; i < d; ++i) in[i] = vects[pl.vs[i]];
+        for (int i = 0; i < pl.dn; ++i) out[i] = vects[pl.nr[i]];
+        RS_TRY(matmul(rs, gm.data(), pl.dn, d, in, 0, out, 0, 1, lens[idx[0]], false, as_stream(stream)));
+    }
+    if (pn > 0) {
+        int idx[2 * kMaxVects];
+        for (int i = 0; i < d; ++i) idx[i] = i;
+        for (int i = 0; i < pn; ++i) idx[d + i] = pl.nr[pl.dn + i];
+        for (int i = 0; i < d + pn; ++i)
+            if (idx[i] >= n) return RS_ERR_INVAL;
+        RS_TRY(check_encode_idx(lens, idx, d + pn));
+        std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
+        for (int i = 0; i < d; ++i) in[i] = vects[i];
+        for (int i = 0; i < pn; ++i) out[i] = vects[pl.nr[pl.dn + i]];
+        RS_TRY(matmul(rs, gm.data(), pn, d, in, 0, out, 0, 1, lens[0], false, as_stream(stream)));
+    }
+    return RS_OK;
+}
+
+int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
+                     const int* survived, int ns, const int* need, int nn, void* stream) {
+    if (!rs || nstripes < 0 || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+    ReconstPlan pl;
+    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
+    if (rc) return rc;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (nstripes == 0) return RS_OK;
+    if (!base) return RS_ERR_INVAL;
+    const int d = rs->d, pn = pl.nnr - pl.dn;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    if (pl.dn > 0) {
+        std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
+        RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
+        for (int i = 0; i < d; ++i) in[i] = base + pl.vs[i] * vect_stride;
+        for (int i = 0; i < pl.dn; ++i) out[i] = base + pl.nr[i] * vect_stride;
+        RS_TRY(matmul(rs, gm.data(), pl.dn, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
+                      as_stream(stream)));
+    }
+    if (pn > 0) {
+        std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
+        for (int i = 0; i < d; ++i) in[i] = base + i * vect_stride;
+        for (int i = 0; i < pn; ++i) out[i] = base + pl.nr[pl.dn + i] * vect_stride;
+        RS_TRY(matmul(rs, gm.data(), pn, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
+                      as_stream(stream)));
+    }
+    return RS_OK;
+}
+
+// ---------------------------------------------------------------- Update
+
+int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
+              uint8_t* const* parity, const size_t* parity_lens, int np) {
+    if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
+    RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
+    if (!old_data || !new_data) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const int p = rs->p;
+    const size_t size = new_len;
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    size_t pitch = 0;
+    RS_TRY(ensure_stage(rs, 2 + p, size, &pitch));
+    const uint8_t* in[2] = {rs->stage, rs->stage + pitch};
+    uint8_t* out[kMaxVects];
+    RS_TRY(h2d(rs, rs->stage, old_data, size));
+    RS_TRY(h2d(rs, rs->stage + pitch, new_data, size));
+    for (int j = 0; j < p; ++j) {
+        out[j] = rs->stage + (2 + j) * pitch;
+        RS_TRY(h2d(rs, out[j], parity[j], size));
+    }
+    std::vector<uint8_t> gm = update_matrix(rs, row);
+    RS_TRY(matmul(rs, gm.data(), p, 2, in, 0, out, 0, 1, size, true, rs->stream));
+    for (int j = 0; j < p; ++j) RS_TRY(d2h(rs, parity[j], out[j], size));
+    return sync(rs);
+}
+
+int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
+                  uint8_t* const* parity, const size_t* parity_lens, int np, void* stream) {
+    if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
+    RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
+    if (!old_data || !new_data) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[2] = {old_data, new_data};
+    std::vector<uint8_t> gm = update_matrix(rs, row);
+    return matmul(rs, gm.data(), rs->p, 2, in, 0, parity, 0, 1, new_len, true, as_stream(stream));
+}
+
+int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride, const uint8_t* new_base,
+                    int64_t new_stride, int row, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                    int nstripes, size_t len, void* stream) {
+    if (!rs || nstripes < 0) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (row >= rs->d || row < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
+    if (nstripes == 0) return RS_OK;
+    if (!old_base || !new_base || !base) return RS_ERR_INVAL;
+    // One launch shares a single input stripe stride: old and new must step alike.
+    if (nstripes > 1 && old_stride != new_stride) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[2] = {old_base, new_base};
+    uint8_t* out[kMaxVects];
+    for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
+    std::vector<uint8_t> gm = update_matrix(rs, row);
+    return matmul(rs, gm.data(), rs->p, 2, in, old_stride, out, stripe_stride, nstripes, len, true,
+                  as_stream(stream));
+}
+
+// ---------------------------------------------------------------- Replace
+
+int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows, int nr,
+               uint8_t* const* parity, const size_t* parity_lens, int np) {
+    if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
+        (np > 0 && (!parity || !parity_lens)))
+        return RS_ERR_INVAL;
+    RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const int p = rs->p;
+    const size_t size = data_lens[0];
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    size_t pitch = 0;
+    RS_TRY(ensure_stage(rs, nd + p, size, &pitch));
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    for (int i = 0; i < nd; ++i) {
+        in[i] = rs->stage + i * pitch;
+        RS_TRY(h2d(rs, rs->stage + i * pitch, data[i], size));
+    }
+    for (int j = 0; j < p; ++j) {
+        out[j] = rs->stage + (nd + j) * pitch;
+        RS_TRY(h2d(rs, out[j], parity[j], size));
+    }
+    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+    RS_TRY(matmul(rs, gm.data(), p, nr, in, 0, out, 0, 1, size, true, rs->stream));
+    for (int j = 0; j < p; ++j) RS_TRY(d2h(rs, parity[j], out[j], size));
+    return sync(rs);
+}
+
+int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows,
+                   int nr, uint8_t* const* parity, const size_t* parity_lens, int np, void* stream) {
+    if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
+        (np > 0 && (!parity || !parity_lens)))
+        return RS_ERR_INVAL;
+    RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+    return matmul(rs, gm.data(), rs->p, nr, data, 0, parity, 0, 1, data_lens[0], true, as_stream(stream));
+}
+
+int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_stripe_stride, int64_t data_vect_stride,
+                     const int* replace_rows, int nr, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                     int nstripes, size_t len, void* stream) {
+    if (!rs || nstripes < 0 || (nr > 0 && !replace_rows)) return RS_ERR_INVAL;
+    if (nr > rs->d) return RS_ERR_TOO_MANY_REPLACE;
+    if (nr <= 0) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    for (int i = 0; i < nr; ++i)
+        if (replace_rows[i] >= rs->d || replace_rows[i] < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
+    if (nstripes == 0) return RS_OK;
+    if (!data_base || !base) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    for (int i = 0; i < nr; ++i) in[i] = data_base + i * data_vect_stride;
+    for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
+    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+    return matmul(rs, gm.data(), rs->p, nr, in, data_stripe_stride, out, stripe_stride, nstripes, len, true,
+                  as_stream(stream));
+}
+
+// ---------------------------------------------------------------- generic product
+
+int rs_gf_matmul_batch(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* in_base,
+                       int64_t in_stripe_stride, int64_t in_vect_stride, const int* in_map, uint8_t* out_base,
+                       int64_t out_stripe_stride, int64_t out_vect_stride, const int* out_map, int nstripes,
+                       size_t len, int accumulate, void* stream) {
+    if (!rs || !mat || rows <= 0 || cols <= 0 || rows + cols > kMaxPtrs || nstripes < 0) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (nstripes == 0) return RS_OK;
+    if (!in_base || !out_base) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const uint8_t* in[kMaxPtrs];
+    uint8_t* out[kMaxPtrs];
+    for (int c = 0; c < cols; ++c) in[c] = in_base + (in_map ? in_map[c] : c) * in_vect_stride;
+    for (int r = 0; r < rows; ++r) out[r] = out_base + (out_map ? out_map[r] : r) * out_vect_stride;
+    return matmul(rs, mat, rows, cols, in, in_stripe_stride, out, out_stripe_stride, nstripes, len, accumulate != 0,
+                  as_stream(stream));
+}
+
+}  // extern "C"

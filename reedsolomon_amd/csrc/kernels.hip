@@ -1,0 +1,335 @@
+// kernels.hip — CDNA4 (gfx950) kernels for the GF(2^8) matrix product.
+//
+// Replaces the reference's hot loops: the chunk loop
+// rs.go:146-153, the d x p call loop of encodePart rs.go:181-188 and the
+// AVX2 split-nibble kernel gmu_amd64.s:40-329 (mulVectAVX2 / mulVectXORAVX2),
+// plus the scalar tail gmu.go:11-23.
+//
+// Design:
+//  * One launch covers every stripe, every row and every column.  A lane
+//    owns a 16-byte column slice of every vector of its stripe: it streams
+//    the k input slices (global_load_dwordx4, coalesced 1 KiB per wave
+//    instruction), keeps the m output slices in VGPRs, and stores each once.
+//    HBM traffic is the algorithmic (k+m)*len per stripe.
+//  * Multiply-by-constant on four packed bytes = three v_perm_b32 lookups
+//    into 8/8/4-entry byte tables (bit groups {0-2},{3-5},{6-7} of x; the
+//    map x -> c*x is GF(2)-linear, so the three partial products XOR).  The
+//    bit-group extraction is shared by all m rows; per (row, column, dword)
+//    the cost is 3 v_perm + ~1.5 XOR (v_bitop3 xor3).  No MFMA: this is
+//    byte-table work.
+//  * The per-coefficient tables (5 dwords each) are staged once per
+//    workgroup into LDS; the inner loop reads one column's tables with
+//    wave-uniform ds_read_b128 (broadcast) and keeps them in VGPRs for the
+//    lane's 16*VPT bytes.
+//  * Rows beyond the launch's row group and columns beyond `cols` (padding
+//    up to the batch width KB) use all-zero tables, so every lane runs the
+//    same straight-line code: no per-column branches around loads.
+//  * Bytes that are not covered by the aligned 16-byte body (len % 16, or
+//    vectors whose base/stride is not 16-byte aligned) go to a byte-granular
+//    kernel with identical arithmetic.
+#include "kernels.hpp"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace rsamd {
+
+constexpr int kBlock = 256;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;        // global (HBM) 16-byte word
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;  // LDS 16-byte word
+
+LaunchTuning& tuning() {
+    static LaunchTuning t = [] {
+        LaunchTuning x{};
+        const char* g = std::getenv("RSAMD_MAX_GRID");
+        x.max_grid = g ? std::atoi(g) : 0;
+        const char* v = std::getenv("RSAMD_VPT");
+        x.vpt = v ? std::atoi(v) : 1;
+        if (x.vpt != 2) x.vpt = 1;
+        const char* n = std::getenv("RSAMD_NT_STORE");
+        x.nt_store = n ? std::atoi(n) : 1;
+        return x;
+    }();
+    return t;
+}
+
+// c * x for the four bytes of x, given the bit-group indices of x and the
+// coefficient's perm table (t[0..4], see gf256.hpp perm_table()).
+__device__ __forceinline__ uint32_t gf_mul_packed(uint32_t i0, uint32_t i1, uint32_t i2,
+                                                  const uint32_t* t) {
+    return __builtin_amdgcn_perm(t[1], t[0], i0) ^ __builtin_amdgcn_perm(t[3], t[2], i1) ^
+           __builtin_amdgcn_perm(t[4], t[4], i2);
+}
+
+__device__ __forceinline__ void split_groups(uint32_t x, uint32_t& i0, uint32_t& i1, uint32_t& i2) {
+    i0 = x & 0x07070707u;
+    i1 = (x >> 3) & 0x07070707u;
+    i2 = (x >> 6) & 0x03030303u;
+}
+
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+
+// Vector addresses live in the kernarg block as integers; casting them to
+// address_space(1) pointers makes the compiler emit global_* (not flat_*)
+// memory instructions.
+__device__ __forceinline__ const g_u8* in_ptr(const MatmulArgs& a, int col, int s) {
+    return reinterpret_cast<const g_u8*>(a.ptr[col]) + static_cast<int64_t>(s) * a.in_ss;
+}
+__device__ __forceinline__ g_u8* out_ptr(const MatmulArgs& a, int row, int s) {
+    return reinterpret_cast<g_u8*>(a.ptr[a.cols + row]) + static_cast<int64_t>(s) * a.out_ss;
+}
+
+// ---------------------------------------------------------------------------
+// Vector kernel: the aligned 16-byte body of every vector of every stripe.
+//   KB   columns per load batch (all KB loads are issued before the math)
+//   KFIX cols == KB exactly (fully unrolled single batch)
+//   MC   rows per pass (row groups loop when rows > MC)
+//   ACC  XOR into the outputs (Update / Replace) instead of overwriting
+//   VPT  16-byte units per lane per chunk
+// ---------------------------------------------------------------------------
+template <int KB, bool KFIX, int MC, bool ACC, int VPT>
+__global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
+    constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
+    constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+    const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
+
+    const int cols = KFIX ? KB : a.cols;
+    const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
+    const uint64_t nunits = a.body >> 4;
+    const int tid = threadIdx.x;
+
+    for (int rg = 0; rg < a.rows; rg += MC) {
+        if (rg) __syncthreads();  // previous group's readers are done with LDS
+        // Stage this row group's tables: column i, row rr, entry e -> lds32[i*COLD + rr*5 + e].
+        for (int idx = tid; idx < ncols_pad * COLD; idx += kBlock) {
+            const int i = idx / COLD;
+            const int w = idx - i * COLD;
+            const int rr = w / 5;
+            uint32_t v = 0;
+            if (i < cols && rr < MC && rg + rr < a.rows)
+                v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + rg + rr) * 5 + (w - rr * 5)];
+            lds32[idx] = v;
+        }
+        __syncthreads();
+
+        const int nrows = (a.rows - rg) < MC ? (a.rows - rg) : MC;
+        for (int64_t chunk = blockIdx.x; chunk < a.total_chunks; chunk += gridDim.x) {
+            const int s = static_cast<int>(chunk / a.chunks_per_stripe);
+            const int64_t cb = chunk - static_cast<int64_t>(s) * a.chunks_per_stripe;
+            uint64_t off[VPT];
+            bool ok[VPT];
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                const uint64_t u = static_cast<uint64_t>(cb) * a.units_per_chunk + v * kBlock + tid;
+                ok[v] = u < nunits;
+                off[v] = (ok[v] ? u : 0) * 16;  // clamp: out-of-range lanes read unit 0, store nothing
+            }
+
+            uint32_t acc[MC][VPT][4];
+#pragma unroll
+            for (int r = 0; r < MC; ++r)
+#pragma unroll
+                for (int v = 0; v < VPT; ++v)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[r][v][q] = 0;
+            if (ACC) {
+#pragma unroll
+                for (int r = 0; r < MC; ++r)
+                    if (r < nrows)
+#pragma unroll
+                        for (int v = 0; v < VPT; ++v) {
+                            const u32x4 o = *reinterpret_cast<const g_u32x4*>(out_ptr(a, rg + r, s) + off[v]);
+                            acc[r][v][0] = o.x; acc[r][v][1] = o.y; acc[r][v][2] = o.z; acc[r][v][3] = o.w;
+                        }
+            }
+
+            for (int i0 = 0; i0 < ncols_pad; i0 += KB) {
+                // Issue all KB column loads of this batch first (KB*16*VPT bytes in flight per lane).
+                u32x4 x[KB][VPT];
+#pragma unroll
+                for (int b = 0; b < KB; ++b) {
+                    int c = i0 + b;
+                    if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
+                    const g_u8* p = in_ptr(a, c, s);
+#pragma unroll
+                    for (int v = 0; v < VPT; ++v) x[b][v] = *reinterpret_cast<const g_u32x4*>(p + off[v]);
+                }
+                // Tables of column b+1 are read from LDS while column b is computed.
+                u32x4 tv[2][COLW];
+#pragma unroll
+                for (int w = 0; w < COLW; ++w) tv[0][w] = lds_tab[i0 * COLW + w];
+#pragma unroll
+                for (int b = 0; b < KB; ++b) {
+                    // Scheduling fence: keeps each column's LDS reads next to its math
+                    // (hoisted, all k*MC tables would pin ~200 VGPRs: one wave/SIMD).
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (b + 1 < KB) {
+#pragma unroll
+                        for (int w = 0; w < COLW; ++w) tv[(b + 1) & 1][w] = lds_tab[(i0 + b + 1) * COLW + w];
+                    }
+                    uint32_t t[COLD];
+#pragma unroll
+                    for (int w = 0; w < COLW; ++w) {
+                        t[4 * w + 0] = tv[b & 1][w].x; t[4 * w + 1] = tv[b & 1][w].y;
+                        t[4 * w + 2] = tv[b & 1][w].z; t[4 * w + 3] = tv[b & 1][w].w;
+                    }
+#pragma unroll
+                    for (int v = 0; v < VPT; ++v) {
+                        const uint32_t xs[4] = {x[b][v].x, x[b][v].y, x[b][v].z, x[b][v].w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            uint32_t g0, g1, g2;
+                            split_groups(xs[q], g0, g1, g2);
+#pragma unroll
+                            for (int r = 0; r < MC; ++r) acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, &t[r * 5]);
+                        }
+                    }
+                    // Pin the running sums per column: stops LLVM from reassociating
+                    // the XOR chains across columns (which keeps every column's
+                    // partial products live and spills to AGPRs).
+#pragma unroll
+                    for (int r = 0; r < MC; ++r)
+#pragma unroll
+                        for (int v = 0; v < VPT; ++v)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(acc[r][v][q]));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+
+#pragma unroll
+            for (int r = 0; r < MC; ++r) {
+                if (r < nrows) {
+#pragma unroll
+                    for (int v = 0; v < VPT; ++v) {
+                        if (!ok[v]) continue;
+                        g_u32x4* o = reinterpret_cast<g_u32x4*>(out_ptr(a, rg + r, s) + off[v]);
+                        u32x4 val;
+                        val.x = acc[r][v][0]; val.y = acc[r][v][1]; val.z = acc[r][v][2]; val.w = acc[r][v][3];
+                        if (ACC || !a.nt_store) *o = val;
+                        else __builtin_nontemporal_store(val, o);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Byte kernel: any alignment, bytes [start, len) of every vector.  One lane
+// per (stripe, 4-byte group); tables are read straight from global memory.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void gf_matmul_bytes(const MatmulArgs a, uint64_t start,
+                                                          uint64_t groups_per_stripe) {
+    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t total = groups_per_stripe * static_cast<uint64_t>(a.nstripes);
+    if (gid >= total) return;
+    const int s = static_cast<int>(gid / groups_per_stripe);
+    const uint64_t pos = start + (gid - static_cast<uint64_t>(s) * groups_per_stripe) * 4;
+    const int nb = (a.len - pos) < 4 ? static_cast<int>(a.len - pos) : 4;
+
+    for (int r = 0; r < a.rows; ++r) {
+        uint32_t acc = 0;
+        g_u8* o = out_ptr(a, r, s) + pos;
+        if (a.accumulate)
+            for (int q = 0; q < nb; ++q) acc |= static_cast<uint32_t>(o[q]) << (8 * q);
+        for (int c = 0; c < a.cols; ++c) {
+            const g_u8* p = in_ptr(a, c, s) + pos;
+            uint32_t x = 0;
+            for (int q = 0; q < nb; ++q) x |= static_cast<uint32_t>(p[q]) << (8 * q);
+            uint32_t g0, g1, g2;
+            split_groups(x, g0, g1, g2);
+            uint32_t t[5];
+            const uint32_t* tg = a.tables + (static_cast<int64_t>(c) * a.rows_pad + r) * 5;
+            for (int e = 0; e < 5; ++e) t[e] = tg[e];
+            acc ^= gf_mul_packed(g0, g1, g2, t);
+        }
+        for (int q = 0; q < nb; ++q) o[q] = static_cast<uint8_t>(acc >> (8 * q));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side dispatch.
+// ---------------------------------------------------------------------------
+using VecKernel = void (*)(const MatmulArgs);
+
+struct Variant {
+    VecKernel fn;
+    int kb, mc, vpt;
+    bool kfix;
+    const char* name;
+};
+
+#define RSAMD_VARIANT(KB, KFIX, MC, ACC, VPT) \
+    Variant { gf_matmul_vec<KB, KFIX, MC, ACC, VPT>, KB, MC, VPT, KFIX, \
+              "gf_matmul_vec<" #KB "," #KFIX "," #MC "," #ACC "," #VPT ">" }
+
+static Variant pick(int rows, int cols, bool acc, int vpt) {
+    // Specialised shapes: the BASELINE configs (10+4, 12+4 encode; 10-column
+    // reconst with 1-4 outputs; 10+4 Update = 2 columns, accumulate).
+    if (!acc) {
+        if (cols == 10 && rows > 2 && rows <= 4)
+            return vpt == 2 ? RSAMD_VARIANT(10, true, 4, false, 2) : RSAMD_VARIANT(10, true, 4, false, 1);
+        if (cols == 12 && rows > 2 && rows <= 4)
+            return vpt == 2 ? RSAMD_VARIANT(12, true, 4, false, 2) : RSAMD_VARIANT(12, true, 4, false, 1);
+        if (cols == 10 && rows == 1) return RSAMD_VARIANT(10, true, 1, false, 1);
+        if (cols == 10 && rows == 2) return RSAMD_VARIANT(10, true, 2, false, 1);
+        if (rows == 1) return RSAMD_VARIANT(4, false, 1, false, 1);
+        if (rows == 2) return RSAMD_VARIANT(4, false, 2, false, 1);
+        if (rows <= 4) return RSAMD_VARIANT(4, false, 4, false, 1);
+        return RSAMD_VARIANT(4, false, 8, false, 1);
+    }
+    if (cols == 2 && rows > 2 && rows <= 4) return RSAMD_VARIANT(2, true, 4, true, 1);
+    if (rows == 1) return RSAMD_VARIANT(4, false, 1, true, 1);
+    if (rows == 2) return RSAMD_VARIANT(4, false, 2, true, 1);
+    if (rows <= 4) return RSAMD_VARIANT(4, false, 4, true, 1);
+    return RSAMD_VARIANT(4, false, 8, true, 1);
+}
+
+const char* vector_kernel_name(int rows, int cols, int accumulate) {
+    return pick(rows, cols, accumulate != 0, tuning().vpt).name;
+}
+
+static bool aligned16(uint64_t v) { return (v & 15u) == 0; }
+
+hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
+    if (a.len == 0 || a.nstripes <= 0 || a.rows <= 0 || a.cols <= 0) return hipSuccess;
+    // Vector body only when every base pointer and both stripe strides are
+    // 16-byte aligned (global_load/store_dwordx4 on naturally aligned data).
+    bool aligned = aligned16(static_cast<uint64_t>(a.in_ss)) && aligned16(static_cast<uint64_t>(a.out_ss));
+    for (int v = 0; v < a.cols + a.rows && aligned; ++v) aligned = aligned16(a.ptr[v]);
+    a.body = aligned ? (a.len & ~static_cast<uint64_t>(15)) : 0;
+    a.tail_start = a.body;
+
+    if (a.body) {
+        const LaunchTuning& tu = tuning();
+        const Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt);
+        a.units_per_chunk = kBlock * var.vpt;
+        a.nt_store = tu.nt_store;
+        const uint64_t nunits = a.body >> 4;
+        a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
+        a.total_chunks = a.chunks_per_stripe * a.nstripes;
+        int64_t grid = a.total_chunks;
+        if (tu.max_grid > 0 && grid > tu.max_grid) grid = tu.max_grid;
+        const int ncols_pad = var.kfix ? var.kb : ((a.cols + var.kb - 1) / var.kb) * var.kb;
+        const int cold = ((var.mc * 5 + 3) / 4) * 4;
+        const size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
+        hipLaunchKernelGGL(var.fn, dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds, stream, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (a.tail_start < a.len) {
+        const uint64_t groups = (a.len - a.tail_start + 3) / 4;
+        const uint64_t total = groups * static_cast<uint64_t>(a.nstripes);
+        const uint64_t grid = (total + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(gf_matmul_bytes, dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, stream, a,
+                           a.tail_start, groups);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace rsamd

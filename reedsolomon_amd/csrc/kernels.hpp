@@ -1,0 +1,54 @@
+// kernels.hpp — launch interface of the GF(2^8) matrix-product kernels.
+//
+// Everything in the reference's hot path reduces to one primitive
+// (rs.go:175-203 encodePart over gmu.go:4-9 / gmu_amd64.s):
+//     out[r] (=|^=) XOR_c  G[r][c] (x) in[c]          byte-wise
+// applied to every stripe of a batch.  One launch computes it for all rows,
+// all columns and all stripes; a lane keeps its slice of every output row in
+// VGPRs, so each input byte is read from HBM once and each output byte is
+// written once (no d*p call fan-out, no chunking for cache).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rsamd {
+
+constexpr int kMaxPtrs = 260;  // inputs + outputs of one launch (d+p <= 256, Update adds 1)
+
+// Kernel arguments (passed by value, ~2.2 KB of kernarg).  Vector v of
+// stripe s is at  ptr[v] + s * (v < cols ? in_ss : out_ss).
+struct MatmulArgs {
+    const uint32_t* tables;   // device perm tables, [cols][rows_pad][5] dwords
+    int rows, cols, rows_pad;
+    int nstripes;
+    int accumulate;           // 0: overwrite (Encode), 1: XOR into out (updateOnly)
+    int units_per_chunk;      // 16-byte units per workgroup-chunk (block * vpt)
+    int nt_store;             // non-temporal output stores (overwrite mode)
+    uint64_t len;             // bytes per vector
+    uint64_t body;            // bytes handled by the vector kernel (multiple of 16)
+    uint64_t tail_start;      // first byte handled by the byte kernel
+    int64_t in_ss, out_ss;    // stripe strides in bytes
+    int64_t chunks_per_stripe;
+    int64_t total_chunks;
+    uint64_t ptr[kMaxPtrs];   // inputs [0, cols), outputs [cols, cols+rows)
+};
+
+// Launch tuning knobs (read from the environment once).
+struct LaunchTuning {
+    int max_grid;     // cap on workgroups of the vector kernel (0 = one per chunk)
+    int vpt;          // 16-byte units per lane per chunk (1 or 2)
+    int nt_store;     // non-temporal parity stores
+};
+LaunchTuning& tuning();
+
+// Enqueue the product on `stream`.  Splits the work into the 16-byte vector
+// body (aligned pointers/strides) and a byte-granular remainder.  Returns a
+// hipError_t.
+hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream);
+
+// Human-readable name of the vector kernel instantiation that
+// launch_gf_matmul picks for (rows, cols, accumulate) — used by the profiler
+// scripts to find the dominant kernel in rocprof output.
+const char* vector_kernel_name(int rows, int cols, int accumulate);
+
+}  // namespace rsamd

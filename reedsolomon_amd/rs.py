@@ -1,0 +1,372 @@
+"""Python mirror of templexxx/reedsolomon's public API on top of librsamd.
+
+    import reedsolomon_amd as reedsolomon
+    r = reedsolomon.New(10, 4)            # rs.go:54
+    r.Encode(vects)                       # rs.go:104  (vects: 14 writable uint8 buffers)
+    r.Reconst(vects, survived, need)      # rs.go:221
+    r.Update(old, new, row, parity)       # rs.go:424
+    r.Replace(data, rows, parity)         # rs.go:492
+
+Same names, argument meaning, in-place outputs and error behaviour as the
+Go methods: every reference sentinel error is an exception class here
+(ErrMismatchVects, ErrTooManyLost, ...) raised where the Go method returns
+it.  Host buffers are numpy uint8 arrays, bytearrays or writable
+memoryviews.  The *_dev / *_batch methods take torch uint8 tensors that live
+on the GPU and run asynchronously on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from ._lib import c_u8p, lib
+
+
+# ---------------------------------------------------------------- errors
+
+class RSError(Exception):
+    """Base of every codec error; ``code`` is the C ABI return code."""
+
+    code = -1
+
+    def __init__(self, msg: str | None = None):
+        super().__init__(msg if msg is not None else lib().rs_strerror(self.code).decode())
+
+
+class ErrIllegalVects(RSError):        # rs.go:44
+    code = 1
+
+
+class ErrMismatchVects(RSError):       # rs.go:114
+    code = 2
+
+
+class ErrZeroVectSize(RSError):        # rs.go:115
+    code = 3
+
+
+class ErrMismatchVectSize(RSError):    # rs.go:116
+    code = 4
+
+
+class ErrNoNeedReconst(RSError):       # rs.go:240 (swallowed by Reconst)
+    code = 5
+
+
+class ErrTooManyLost(RSError):         # rs.go:241
+    code = 6
+
+
+class ErrMismatchParityNum(RSError):   # rs.go:452
+    code = 7
+
+
+class ErrIllegalVectIndex(RSError):    # rs.go:453
+    code = 8
+
+
+class ErrTooManyReplace(RSError):      # rs.go:532
+    code = 9
+
+
+class ErrMismatchReplace(RSError):     # rs.go:533
+    code = 10
+
+
+class ErrNotSquare(RSError):           # matrix.go:81
+    code = 11
+
+
+class ErrSingularMatrix(RSError):      # matrix.go:82
+    code = 12
+
+
+class ErrInvalidArgument(RSError):     # inputs the reference panics on
+    code = 13
+
+
+class ErrDevice(RSError):              # HIP runtime failure
+    code = 14
+
+
+class ErrNoMemory(RSError):
+    code = 15
+
+
+_ERRORS = {cls.code: cls for cls in (
+    ErrIllegalVects, ErrMismatchVects, ErrZeroVectSize, ErrMismatchVectSize, ErrNoNeedReconst,
+    ErrTooManyLost, ErrMismatchParityNum, ErrIllegalVectIndex, ErrTooManyReplace, ErrMismatchReplace,
+    ErrNotSquare, ErrSingularMatrix, ErrInvalidArgument, ErrDevice, ErrNoMemory)}
+
+
+def _check(rc: int) -> None:
+    if rc:
+        raise _ERRORS.get(rc, RSError)()
+
+
+# ---------------------------------------------------------------- marshalling
+
+def _host_array(buf, writable: bool) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        a = buf
+    else:
+        a = np.frombuffer(buf, dtype=np.uint8)
+    if a.dtype != np.uint8 or a.ndim != 1 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("vectors must be 1-D contiguous uint8 buffers")
+    if writable and not a.flags["WRITEABLE"]:
+        raise TypeError("output vector is read-only")
+    return a
+
+
+def _host_vecs(bufs: Sequence, writable: bool):
+    arrs = [_host_array(b, writable) for b in bufs]
+    n = len(arrs)
+    ptrs = (c_u8p * max(n, 1))()
+    lens = (ctypes.c_size_t * max(n, 1))()
+    for i, a in enumerate(arrs):
+        ptrs[i] = a.ctypes.data_as(c_u8p)
+        lens[i] = a.size
+    return arrs, ptrs, lens, n
+
+
+def _dev_vecs(tensors: Sequence):
+    n = len(tensors)
+    ptrs = (c_u8p * max(n, 1))()
+    lens = (ctypes.c_size_t * max(n, 1))()
+    for i, t in enumerate(tensors):
+        _check_tensor(t)
+        ptrs[i] = ctypes.cast(ctypes.c_void_p(t.data_ptr()), c_u8p)
+        lens[i] = t.numel()
+    return ptrs, lens, n
+
+
+def _check_tensor(t) -> None:
+    import torch
+
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or not t.is_cuda:
+        raise TypeError("device vectors must be torch.uint8 tensors on a GPU")
+    if not t.is_contiguous():
+        raise TypeError("device vectors must be contiguous")
+
+
+def _ints(xs):
+    xs = [int(x) for x in (xs or [])]
+    return (ctypes.c_int * max(len(xs), 1))(*xs), len(xs)
+
+
+def _stream(stream) -> ctypes.c_void_p:
+    if stream is None:
+        import torch
+
+        stream = torch.cuda.current_stream()
+    if hasattr(stream, "cuda_stream"):
+        stream = stream.cuda_stream
+    return ctypes.c_void_p(int(stream))
+
+
+# ---------------------------------------------------------------- codec
+
+class RS:
+    """Reed-Solomon encoder/decoder (rs.go:22-42).  Create with :func:`New`."""
+
+    def __init__(self, handle: ctypes.c_void_p, device: int):
+        self._h = handle
+        self.device = device
+        L = lib()
+        self.DataNum = L.rs_data_num(handle)
+        self.ParityNum = L.rs_parity_num(handle)
+        d, p = self.DataNum, self.ParityNum
+        g = np.zeros(d * p, np.uint8)
+        _check(L.rs_gen_matrix(handle, g.ctypes.data_as(c_u8p)))
+        e = np.zeros((d + p) * d, np.uint8)
+        _check(L.rs_enc_matrix(handle, e.ctypes.data_as(c_u8p)))
+        self.GenMatrix = g            # p x d, row-major: G[j*d+i]   (rs.go:31)
+        self.encMatrix = e            # (d+p) x d                      (rs.go:30)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                lib().rs_free(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------ host memory (Go API)
+
+    def Encode(self, vects: Sequence) -> None:
+        """rs.go:104 — vects[d:] = GenMatrix x vects[:d]."""
+        _, ptrs, lens, n = _host_vecs(vects, writable=False)
+        _check(lib().rs_encode(self._h, ptrs, lens, n))
+
+    def Reconst(self, vects: Sequence, survived: Sequence[int] | None, needReconst: Sequence[int] | None) -> None:
+        """rs.go:221 — rebuild vects[needReconst] from vects[survived]."""
+        _, ptrs, lens, n = _host_vecs(vects, writable=False)
+        s, ns = _ints(survived)
+        q, nq = _ints(needReconst)
+        _check(lib().rs_reconst(self._h, ptrs, lens, n, s, ns, q, nq))
+
+    def Update(self, oldData, newData, row: int, parity: Sequence) -> None:
+        """rs.go:424 — parity[j] ^= G[j][row] x (oldData ^ newData)."""
+        o = _host_array(oldData, False)
+        w = _host_array(newData, False)
+        _, ptrs, lens, n = _host_vecs(parity, writable=True)
+        _check(lib().rs_update(self._h, o.ctypes.data_as(c_u8p), o.size, w.ctypes.data_as(c_u8p), w.size,
+                               int(row), ptrs, lens, n))
+
+    def Replace(self, data: Sequence, replaceRows: Sequence[int], parity: Sequence) -> None:
+        """rs.go:492 — parity[j] ^= sum_k G[j][replaceRows[k]] x data[k]."""
+        _, dptrs, dlens, nd = _host_vecs(data, writable=False)
+        r, nr = _ints(replaceRows)
+        _, pptrs, plens, np_ = _host_vecs(parity, writable=True)
+        _check(lib().rs_replace(self._h, dptrs, dlens, nd, r, nr, pptrs, plens, np_))
+
+    # ------------------------------------------------ device memory, one stripe
+
+    def encode_dev(self, vects: Sequence, stream=None) -> None:
+        ptrs, lens, n = _dev_vecs(vects)
+        _check(lib().rs_encode_dev(self._h, ptrs, lens, n, _stream(stream)))
+
+    def reconst_dev(self, vects: Sequence, survived, needReconst, stream=None) -> None:
+        ptrs, lens, n = _dev_vecs(vects)
+        s, ns = _ints(survived)
+        q, nq = _ints(needReconst)
+        _check(lib().rs_reconst_dev(self._h, ptrs, lens, n, s, ns, q, nq, _stream(stream)))
+
+    def update_dev(self, oldData, newData, row: int, parity: Sequence, stream=None) -> None:
+        _check_tensor(oldData)
+        _check_tensor(newData)
+        ptrs, lens, n = _dev_vecs(parity)
+        _check(lib().rs_update_dev(
+            self._h, ctypes.cast(ctypes.c_void_p(oldData.data_ptr()), c_u8p), oldData.numel(),
+            ctypes.cast(ctypes.c_void_p(newData.data_ptr()), c_u8p), newData.numel(), int(row), ptrs, lens, n,
+            _stream(stream)))
+
+    def replace_dev(self, data: Sequence, replaceRows, parity: Sequence, stream=None) -> None:
+        dptrs, dlens, nd = _dev_vecs(data)
+        r, nr = _ints(replaceRows)
+        pptrs, plens, np_ = _dev_vecs(parity)
+        _check(lib().rs_replace_dev(self._h, dptrs, dlens, nd, r, nr, pptrs, plens, np_, _stream(stream)))
+
+    # ------------------------------------------------ device memory, batched stripes
+
+    @staticmethod
+    def _stripes(buf, nvec: int):
+        """buf: uint8 GPU tensor [S, nvec, len] (any strides with unit inner stride)."""
+        _check_tensor_any(buf)
+        if buf.dim() != 3 or buf.shape[1] < nvec or buf.stride(2) != 1:
+            raise TypeError(f"expected a [stripes, >= {nvec}, len] uint8 GPU tensor with unit inner stride")
+        return ctypes.c_void_p(buf.data_ptr()), buf.stride(0), buf.stride(1), buf.shape[0], buf.shape[2]
+
+    def encode_batch(self, buf, stream=None) -> None:
+        """Encode every stripe of buf[S, d+p, len] (the north-star hot path)."""
+        base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
+        _check(lib().rs_encode_batch(self._h, base, ss, vs, S, n, _stream(stream)))
+
+    def reconst_batch(self, buf, survived, needReconst, stream=None) -> None:
+        base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
+        s, ns = _ints(survived)
+        q, nq = _ints(needReconst)
+        _check(lib().rs_reconst_batch(self._h, base, ss, vs, S, n, s, ns, q, nq, _stream(stream)))
+
+    def update_batch(self, old, new, row: int, buf, stream=None) -> None:
+        """old/new: [S, len] GPU tensors; parity rows of buf[S, d+p, len] are updated."""
+        base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
+        for t in (old, new):
+            _check_tensor_any(t)
+            if t.dim() != 2 or t.shape[0] != S or t.shape[1] != n or t.stride(1) != 1:
+                raise TypeError("old/new must be [stripes, len] uint8 GPU tensors")
+        _check(lib().rs_update_batch(self._h, ctypes.c_void_p(old.data_ptr()), old.stride(0),
+                                     ctypes.c_void_p(new.data_ptr()), new.stride(0), int(row), base, ss, vs, S, n,
+                                     _stream(stream)))
+
+    def replace_batch(self, data, replaceRows, buf, stream=None) -> None:
+        """data: [S, rn, len] GPU tensor of replacement vectors."""
+        base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
+        _check_tensor_any(data)
+        if data.dim() != 3 or data.shape[0] != S or data.shape[2] != n or data.stride(2) != 1:
+            raise TypeError("data must be a [stripes, rn, len] uint8 GPU tensor")
+        r, nr = _ints(replaceRows)
+        if data.shape[1] != nr:
+            raise ErrMismatchReplace()
+        _check(lib().rs_replace_batch(self._h, ctypes.c_void_p(data.data_ptr()), data.stride(0), data.stride(1),
+                                      r, nr, base, ss, vs, S, n, _stream(stream)))
+
+    def gf_matmul_batch(self, mat: np.ndarray, src, in_map, dst, out_map, accumulate=False, stream=None) -> None:
+        """dst[:, out_map[r]] (=|^=) sum_c mat[r, c] x src[:, in_map[c]] for every stripe."""
+        mat = np.ascontiguousarray(mat, dtype=np.uint8)
+        rows, cols = mat.shape
+        _check_tensor_any(src)
+        _check_tensor_any(dst)
+        if src.dim() != 3 or dst.dim() != 3 or src.shape[0] != dst.shape[0] or src.shape[2] != dst.shape[2]:
+            raise TypeError("src/dst must be [stripes, vectors, len] uint8 GPU tensors")
+        im, _ = _ints(in_map if in_map is not None else range(cols))
+        om, _ = _ints(out_map if out_map is not None else range(rows))
+        _check(lib().rs_gf_matmul_batch(
+            self._h, mat.ctypes.data_as(c_u8p), rows, cols, ctypes.c_void_p(src.data_ptr()), src.stride(0),
+            src.stride(1), im, ctypes.c_void_p(dst.data_ptr()), dst.stride(0), dst.stride(1), om,
+            src.shape[0], src.shape[2], int(bool(accumulate)), _stream(stream)))
+
+    # ------------------------------------------------ host-side planning
+
+    def plan_reconst(self, survived, needReconst):
+        """checkReconst rs.go:264-325 -> (survived, needReconst(sorted, data first), dataNeedReconstN)."""
+        s, ns = _ints(survived)
+        q, nq = _ints(needReconst)
+        vs = (ctypes.c_int * 256)()
+        nr = (ctypes.c_int * 256)()
+        nvs, nnr, dn = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().rs_plan_reconst(self._h, s, ns, q, nq, vs, ctypes.byref(nvs), nr, ctypes.byref(nnr),
+                                     ctypes.byref(dn)))
+        return list(vs[: nvs.value]), list(nr[: nnr.value]), dn.value
+
+    def reconst_matrix(self, survived, needReconst) -> np.ndarray:
+        """getReconstMatrix rs.go:382-412 (through the inverse cache)."""
+        s, ns = _ints(survived)
+        q, nq = _ints(needReconst)
+        out = np.zeros(max(nq, 1) * self.DataNum, np.uint8)
+        _check(lib().rs_reconst_matrix(self._h, s, q, nq, out.ctypes.data_as(c_u8p)))
+        return out[: nq * self.DataNum]
+
+    def inverse_cache_size(self) -> int:
+        return int(lib().rs_inverse_cache_size(self._h))
+
+
+def _check_tensor_any(t) -> None:
+    import torch
+
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or not t.is_cuda:
+        raise TypeError("expected a torch.uint8 tensor on a GPU")
+
+
+def New(dataNum: int, parityNum: int, device: int = -1) -> RS:
+    """rs.go:54 — validates d>0, p>0, d+p<=256 (else ErrIllegalVects)."""
+    h = ctypes.c_void_p()
+    _check(lib().rs_new(int(dataNum), int(parityNum), int(device), ctypes.byref(h)))
+    return RS(h, device)
+
+
+# ---------------------------------------------------------------- free helpers
+
+def invert(m, n: int) -> np.ndarray:
+    """matrix.go:85-147 (raises ErrNotSquare / ErrSingularMatrix)."""
+    m = np.ascontiguousarray(np.frombuffer(bytes(m), np.uint8) if not isinstance(m, np.ndarray) else m,
+                             dtype=np.uint8)
+    out = np.zeros(max(n * n, 1), np.uint8)
+    _check(lib().rs_matrix_invert(m.ctypes.data_as(c_u8p), m.size, int(n), out.ctypes.data_as(c_u8p)))
+    return out[: n * n]
+
+
+def inverse_cache_key(survived) -> int:
+    s, ns = _ints(survived)
+    return int(lib().rs_inverse_cache_key(s, ns))
+
+
+def gf_mul(a: int, b: int) -> int:
+    return int(lib().rs_gf_mul(a, b))
+
+
+def device_count() -> int:
+    return int(lib().rs_device_count())

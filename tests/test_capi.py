@@ -1,0 +1,201 @@
+"""C ABI checks that need no GPU: the library loads, exports every symbol of
+include/rs_amd.h, and its host-side logic (checks, planning, matrices,
+inverse cache) equals the oracle's."""
+import itertools
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "rs_amd.h")).read()
+    return sorted(set(re.findall(r"^RS_API\s+[\w\s\*]+?\b(rs_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_api():
+    syms = _header_symbols()
+    for s in ("rs_new", "rs_encode", "rs_reconst", "rs_update", "rs_replace", "rs_encode_batch"):
+        assert s in syms
+    assert len(syms) >= 25
+
+
+def test_library_exports_every_header_symbol(rslib):
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", rslib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (rs_\w+)", out))
+    missing = [s for s in _header_symbols() if s not in exported]
+    assert not missing, missing
+    # ctypes binds each one
+    lib = rslib.lib()
+    for s in _header_symbols():
+        assert hasattr(lib, s)
+    # nothing but the C ABI leaks out
+    assert all(s.startswith("rs_") for s in exported)
+
+
+def test_python_binding_covers_header(rslib):
+    from reedsolomon_amd._lib import SIGNATURES
+
+    assert sorted(SIGNATURES) == _header_symbols()
+
+
+def test_error_codes_match_oracle():
+    """include/rs_amd.h and oracle/rs_oracle.h number the errors identically."""
+    h = open(os.path.join(ROOT, "include", "rs_amd.h")).read()
+    o = open(os.path.join(ROOT, "oracle", "rs_oracle.h")).read()
+    prod = dict(re.findall(r"RS_ERR_(\w+) = (\d+)", h))
+    orac = dict(re.findall(r"ORC_ERR_(\w+) = (\d+)", o))
+    assert orac and all(prod[k] == v for k, v in orac.items())
+
+
+def test_error_text(rslib):
+    L = rslib.lib()
+    texts = {1: "illegal data/parity number: <= 0 or data+parity > 256", 2: "too few/many vectors given",
+             3: "vector size is 0", 4: "vectors size mismatched", 5: "no need reconst", 6: "too many lost",
+             7: "parity number mismatched", 8: "illegal vect index", 9: "too many data for replacing",
+             10: "number of replaceRows and data mismatch", 11: "not a square matrix", 12: "matrix is singular"}
+    for code, t in texts.items():  # rs.go:44,113-117,239-242,451-454,531-534; matrix.go:81-82
+        assert L.rs_strerror(code).decode() == t
+
+
+def test_new_validation(rslib):  # rs.go:61-63
+    R = rslib
+    for d, p in [(0, 1), (1, 0), (-1, 4), (200, 57), (256, 1)]:
+        with pytest.raises(R.ErrIllegalVects):
+            R.New(d, p)
+    for d, p in [(1, 1), (255, 1), (1, 255), (128, 128), (10, 4)]:
+        r = R.New(d, p)
+        assert (r.DataNum, r.ParityNum) == (d, p)
+
+
+@pytest.mark.parametrize("d,p", [(1, 1), (4, 4), (5, 5), (10, 4), (12, 4), (17, 3), (64, 64), (200, 56)])
+def test_matrices_match_oracle(rslib, orc, d, p):
+    r = rslib.New(d, p)
+    assert np.array_equal(r.encMatrix, orc.make_encode_matrix(d, p))
+    assert np.array_equal(r.GenMatrix, orc.gen_matrix(d, p))
+
+
+def test_gf_mul_table(rslib, orc):
+    mul = orc.tables()["mul"]
+    for a in range(0, 256, 7):
+        for b in range(256):
+            assert rslib.gf_mul(a, b) == mul[a, b]
+
+
+def test_invert_kats_and_random(rslib, orc):
+    import json
+
+    kats = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")))["matrix_invert"]
+    errs = {11: rslib.ErrNotSquare, 12: rslib.ErrSingularMatrix}
+    for c in kats["cases"]:
+        if c["err"]:
+            with pytest.raises(errs[c["err"]]):
+                rslib.invert(np.array(c["m"], np.uint8), c["n"])
+        else:
+            assert rslib.invert(np.array(c["m"], np.uint8), c["n"]).tolist() == c["expect"]
+    rng = np.random.default_rng(11)
+    for n in (1, 2, 3, 7, 16, 40):
+        for _ in range(10):
+            m = rng.integers(0, 256, n * n, dtype=np.uint8)
+            rc, exp = orc.invert(m, n)
+            if rc:
+                with pytest.raises(rslib.RSError):
+                    rslib.invert(m, n)
+            else:
+                assert np.array_equal(rslib.invert(m, n), exp)
+
+
+def test_inverse_cache_key(rslib, orc):
+    rng = np.random.default_rng(12)
+    for _ in range(200):
+        s = sorted(rng.choice(64, int(rng.integers(1, 64)), replace=False).tolist())
+        assert rslib.inverse_cache_key(s) == orc.inverse_cache_key(s)
+    assert rslib.inverse_cache_key(list(range(64))) == 2 ** 64 - 1
+
+
+def test_plan_reconst_matches_oracle(rslib, orc):
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(13)
+    cases = [([], []), ([], [0]), ([], [13]), ([1, 2, 3], [0, 1]), ([14], [0]), ([0], [-1]),
+             ([], [0, 1, 2, 3, 4]), (list(range(1, 14)), [0, 10])]
+    for _ in range(500):
+        ns, nn = int(rng.integers(0, 15)), int(rng.integers(0, 6))
+        cases.append((rng.choice(14, ns, replace=False).tolist(), rng.choice(14, nn, replace=False).tolist()))
+    for surv, need in cases:
+        rc, vs, nr, dn = orc.check_reconst(d, p, surv, need)
+        if rc:
+            with pytest.raises(rslib.RSError) as ei:
+                r.plan_reconst(surv, need)
+            assert ei.value.code == rc
+        else:
+            assert r.plan_reconst(surv, need) == (vs, nr, dn)
+
+
+def test_reconst_matrix_and_cache(rslib, orc):
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    em = orc.make_encode_matrix(d, p).reshape(d + p, d)
+    n_patterns = 0
+    for lost in itertools.combinations(range(d + p), 3):
+        surv = [i for i in range(d + p) if i not in lost][:d]
+        need = [i for i in lost if i < d]
+        if not need:
+            continue
+        rc, inv = orc.invert(np.ascontiguousarray(em[surv]).ravel(), d)
+        assert rc == 0
+        exp = inv.reshape(d, d)[need].ravel()
+        assert np.array_equal(r.reconst_matrix(surv, need), exp)
+        assert np.array_equal(r.reconst_matrix(surv, need), exp)  # cache hit returns the same bytes
+        n_patterns += 1
+    assert r.inverse_cache_size() == len({tuple([i for i in range(d + p) if i not in lost][:d])
+                                          for lost in itertools.combinations(range(d + p), 3)
+                                          if any(i < d for i in lost)})
+
+
+def test_cache_disabled_when_wide(rslib):  # rs.go:70 (d+p <= 64 only)
+    r = rslib.New(40, 30)
+    r.reconst_matrix(list(range(1, 41)), [0])
+    assert r.inverse_cache_size() == 0
+
+
+def _z(n):
+    return np.zeros(n, np.uint8)
+
+
+def test_host_checks_before_device(rslib, orc):
+    """Malformed calls return the reference's error with no GPU present."""
+    R = rslib
+    r = R.New(10, 4)
+    cases = [
+        (lambda: r.Encode([_z(8)] * 13), 2),
+        (lambda: r.Encode([_z(0)] + [_z(8)] * 13), 3),
+        (lambda: r.Encode([_z(8)] * 13 + [_z(9)]), 4),
+        (lambda: r.Reconst([_z(8)] * 14, [14], [0]), 1),
+        (lambda: r.Reconst([_z(8)] * 14, [], [0, 1, 2, 3, 4]), 6),
+        (lambda: r.Update(_z(8), _z(8), 0, [_z(8)] * 3), 7),
+        (lambda: r.Update(_z(8), _z(0), 0, [_z(8)] * 4), 3),
+        (lambda: r.Update(_z(7), _z(8), 0, [_z(8)] * 4), 4),
+        (lambda: r.Update(_z(8), _z(8), 0, [_z(8)] * 3 + [_z(7)]), 4),
+        (lambda: r.Update(_z(8), _z(8), -1, [_z(8)] * 4), 8),
+        (lambda: r.Replace([_z(8)] * 11, list(range(11)), [_z(8)] * 4), 9),
+        (lambda: r.Replace([_z(8)] * 2, [0], [_z(8)] * 4), 10),
+        (lambda: r.Replace([_z(8)] * 2, [0, 1], [_z(8)] * 3), 7),
+        (lambda: r.Replace([_z(0)] * 2, [0, 1], [_z(8)] * 4), 3),
+        (lambda: r.Replace([_z(8), _z(9)], [0, 1], [_z(8)] * 4), 4),
+        (lambda: r.Replace([_z(8)] * 2, [0, 1], [_z(8)] * 3 + [_z(1)]), 4),
+        (lambda: r.Replace([_z(8)] * 2, [0, 10], [_z(8)] * 4), 8),
+        (lambda: r.Replace([], [], [_z(8)] * 4), 13),
+    ]
+    for fn, code in cases:
+        with pytest.raises(R.RSError) as ei:
+            fn()
+        assert ei.value.code == code
+    # nothing to rebuild: Reconst swallows ErrNoNeedReconst (rs.go:225-228)
+    r.Reconst([_z(8)] * 14, [0, 1], [])

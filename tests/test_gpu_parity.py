@@ -1,0 +1,429 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact for every byte (integer GF(2^8) work: no tolerance).  Mirrors
+the reference's own tests (rs_test.go) at the sizes the oracle finishes in
+seconds, plus size-independent properties (encode -> erase -> reconst round
+trips, linearity) at BASELINE.json's full 10+4 / 1 MiB x 256-stripe size.
+"""
+import itertools
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    torch.cuda.init()
+    return torch
+
+
+def _rand(rng, *shape):
+    return rng.integers(0, 256, shape, dtype=np.uint8)
+
+
+def _oracle_encode(orc, d, p, data_list):
+    size = data_list[0].size
+    v = [x.copy() for x in data_list] + [np.zeros(size, np.uint8) for _ in range(p)]
+    assert orc.encode(d, p, v) == 0
+    return v[d:]
+
+
+# ---------------------------------------------------------------- Encode (host API)
+
+def test_encode_all_sizes_1_to_1024(rslib, orc, torch_dev):  # TestRS_Encode rs_test.go:72-137
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(100)
+    gen = orc.gen_matrix(d, p)
+    for size in range(1, 1025):
+        data = [_rand(rng, size) for _ in range(d)]
+        act = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
+        r.Encode(act)
+        exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+        orc.naive_mul(gen, d, p, exp)
+        for j in range(d, d + p):
+            assert np.array_equal(act[j], exp[j]), (size, j)
+
+
+@pytest.mark.parametrize("d,p,size", [
+    (1, 1, 1000), (2, 2, 4097), (3, 2, 65536 + 3), (5, 5, 8192), (10, 4, 1 << 20), (12, 4, 1 << 20),
+    (17, 3, 12345), (28, 4, 8192), (10, 8, 4096), (6, 12, 3000), (64, 64, 2048), (128, 128, 512),
+    (200, 56, 300), (255, 1, 1024), (1, 255, 257),
+])
+def test_encode_shapes(rslib, orc, torch_dev, d, p, size):
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(d * 1000 + p)
+    data = [_rand(rng, size) for _ in range(d)]
+    act = [x.copy() for x in data] + [np.full(size, 0x5A, np.uint8) for _ in range(p)]
+    r.Encode(act)
+    exp = _oracle_encode(orc, d, p, data)
+    for j in range(p):
+        assert np.array_equal(act[d + j], exp[j]), j
+
+
+def test_rs_mul_kat_on_gpu(rslib, torch_dev):  # TestRS_mul rs_test.go:24-49
+    r = rslib.New(5, 5)
+    v = [np.array([x], np.uint8) for x in (0, 4, 2, 6, 8)] + [np.zeros(1, np.uint8) for _ in range(5)]
+    r.Encode(v)
+    assert [int(x[0]) for x in v[5:]] == [97, 173, 218, 107, 110]
+
+
+# ---------------------------------------------------------------- Encode (device, batched)
+
+def test_encode_batch_vs_oracle(rslib, orc, torch_dev):
+    torch = torch_dev
+    rng = np.random.default_rng(101)
+    for d, p, S, n in [(10, 4, 64, 8192), (12, 4, 8, 65536), (10, 4, 3, 1000), (4, 2, 5, 48), (10, 4, 2, 1 << 20)]:
+        r = rslib.New(d, p)
+        host = _rand(rng, S, d + p, n)
+        host[:, d:] = 0xA5
+        buf = torch.from_numpy(host).cuda()
+        r.encode_batch(buf)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
+        assert np.array_equal(got[:, d:], exp), (d, p, S, n)
+        assert np.array_equal(got[:, :d], host[:, :d])
+
+
+def test_encode_batch_full_size_round_trip(rslib, orc, torch_dev):
+    """BASELINE config 2 at full size: 256 stripes x (10+4) x 1 MiB (3.5 GiB)."""
+    torch = torch_dev
+    d, p, S, n = 10, 4, 256, 1 << 20
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    buf = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    buf[:, d:] = 0xA5
+    r.encode_batch(buf)
+    torch.cuda.synchronize()
+    # spot-check stripes against the oracle
+    for s in (0, 137, S - 1):
+        host = buf[s].cpu().numpy()
+        exp = _oracle_encode(orc, d, p, [host[i].copy() for i in range(d)])
+        for j in range(p):
+            assert np.array_equal(host[d + j], exp[j]), (s, j)
+    # erase 4 vectors of every stripe (two data, two parity), rebuild, compare
+    ref = buf.clone()
+    lost = [0, 7, 11, 13]
+    buf[:, lost] = 0
+    r.reconst_batch(buf, [], lost)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    # linearity: parity(a ^ b) == parity(a) ^ parity(b) on a slice of stripes
+    a = ref[:8].clone()
+    b = torch.randint(0, 256, a.shape, dtype=torch.uint8, device="cuda", generator=g)
+    c = a ^ b
+    r.encode_batch(b)
+    r.encode_batch(c)
+    torch.cuda.synchronize()
+    assert torch.equal(c[:, d:], a[:, d:] ^ b[:, d:])
+
+
+def test_encode_dev_single_stripe(rslib, orc, torch_dev):
+    torch = torch_dev
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(102)
+    for size in (1, 15, 16, 17, 31, 33, 255, 1024, 8192, 100003):
+        data = [_rand(rng, size) for _ in range(d)]
+        vecs = [torch.from_numpy(x).cuda() for x in data] + [torch.full((size,), 7, dtype=torch.uint8,
+                                                                          device="cuda") for _ in range(p)]
+        r.encode_dev(vecs)
+        torch.cuda.synchronize()
+        exp = _oracle_encode(orc, d, p, data)
+        for j in range(p):
+            assert np.array_equal(vecs[d + j].cpu().numpy(), exp[j]), (size, j)
+
+
+def test_unaligned_device_vectors(rslib, orc, torch_dev):
+    """Go slices can start anywhere: odd offsets take the byte-granular kernel."""
+    torch = torch_dev
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(103)
+    for size in (1, 7, 16, 100, 4099):
+        big = torch.from_numpy(_rand(rng, (d + p) * (size + 64) + 64)).cuda()
+        vecs = [big[3 + i * (size + 37): 3 + i * (size + 37) + size] for i in range(d + p)]
+        data = [v.cpu().numpy().copy() for v in vecs[:d]]
+        r.encode_dev(vecs)
+        torch.cuda.synchronize()
+        exp = _oracle_encode(orc, d, p, data)
+        for j in range(p):
+            assert np.array_equal(vecs[d + j].cpu().numpy(), exp[j]), (size, j)
+        for i in range(d):
+            assert np.array_equal(vecs[i].cpu().numpy(), data[i])
+
+
+# ---------------------------------------------------------------- Reconst
+
+def _gen_idx(rng, d, p, survived_n, need_n):  # genIdxForTest helper_test.go:24-63
+    survived_n = max(survived_n, d)
+    need_n = min(need_n, p)
+    if survived_n + need_n > d + p:
+        survived_n = d
+    need = rng.permutation(d + p)[:need_n].tolist()
+    surv = []
+    for i in rng.permutation(d + p).tolist():
+        if len(surv) == survived_n:
+            break
+        if i not in need:
+            surv.append(i)
+    return sorted(surv), sorted(need)
+
+
+def test_reconst_host_round_trip(rslib, orc, torch_dev):  # TestRS_Reconst rs_test.go:165-217
+    d, p, size = 10, 4, 1024
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(104)
+    for _ in range(128):
+        exp = [_rand(rng, size) for _ in range(d)] + [np.zeros(size, np.uint8) for _ in range(p)]
+        r.Encode(exp)
+        surv, need = _gen_idx(rng, d, p, int(rng.integers(d + p)), int(rng.integers(p + 1)))
+        act = [np.zeros(size, np.uint8) for _ in range(d + p)]
+        for i in surv:
+            act[i][:] = exp[i]
+        for n_ in need:
+            if rng.integers(4) == 1:
+                act[n_][:] = _rand(rng, size)
+        ora = [x.copy() for x in act]
+        r.Reconst(act, surv, need)
+        assert orc.reconst(d, p, ora, surv, need) == 0
+        for n_ in need:
+            assert np.array_equal(act[n_], exp[n_])
+        for i in range(d + p):  # every byte the oracle wrote, we wrote identically
+            assert np.array_equal(act[i], ora[i])
+
+
+def test_reconst_batch_every_pattern(rslib, torch_dev):
+    """All C(14,1..4) erasure patterns of 10+4 (8 KiB, BASELINE config 3)."""
+    torch = torch_dev
+    d, p, S, n = 10, 4, 4, 8192
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    ref = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(ref)
+    work = torch.empty_like(ref)
+    npat = 0
+    for k in range(1, p + 1):
+        for lost in itertools.combinations(range(d + p), k):
+            work.copy_(ref)
+            work[:, list(lost)] = 0x3C
+            r.reconst_batch(work, [], list(lost))
+            npat += 1
+            if npat % 64 == 0:
+                torch.cuda.synchronize()
+            assert torch.equal(work, ref), lost
+    assert npat == 14 + 91 + 364 + 1001
+
+
+def test_reconst_dev_and_explicit_survived(rslib, orc, torch_dev):
+    torch = torch_dev
+    d, p, size = 10, 4, 8192 + 5
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(105)
+    for _ in range(32):
+        exp = [_rand(rng, size) for _ in range(d)] + [np.zeros(size, np.uint8) for _ in range(p)]
+        r.Encode(exp)
+        surv, need = _gen_idx(rng, d, p, int(rng.integers(d + p)), int(rng.integers(1, p + 1)))
+        vecs = [torch.from_numpy(x.copy()).cuda() for x in exp]
+        for n_ in need:
+            vecs[n_].fill_(0)
+        r.reconst_dev(vecs, surv, need)
+        torch.cuda.synchronize()
+        for n_ in need:
+            assert np.array_equal(vecs[n_].cpu().numpy(), exp[n_])
+
+
+def test_reconst_too_many_lost(rslib, torch_dev):
+    r = rslib.New(10, 4)
+    v = [np.zeros(64, np.uint8) for _ in range(14)]
+    with pytest.raises(rslib.ErrTooManyLost):
+        r.Reconst(v, [], [0, 1, 2, 3, 4])
+
+
+# ---------------------------------------------------------------- Update / Replace
+
+def test_update_every_row(rslib, orc, torch_dev):  # TestRS_Update rs_test.go:219-266
+    torch = torch_dev
+    d, p, size = 10, 4, 1024 + 3
+    rng = np.random.default_rng(106)
+    r = rslib.New(d, p)
+    for row in range(d):
+        exp = [_rand(rng, size) for _ in range(d)] + [np.zeros(size, np.uint8) for _ in range(p)]
+        act = [x.copy() for x in exp]
+        r.Encode(act)
+        new = _rand(rng, size)
+        ora = [x.copy() for x in act]
+        r.Update(act[row], new, row, act[d:])
+        assert orc.update(d, p, ora[row], new, row, ora[d:]) == 0
+        exp[row] = new.copy()
+        r.Encode(exp)
+        for j in range(d, d + p):
+            assert np.array_equal(act[j], exp[j])
+            assert np.array_equal(act[j], ora[j])
+        # device single-stripe variant
+        dv = [torch.from_numpy(x.copy()).cuda() for x in ora]
+        dv_old = torch.from_numpy(exp[row].copy()).cuda()
+        dv_new = torch.from_numpy(_rand(rng, size)).cuda()
+        r.update_dev(dv_old, dv_new, row, dv[d:])
+        torch.cuda.synchronize()
+        exp2 = [x.copy() for x in exp]
+        exp2[row] = dv_new.cpu().numpy()
+        r.Encode(exp2)
+        for j in range(p):
+            assert np.array_equal(dv[d + j].cpu().numpy(), exp2[d + j])
+
+
+def test_update_batch(rslib, orc, torch_dev):
+    torch = torch_dev
+    d, p, S, n = 10, 4, 16, 8192
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(8)
+    buf = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(buf)
+    for row in range(d):
+        new = torch.randint(0, 256, (S, n), dtype=torch.uint8, device="cuda", generator=g)
+        old = buf[:, row].clone()
+        r.update_batch(old, new, row, buf)
+        buf[:, row] = new
+        exp = buf.clone()
+        r.encode_batch(exp)
+        torch.cuda.synchronize()
+        assert torch.equal(buf, exp), row
+
+
+def _replace_rows(rng, d):  # makeReplaceRowRandom rs_test.go:333-353
+    n = int(rng.integers(d + 1))
+    s = []
+    while len(s) < n:
+        v = int(rng.integers(d))
+        if v not in s:
+            s.append(v)
+    return s or [0]
+
+
+@pytest.mark.parametrize("to_zero", [True, False])
+def test_replace_host(rslib, orc, torch_dev, to_zero):  # TestRS_Replace rs_test.go:268-331
+    d, p, size = 10, 4, 1024
+    rng = np.random.default_rng(107 + to_zero)
+    r = rslib.New(d, p)
+    for _ in range(128):
+        rows = _replace_rows(rng, d)
+        exp = [_rand(rng, size) for _ in range(d)] + [np.zeros(size, np.uint8) for _ in range(p)]
+        act = [x.copy() for x in exp]
+        data = [exp[rr].copy() for rr in rows]
+        if to_zero:
+            for rr in rows:
+                exp[rr] = np.zeros(size, np.uint8)
+        r.Encode(exp)
+        if not to_zero:
+            for rr in rows:
+                act[rr] = np.zeros(size, np.uint8)
+        r.Encode(act)
+        ora = [x.copy() for x in act[d:]]
+        r.Replace(data, rows, act[d:])
+        assert orc.replace(d, p, data, rows, ora) == 0
+        for j in range(p):
+            assert np.array_equal(act[d + j], exp[d + j])
+            assert np.array_equal(act[d + j], ora[j])
+
+
+def test_replace_batch_1_to_6_rows(rslib, torch_dev):  # BASELINE config 5 (rn = 1..6)
+    torch = torch_dev
+    d, p, S, n = 10, 4, 32, 8192
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for rn in range(1, 7):
+        full = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+        rows = list(range(rn))
+        zeroed = full.clone()
+        zeroed[:, rows] = 0
+        r.encode_batch(full)
+        r.encode_batch(zeroed)
+        data = full[:, rows].contiguous()
+        r.replace_batch(data, rows, zeroed)  # zero -> data
+        torch.cuda.synchronize()
+        assert torch.equal(zeroed[:, d:], full[:, d:]), rn
+
+
+def test_replace_dev(rslib, torch_dev):
+    torch = torch_dev
+    d, p, n = 10, 4, 4096 + 9
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(10)
+    full = torch.randint(0, 256, (d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    vec = [full[i].contiguous() for i in range(d + p)]
+    r.encode_dev(vec)
+    rows = [2, 5, 9]
+    zero = [v.clone() for v in vec]
+    for rr in rows:
+        zero[rr].zero_()
+    r.encode_dev(zero)
+    r.replace_dev([vec[rr] for rr in rows], rows, zero[d:])
+    torch.cuda.synchronize()
+    for j in range(d, d + p):
+        assert torch.equal(zero[j], vec[j])
+
+
+# ---------------------------------------------------------------- generic product
+
+@pytest.mark.parametrize("rows,cols,acc", [(1, 1, False), (3, 7, True), (9, 5, False), (20, 33, True),
+                                           (4, 10, False), (2, 2, True), (8, 3, False)])
+def test_gf_matmul_batch(rslib, orc, torch_dev, rows, cols, acc):
+    torch = torch_dev
+    rng = np.random.default_rng(rows * 100 + cols)
+    S, n = 3, 5000
+    mat = _rand(rng, rows, cols)
+    src = _rand(rng, S, cols, n)
+    dst0 = _rand(rng, S, rows, n)
+    r = rslib.New(10, 4)
+    dsrc = torch.from_numpy(src).cuda()
+    ddst = torch.from_numpy(dst0.copy()).cuda()
+    r.gf_matmul_batch(mat, dsrc, None, ddst, None, accumulate=acc)
+    torch.cuda.synchronize()
+    exp = orc.encode_numpy(mat, src)
+    if acc:
+        exp ^= dst0
+    assert np.array_equal(ddst.cpu().numpy(), exp)
+
+
+def test_concurrent_host_calls(rslib, orc, torch_dev):
+    """*RS is safe for concurrent use (rs.go: immutable but for the cache)."""
+    d, p, size = 10, 4, 20000
+    r = rslib.New(d, p)
+    errors = []
+
+    def worker(seed):
+        try:
+            rng = np.random.default_rng(seed)
+            for _ in range(10):
+                data = [_rand(rng, size) for _ in range(d)]
+                v = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                r.Encode(v)
+                exp = _oracle_encode(orc, d, p, data)
+                for j in range(p):
+                    if not np.array_equal(v[d + j], exp[j]):
+                        errors.append((seed, j))
+                lost = sorted(rng.choice(d + p, 3, replace=False).tolist())
+                w = [x.copy() for x in v]
+                for i in lost:
+                    w[i][:] = 0
+                r.Reconst(w, [], lost)
+                for i in lost:
+                    if not np.array_equal(w[i], v[i]):
+                        errors.append((seed, "reconst", i))
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
