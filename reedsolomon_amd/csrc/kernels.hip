@@ -49,6 +49,10 @@ LaunchTuning& tuning() {
         if (x.vpt != 2) x.vpt = 1;
         const char* n = std::getenv("RSAMD_NT_STORE");
         x.nt_store = n ? std::atoi(n) : 1;
+        const char* e = std::getenv("RSAMD_VAR");
+        x.var = e ? std::atoi(e) : -1;
+        const char* l = std::getenv("RSAMD_LDS_PAD");
+        x.lds_pad = l ? std::atoi(l) : 0;
         return x;
     }();
     return t;
@@ -87,8 +91,21 @@ __device__ __forceinline__ g_u8* out_ptr(const MatmulArgs& a, int row, int s) {
 //   MC   rows per pass (row groups loop when rows > MC)
 //   ACC  XOR into the outputs (Update / Replace) instead of overwriting
 //   VPT  16-byte units per lane per chunk
+//   VAR  code-shape flags (kVar* below); the default is kVarDefault
 // ---------------------------------------------------------------------------
-template <int KB, bool KFIX, int MC, bool ACC, int VPT>
+enum : int {
+    kVarXorOnly = 1,     // DIAGNOSTIC: acc ^= x instead of the GF product (memory ceiling of the pattern)
+    kVarNtLoad = 2,      // non-temporal input loads
+    kVarSingleTab = 4,   // no LDS table prefetch across columns (fewer VGPRs)
+    kVarBitop3 = 8,      // explicit v_bitop3 (xor3) accumulation
+};
+constexpr int kVarDefault = kVarBitop3 | kVarSingleTab;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR = kVarDefault>
 __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
     constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
@@ -154,20 +171,32 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
                     if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
                     const g_u8* p = in_ptr(a, c, s);
 #pragma unroll
-                    for (int v = 0; v < VPT; ++v) x[b][v] = *reinterpret_cast<const g_u32x4*>(p + off[v]);
+                    for (int v = 0; v < VPT; ++v) {
+                        const g_u32x4* src = reinterpret_cast<const g_u32x4*>(p + off[v]);
+                        if (VAR & kVarNtLoad) x[b][v] = __builtin_nontemporal_load(src);
+                        else x[b][v] = *src;
+                    }
                 }
                 // Tables of column b+1 are read from LDS while column b is computed.
+                constexpr bool kPrefetchTab = !(VAR & kVarSingleTab);
                 u32x4 tv[2][COLW];
+                if (kPrefetchTab) {
 #pragma unroll
-                for (int w = 0; w < COLW; ++w) tv[0][w] = lds_tab[i0 * COLW + w];
+                    for (int w = 0; w < COLW; ++w) tv[0][w] = lds_tab[i0 * COLW + w];
+                }
 #pragma unroll
                 for (int b = 0; b < KB; ++b) {
                     // Scheduling fence: keeps each column's LDS reads next to its math
                     // (hoisted, all k*MC tables would pin ~200 VGPRs: one wave/SIMD).
                     __builtin_amdgcn_sched_barrier(0);
-                    if (b + 1 < KB) {
+                    if (kPrefetchTab) {
+                        if (b + 1 < KB) {
 #pragma unroll
-                        for (int w = 0; w < COLW; ++w) tv[(b + 1) & 1][w] = lds_tab[(i0 + b + 1) * COLW + w];
+                            for (int w = 0; w < COLW; ++w) tv[(b + 1) & 1][w] = lds_tab[(i0 + b + 1) * COLW + w];
+                        }
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < COLW; ++w) tv[b & 1][w] = lds_tab[(i0 + b) * COLW + w];
                     }
                     uint32_t t[COLD];
 #pragma unroll
@@ -180,10 +209,25 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
                         const uint32_t xs[4] = {x[b][v].x, x[b][v].y, x[b][v].z, x[b][v].w};
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
+                            if (VAR & kVarXorOnly) {
+#pragma unroll
+                                for (int r = 0; r < MC; ++r) acc[r][v][q] ^= xs[q] ^ t[r * 5];
+                                continue;
+                            }
                             uint32_t g0, g1, g2;
                             split_groups(xs[q], g0, g1, g2);
 #pragma unroll
-                            for (int r = 0; r < MC; ++r) acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, &t[r * 5]);
+                            for (int r = 0; r < MC; ++r) {
+                                const uint32_t* tr = &t[r * 5];
+                                if (VAR & kVarBitop3) {
+                                    const uint32_t p0 = __builtin_amdgcn_perm(tr[1], tr[0], g0);
+                                    const uint32_t p1 = __builtin_amdgcn_perm(tr[3], tr[2], g1);
+                                    const uint32_t p2 = __builtin_amdgcn_perm(tr[4], tr[4], g2);
+                                    acc[r][v][q] = xor3(xor3(acc[r][v][q], p0, p1), p2, 0);
+                                } else {
+                                    acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, tr);
+                                }
+                            }
                         }
                     }
                     // Pin the running sums per column: stops LLVM from reassociating
@@ -265,8 +309,37 @@ struct Variant {
 #define RSAMD_VARIANT(KB, KFIX, MC, ACC, VPT) \
     Variant { gf_matmul_vec<KB, KFIX, MC, ACC, VPT>, KB, MC, VPT, KFIX, \
               "gf_matmul_vec<" #KB "," #KFIX "," #MC "," #ACC "," #VPT ">" }
+#define RSAMD_VARIANT_V(KB, KFIX, MC, ACC, VPT, VAR) \
+    Variant { gf_matmul_vec<KB, KFIX, MC, ACC, VPT, VAR>, KB, MC, VPT, KFIX, \
+              "gf_matmul_vec<" #KB "," #KFIX "," #MC "," #ACC "," #VPT "," #VAR ">" }
+
+// Experimental code shapes of the 10+4 encode kernel (RSAMD_VAR=<flags>),
+// used by tools/sweep.sh to A/B variants in separate processes.
+static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* out) {
+    const int var = tuning().var;
+    if (var < 0 || acc || cols != 10 || rows <= 2 || rows > 4) return false;
+#define RSAMD_CASE(V)                                                                                  \
+    case V:                                                                                           \
+        *out = vpt == 2 ? RSAMD_VARIANT_V(10, true, 4, false, 2, V) : RSAMD_VARIANT_V(10, true, 4, false, 1, V); \
+        return true;
+    switch (var) {
+        RSAMD_CASE(0)
+        RSAMD_CASE(1)
+        RSAMD_CASE(2)
+        RSAMD_CASE(4)
+        RSAMD_CASE(6)
+        RSAMD_CASE(8)
+        RSAMD_CASE(10)
+        RSAMD_CASE(12)
+        RSAMD_CASE(14)
+        default: return false;
+    }
+#undef RSAMD_CASE
+}
 
 static Variant pick(int rows, int cols, bool acc, int vpt) {
+    Variant ex;
+    if (pick_experimental(rows, cols, acc, vpt, &ex)) return ex;
     // Specialised shapes: the BASELINE configs (10+4, 12+4 encode; 10-column
     // reconst with 1-4 outputs; 10+4 Update = 2 columns, accumulate).
     if (!acc) {
@@ -315,7 +388,8 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         if (tu.max_grid > 0 && grid > tu.max_grid) grid = tu.max_grid;
         const int ncols_pad = var.kfix ? var.kb : ((a.cols + var.kb - 1) / var.kb) * var.kb;
         const int cold = ((var.mc * 5 + 3) / 4) * 4;
-        const size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
+        size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
+        if (tu.lds_pad > 0 && static_cast<size_t>(tu.lds_pad) > lds) lds = tu.lds_pad;  // occupancy experiments
         hipLaunchKernelGGL(var.fn, dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds, stream, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

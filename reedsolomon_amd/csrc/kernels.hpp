@@ -38,6 +38,8 @@ struct LaunchTuning {
     int max_grid;     // cap on workgroups of the vector kernel (0 = one per chunk)
     int vpt;          // 16-byte units per lane per chunk (1 or 2)
     int nt_store;     // non-temporal parity stores
+    int var;          // experimental 10+4 code shape (RSAMD_VAR), -1 = default
+    int lds_pad;      // minimum dynamic LDS per workgroup (caps occupancy; experiments)
 };
 LaunchTuning& tuning();
 

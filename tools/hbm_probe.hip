@@ -1,0 +1,113 @@
+// hbm_probe.hip — HBM calibration kernels (measurement tool, not product).
+// Gives the achievable bandwidth of plain access patterns on this MI355X so
+// the encode kernel's rate can be read against them.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+__global__ __launch_bounds__(256) void k_copy(const g_u32x4* src, g_u32x4* dst, uint64_t n, int nt) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    u32x4 v = src[i];
+    if (nt) __builtin_nontemporal_store(v, dst + i); else dst[i] = v;
+}
+
+__global__ __launch_bounds__(256) void k_read(const g_u32x4* src, g_u32x4* dst, uint64_t n, int per) {
+    uint64_t base = ((uint64_t)blockIdx.x * 256 * per) + threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll 8
+    for (int j = 0; j < per; ++j) {
+        uint64_t i = base + (uint64_t)j * 256;
+        if (i < n) acc ^= src[i];
+    }
+    if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) dst[0] = acc;  // keeps loads live, never stores
+}
+
+__global__ __launch_bounds__(256) void k_write(g_u32x4* dst, uint64_t n, int nt) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    u32x4 v = {(uint32_t)i, 1u, 2u, 3u};
+    if (nt) __builtin_nontemporal_store(v, dst + i); else dst[i] = v;
+}
+
+// The encode access pattern with the math replaced by XOR: stripe s, vectors
+// of `vec` bytes, k inputs then m outputs; each workgroup covers `units`
+// 16-byte units of every vector (units = 256 * upl, lane-interleaved).
+template <int K, int M, int UPL>
+__global__ __launch_bounds__(256) void k_pattern(uint8_t* base, uint64_t vec, uint64_t stripe_stride,
+                                                 uint64_t chunks_per_stripe, int nstripes, int mapping) {
+    const uint64_t chunk = blockIdx.x;
+    uint64_t s = chunk / chunks_per_stripe, cb = chunk % chunks_per_stripe;
+    if (mapping == 1) { s = chunk % nstripes; cb = chunk / nstripes; }
+    const __attribute__((address_space(1))) uint8_t* sp =
+        (const __attribute__((address_space(1))) uint8_t*)(base + s * stripe_stride);
+    u32x4 x[K][UPL];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int u = 0; u < UPL; ++u)
+            x[i][u] = *(const g_u32x4*)(sp + i * vec + (cb * 256 * UPL + u * 256 + threadIdx.x) * 16);
+    if (M == 0) {  // read-only variant: keep the loads live without storing
+        u32x4 a = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int u = 0; u < UPL; ++u) a ^= x[i][u];
+        if (a.x == 0x9e3779b9u && a.y == 0x7f4a7c15u) *(g_u32x4*)(base) = a;
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int u = 0; u < UPL; ++u) {
+            u32x4 a = {(uint32_t)j, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < K; ++i) a ^= x[i][u];
+            __builtin_nontemporal_store(a, (g_u32x4*)(sp + (K + j) * vec + (cb * 256 * UPL + u * 256 + threadIdx.x) * 16));
+        }
+}
+
+extern "C" {
+int probe_copy(void* src, void* dst, uint64_t bytes, int nt, void* stream) {
+    uint64_t n = bytes / 16;
+    hipLaunchKernelGGL(k_copy, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const g_u32x4*)src, (g_u32x4*)dst, n, nt);
+    return hipGetLastError();
+}
+int probe_read(void* src, void* dst, uint64_t bytes, int per, void* stream) {
+    uint64_t n = bytes / 16;
+    uint64_t blocks = (n + 256ull * per - 1) / (256ull * per);
+    hipLaunchKernelGGL(k_read, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const g_u32x4*)src,
+                       (g_u32x4*)dst, n, per);
+    return hipGetLastError();
+}
+int probe_write(void* dst, uint64_t bytes, int nt, void* stream) {
+    uint64_t n = bytes / 16;
+    hipLaunchKernelGGL(k_write, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (g_u32x4*)dst, n, nt);
+    return hipGetLastError();
+}
+int probe_pattern(void* base, uint64_t vec, uint64_t pitch, uint64_t stripe_stride, int nstripes, int upl,
+                  int mapping, void* stream) {
+    uint64_t cps = vec / (256ull * 16 * upl);
+    dim3 g(cps * nstripes);
+    uint8_t* b = (uint8_t*)base;
+    if (upl == 1) hipLaunchKernelGGL((k_pattern<10, 4, 1>), g, dim3(256), 0, (hipStream_t)stream, b, pitch, stripe_stride, cps, nstripes, mapping);
+    else if (upl == 2) hipLaunchKernelGGL((k_pattern<10, 4, 2>), g, dim3(256), 0, (hipStream_t)stream, b, pitch, stripe_stride, cps, nstripes, mapping);
+    else if (upl == 4) hipLaunchKernelGGL((k_pattern<10, 4, 4>), g, dim3(256), 0, (hipStream_t)stream, b, pitch, stripe_stride, cps, nstripes, mapping);
+    else return -1;
+    return hipGetLastError();
+}
+// k/m sweep of the pattern (upl = 1, mapping 0)
+int probe_pattern_km(void* base, uint64_t vec, uint64_t pitch, uint64_t stripe_stride, int nstripes, int k, int m,
+                     void* stream) {
+    uint64_t cps = vec / (256ull * 16);
+    dim3 g(cps * nstripes);
+    uint8_t* b = (uint8_t*)base;
+#define KM(K, M) if (k == K && m == M) { hipLaunchKernelGGL((k_pattern<K, M, 1>), g, dim3(256), 0, (hipStream_t)stream, b, pitch, stripe_stride, cps, nstripes, 0); return hipGetLastError(); }
+    KM(1, 1) KM(2, 2) KM(4, 4) KM(7, 7) KM(10, 0) KM(14, 0) KM(4, 0) KM(10, 4) KM(10, 2) KM(12, 4) KM(6, 3) KM(10, 10)
+#undef KM
+    return -1;
+}
+}

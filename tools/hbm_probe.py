@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""HBM calibration on the GPU box: plain copy / read / write and the 10+4
+encode access pattern (XOR instead of GF math), GB/s from HIP events.
+Measurement tool only."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_build", "libhbmprobe.so")
+
+
+def build():
+    if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(os.path.join(HERE, "hbm_probe.hip")):
+        os.makedirs(os.path.dirname(SO), exist_ok=True)
+        subprocess.run(["hipcc", "-O3", "-shared", "-fPIC", "--offload-arch=gfx950",
+                        os.path.join(HERE, "hbm_probe.hip"), "-o", SO], check=True)
+    return SO
+
+
+def main():
+    build()
+    import torch
+
+    L = ctypes.CDLL(SO)
+    for f in ("probe_copy", "probe_read", "probe_write", "probe_pattern"):
+        getattr(L, f).restype = ctypes.c_int
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    GB = 3.5 * 2 ** 30
+    a = torch.randint(0, 256, (int(GB),), dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    res = {}
+
+    def timeit(name, fn, nbytes, iters=30, warm=5):
+        for _ in range(warm):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record(st)
+        for _ in range(iters):
+            fn()
+        e.record(st)
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / iters / 1e3
+        res[name] = round(nbytes / t / 1e9, 1)
+        print(f"{name:32s} {res[name]:8.1f} GB/s  ({t*1e3:.3f} ms)", flush=True)
+
+    n = a.numel()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    basic = os.environ.get("PROBE_BASIC", "1") != "0"
+    if basic:
+        basic_probes(L, a, b, n, vp, sp, timeit)
+    pattern_probes(L, a, n, vp, sp, timeit)
+    os.makedirs("gpurun_out", exist_ok=True)
+    json.dump(res, open("gpurun_out/hbm_probe.json", "w"), indent=1)
+
+
+def basic_probes(L, a, b, n, vp, sp, timeit):
+    timeit("copy (read+write)", lambda: L.probe_copy(vp(a), vp(b), ctypes.c_uint64(n // 2), 0, sp), n // 2 * 2)
+    timeit("copy nt-store", lambda: L.probe_copy(vp(a), vp(b), ctypes.c_uint64(n // 2), 1, sp), n // 2 * 2)
+    timeit("torch copy_", lambda: b.copy_(a), 2 * n)
+    for per in (1, 4, 16):
+        timeit(f"read-only per={per}", lambda: L.probe_read(vp(a), vp(b), ctypes.c_uint64(n), per, sp), n)
+    timeit("write-only", lambda: L.probe_write(vp(b), ctypes.c_uint64(n), 0, sp), n)
+    timeit("write-only nt", lambda: L.probe_write(vp(b), ctypes.c_uint64(n), 1, sp), n)
+
+
+def pattern_probes(L, a, n, vp, sp, timeit):
+    if os.environ.get("PROBE_KM", "0") == "1":
+        vec = 1 << 20
+        for k, m in ((1, 1), (2, 2), (4, 4), (7, 7), (10, 10), (4, 0), (10, 0), (14, 0), (10, 2), (10, 4), (12, 4), (6, 3)):
+            S = min(256, int(n // ((k + m) * vec)))
+            timeit(f"pattern k={k} m={m}",
+                   lambda: L.probe_pattern_km(vp(a), ctypes.c_uint64(vec), ctypes.c_uint64(vec),
+                                              ctypes.c_uint64((k + m) * vec), S, k, m, sp),
+                   S * (k + m) * vec, iters=20)
+        return
+    S, vec = 240, 1 << 20
+    for pad in (0, 256, 4096, 65536, 3 * 4096 + 256):
+        for sspad in (0, 8192 + 512):
+            pitch = vec + pad
+            sstride = 14 * pitch + sspad
+            for mapping in (0, 1):
+                for upl in (1, 2):
+                    if S * sstride > n:
+                        continue
+                    timeit(f"pattern pad={pad} sspad={sspad} map={mapping} upl={upl}",
+                           lambda: L.probe_pattern(vp(a), ctypes.c_uint64(vec), ctypes.c_uint64(pitch),
+                                                   ctypes.c_uint64(sstride), S, upl, mapping, sp),
+                           S * 14 * vec, iters=20)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
