@@ -150,8 +150,9 @@ RS_API int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int6
                      const int* need, int nn, void* stream);
 
 /* Update: old/new vectors of stripe s at old_base + s*old_stride and
- * new_base + s*new_stride; parity vectors are vectors d..d+p of the stripe
- * layout above. */
+ * new_base + s*new_stride (one launch steps both inputs alike: the two
+ * strides must be equal when nstripes > 1); parity vectors are vectors
+ * d..d+p of the stripe layout above. */
 RS_API int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride,
                     const uint8_t* new_base, int64_t new_stride, int row,
                     uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
@@ -163,6 +164,22 @@ RS_API int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_str
                      int64_t data_vect_stride, const int* replace_rows, int nr,
                      uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                      int nstripes, size_t len, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Host-resident batches (the path storage callers see: stripes arrive in
+ * host memory from disk or the network).  Layout as for rs_encode_batch but
+ * `base` is a HOST pointer.  The call pipelines H2D copies of the data
+ * vectors, the device encode and D2H copies of the parity vectors over
+ * `streams` HIP streams with `stripes_per_chunk` stripes per step, and
+ * returns when every parity byte is back in host memory.  Host memory should
+ * be pinned (rs_host_register) for full PCIe rate.
+ * ------------------------------------------------------------------------ */
+RS_API int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                                int nstripes, size_t len, int stripes_per_chunk, int streams);
+
+/* Page-lock / unlock caller memory for DMA (hipHostRegister). */
+RS_API int rs_host_register(void* ptr, size_t bytes);
+RS_API int rs_host_unregister(void* ptr);
 
 /* ------------------------------------------------------------------------
  * Generic GF(2^8) matrix product over device vectors — the primitive all of

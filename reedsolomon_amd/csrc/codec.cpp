@@ -836,6 +836,69 @@ int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_stripe_str
                   as_stream(stream));
 }
 
+// ---------------------------------------------------------------- host-resident pipeline
+
+int rs_host_register(void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return RS_ERR_INVAL;
+    return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+
+int rs_host_unregister(void* ptr) {
+    if (!ptr) return RS_ERR_INVAL;
+    return hipHostUnregister(ptr) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+
+int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
+                         size_t len, int stripes_per_chunk, int streams) {
+    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (nstripes == 0) return RS_OK;
+    if (stripes_per_chunk <= 0) stripes_per_chunk = 8;
+    if (streams <= 0) streams = 3;
+    if (streams > 8) streams = 8;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    const int d = rs->d, p = rs->p;
+    const size_t pitch = rup(len, 256);
+    const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);  // device stripe stride
+    const size_t slot_bytes = static_cast<size_t>(dstripe) * stripes_per_chunk;
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    // One staging slot and one stream per pipeline lane; a lane's next chunk
+    // reuses its slot only after its previous D2H (same stream: ordered).
+    uint8_t* ring = nullptr;
+    if (hipMalloc(&ring, slot_bytes * streams) != hipSuccess) return RS_ERR_DEVICE;
+    hipStream_t st[8] = {};
+    int rc = RS_OK;
+    for (int i = 0; i < streams && rc == RS_OK; ++i)
+        if (hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess) rc = RS_ERR_DEVICE;
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    for (int c0 = 0, lane = 0; c0 < nstripes && rc == RS_OK; c0 += stripes_per_chunk, lane = (lane + 1) % streams) {
+        const int cn = std::min(stripes_per_chunk, nstripes - c0);
+        uint8_t* slot = ring + static_cast<size_t>(lane) * slot_bytes;
+        uint8_t* hb = base + static_cast<int64_t>(c0) * stripe_stride;
+        for (int i = 0; i < d && rc == RS_OK; ++i)  // data vector i of cn stripes: one 2-D copy
+            if (hipMemcpy2DAsync(slot + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len, cn,
+                                 hipMemcpyHostToDevice, st[lane]) != hipSuccess)
+                rc = RS_ERR_DEVICE;
+        if (rc) break;
+        for (int i = 0; i < d; ++i) in[i] = slot + i * pitch;
+        for (int j = 0; j < p; ++j) out[j] = slot + (d + j) * pitch;
+        rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, st[lane]);
+        for (int j = 0; j < p && rc == RS_OK; ++j)
+            if (hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, slot + (d + j) * pitch, dstripe, len, cn,
+                                 hipMemcpyDeviceToHost, st[lane]) != hipSuccess)
+                rc = RS_ERR_DEVICE;
+    }
+    for (int i = 0; i < streams; ++i)
+        if (st[i]) {
+            if (hipStreamSynchronize(st[i]) != hipSuccess) rc = RS_ERR_DEVICE;
+            (void)hipStreamDestroy(st[i]);
+        }
+    (void)hipFree(ring);
+    return rc;
+}
+
 // ---------------------------------------------------------------- generic product
 
 int rs_gf_matmul_batch(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* in_base,

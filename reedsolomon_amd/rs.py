@@ -294,6 +294,25 @@ class RS:
         _check(lib().rs_replace_batch(self._h, ctypes.c_void_p(data.data_ptr()), data.stride(0), data.stride(1),
                                       r, nr, base, ss, vs, S, n, _stream(stream)))
 
+    def encode_host_batch(self, buf, stripes_per_chunk: int = 8, streams: int = 3) -> None:
+        """Encode stripes held in HOST memory: buf is a [S, d+p, len] uint8
+        numpy array or CPU torch tensor (pin it for full PCIe rate).  Pipelined
+        H2D -> encode -> D2H; returns when parity is back in host memory."""
+        import numpy as _np
+
+        if isinstance(buf, _np.ndarray):
+            if buf.dtype != _np.uint8 or buf.ndim != 3 or buf.strides[2] != 1:
+                raise TypeError("expected a [stripes, d+p, len] uint8 array with unit inner stride")
+            ptr, ss, vs, S, n = buf.ctypes.data, buf.strides[0], buf.strides[1], buf.shape[0], buf.shape[2]
+        else:
+            if buf.dtype.__str__() != "torch.uint8" or buf.is_cuda or buf.dim() != 3 or buf.stride(2) != 1:
+                raise TypeError("expected a [stripes, d+p, len] uint8 CPU tensor with unit inner stride")
+            ptr, ss, vs, S, n = buf.data_ptr(), buf.stride(0), buf.stride(1), buf.shape[0], buf.shape[2]
+        if buf.shape[1] < self.DataNum + self.ParityNum:
+            raise TypeError("buffer holds fewer than d+p vectors per stripe")
+        _check(lib().rs_encode_host_batch(self._h, ctypes.c_void_p(ptr), ss, vs, S, n, int(stripes_per_chunk),
+                                          int(streams)))
+
     def gf_matmul_batch(self, mat: np.ndarray, src, in_map, dst, out_map, accumulate=False, stream=None) -> None:
         """dst[:, out_map[r]] (=|^=) sum_c mat[r, c] x src[:, in_map[c]] for every stripe."""
         mat = np.ascontiguousarray(mat, dtype=np.uint8)
@@ -366,6 +385,14 @@ def inverse_cache_key(survived) -> int:
 
 def gf_mul(a: int, b: int) -> int:
     return int(lib().rs_gf_mul(a, b))
+
+
+def host_register(ptr: int, nbytes: int) -> None:
+    _check(lib().rs_host_register(ctypes.c_void_p(ptr), nbytes))
+
+
+def host_unregister(ptr: int) -> None:
+    _check(lib().rs_host_unregister(ctypes.c_void_p(ptr)))
 
 
 def device_count() -> int:

@@ -427,3 +427,21 @@ def test_concurrent_host_calls(rslib, orc, torch_dev):
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
+    """Host-resident stripes: pinned and pageable, ragged chunking."""
+    torch = torch_dev
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(108)
+    for S, n, spc, st in ((7, 8192 + 3, 3, 2), (20, 65536, 8, 3), (1, 100, 8, 3)):
+        host = _rand(rng, S, d + p, n)
+        exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
+        a = host.copy()
+        r.encode_host_batch(a, spc, st)
+        assert np.array_equal(a[:, d:], exp)
+        assert np.array_equal(a[:, :d], host[:, :d])
+        pinned = torch.from_numpy(host.copy()).pin_memory()
+        r.encode_host_batch(pinned, spc, st)
+        assert np.array_equal(pinned.numpy()[:, d:], exp)

@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Per-operation throughput on one MI355X (BASELINE.json configs 2-5) plus
+the host-resident end-to-end rate.  Writes gpurun_out/ops_bench.json.
+
+Formulas follow the reference's benchmarks (README.md:129-161,
+rs_test.go:450,489,556,598):
+  Encode   (k+m)*vec          Reconst  (k+lost)*vec
+  Update   (2+2m)*vec         Replace  (rn+2m)*vec
+Device-resident numbers time HIP events around back-to-back launches on one
+stream; end-to-end numbers time host wall clock around the pinned pipeline.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import reedsolomon_amd as rs  # noqa: E402
+
+GiB = 2 ** 30
+out = {}
+
+
+def dev_time(fn, iters=50, warm=20):
+    st = torch.cuda.current_stream()
+    for _ in range(warm):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record(st)
+    for _ in range(iters):
+        fn()
+    b.record(st)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters / 1e3
+
+
+def rec(name, nbytes, t, **kw):
+    out[name] = dict(GiBps=round(nbytes / t / GiB, 2), us_per_call=round(t * 1e6, 2), **kw)
+    print(f"{name:44s} {nbytes / t / GiB:10.2f} GiB/s  {t * 1e6:10.2f} us/call", flush=True)
+
+
+def main():
+    g = torch.Generator(device="cuda").manual_seed(42)
+    # ---- encode, device-resident
+    for k, m, vec, S in ((10, 4, 1 << 20, 256), (12, 4, 1 << 20, 256), (10, 4, 8 << 10, 32768), (10, 4, 8 << 10, 1)):
+        r = rs.New(k, m)
+        buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+        t = dev_time(lambda: r.encode_batch(buf))
+        rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
+        del buf
+    # ---- reconst 10+4 @ 8 KiB, 1-4 lost data shards (config 3)
+    k, m, vec, S = 10, 4, 8 << 10, 32768
+    r = rs.New(k, m)
+    buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(buf)
+    for lost in ([0], [0, 5], [0, 5, 9], [0, 3, 5, 9]):
+        t = dev_time(lambda: r.reconst_batch(buf, [], lost))
+        rec(f"reconst 10+4 8KiB lost={len(lost)} data x{S}", S * (k + len(lost)) * vec, t)
+        t1 = dev_time(lambda: r.reconst_batch(buf[:1], [], lost))
+        rec(f"reconst 10+4 8KiB lost={len(lost)} data x1", (k + len(lost)) * vec, t1)
+    # ---- update / replace 10+4 @ 8 KiB (config 5)
+    old = buf[:, 3].clone()
+    new = torch.randint(0, 256, (S, vec), dtype=torch.uint8, device="cuda", generator=g)
+    t = dev_time(lambda: r.update_batch(old, new, 3, buf))
+    rec(f"update 10+4 8KiB x{S}", S * (2 + 2 * m) * vec, t)
+    for rn in range(1, 7):
+        data = torch.randint(0, 256, (S, rn, vec), dtype=torch.uint8, device="cuda", generator=g)
+        t = dev_time(lambda: r.replace_batch(data, list(range(rn)), buf))
+        rec(f"replace 10+4 8KiB rn={rn} x{S}", S * (rn + 2 * m) * vec, t)
+    del buf
+    torch.cuda.empty_cache()
+    # ---- host-resident end-to-end (pinned), 10+4 @ 1 MiB
+    k, m, vec, S = 10, 4, 1 << 20, 128
+    r = rs.New(k, m)
+    host = torch.empty((S, k + m, vec), dtype=torch.uint8, pin_memory=True)
+    host.copy_(torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g).cpu())
+    for spc, nst in ((4, 2), (8, 3), (16, 3), (16, 4)):
+        r.encode_host_batch(host, spc, nst)  # warm
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            r.encode_host_batch(host, spc, nst)
+        t = (time.perf_counter() - t0) / reps
+        rec(f"encode 10+4 1MiB x{S} host->host pinned spc={spc} streams={nst}", S * (k + m) * vec, t)
+    # PCIe reference rates
+    dbuf = torch.empty((S * k * vec,), dtype=torch.uint8, device="cuda")
+    hflat = host.view(-1)[: S * k * vec]
+    t0 = time.perf_counter()
+    dbuf.copy_(hflat, non_blocking=True)
+    torch.cuda.synchronize()
+    rec("H2D pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    hflat.copy_(dbuf, non_blocking=True)
+    torch.cuda.synchronize()
+    rec("D2H pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
+    # verify the pipelined parity against a device encode of the same stripes
+    chk = host[:4].cuda()
+    ref = chk.clone()
+    r.encode_batch(ref)
+    torch.cuda.synchronize()
+    assert torch.equal(chk, ref), "host pipeline parity mismatch"
+    # ---- host-memory Go-API calls (pageable numpy buffers), per-call latency
+    import numpy as np
+
+    for vec in (8 << 10, 1 << 20):
+        rng = np.random.default_rng(1)
+        v = [rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] + [np.zeros(vec, np.uint8)
+                                                                             for _ in range(m)]
+        for _ in range(5):
+            r.Encode(v)
+        n = 50 if vec > 65536 else 500
+        t0 = time.perf_counter()
+        for _ in range(n):
+            r.Encode(v)
+        t = (time.perf_counter() - t0) / n
+        rec(f"Encode() host API pageable 10+4 {vec >> 10}KiB", (k + m) * vec, t)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ops_bench.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
