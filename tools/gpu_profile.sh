@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
-    python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --steps 20 --warmup 5 > "$OUT/kt_bench.log" 2>&1
+    python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 > "$OUT/kt_bench.log" 2>&1
 tail -1 "$OUT/kt_bench.log"
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C"
