@@ -47,6 +47,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="10+4@1MiB", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=0, help="stripes per GPU (default: per config)")
+    ap.add_argument("--layout", default=os.environ.get("RSAMD_BENCH_LAYOUT", "split"), choices=("split", "interleaved"),
+                    help="split: data [S][k][vec] and parity [S][m][vec] in separate buffers; "
+                         "interleaved: one [S][k+m][vec] buffer")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--verify", type=int, default=1, help="encode->erase->reconst self-check of one stripe per rank")
     return ap.parse_args(argv)
@@ -196,15 +199,23 @@ def main(argv=None):
     # Synthetic stripes: uniform random data seeded per (seed, rank); parity
     # pre-filled with 0xA5 so an encode that skipped a byte would show.
     g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
-    buf = torch.empty((S, k + m, vec), dtype=torch.uint8, device=dev)
+    if args.layout == "interleaved":
+        buf = torch.empty((S, k + m, vec), dtype=torch.uint8, device=dev)
+        data, parity = buf[:, :k], buf[:, k:]
+    else:
+        data = torch.empty((S, k, vec), dtype=torch.uint8, device=dev)
+        parity = torch.empty((S, m, vec), dtype=torch.uint8, device=dev)
     for s0 in range(0, S, 32):
-        s1 = min(S, s0 + 32)
-        buf[s0:s1, :k].random_(0, 256, generator=g)
-    buf[:, k:].fill_(0xA5)
+        data[s0:s0 + 32].random_(0, 256, generator=g)
+    parity.fill_(0xA5)
     torch.cuda.synchronize(dev)
 
-    def step(_i):
-        codec.encode_batch(buf, stream=stream)
+    if args.layout == "interleaved":
+        def step(_i):
+            codec.encode_batch(buf, stream=stream)
+    else:
+        def step(_i):
+            codec.encode_batch_split(data, parity, stream=stream)
 
     for _ in range(args.warmup):
         step(0)
@@ -213,12 +224,19 @@ def main(argv=None):
     if args.verify:
         # Self-check without the oracle (bench must not run it outside the
         # CPU-baseline leg): erase 4 vectors of one stripe, rebuild, compare.
-        one = buf[S // 2: S // 2 + 1]
-        ref = one.clone()
-        one[:, [0, 3, k, k + m - 1]] = 0
-        codec.reconst_batch(one, [], [0, 3, k, k + m - 1], stream=stream)
+        sl = slice(S // 2, S // 2 + 1)
+        ref_d, ref_p = data[sl].clone(), parity[sl].clone()
+        lost = [0, 3, k, k + m - 1]
+        data[sl, 0] = 0
+        data[sl, 3] = 0
+        parity[sl, 0] = 0
+        parity[sl, m - 1] = 0
+        if args.layout == "interleaved":
+            codec.reconst_batch(buf[sl], [], lost, stream=stream)
+        else:
+            codec.reconst_batch_split(data[sl], parity[sl], [], lost, stream=stream)
         torch.cuda.synchronize(dev)
-        if not torch.equal(one, ref):
+        if not (torch.equal(data[sl], ref_d) and torch.equal(parity[sl], ref_p)):
             raise SystemExit(f"rank {rank}: encode/reconst round trip failed (stripe {lo + S // 2})")
 
     # Kernel time: HIP events on the launch stream around every timed launch.
@@ -258,6 +276,8 @@ def main(argv=None):
             "config": {
                 "workload": f"RS encode {k}+{m}, {vec} B vectors, {S} stripes per GPU, device-resident",
                 "k": k, "m": m, "vector_bytes": vec, "stripes_per_gpu": S,
+                "layout": ("data [S][k][vec] and parity [S][m][vec] in separate HBM buffers"
+                           if args.layout == "split" else "one [S][k+m][vec] HBM buffer"),
                 "parallelism": f"stripes partitioned over {n_gpus} GPU(s), no collective",
                 "kernel": _kernel_name(k, m),
             },

@@ -143,6 +143,24 @@ RS_API int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* da
 RS_API int rs_encode_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                     int nstripes, size_t len, void* stream);
 
+/* A batch layout with data and parity in possibly separate regions:
+ * data vector i (< d) of stripe s:   data_base   + s*data_stripe_stride   + i*data_vect_stride
+ * parity vector j (< p) of stripe s: parity_base + s*parity_stripe_stride + j*parity_vect_stride
+ * (rs_encode_batch's interleaved [S][d+p][len] layout is the special case
+ * parity_base = base + d*vect_stride with equal strides). */
+typedef struct rs_layout {
+    uint8_t* data_base;
+    int64_t data_stripe_stride;
+    int64_t data_vect_stride;
+    uint8_t* parity_base;
+    int64_t parity_stripe_stride;
+    int64_t parity_vect_stride;
+} rs_layout_t;
+
+RS_API int rs_encode_batch_layout(rs_t* rs, const rs_layout_t* layout, int nstripes, size_t len, void* stream);
+RS_API int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* layout, int nstripes, size_t len,
+                                   const int* survived, int ns, const int* need, int nn, void* stream);
+
 /* Reconst every stripe with the same survived/need pattern
  * (one host plan + one cached matrix, then at most two device passes). */
 RS_API int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
@@ -150,9 +168,8 @@ RS_API int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int6
                      const int* need, int nn, void* stream);
 
 /* Update: old/new vectors of stripe s at old_base + s*old_stride and
- * new_base + s*new_stride (one launch steps both inputs alike: the two
- * strides must be equal when nstripes > 1); parity vectors are vectors
- * d..d+p of the stripe layout above. */
+ * new_base + s*new_stride; parity vectors are vectors d..d+p of the stripe
+ * layout above. */
 RS_API int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride,
                     const uint8_t* new_base, int64_t new_stride, int row,
                     uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
@@ -220,6 +237,11 @@ RS_API uint64_t rs_inverse_cache_key(const int* survived, int ns);
 
 /* Number of inverse matrices currently cached (rs.go:33-39). */
 RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
+
+/* Expert launch knobs, process-wide (for A/B experiments; defaults are the
+ * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad".  Returns
+ * RS_OK, or RS_ERR_INVAL for an unknown name. */
+RS_API int rs_tune(const char* name, int value);
 
 /* GF(2^8) multiply (gmu.go:26-28) — for tests. */
 RS_API uint8_t rs_gf_mul(uint8_t a, uint8_t b);

@@ -26,6 +26,16 @@ c_i64 = ctypes.c_int64
 c_sz = ctypes.c_size_t
 c_int = ctypes.c_int
 
+
+class RSLayout(ctypes.Structure):
+    """rs_layout_t (include/rs_amd.h)."""
+    _fields_ = [("data_base", ctypes.c_void_p), ("data_stripe_stride", ctypes.c_int64),
+                ("data_vect_stride", ctypes.c_int64), ("parity_base", ctypes.c_void_p),
+                ("parity_stripe_stride", ctypes.c_int64), ("parity_vect_stride", ctypes.c_int64)]
+
+
+c_layoutp = ctypes.POINTER(RSLayout)
+
 # name -> (restype, argtypes); mirrors include/rs_amd.h
 SIGNATURES = {
     "rs_strerror": (ctypes.c_char_p, [c_int]),
@@ -46,6 +56,8 @@ SIGNATURES = {
     "rs_update_dev": (c_int, [c_void, c_u8p, c_sz, c_u8p, c_sz, c_int, c_u8pp, c_sizep, c_int, c_void]),
     "rs_replace_dev": (c_int, [c_void, c_u8pp, c_sizep, c_int, c_intp, c_int, c_u8pp, c_sizep, c_int, c_void]),
     "rs_encode_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_void]),
+    "rs_encode_batch_layout": (c_int, [c_void, c_layoutp, c_int, c_sz, c_void]),
+    "rs_reconst_batch_layout": (c_int, [c_void, c_layoutp, c_int, c_sz, c_intp, c_int, c_intp, c_int, c_void]),
     "rs_reconst_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_intp, c_int, c_intp, c_int,
                                  c_void]),
     "rs_update_batch": (c_int, [c_void, c_void, c_i64, c_void, c_i64, c_int, c_void, c_i64, c_i64, c_int, c_sz,
@@ -63,6 +75,7 @@ SIGNATURES = {
     "rs_inverse_cache_key": (ctypes.c_uint64, [c_intp, c_int]),
     "rs_inverse_cache_size": (c_i64, [c_void]),
     "rs_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
+    "rs_tune": (c_int, [ctypes.c_char_p, c_int]),
 }
 
 

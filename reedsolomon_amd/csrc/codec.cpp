@@ -212,10 +212,11 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
 }
 
 // One launch of the product: out[r] (=|^=) sum_c mat[r][c] * in[c] on every
-// stripe.  in_ptrs/out_ptrs are stripe-0 addresses; stripe s adds s*ss.
-int matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs, int64_t in_ss,
-           uint8_t* const* out_ptrs, int64_t out_ss, int nstripes, uint64_t len, bool accumulate,
-           hipStream_t stream) {
+// stripe.  in_ptrs/out_ptrs are stripe-0 addresses; vector v of stripe s adds
+// s * ss[sid[v]] (sid == nullptr: all inputs use ss[0], all outputs ss[1]).
+int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs,
+              const uint8_t* in_sid, uint8_t* const* out_ptrs, const uint8_t* out_sid, const int64_t ss[4],
+              int nstripes, uint64_t len, bool accumulate, hipStream_t stream) {
     if (rows <= 0 || cols <= 0 || nstripes <= 0 || len == 0) return RS_OK;
     if (rows + cols > kMaxPtrs) return RS_ERR_INVAL;
     MatmulArgs a;
@@ -227,12 +228,35 @@ int matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* cons
     a.nstripes = nstripes;
     a.accumulate = accumulate ? 1 : 0;
     a.len = len;
-    a.in_ss = in_ss;
-    a.out_ss = out_ss;
-    for (int c = 0; c < cols; ++c) a.ptr[c] = reinterpret_cast<uint64_t>(in_ptrs[c]);
-    for (int r = 0; r < rows; ++r) a.ptr[cols + r] = reinterpret_cast<uint64_t>(out_ptrs[r]);
+    for (int i = 0; i < 4; ++i) a.ss[i] = ss[i];
+    for (int c = 0; c < cols; ++c) {
+        a.ptr[c] = reinterpret_cast<uint64_t>(in_ptrs[c]);
+        a.sid[c] = in_sid ? in_sid[c] : 0;
+    }
+    for (int r = 0; r < rows; ++r) {
+        a.ptr[cols + r] = reinterpret_cast<uint64_t>(out_ptrs[r]);
+        a.sid[cols + r] = out_sid ? out_sid[r] : 1;
+    }
     return launch_gf_matmul(a, stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
 }
+
+int matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs, int64_t in_ss,
+           uint8_t* const* out_ptrs, int64_t out_ss, int nstripes, uint64_t len, bool accumulate,
+           hipStream_t stream) {
+    const int64_t ss[4] = {in_ss, out_ss, 0, 0};
+    return matmul_ex(rs, mat, rows, cols, in_ptrs, nullptr, out_ptrs, nullptr, ss, nstripes, len, accumulate,
+                     stream);
+}
+
+// Address of vector v (0..d+p) of stripe 0 and its stride selector under a layout.
+struct LayoutAddr {
+    const rs_layout_t* L;
+    int d;
+    uint8_t* ptr(int v) const {
+        return v < d ? L->data_base + v * L->data_vect_stride : L->parity_base + (v - d) * L->parity_vect_stride;
+    }
+    uint8_t sid(int v) const { return v < d ? 0 : 1; }
+};
 
 // ---------------------------------------------------------------- reference checks
 
@@ -500,6 +524,19 @@ int rs_enc_matrix(const rs_t* rs, uint8_t* out) {
 
 uint8_t rs_gf_mul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
 
+int rs_tune(const char* name, int value) {
+    if (!name) return RS_ERR_INVAL;
+    LaunchTuning& t = tuning();
+    const std::string n(name);
+    if (n == "max_grid") t.max_grid = value;
+    else if (n == "vpt") t.vpt = value == 2 ? 2 : 1;
+    else if (n == "nt_store") t.nt_store = value;
+    else if (n == "var") t.var = value;
+    else if (n == "lds_pad") t.lds_pad = value;
+    else return RS_ERR_INVAL;
+    return RS_OK;
+}
+
 int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out) {
     if (n < 0 || (!m && m_len) || !out) return RS_ERR_INVAL;
     return invert(m, m_len, n, out);
@@ -559,19 +596,26 @@ int rs_encode_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, vo
     return matmul(rs, rs->gen(), rs->p, rs->d, vects, 0, vects + rs->d, 0, 1, lens[0], false, as_stream(stream));
 }
 
-int rs_encode_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
-                    void* stream) {
-    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+int rs_encode_batch_layout(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, void* stream) {
+    if (!rs || !L || nstripes < 0 || (nstripes > 0 && (!L->data_base || !L->parity_base))) return RS_ERR_INVAL;
     if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
     if (nstripes == 0) return RS_OK;
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
+    const LayoutAddr A{L, rs->d};
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
-    for (int i = 0; i < rs->d; ++i) in[i] = base + i * vect_stride;
-    for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
-    return matmul(rs, rs->gen(), rs->p, rs->d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
-                  as_stream(stream));
+    for (int i = 0; i < rs->d; ++i) in[i] = A.ptr(i);
+    for (int j = 0; j < rs->p; ++j) out[j] = A.ptr(rs->d + j);
+    return matmul(rs, rs->gen(), rs->p, rs->d, in, L->data_stripe_stride, out, L->parity_stripe_stride, nstripes,
+                  len, false, as_stream(stream));
+}
+
+int rs_encode_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
+                    void* stream) {
+    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+    const rs_layout_t L{base, stripe_stride, vect_stride, base + rs->d * vect_stride, stripe_stride, vect_stride};
+    return rs_encode_batch_layout(rs, &L, nstripes, len, stream);
 }
 
 // ---------------------------------------------------------------- Reconst
@@ -678,37 +722,57 @@ int rs_reconst_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, c
     return RS_OK;
 }
 
-int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
-                     const int* survived, int ns, const int* need, int nn, void* stream) {
-    if (!rs || nstripes < 0 || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const int* survived, int ns,
+                            const int* need, int nn, void* stream) {
+    if (!rs || !L || nstripes < 0 || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
     ReconstPlan pl;
     int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
     if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
     if (rc) return rc;
     if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
     if (nstripes == 0) return RS_OK;
-    if (!base) return RS_ERR_INVAL;
+    if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
     const int d = rs->d, pn = pl.nnr - pl.dn;
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
+    const LayoutAddr A{L, d};
+    const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
-    if (pl.dn > 0) {
+    uint8_t isid[kMaxVects], osid[kMaxVects];  // stride selectors (copied into the dword kernel array)
+    if (pl.dn > 0) {  // reconstData rs.go:327-349: inputs = first d survivors (data or parity)
         std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
         RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
-        for (int i = 0; i < d; ++i) in[i] = base + pl.vs[i] * vect_stride;
-        for (int i = 0; i < pl.dn; ++i) out[i] = base + pl.nr[i] * vect_stride;
-        RS_TRY(matmul(rs, gm.data(), pl.dn, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
-                      as_stream(stream)));
+        for (int i = 0; i < d; ++i) {
+            in[i] = A.ptr(pl.vs[i]);
+            isid[i] = A.sid(pl.vs[i]);
+        }
+        for (int i = 0; i < pl.dn; ++i) {
+            out[i] = A.ptr(pl.nr[i]);
+            osid[i] = A.sid(pl.nr[i]);
+        }
+        RS_TRY(matmul_ex(rs, gm.data(), pl.dn, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream)));
     }
-    if (pn > 0) {
+    if (pn > 0) {  // reconstParity rs.go:351-373: inputs = all data vectors
         std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
-        for (int i = 0; i < d; ++i) in[i] = base + i * vect_stride;
-        for (int i = 0; i < pn; ++i) out[i] = base + pl.nr[pl.dn + i] * vect_stride;
-        RS_TRY(matmul(rs, gm.data(), pn, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
-                      as_stream(stream)));
+        for (int i = 0; i < d; ++i) {
+            in[i] = A.ptr(i);
+            isid[i] = 0;
+        }
+        for (int i = 0; i < pn; ++i) {
+            out[i] = A.ptr(pl.nr[pl.dn + i]);
+            osid[i] = 1;
+        }
+        RS_TRY(matmul_ex(rs, gm.data(), pn, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream)));
     }
     return RS_OK;
+}
+
+int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
+                     const int* survived, int ns, const int* need, int nn, void* stream) {
+    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+    const rs_layout_t L{base, stripe_stride, vect_stride, base + rs->d * vect_stride, stripe_stride, vect_stride};
+    return rs_reconst_batch_layout(rs, &L, nstripes, len, survived, ns, need, nn, stream);
 }
 
 // ---------------------------------------------------------------- Update
@@ -759,16 +823,19 @@ int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride, const
     if (row >= rs->d || row < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
     if (nstripes == 0) return RS_OK;
     if (!old_base || !new_base || !base) return RS_ERR_INVAL;
-    // One launch shares a single input stripe stride: old and new must step alike.
-    if (nstripes > 1 && old_stride != new_stride) return RS_ERR_INVAL;
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
     const uint8_t* in[2] = {old_base, new_base};
+    const uint8_t isid[2] = {0, 1};
     uint8_t* out[kMaxVects];
-    for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
+    uint8_t osid[kMaxVects];
+    for (int j = 0; j < rs->p; ++j) {
+        out[j] = base + (rs->d + j) * vect_stride;
+        osid[j] = 2;
+    }
+    const int64_t ss[4] = {old_stride, new_stride, stripe_stride, 0};
     std::vector<uint8_t> gm = update_matrix(rs, row);
-    return matmul(rs, gm.data(), rs->p, 2, in, old_stride, out, stripe_stride, nstripes, len, true,
-                  as_stream(stream));
+    return matmul_ex(rs, gm.data(), rs->p, 2, in, isid, out, osid, ss, nstripes, len, true, as_stream(stream));
 }
 
 // ---------------------------------------------------------------- Replace

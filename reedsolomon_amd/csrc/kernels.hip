@@ -78,10 +78,12 @@ typedef __attribute__((address_space(1))) uint8_t g_u8;
 // address_space(1) pointers makes the compiler emit global_* (not flat_*)
 // memory instructions.
 __device__ __forceinline__ const g_u8* in_ptr(const MatmulArgs& a, int col, int s) {
-    return reinterpret_cast<const g_u8*>(a.ptr[col]) + static_cast<int64_t>(s) * a.in_ss;
+    return reinterpret_cast<const g_u8*>(a.ptr[col]) + static_cast<int64_t>(s) * a.ss[a.sid[col] & 3];
 }
-__device__ __forceinline__ g_u8* out_ptr(const MatmulArgs& a, int row, int s) {
-    return reinterpret_cast<g_u8*>(a.ptr[a.cols + row]) + static_cast<int64_t>(s) * a.out_ss;
+// `cols` is passed separately so specialised kernels index with a constant.
+__device__ __forceinline__ g_u8* out_ptr(const MatmulArgs& a, int cols, int row, int s) {
+    const int v = cols + row;
+    return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
 }
 
 // ---------------------------------------------------------------------------
@@ -99,13 +101,48 @@ enum : int {
     kVarSingleTab = 4,   // no LDS table prefetch across columns (fewer VGPRs)
     kVarBitop3 = 8,      // explicit v_bitop3 (xor3) accumulation
 };
-constexpr int kVarDefault = kVarBitop3 | kVarSingleTab;
+constexpr int kVarDefault = kVarBitop3 | kVarSingleTab | kVarNtLoad;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR = kVarDefault>
+// 16-byte load / store of vector data.  LAUX / SAUX >= 0 select buffer
+// instructions with that cache-policy immediate (bit0 sc0, bit1 nt, bit4 sc1
+// on gfx950); -1 keeps global_load/store (nt per VAR / nt_store).  The buffer
+// descriptor is built from wave-uniform values (kernarg pointer + stripe
+// base), so no waterfall loop is generated (cdna_hip_programming.md T20).
+template <int AUX>
+__device__ __forceinline__ u32x4 load16(const g_u8* base, uint64_t off, uint32_t nbytes, bool nt) {
+    if constexpr (AUX >= 0) {
+        __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, static_cast<int>(nbytes), 0x00020000);
+        return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, AUX);
+    } else {
+        const g_u32x4* src = reinterpret_cast<const g_u32x4*>(base + off);
+        return nt ? __builtin_nontemporal_load(src) : *src;
+    }
+}
+
+template <int AUX>
+__device__ __forceinline__ void store16(g_u8* base, uint64_t off, uint32_t nbytes, u32x4 val, bool nt) {
+    if constexpr (AUX >= 0) {
+        __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, static_cast<int>(nbytes), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(val, r, static_cast<int>(off), 0, AUX);
+    } else {
+        g_u32x4* o = reinterpret_cast<g_u32x4*>(base + off);
+        if (nt) __builtin_nontemporal_store(val, o);
+        else *o = val;
+    }
+}
+
+// Default cache policy of the vector kernel: buffer_load/store ... nt (aux 2).
+// Measured in-process on MI355X (tools/ab.py): 0.590 ms vs 0.632 ms for
+// global_load/store nt on the 10+4 @ 1 MiB x 256 launch.
+constexpr int kAuxNt = 2;
+
+template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR = kVarDefault, int LAUX = kAuxNt, int SAUX = kAuxNt>
 __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
     constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
@@ -157,7 +194,8 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
                     if (r < nrows)
 #pragma unroll
                         for (int v = 0; v < VPT; ++v) {
-                            const u32x4 o = *reinterpret_cast<const g_u32x4*>(out_ptr(a, rg + r, s) + off[v]);
+                            const u32x4 o = load16<LAUX>(out_ptr(a, cols, rg + r, s), off[v],
+                                                         static_cast<uint32_t>(a.body), false);
                             acc[r][v][0] = o.x; acc[r][v][1] = o.y; acc[r][v][2] = o.z; acc[r][v][3] = o.w;
                         }
             }
@@ -171,11 +209,8 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
                     if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
                     const g_u8* p = in_ptr(a, c, s);
 #pragma unroll
-                    for (int v = 0; v < VPT; ++v) {
-                        const g_u32x4* src = reinterpret_cast<const g_u32x4*>(p + off[v]);
-                        if (VAR & kVarNtLoad) x[b][v] = __builtin_nontemporal_load(src);
-                        else x[b][v] = *src;
-                    }
+                    for (int v = 0; v < VPT; ++v)
+                        x[b][v] = load16<LAUX>(p, off[v], static_cast<uint32_t>(a.body), (VAR & kVarNtLoad) != 0);
                 }
                 // Tables of column b+1 are read from LDS while column b is computed.
                 constexpr bool kPrefetchTab = !(VAR & kVarSingleTab);
@@ -249,11 +284,10 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
 #pragma unroll
                     for (int v = 0; v < VPT; ++v) {
                         if (!ok[v]) continue;
-                        g_u32x4* o = reinterpret_cast<g_u32x4*>(out_ptr(a, rg + r, s) + off[v]);
                         u32x4 val;
                         val.x = acc[r][v][0]; val.y = acc[r][v][1]; val.z = acc[r][v][2]; val.w = acc[r][v][3];
-                        if (ACC || !a.nt_store) *o = val;
-                        else __builtin_nontemporal_store(val, o);
+                        store16<SAUX>(out_ptr(a, cols, rg + r, s), off[v], static_cast<uint32_t>(a.body), val,
+                                      a.nt_store != 0);
                     }
                 }
             }
@@ -276,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_bytes(const MatmulArgs a, ui
 
     for (int r = 0; r < a.rows; ++r) {
         uint32_t acc = 0;
-        g_u8* o = out_ptr(a, r, s) + pos;
+        g_u8* o = out_ptr(a, a.cols, r, s) + pos;
         if (a.accumulate)
             for (int q = 0; q < nb; ++q) acc |= static_cast<uint32_t>(o[q]) << (8 * q);
         for (int c = 0; c < a.cols; ++c) {
@@ -312,6 +346,12 @@ struct Variant {
 #define RSAMD_VARIANT_V(KB, KFIX, MC, ACC, VPT, VAR) \
     Variant { gf_matmul_vec<KB, KFIX, MC, ACC, VPT, VAR>, KB, MC, VPT, KFIX, \
               "gf_matmul_vec<" #KB "," #KFIX "," #MC "," #ACC "," #VPT "," #VAR ">" }
+#define RSAMD_VARIANT_G(KB, KFIX, MC, ACC) \
+    Variant { gf_matmul_vec<KB, KFIX, MC, ACC, 1, kVarDefault, -1, -1>, KB, MC, 1, KFIX, \
+              "gf_matmul_vec<" #KB "," #KFIX "," #MC "," #ACC ",1,global>" }
+#define RSAMD_VARIANT_AUX(VAR, LAUX, SAUX) \
+    Variant { gf_matmul_vec<10, true, 4, false, 1, VAR, LAUX, SAUX>, 10, 4, 1, true, \
+              "gf_matmul_vec<10,true,4,false,1," #VAR "," #LAUX "," #SAUX ">" }
 
 // Experimental code shapes of the 10+4 encode kernel (RSAMD_VAR=<flags>),
 // used by tools/sweep.sh to A/B variants in separate processes.
@@ -322,6 +362,21 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
     case V:                                                                                           \
         *out = vpt == 2 ? RSAMD_VARIANT_V(10, true, 4, false, 2, V) : RSAMD_VARIANT_V(10, true, 4, false, 1, V); \
         return true;
+    // var >= 100: buffer-instruction cache-policy experiments (body < 2 GiB)
+    switch (var) {
+        case 100: *out = RSAMD_VARIANT_AUX(12, 2, 2); return true;     // nt / nt
+        case 101: *out = RSAMD_VARIANT_AUX(12, 18, 2); return true;    // nt sc1 / nt
+        case 102: *out = RSAMD_VARIANT_AUX(12, 3, 2); return true;     // sc0 nt / nt
+        case 103: *out = RSAMD_VARIANT_AUX(12, 2, 3); return true;     // nt / sc0 nt
+        case 104: *out = RSAMD_VARIANT_AUX(12, 2, 18); return true;    // nt / sc1 nt
+        case 105: *out = RSAMD_VARIANT_AUX(12, 2, 0); return true;     // nt / default
+        case 106: *out = RSAMD_VARIANT_AUX(12, 19, 19); return true;   // sc0 sc1 nt both
+        case 107: *out = RSAMD_VARIANT_AUX(12, 16, 2); return true;    // sc1 / nt
+        case 108: *out = RSAMD_VARIANT_AUX(14, -1, -1); return true;   // global nt loads / global nt stores
+        case 109: *out = RSAMD_VARIANT_AUX(8, 2, 2); return true;      // buffer nt, double-buffered tables
+        case 110: *out = RSAMD_VARIANT_AUX(13, 2, 2); return true;     // DIAGNOSTIC xor-only, buffer nt
+        default: break;
+    }
     switch (var) {
         RSAMD_CASE(0)
         RSAMD_CASE(1)
@@ -337,7 +392,21 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
 #undef RSAMD_CASE
 }
 
-static Variant pick(int rows, int cols, bool acc, int vpt) {
+static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 GiB
+    if (!acc) {
+        if (rows == 1) return RSAMD_VARIANT_G(4, false, 1, false);
+        if (rows == 2) return RSAMD_VARIANT_G(4, false, 2, false);
+        if (rows <= 4) return RSAMD_VARIANT_G(4, false, 4, false);
+        return RSAMD_VARIANT_G(4, false, 8, false);
+    }
+    if (rows == 1) return RSAMD_VARIANT_G(4, false, 1, true);
+    if (rows == 2) return RSAMD_VARIANT_G(4, false, 2, true);
+    if (rows <= 4) return RSAMD_VARIANT_G(4, false, 4, true);
+    return RSAMD_VARIANT_G(4, false, 8, true);
+}
+
+static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body) {
+    if (body >= (uint64_t{1} << 31)) return pick_global(rows, acc);
     Variant ex;
     if (pick_experimental(rows, cols, acc, vpt, &ex)) return ex;
     // Specialised shapes: the BASELINE configs (10+4, 12+4 encode; 10-column
@@ -362,7 +431,7 @@ static Variant pick(int rows, int cols, bool acc, int vpt) {
 }
 
 const char* vector_kernel_name(int rows, int cols, int accumulate) {
-    return pick(rows, cols, accumulate != 0, tuning().vpt).name;
+    return pick(rows, cols, accumulate != 0, tuning().vpt, 0).name;
 }
 
 static bool aligned16(uint64_t v) { return (v & 15u) == 0; }
@@ -371,14 +440,15 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     if (a.len == 0 || a.nstripes <= 0 || a.rows <= 0 || a.cols <= 0) return hipSuccess;
     // Vector body only when every base pointer and both stripe strides are
     // 16-byte aligned (global_load/store_dwordx4 on naturally aligned data).
-    bool aligned = aligned16(static_cast<uint64_t>(a.in_ss)) && aligned16(static_cast<uint64_t>(a.out_ss));
-    for (int v = 0; v < a.cols + a.rows && aligned; ++v) aligned = aligned16(a.ptr[v]);
+    bool aligned = true;
+    for (int v = 0; v < a.cols + a.rows && aligned; ++v)
+        aligned = aligned16(a.ptr[v]) && (a.nstripes == 1 || aligned16(static_cast<uint64_t>(a.ss[a.sid[v] & 3])));
     a.body = aligned ? (a.len & ~static_cast<uint64_t>(15)) : 0;
     a.tail_start = a.body;
 
     if (a.body) {
         const LaunchTuning& tu = tuning();
-        const Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt);
+        const Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt, a.body);
         a.units_per_chunk = kBlock * var.vpt;
         a.nt_store = tu.nt_store;
         const uint64_t nunits = a.body >> 4;

@@ -15,8 +15,10 @@ namespace rsamd {
 
 constexpr int kMaxPtrs = 260;  // inputs + outputs of one launch (d+p <= 256, Update adds 1)
 
-// Kernel arguments (passed by value, ~2.2 KB of kernarg).  Vector v of
-// stripe s is at  ptr[v] + s * (v < cols ? in_ss : out_ss).
+// Kernel arguments (passed by value, ~3.2 KB of kernarg).  Vector v of
+// stripe s is at  ptr[v] + s * ss[sid[v]]: each vector picks one of four
+// stripe strides, so inputs and outputs may live in differently strided
+// regions (e.g. data and parity in separate buffers).
 struct MatmulArgs {
     const uint32_t* tables;   // device perm tables, [cols][rows_pad][5] dwords
     int rows, cols, rows_pad;
@@ -27,10 +29,12 @@ struct MatmulArgs {
     uint64_t len;             // bytes per vector
     uint64_t body;            // bytes handled by the vector kernel (multiple of 16)
     uint64_t tail_start;      // first byte handled by the byte kernel
-    int64_t in_ss, out_ss;    // stripe strides in bytes
+    int64_t ss[4];            // stripe strides in bytes, selected per vector by sid
     int64_t chunks_per_stripe;
     int64_t total_chunks;
     uint64_t ptr[kMaxPtrs];   // inputs [0, cols), outputs [cols, cols+rows)
+    uint32_t sid[kMaxPtrs];   // stride selector of each vector (0..3); dwords so the
+                              // kernel reads them with scalar loads
 };
 
 // Launch tuning knobs (read from the environment once).

@@ -21,7 +21,7 @@ from typing import Sequence
 
 import numpy as np
 
-from ._lib import c_u8p, lib
+from ._lib import RSLayout, c_u8p, lib
 
 
 # ---------------------------------------------------------------- errors
@@ -264,6 +264,29 @@ class RS:
         """Encode every stripe of buf[S, d+p, len] (the north-star hot path)."""
         base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
         _check(lib().rs_encode_batch(self._h, base, ss, vs, S, n, _stream(stream)))
+
+    def _split_layout(self, data, parity):
+        _check_tensor_any(data)
+        _check_tensor_any(parity)
+        d, p = self.DataNum, self.ParityNum
+        if data.dim() != 3 or parity.dim() != 3 or data.shape[0] != parity.shape[0] or \
+                data.shape[2] != parity.shape[2] or data.shape[1] < d or parity.shape[1] < p or \
+                data.stride(2) != 1 or parity.stride(2) != 1:
+            raise TypeError("expected data [S, >=d, len] and parity [S, >=p, len] uint8 GPU tensors")
+        L = RSLayout(data.data_ptr(), data.stride(0), data.stride(1), parity.data_ptr(), parity.stride(0),
+                     parity.stride(1))
+        return L, data.shape[0], data.shape[2]
+
+    def encode_batch_split(self, data, parity, stream=None) -> None:
+        """Encode S stripes whose data [S, d, len] and parity [S, p, len] live in separate buffers."""
+        L, S, n = self._split_layout(data, parity)
+        _check(lib().rs_encode_batch_layout(self._h, ctypes.byref(L), S, n, _stream(stream)))
+
+    def reconst_batch_split(self, data, parity, survived, needReconst, stream=None) -> None:
+        L, S, n = self._split_layout(data, parity)
+        s, ns = _ints(survived)
+        q, nq = _ints(needReconst)
+        _check(lib().rs_reconst_batch_layout(self._h, ctypes.byref(L), S, n, s, ns, q, nq, _stream(stream)))
 
     def reconst_batch(self, buf, survived, needReconst, stream=None) -> None:
         base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)

@@ -445,3 +445,44 @@ def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
         pinned = torch.from_numpy(host.copy()).pin_memory()
         r.encode_host_batch(pinned, spc, st)
         assert np.array_equal(pinned.numpy()[:, d:], exp)
+
+
+def test_split_layout_encode_reconst(rslib, orc, torch_dev):
+    """Data and parity in separate buffers (rs_layout_t)."""
+    torch = torch_dev
+    d, p, S, n = 10, 4, 6, 8192 + 48
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    data = torch.randint(0, 256, (S, d, n), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    torch.cuda.synchronize()
+    exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), data.cpu().numpy())
+    assert np.array_equal(parity.cpu().numpy(), exp)
+    ref_d, ref_p = data.clone(), parity.clone()
+    for lost in ([0], [3, 12], [1, 2, 10, 13], [11], [0, 9, 10, 11]):
+        data.copy_(ref_d)
+        parity.copy_(ref_p)
+        for v in lost:
+            (data[:, v] if v < d else parity[:, v - d]).fill_(0x77)
+        r.reconst_batch_split(data, parity, [], lost)
+        torch.cuda.synchronize()
+        assert torch.equal(data, ref_d) and torch.equal(parity, ref_p), lost
+
+
+def test_update_batch_distinct_strides(rslib, torch_dev):
+    torch = torch_dev
+    d, p, S, n = 10, 4, 5, 4096
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    buf = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(buf)
+    old = buf[:, 4].clone()                                   # stride n
+    new_big = torch.randint(0, 256, (S, 3, n), dtype=torch.uint8, device="cuda", generator=g)
+    new = new_big[:, 1]                                       # stride 3n
+    r.update_batch(old, new, 4, buf)
+    buf[:, 4] = new
+    exp = buf.clone()
+    r.encode_batch(exp)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, exp)

@@ -38,7 +38,14 @@ __global__ __launch_bounds__(256) void k_write(g_u32x4* dst, uint64_t n, int nt)
 template <int K, int M, int UPL>
 __global__ __launch_bounds__(256) void k_pattern(uint8_t* base, uint64_t vec, uint64_t stripe_stride,
                                                  uint64_t chunks_per_stripe, int nstripes, int mapping) {
-    const uint64_t chunk = blockIdx.x;
+    uint64_t chunk = blockIdx.x;
+    if (mapping == 2) {  // XCD-contiguous: blocks sharing an XCD (b % 8) take one contiguous range
+        const uint64_t nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = chunk % 8;
+        chunk = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + chunk / 8;
+    } else if (mapping == 3) {  // chunk-major across stripes in groups of 8 stripes
+        const uint64_t g = chunk / (8 * chunks_per_stripe), w = chunk % (8 * chunks_per_stripe);
+        chunk = (g * 8 + w % 8) * chunks_per_stripe + w / 8;
+    }
     uint64_t s = chunk / chunks_per_stripe, cb = chunk % chunks_per_stripe;
     if (mapping == 1) { s = chunk % nstripes; cb = chunk / nstripes; }
     const __attribute__((address_space(1))) uint8_t* sp =
@@ -69,7 +76,33 @@ __global__ __launch_bounds__(256) void k_pattern(uint8_t* base, uint64_t vec, ui
         }
 }
 
+// Same pattern with the parity vectors in their own region (pbase).
+template <int K, int M>
+__global__ __launch_bounds__(256) void k_pattern_sep(uint8_t* base, uint8_t* pbase, uint64_t vec, uint64_t dss,
+                                                     uint64_t pss, uint64_t cps) {
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t s = chunk / cps, cb = chunk % cps;
+    const uint64_t off = (cb * 256 + threadIdx.x) * 16;
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = *(const g_u32x4*)(base + s * dss + i * vec + off);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        u32x4 a = {(uint32_t)j, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < K; ++i) a ^= x[i];
+        __builtin_nontemporal_store(a, (g_u32x4*)(pbase + s * pss + j * vec + off));
+    }
+}
+
 extern "C" {
+int probe_pattern_sep(void* base, void* pbase, uint64_t vec, uint64_t dss, uint64_t pss, int nstripes, void* stream) {
+    uint64_t cps = vec / 4096;
+    hipLaunchKernelGGL((k_pattern_sep<10, 4>), dim3(cps * nstripes), dim3(256), 0, (hipStream_t)stream,
+                       (uint8_t*)base, (uint8_t*)pbase, vec, dss, pss, cps);
+    return hipGetLastError();
+}
+
 int probe_copy(void* src, void* dst, uint64_t bytes, int nt, void* stream) {
     uint64_t n = bytes / 16;
     hipLaunchKernelGGL(k_copy, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,

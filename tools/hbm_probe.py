@@ -70,6 +70,61 @@ def basic_probes(L, a, b, n, vp, sp, timeit):
 
 
 def pattern_probes(L, a, n, vp, sp, timeit):
+    if os.environ.get("PROBE_SEP", "0") == "1":
+        vec = 1 << 20
+        S = 240
+        import torch
+        b = torch.empty(S * 4 * vec + (64 << 20), dtype=torch.uint8, device="cuda")
+        for poff in (0, 4096, 1 << 20, 3 << 19, 5 << 18):
+            assert poff + S * 4 * vec <= b.numel() and S * 10 * vec <= n
+            timeit(f"10+4 separate parity buffer, offset {poff >> 10}K",
+                   lambda: L.probe_pattern_sep(vp(a), ctypes.c_void_p(b.data_ptr() + poff), ctypes.c_uint64(vec),
+                                               ctypes.c_uint64(10 * vec), ctypes.c_uint64(4 * vec), S, sp),
+                   S * 14 * vec, iters=20)
+        for dss_pad in (0,):
+            need = S * (10 * vec + dss_pad) + S * 4 * vec
+            assert need <= n, "probe case out of bounds"
+            timeit(f"10+4 same buffer, parity after all data, dss pad {dss_pad >> 10}K",
+                   lambda: L.probe_pattern_sep(vp(a), ctypes.c_void_p(a.data_ptr() + S * (10 * vec + dss_pad)),
+                                               ctypes.c_uint64(vec), ctypes.c_uint64(10 * vec + dss_pad),
+                                               ctypes.c_uint64(4 * vec), S, sp),
+                   S * 14 * vec, iters=20)
+        assert S * 14 * vec <= n
+        timeit("10+4 interleaved layout (reference)",
+               lambda: L.probe_pattern_sep(vp(a), ctypes.c_void_p(a.data_ptr() + 10 * vec), ctypes.c_uint64(vec),
+                                           ctypes.c_uint64(14 * vec), ctypes.c_uint64(14 * vec), S, sp),
+               S * 14 * vec, iters=20)
+        return
+    if os.environ.get("PROBE_MAP", "0") == "1":
+        vec = 1 << 20
+        S = 240
+        for mapping in (0, 2, 3):
+            for pad, sspad in ((0, 0), (0, 1 << 20), (512 << 10, 0), (1 << 20, 0), (128 << 10, 0), (8192, 0),
+                               (0, 4096), (2048, 2048), (32 << 10, 0), (192 << 10, 0)):
+                pitch = vec + pad
+                sstride = 14 * pitch + sspad
+                if (S - 1) * sstride + 13 * pitch + vec > n:  # bounds
+                    continue
+                timeit(f"10+4 map={mapping} pitch=1M+{pad >> 10}K sspad={sspad >> 10}K",
+                       lambda: L.probe_pattern(vp(a), ctypes.c_uint64(vec), ctypes.c_uint64(pitch),
+                                               ctypes.c_uint64(sstride), S, 1, mapping, sp),
+                       S * 14 * vec, iters=20)
+        return
+    if os.environ.get("PROBE_VEC", "0") == "1":
+        half = (n // 2) // 4096 * 4096
+        timeit("flat copy, same allocation halves",
+               lambda: L.probe_copy(vp(a), ctypes.c_void_p(a.data_ptr() + half), ctypes.c_uint64(half), 0, sp),
+               2 * half)
+        for k, m in ((1, 1), (10, 4), (10, 0)):
+            for vec in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+                S = int(n // ((k + m) * vec))
+                if S < 1:
+                    continue
+                timeit(f"pattern k={k} m={m} vec={vec >> 10}KiB S={S}",
+                       lambda: L.probe_pattern_km(vp(a), ctypes.c_uint64(vec), ctypes.c_uint64(vec),
+                                                  ctypes.c_uint64((k + m) * vec), S, k, m, sp),
+                       S * (k + m) * vec, iters=20)
+        return
     if os.environ.get("PROBE_KM", "0") == "1":
         vec = 1 << 20
         for k, m in ((1, 1), (2, 2), (4, 4), (7, 7), (10, 10), (4, 0), (10, 0), (14, 0), (10, 2), (10, 4), (12, 4), (6, 3)):
@@ -86,7 +141,7 @@ def pattern_probes(L, a, n, vp, sp, timeit):
             sstride = 14 * pitch + sspad
             for mapping in (0, 1):
                 for upl in (1, 2):
-                    if S * sstride > n:
+                    if S * sstride > n:  # bounds: every stripe must fit the buffer
                         continue
                     timeit(f"pattern pad={pad} sspad={sspad} map={mapping} upl={upl}",
                            lambda: L.probe_pattern(vp(a), ctypes.c_uint64(vec), ctypes.c_uint64(pitch),

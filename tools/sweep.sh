@@ -7,7 +7,7 @@ CFG="${CFG:-10+4@1MiB}"
 run() {
   local tag="$1"; shift
   local line
-  line=$(env "$@" timeout -k 10 300 python -u bench.py --config "$CFG" --cpu-seconds 0 --steps 40 --warmup 10 --verify 0 2>/dev/null | tail -1)
+  line=$(env "$@" timeout -k 10 300 python -u bench.py --config "$CFG" --cpu-seconds 0 2>/dev/null | tail -1)
   local rc=$?
   python3 - "$tag" "$line" <<'PY'
 import json, sys
