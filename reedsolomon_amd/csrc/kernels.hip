@@ -142,7 +142,10 @@ __device__ __forceinline__ void store16(g_u8* base, uint64_t off, uint32_t nbyte
 // global_load/store nt on the 10+4 @ 1 MiB x 256 launch.
 constexpr int kAuxNt = 2;
 
-template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR = kVarDefault, int LAUX = kAuxNt, int SAUX = kAuxNt>
+//   WIN  0: issue all KB column loads up front; >0: rolling window of WIN
+//        columns in flight per lane (fewer VGPRs, more resident waves)
+template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR = kVarDefault, int LAUX = kAuxNt, int SAUX = kAuxNt,
+          int WIN = 0>
 __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
     constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
@@ -201,17 +204,20 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
             }
 
             for (int i0 = 0; i0 < ncols_pad; i0 += KB) {
-                // Issue all KB column loads of this batch first (KB*16*VPT bytes in flight per lane).
+                // Issue the column loads of this batch first (KB*16*VPT bytes in flight
+                // per lane), or the first WIN of them with the rest rolled in below.
+                constexpr int kFirst = (WIN > 0 && WIN < KB) ? WIN : KB;
                 u32x4 x[KB][VPT];
-#pragma unroll
-                for (int b = 0; b < KB; ++b) {
+                auto load_col = [&](int b) {
                     int c = i0 + b;
                     if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
                     const g_u8* p = in_ptr(a, c, s);
 #pragma unroll
                     for (int v = 0; v < VPT; ++v)
                         x[b][v] = load16<LAUX>(p, off[v], static_cast<uint32_t>(a.body), (VAR & kVarNtLoad) != 0);
-                }
+                };
+#pragma unroll
+                for (int b = 0; b < kFirst; ++b) load_col(b);
                 // Tables of column b+1 are read from LDS while column b is computed.
                 constexpr bool kPrefetchTab = !(VAR & kVarSingleTab);
                 u32x4 tv[2][COLW];
@@ -274,6 +280,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
                         for (int v = 0; v < VPT; ++v)
 #pragma unroll
                             for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(acc[r][v][q]));
+                    if (b + kFirst < KB) load_col(b + kFirst);  // rolling window refill
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -349,6 +356,13 @@ struct Variant {
 #define RSAMD_VARIANT_G(KB, KFIX, MC, ACC) \
     Variant { gf_matmul_vec<KB, KFIX, MC, ACC, 1, kVarDefault, -1, -1>, KB, MC, 1, KFIX, \
               "gf_matmul_vec<" #KB "," #KFIX "," #MC "," #ACC ",1,global>" }
+// Specialised encode kernels: rolling 5-column load window (73 VGPRs, 6 waves/SIMD).
+#define RSAMD_VARIANT_W5(K) \
+    Variant { gf_matmul_vec<K, true, 4, false, 1, kVarDefault, kAuxNt, kAuxNt, 5>, K, 4, 1, true, \
+              "gf_matmul_vec<" #K ",true,4,false,1,win5>" }
+#define RSAMD_VARIANT_WIN(W) \
+    Variant { gf_matmul_vec<10, true, 4, false, 1, kVarDefault, kAuxNt, kAuxNt, W>, 10, 4, 1, true, \
+              "gf_matmul_vec<10,true,4,false,1,win" #W ">" }
 #define RSAMD_VARIANT_AUX(VAR, LAUX, SAUX) \
     Variant { gf_matmul_vec<10, true, 4, false, 1, VAR, LAUX, SAUX>, 10, 4, 1, true, \
               "gf_matmul_vec<10,true,4,false,1," #VAR "," #LAUX "," #SAUX ">" }
@@ -375,6 +389,11 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
         case 108: *out = RSAMD_VARIANT_AUX(14, -1, -1); return true;   // global nt loads / global nt stores
         case 109: *out = RSAMD_VARIANT_AUX(8, 2, 2); return true;      // buffer nt, double-buffered tables
         case 110: *out = RSAMD_VARIANT_AUX(13, 2, 2); return true;     // DIAGNOSTIC xor-only, buffer nt
+        case 123: *out = RSAMD_VARIANT_WIN(3); return true;
+        case 124: *out = RSAMD_VARIANT_WIN(4); return true;
+        case 125: *out = RSAMD_VARIANT_WIN(5); return true;
+        case 126: *out = RSAMD_VARIANT_WIN(6); return true;
+        case 128: *out = RSAMD_VARIANT_WIN(8); return true;
         default: break;
     }
     switch (var) {
@@ -413,9 +432,9 @@ static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body) {
     // reconst with 1-4 outputs; 10+4 Update = 2 columns, accumulate).
     if (!acc) {
         if (cols == 10 && rows > 2 && rows <= 4)
-            return vpt == 2 ? RSAMD_VARIANT(10, true, 4, false, 2) : RSAMD_VARIANT(10, true, 4, false, 1);
+            return vpt == 2 ? RSAMD_VARIANT(10, true, 4, false, 2) : RSAMD_VARIANT_W5(10);
         if (cols == 12 && rows > 2 && rows <= 4)
-            return vpt == 2 ? RSAMD_VARIANT(12, true, 4, false, 2) : RSAMD_VARIANT(12, true, 4, false, 1);
+            return vpt == 2 ? RSAMD_VARIANT(12, true, 4, false, 2) : RSAMD_VARIANT_W5(12);
         if (cols == 10 && rows == 1) return RSAMD_VARIANT(10, true, 1, false, 1);
         if (cols == 10 && rows == 2) return RSAMD_VARIANT(10, true, 2, false, 1);
         if (rows == 1) return RSAMD_VARIANT(4, false, 1, false, 1);
