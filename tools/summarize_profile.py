@@ -25,7 +25,9 @@ shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "k
 
 def per_launch(counter):
     rows = list(csv.DictReader(open(os.path.join(src, f"pmc_{counter}", "pmc_counter_collection.csv"))))
-    vals = [float(r["Counter_Value"]) for r in rows if "gf_matmul_vec" in r["Kernel_Name"]]
+    names = [r["Kernel_Name"] for r in rows if "gf_matmul_vec" in r["Kernel_Name"]]
+    dom = statistics.mode(names)
+    vals = [float(r["Counter_Value"]) for r in rows if r["Kernel_Name"] == dom]
     return vals
 
 
@@ -33,14 +35,20 @@ fetch = per_launch("FETCH_SIZE")
 write = per_launch("WRITE_SIZE")
 f_b = statistics.median(fetch) * 1024 * 2
 w_b = statistics.median(write) * 1024
-trace = [r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv"))) if "gf_matmul_vec" in r["Kernel_Name"]]
+trace_all = [r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv")))
+             if "gf_matmul_vec" in r["Kernel_Name"]]
+dominant = statistics.mode([r["Kernel_Name"] for r in trace_all])
+trace = [r for r in trace_all if r["Kernel_Name"] == dominant]
 durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
+steps = int(os.environ.get("BENCH_STEPS", "100"))
 summary = {
     "config": cfg,
     "kernel": trace[0]["Kernel_Name"] if trace else None,
     "launches_traced": len(durs),
-    "duration_ns_mean": statistics.mean(durs) if durs else None,
-    "duration_ns_median": statistics.median(durs) if durs else None,
+    "duration_ns_mean_all_launches": statistics.mean(durs) if durs else None,
+    "duration_ns_mean_timed_region": statistics.mean(durs[-steps:]) if durs else None,
+    "timed_region_note": f"last {steps} launches = bench.py's timed steps (the earlier ones are the self-check "
+                         "and warm-up, which include the post-idle power transient)",
     "FETCH_SIZE_KiB_median": statistics.median(fetch),
     "WRITE_SIZE_KiB_median": statistics.median(write),
     "hbm_read_bytes_per_launch (FETCH_SIZE*1024*2)": f_b,
