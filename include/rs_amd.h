@@ -161,6 +161,16 @@ RS_API int rs_encode_batch_layout(rs_t* rs, const rs_layout_t* layout, int nstri
 RS_API int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* layout, int nstripes, size_t len,
                                    const int* survived, int ns, const int* need, int nn, void* stream);
 
+/* Reconst a batch where every stripe has its own erasure pattern (SURVEY
+ * §8f.1): need_masks[s] has bit v set when vector v of stripe s must be
+ * rebuilt (all other vectors of that stripe are survivors, i.e. Reconst's
+ * "empty survived" form, rs.go:281-285); 0 skips the stripe.  Stripes are
+ * grouped by pattern on the host; each distinct pattern costs one inverse
+ * (cached) and one or two launches over its stripes.  Requires d+p <= 64.
+ * Every pattern is validated (RS_ERR_TOO_MANY_LOST, ...) before any launch. */
+RS_API int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* layout, int nstripes, size_t len,
+                                  const uint64_t* need_masks, void* stream);
+
 /* Reconst every stripe with the same survived/need pattern
  * (one host plan + one cached matrix, then at most two device passes). */
 RS_API int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,

@@ -58,6 +58,7 @@ SIGNATURES = {
     "rs_encode_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_void]),
     "rs_encode_batch_layout": (c_int, [c_void, c_layoutp, c_int, c_sz, c_void]),
     "rs_reconst_batch_layout": (c_int, [c_void, c_layoutp, c_int, c_sz, c_intp, c_int, c_intp, c_int, c_void]),
+    "rs_reconst_batch_multi": (c_int, [c_void, c_layoutp, c_int, c_sz, ctypes.POINTER(ctypes.c_uint64), c_void]),
     "rs_reconst_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_intp, c_int, c_intp, c_int,
                                  c_void]),
     "rs_update_batch": (c_int, [c_void, c_void, c_i64, c_void, c_i64, c_int, c_void, c_i64, c_i64, c_int, c_sz,

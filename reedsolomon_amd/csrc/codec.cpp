@@ -216,7 +216,7 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
 // s * ss[sid[v]] (sid == nullptr: all inputs use ss[0], all outputs ss[1]).
 int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs,
               const uint8_t* in_sid, uint8_t* const* out_ptrs, const uint8_t* out_sid, const int64_t ss[4],
-              int nstripes, uint64_t len, bool accumulate, hipStream_t stream) {
+              int nstripes, uint64_t len, bool accumulate, hipStream_t stream, const int32_t* stripe_ids = nullptr) {
     if (rows <= 0 || cols <= 0 || nstripes <= 0 || len == 0) return RS_OK;
     if (rows + cols > kMaxPtrs) return RS_ERR_INVAL;
     MatmulArgs a;
@@ -229,6 +229,7 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     a.accumulate = accumulate ? 1 : 0;
     a.len = len;
     for (int i = 0; i < 4; ++i) a.ss[i] = ss[i];
+    a.stripe_ids = stripe_ids;
     for (int c = 0; c < cols; ++c) {
         a.ptr[c] = reinterpret_cast<uint64_t>(in_ptrs[c]);
         a.sid[c] = in_sid ? in_sid[c] : 0;
@@ -775,6 +776,97 @@ int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vec
     return rs_reconst_batch_layout(rs, &L, nstripes, len, survived, ns, need, nn, stream);
 }
 
+int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const uint64_t* need_masks,
+                           void* stream) {
+    if (!rs || !L || nstripes < 0 || (nstripes > 0 && !need_masks)) return RS_ERR_INVAL;
+    const int d = rs->d, p = rs->p;
+    if (d + p > 64) return RS_ERR_INVAL;  // masks are 64-bit survivor bitmaps, like the cache key
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    const uint64_t valid = (d + p == 64) ? ~uint64_t{0} : ((uint64_t{1} << (d + p)) - 1);
+    // Group stripes by erasure pattern (host, O(S)); validate every pattern before any launch.
+    std::unordered_map<uint64_t, std::vector<int32_t>> groups;
+    for (int s = 0; s < nstripes; ++s) {
+        const uint64_t m = need_masks[s];
+        if (!m) continue;
+        if (m & ~valid) return RS_ERR_ILLEGAL_VECTS;
+        groups[m].push_back(s);
+    }
+    if (groups.empty()) return RS_OK;
+    struct Group {
+        uint64_t mask;
+        ReconstPlan pl;
+        size_t off, n;
+    };
+    std::vector<Group> plan;
+    std::vector<int32_t> ids;
+    ids.reserve(nstripes);
+    for (auto& kv : groups) {
+        Group gr;
+        gr.mask = kv.first;
+        int need[64], nn = 0;
+        for (int v = 0; v < d + p; ++v)
+            if (kv.first >> v & 1) need[nn++] = v;
+        int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
+        if (rc) return rc;  // RS_ERR_TOO_MANY_LOST for a pattern beyond p erasures
+        gr.off = ids.size();
+        gr.n = kv.second.size();
+        ids.insert(ids.end(), kv.second.begin(), kv.second.end());
+        plan.push_back(gr);
+    }
+    if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    hipStream_t st = as_stream(stream);
+    int32_t* dids = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&dids), ids.size() * sizeof(int32_t), st) != hipSuccess)
+        return RS_ERR_DEVICE;
+    int rc = hipMemcpyAsync(dids, ids.data(), ids.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) == hipSuccess
+                 ? RS_OK
+                 : RS_ERR_DEVICE;
+    const LayoutAddr A{L, d};
+    const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    uint8_t isid[kMaxVects], osid[kMaxVects];
+    for (const Group& gr : plan) {
+        if (rc) break;
+        const ReconstPlan& pl = gr.pl;
+        const int pn = pl.nnr - pl.dn;
+        const int32_t* gids = dids + gr.off;
+        if (pl.dn > 0) {
+            std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
+            rc = reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data());
+            if (rc) break;
+            for (int i = 0; i < d; ++i) {
+                in[i] = A.ptr(pl.vs[i]);
+                isid[i] = A.sid(pl.vs[i]);
+            }
+            for (int i = 0; i < pl.dn; ++i) {
+                out[i] = A.ptr(pl.nr[i]);
+                osid[i] = A.sid(pl.nr[i]);
+            }
+            rc = matmul_ex(rs, gm.data(), pl.dn, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
+                           gids);
+            if (rc) break;
+        }
+        if (pn > 0) {
+            std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
+            for (int i = 0; i < d; ++i) {
+                in[i] = A.ptr(i);
+                isid[i] = 0;
+            }
+            for (int i = 0; i < pn; ++i) {
+                out[i] = A.ptr(pl.nr[pl.dn + i]);
+                osid[i] = 1;
+            }
+            rc = matmul_ex(rs, gm.data(), pn, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
+                           gids);
+        }
+    }
+    (void)hipFreeAsync(dids, st);
+    return rc;
+}
+
 // ---------------------------------------------------------------- Update
 
 int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
@@ -915,53 +1007,92 @@ int rs_host_unregister(void* ptr) {
     return hipHostUnregister(ptr) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
 }
 
+// Host-resident encode: a three-stage pipeline over a ring of `streams`
+// device slots.  H2D copies run on one stream, kernels on a second, D2H on a
+// third, linked by events, so the copy engines of both PCIe directions and
+// the CUs work on different chunks at the same time:
+//     h2d:  [wait slot free] copy data(c)  -> ev_in[slot]
+//     comp: [wait ev_in]     encode(c)     -> ev_enc[slot]
+//     d2h:  [wait ev_enc]    copy parity(c)-> ev_free[slot]
 int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
                          size_t len, int stripes_per_chunk, int streams) {
     if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
     if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
     if (nstripes == 0) return RS_OK;
     if (stripes_per_chunk <= 0) stripes_per_chunk = 8;
-    if (streams <= 0) streams = 3;
-    if (streams > 8) streams = 8;
+    int slots = streams <= 0 ? 3 : std::min(streams, 8);
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
     const int d = rs->d, p = rs->p;
-    const size_t pitch = rup(len, 256);
-    const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);  // device stripe stride
+    // [S][d+p][len] with 256-B-multiple len: data and parity of a stripe are contiguous rows
+    const bool dense = vect_stride == static_cast<int64_t>(len) && len % 256 == 0;
+    const size_t pitch = dense ? len : rup(len, 256);
+    const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);
     const size_t slot_bytes = static_cast<size_t>(dstripe) * stripes_per_chunk;
     std::lock_guard<std::mutex> lk(rs->stage_mu);
-    // One staging slot and one stream per pipeline lane; a lane's next chunk
-    // reuses its slot only after its previous D2H (same stream: ordered).
     uint8_t* ring = nullptr;
-    if (hipMalloc(&ring, slot_bytes * streams) != hipSuccess) return RS_ERR_DEVICE;
-    hipStream_t st[8] = {};
+    if (hipMalloc(&ring, slot_bytes * slots) != hipSuccess) return RS_ERR_DEVICE;
+    hipStream_t sh = nullptr, sc = nullptr, sd = nullptr;
+    std::vector<hipEvent_t> ev_in(slots), ev_enc(slots), ev_free(slots);
     int rc = RS_OK;
-    for (int i = 0; i < streams && rc == RS_OK; ++i)
-        if (hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess) rc = RS_ERR_DEVICE;
+    if (hipStreamCreateWithFlags(&sh, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&sc, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&sd, hipStreamNonBlocking) != hipSuccess)
+        rc = RS_ERR_DEVICE;
+    for (int i = 0; i < slots && rc == RS_OK; ++i)
+        if (hipEventCreateWithFlags(&ev_in[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ev_enc[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ev_free[i], hipEventDisableTiming) != hipSuccess)
+            rc = RS_ERR_DEVICE;
+    auto ok = [&](hipError_t e) {
+        if (e != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
+        return rc == RS_OK;
+    };
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
-    for (int c0 = 0, lane = 0; c0 < nstripes && rc == RS_OK; c0 += stripes_per_chunk, lane = (lane + 1) % streams) {
+    int chunk = 0;
+    for (int c0 = 0; c0 < nstripes && rc == RS_OK; c0 += stripes_per_chunk, ++chunk) {
         const int cn = std::min(stripes_per_chunk, nstripes - c0);
-        uint8_t* slot = ring + static_cast<size_t>(lane) * slot_bytes;
+        const int slot = chunk % slots;
+        uint8_t* dev = ring + static_cast<size_t>(slot) * slot_bytes;
         uint8_t* hb = base + static_cast<int64_t>(c0) * stripe_stride;
-        for (int i = 0; i < d && rc == RS_OK; ++i)  // data vector i of cn stripes: one 2-D copy
-            if (hipMemcpy2DAsync(slot + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len, cn,
-                                 hipMemcpyHostToDevice, st[lane]) != hipSuccess)
-                rc = RS_ERR_DEVICE;
-        if (rc) break;
-        for (int i = 0; i < d; ++i) in[i] = slot + i * pitch;
-        for (int j = 0; j < p; ++j) out[j] = slot + (d + j) * pitch;
-        rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, st[lane]);
-        for (int j = 0; j < p && rc == RS_OK; ++j)
-            if (hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, slot + (d + j) * pitch, dstripe, len, cn,
-                                 hipMemcpyDeviceToHost, st[lane]) != hipSuccess)
-                rc = RS_ERR_DEVICE;
-    }
-    for (int i = 0; i < streams; ++i)
-        if (st[i]) {
-            if (hipStreamSynchronize(st[i]) != hipSuccess) rc = RS_ERR_DEVICE;
-            (void)hipStreamDestroy(st[i]);
+        if (chunk >= slots && !ok(hipStreamWaitEvent(sh, ev_free[slot], 0))) break;
+        if (dense) {  // one 2-D copy: cn rows of d*len bytes
+            if (!ok(hipMemcpy2DAsync(dev, dstripe, hb, stripe_stride, static_cast<size_t>(d) * len, cn,
+                                     hipMemcpyHostToDevice, sh)))
+                break;
+        } else {
+            for (int i = 0; i < d; ++i)
+                if (!ok(hipMemcpy2DAsync(dev + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len, cn,
+                                         hipMemcpyHostToDevice, sh)))
+                    break;
         }
+        if (!ok(hipEventRecord(ev_in[slot], sh)) || !ok(hipStreamWaitEvent(sc, ev_in[slot], 0))) break;
+        for (int i = 0; i < d; ++i) in[i] = dev + i * pitch;
+        for (int j = 0; j < p; ++j) out[j] = dev + (d + j) * pitch;
+        rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, sc);
+        if (rc) break;
+        if (!ok(hipEventRecord(ev_enc[slot], sc)) || !ok(hipStreamWaitEvent(sd, ev_enc[slot], 0))) break;
+        if (dense) {
+            if (!ok(hipMemcpy2DAsync(hb + d * vect_stride, stripe_stride, dev + d * pitch, dstripe,
+                                     static_cast<size_t>(p) * len, cn, hipMemcpyDeviceToHost, sd)))
+                break;
+        } else {
+            for (int j = 0; j < p; ++j)
+                if (!ok(hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, dev + (d + j) * pitch, dstripe,
+                                         len, cn, hipMemcpyDeviceToHost, sd)))
+                    break;
+        }
+        if (!ok(hipEventRecord(ev_free[slot], sd))) break;
+    }
+    for (hipStream_t s : {sh, sc, sd})
+        if (s) {
+            if (hipStreamSynchronize(s) != hipSuccess) rc = RS_ERR_DEVICE;
+            (void)hipStreamDestroy(s);
+        }
+    for (int i = 0; i < slots; ++i)
+        for (hipEvent_t e : {ev_in[i], ev_enc[i], ev_free[i]})
+            if (e) (void)hipEventDestroy(e);
     (void)hipFree(ring);
     return rc;
 }

@@ -173,8 +173,9 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
 
         const int nrows = (a.rows - rg) < MC ? (a.rows - rg) : MC;
         for (int64_t chunk = blockIdx.x; chunk < a.total_chunks; chunk += gridDim.x) {
-            const int s = static_cast<int>(chunk / a.chunks_per_stripe);
-            const int64_t cb = chunk - static_cast<int64_t>(s) * a.chunks_per_stripe;
+            const int si = static_cast<int>(chunk / a.chunks_per_stripe);
+            const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
+            const int s = a.stripe_ids ? a.stripe_ids[si] : si;  // uniform: scalar load
             uint64_t off[VPT];
             bool ok[VPT];
 #pragma unroll
@@ -311,8 +312,9 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_bytes(const MatmulArgs a, ui
     const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const uint64_t total = groups_per_stripe * static_cast<uint64_t>(a.nstripes);
     if (gid >= total) return;
-    const int s = static_cast<int>(gid / groups_per_stripe);
-    const uint64_t pos = start + (gid - static_cast<uint64_t>(s) * groups_per_stripe) * 4;
+    const int si = static_cast<int>(gid / groups_per_stripe);
+    const uint64_t pos = start + (gid - static_cast<uint64_t>(si) * groups_per_stripe) * 4;
+    const int s = a.stripe_ids ? a.stripe_ids[si] : si;
     const int nb = (a.len - pos) < 4 ? static_cast<int>(a.len - pos) : 4;
 
     for (int r = 0; r < a.rows; ++r) {

@@ -30,6 +30,7 @@ struct MatmulArgs {
     uint64_t body;            // bytes handled by the vector kernel (multiple of 16)
     uint64_t tail_start;      // first byte handled by the byte kernel
     int64_t ss[4];            // stripe strides in bytes, selected per vector by sid
+    const int32_t* stripe_ids;  // optional device list: launch stripe i is stripe stripe_ids[i]
     int64_t chunks_per_stripe;
     int64_t total_chunks;
     uint64_t ptr[kMaxPtrs];   // inputs [0, cols), outputs [cols, cols+rows)

@@ -288,6 +288,17 @@ class RS:
         q, nq = _ints(needReconst)
         _check(lib().rs_reconst_batch_layout(self._h, ctypes.byref(L), S, n, s, ns, q, nq, _stream(stream)))
 
+    def reconst_batch_multi(self, data, parity, need_masks, stream=None) -> None:
+        """Per-stripe erasure patterns: need_masks[s] = bitmap of vectors of stripe s to rebuild
+        (data in [S, d, len], parity in [S, p, len]; the interleaved buffer can be passed as
+        data=buf[:, :d], parity=buf[:, d:])."""
+        L, S, n = self._split_layout(data, parity)
+        masks = np.ascontiguousarray(np.asarray(need_masks, dtype=np.uint64))
+        if masks.shape != (S,):
+            raise TypeError("need_masks must hold one mask per stripe")
+        _check(lib().rs_reconst_batch_multi(self._h, ctypes.byref(L), S, n,
+                                            masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _stream(stream)))
+
     def reconst_batch(self, buf, survived, needReconst, stream=None) -> None:
         base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
         s, ns = _ints(survived)

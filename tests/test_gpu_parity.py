@@ -486,3 +486,33 @@ def test_update_batch_distinct_strides(rslib, torch_dev):
     r.encode_batch(exp)
     torch.cuda.synchronize()
     assert torch.equal(buf, exp)
+
+
+def test_reconst_batch_multi_pattern(rslib, torch_dev):
+    """Every stripe with its own erasure set, incl. a ragged tail."""
+    torch = torch_dev
+    d, p, S, n = 10, 4, 96, 8192 + 5
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(13)
+    buf = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(buf)
+    ref = buf.clone()
+    rng = np.random.default_rng(109)
+    masks = np.zeros(S, np.uint64)
+    for s in range(S):
+        k = int(rng.integers(0, p + 1))  # 0 = stripe untouched
+        lost = rng.choice(d + p, k, replace=False)
+        for v in lost:
+            masks[s] |= np.uint64(1) << np.uint64(int(v))
+            buf[s, int(v)] = 0x5C
+    r.reconst_batch_multi(buf[:, :d], buf[:, d:], masks)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    # a pattern beyond p erasures is rejected before anything runs
+    bad = masks.copy()
+    bad[3] = np.uint64(0b11111)
+    work = ref.clone()
+    with pytest.raises(rslib.ErrTooManyLost):
+        r.reconst_batch_multi(work[:, :d], work[:, d:], bad)
+    torch.cuda.synchronize()
+    assert torch.equal(work, ref)

@@ -63,6 +63,18 @@ def main():
         rec(f"reconst 10+4 8KiB lost={len(lost)} data x{S}", S * (k + len(lost)) * vec, t)
         t1 = dev_time(lambda: r.reconst_batch(buf[:1], [], lost))
         rec(f"reconst 10+4 8KiB lost={len(lost)} data x1", (k + len(lost)) * vec, t1)
+    # ---- multi-pattern reconst: every stripe its own 1-4 erasures (16 distinct patterns)
+    import numpy as np
+
+    rng = np.random.default_rng(5)
+    pats = []
+    for _ in range(16):
+        lost = rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False)
+        pats.append(sum(1 << int(v) for v in lost))
+    masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
+    nrec = sum(bin(int(x)).count("1") for x in masks)
+    t = dev_time(lambda: r.reconst_batch_multi(buf[:, :k], buf[:, k:], masks), iters=20, warm=5)
+    rec(f"reconst_multi 10+4 8KiB 16 patterns x{S}", (S * k + nrec) * vec, t)
     # ---- update / replace 10+4 @ 8 KiB (config 5)
     old = buf[:, 3].clone()
     new = torch.randint(0, 256, (S, vec), dtype=torch.uint8, device="cuda", generator=g)
@@ -79,7 +91,7 @@ def main():
     r = rs.New(k, m)
     host = torch.empty((S, k + m, vec), dtype=torch.uint8, pin_memory=True)
     host.copy_(torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g).cpu())
-    for spc, nst in ((4, 2), (8, 3), (16, 3), (16, 4)):
+    for spc, nst in ((2, 3), (4, 3), (8, 3), (8, 4), (16, 3)):
         r.encode_host_batch(host, spc, nst)  # warm
         t0 = time.perf_counter()
         reps = 3
@@ -87,7 +99,7 @@ def main():
             r.encode_host_batch(host, spc, nst)
         t = (time.perf_counter() - t0) / reps
         rec(f"encode 10+4 1MiB x{S} host->host pinned spc={spc} streams={nst}", S * (k + m) * vec, t)
-    # PCIe reference rates
+    # PCIe reference rates (one direction at a time, then both at once)
     dbuf = torch.empty((S * k * vec,), dtype=torch.uint8, device="cuda")
     hflat = host.view(-1)[: S * k * vec]
     t0 = time.perf_counter()
@@ -98,6 +110,19 @@ def main():
     hflat.copy_(dbuf, non_blocking=True)
     torch.cuda.synchronize()
     rec("D2H pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    half = host.numel() // 2
+    ha, hb = host.view(-1)[:half], host.view(-1)[half: 2 * half]
+    da, db = torch.empty(half, dtype=torch.uint8, device="cuda"), torch.empty(half, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s1):
+        da.copy_(ha, non_blocking=True)
+    with torch.cuda.stream(s2):
+        hb.copy_(db, non_blocking=True)
+    torch.cuda.synchronize()
+    rec("H2D + D2H concurrently (torch, sum of both)", 2 * half, time.perf_counter() - t0)
+    del da, db
     # verify the pipelined parity against a device encode of the same stripes
     chk = host[:4].cuda()
     ref = chk.clone()
