@@ -29,6 +29,12 @@
 
 using namespace rsamd;
 
+#define RS_TRY(x)                 \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
+    } while (0)
+
 namespace {
 
 constexpr int kMaxVects = 256;                              // rs.go:47
@@ -320,35 +326,75 @@ int plan_reconst(const rs_t* rs, const int* survived, int ns, const int* need, i
     return RS_OK;
 }
 
-// getReconstMatrix rs.go:382-412 + makeEncMatrixForReconst matrix.go:68-79 +
-// makeReconstMatrix matrix.go:56-64.  survived_d: the first d survivors.
-int reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out) {
+// getReconstMatrixFromCache rs.go:394-412 + makeEncMatrixForReconst
+// matrix.go:68-79: inverse of the encoding-matrix rows of the first d
+// survivors, through the survivor-bitmap cache when enabled.
+int get_inverse(rs_t* rs, const int* survived_d, std::vector<uint8_t>& inv) {
     const int d = rs->d;
-    std::vector<uint8_t> inv;
     const uint64_t key = cache_key(survived_d, d);
-    bool hit = false;
     if (rs->cache_enabled) {
         std::lock_guard<std::mutex> lk(rs->cache_mu);
         auto it = rs->cache.find(key);
         if (it != rs->cache.end()) {
             inv = it->second;
-            hit = true;
+            return RS_OK;
         }
     }
-    if (!hit) {
-        std::vector<uint8_t> sub(static_cast<size_t>(d) * d);
-        for (int i = 0; i < d; ++i)
-            std::memcpy(&sub[static_cast<size_t>(i) * d], &rs->enc[static_cast<size_t>(survived_d[i]) * d], d);
-        inv.resize(sub.size());
-        int rc = invert(sub.data(), sub.size(), d, inv.data());
-        if (rc) return rc;
-        if (rs->cache_enabled && rs->cache_n.fetch_add(1) + 1 <= rs->cache_max) {
-            std::lock_guard<std::mutex> lk(rs->cache_mu);
-            rs->cache.emplace(key, inv);
-        }
+    std::vector<uint8_t> sub(static_cast<size_t>(d) * d);
+    for (int i = 0; i < d; ++i)
+        std::memcpy(&sub[static_cast<size_t>(i) * d], &rs->enc[static_cast<size_t>(survived_d[i]) * d], d);
+    inv.resize(sub.size());
+    int rc = invert(sub.data(), sub.size(), d, inv.data());
+    if (rc) return rc;
+    if (rs->cache_enabled && rs->cache_n.fetch_add(1) + 1 <= rs->cache_max) {
+        std::lock_guard<std::mutex> lk(rs->cache_mu);
+        rs->cache.emplace(key, inv);
     }
+    return RS_OK;
+}
+
+// getReconstMatrix rs.go:382-392 + makeReconstMatrix matrix.go:56-64:
+// rows `need` (data indexes) of the inverse.
+int reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out) {
+    const int d = rs->d;
+    std::vector<uint8_t> inv;
+    RS_TRY(get_inverse(rs, survived_d, inv));
     for (int i = 0; i < nn; ++i)
         std::memcpy(out + static_cast<size_t>(i) * d, &inv[static_cast<size_t>(need[i]) * d], d);
+    return RS_OK;
+}
+
+// One-pass Reconst matrix (nnr x d) over the first d survivors vs[:d]:
+//   lost data row  i : inv[i]                       (reconstData rs.go:327-349)
+//   lost parity row l: enc[l] * inv                 (reconstParity rs.go:351-373 re-encodes
+//                                                    the rebuilt data: enc[l]*(inv*S) = (enc[l]*inv)*S)
+// GF(2^8) arithmetic is exact, so the bytes equal the reference's two passes
+// (survivor data rows of inv are unit rows, reproducing those survivors).
+// With no data lost, vs[:d] = 0..d-1, inv = I and no inverse is computed
+// (as in the reference, which then only runs reconstParity).
+int combined_matrix(rs_t* rs, const int* vs, const int* nr, int nnr, int dn, std::vector<uint8_t>& m) {
+    const int d = rs->d;
+    m.assign(static_cast<size_t>(nnr) * d, 0);
+    std::vector<uint8_t> inv;
+    if (dn > 0) RS_TRY(get_inverse(rs, vs, inv));
+    const auto& T = gf();
+    for (int r = 0; r < nnr; ++r) {
+        uint8_t* row = &m[static_cast<size_t>(r) * d];
+        const int v = nr[r];
+        if (v < d) {
+            std::memcpy(row, &inv[static_cast<size_t>(v) * d], d);
+        } else if (dn == 0) {
+            std::memcpy(row, &rs->enc[static_cast<size_t>(v) * d], d);
+        } else {
+            const uint8_t* e = &rs->enc[static_cast<size_t>(v) * d];
+            for (int t = 0; t < d; ++t) {
+                if (!e[t]) continue;
+                const uint8_t* mt = T.mul[e[t]];
+                const uint8_t* ir = &inv[static_cast<size_t>(t) * d];
+                for (int c = 0; c < d; ++c) row[c] ^= mt[ir[c]];
+            }
+        }
+    }
     return RS_OK;
 }
 
@@ -395,12 +441,6 @@ std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr) {  
     return m;
 }
 
-std::vector<uint8_t> enc_rows(const rs_t* rs, const int* rows, int nrows) {  // reconstParity rs.go:359-362
-    std::vector<uint8_t> m(static_cast<size_t>(nrows) * rs->d);
-    for (int i = 0; i < nrows; ++i)
-        std::memcpy(&m[static_cast<size_t>(i) * rs->d], &rs->enc[static_cast<size_t>(rows[i]) * rs->d], rs->d);
-    return m;
-}
 
 // ---------------------------------------------------------------- host staging
 
@@ -433,11 +473,6 @@ int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
 }
 int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE; }
 
-#define RS_TRY(x)                 \
-    do {                          \
-        int rc_ = (x);            \
-        if (rc_) return rc_;      \
-    } while (0)
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -450,6 +485,30 @@ struct ReconstPlan {
     int vs[kMaxVects], nr[kMaxVects];
     int nvs = 0, nnr = 0, dn = 0;
 };
+
+// The reference's two passes check their own argument sizes in order
+// (reconstData, then reconstParity after the data is rebuilt).  Returns the
+// data-pass check result and, through *parity_rc, the parity-pass one.
+int check_reconst_passes(const rs_t* rs, const ReconstPlan& pl, const size_t* lens, int n, int* parity_rc) {
+    const int d = rs->d, pn = pl.nnr - pl.dn;
+    int idx[2 * kMaxVects];
+    *parity_rc = RS_OK;
+    if (pl.dn > 0) {
+        for (int i = 0; i < d; ++i) idx[i] = pl.vs[i];
+        for (int i = 0; i < pl.dn; ++i) idx[d + i] = pl.nr[i];
+        for (int i = 0; i < d + pl.dn; ++i)
+            if (idx[i] >= n) return RS_ERR_INVAL;  // the reference indexes past len(vects) and panics
+        RS_TRY(check_encode_idx(lens, idx, d + pl.dn));
+    }
+    if (pn > 0) {
+        for (int i = 0; i < d; ++i) idx[i] = i;
+        for (int i = 0; i < pn; ++i) idx[d + i] = pl.nr[pl.dn + i];
+        for (int i = 0; i < d + pn && *parity_rc == RS_OK; ++i)
+            if (idx[i] >= n) *parity_rc = RS_ERR_INVAL;
+        if (*parity_rc == RS_OK) *parity_rc = check_encode_idx(lens, idx, d + pn);
+    }
+    return RS_OK;
+}
 
 }  // namespace
 
@@ -628,58 +687,32 @@ int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const
     int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
     if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;  // rs.go:225-228
     if (rc) return rc;
-    const int d = rs->d, pn = pl.nnr - pl.dn;
     if (!vects || !lens) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    std::lock_guard<std::mutex> lk(rs->stage_mu);
-    size_t pitch = 0;
-    bool staged_data = false;
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    auto slot = [&](int v) { return rs->stage + static_cast<size_t>(v) * pitch; };
-
-    if (pl.dn > 0) {  // reconstData rs.go:327-349
-        int idx[2 * kMaxVects];
-        for (int i = 0; i < d; ++i) idx[i] = pl.vs[i];
-        for (int i = 0; i < pl.dn; ++i) idx[d + i] = pl.nr[i];
-        for (int i = 0; i < d + pl.dn; ++i)
-            if (idx[i] >= n) return RS_ERR_INVAL;
-        RS_TRY(check_encode_idx(lens, idx, d + pl.dn));
-        const size_t size = lens[idx[0]];
-        std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
-        RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
-        RS_TRY(ensure_stage(rs, rs->d + rs->p, size, &pitch));
+    const int d = rs->d;
+    int parity_rc = RS_OK;
+    RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
+    const int rows = parity_rc ? pl.dn : pl.nnr;  // see rs_reconst_dev
+    if (rows > 0) {
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        std::lock_guard<std::mutex> lk(rs->stage_mu);
+        const size_t size = lens[pl.vs[0]];
+        size_t pitch = 0;
+        RS_TRY(ensure_stage(rs, d + rows, size, &pitch));
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
         for (int i = 0; i < d; ++i) {
-            RS_TRY(h2d(rs, slot(pl.vs[i]), vects[pl.vs[i]], size));
-            in[i] = slot(pl.vs[i]);
+            in[i] = rs->stage + static_cast<size_t>(i) * pitch;
+            RS_TRY(h2d(rs, rs->stage + static_cast<size_t>(i) * pitch, vects[pl.vs[i]], size));
         }
-        for (int i = 0; i < pl.dn; ++i) out[i] = slot(pl.nr[i]);
-        RS_TRY(matmul(rs, gm.data(), pl.dn, d, in, 0, out, 0, 1, size, false, rs->stream));
-        for (int i = 0; i < pl.dn; ++i) RS_TRY(d2h(rs, vects[pl.nr[i]], out[i], size));
-        RS_TRY(sync(rs));
-        staged_data = true;
-    }
-    if (pn > 0) {  // reconstParity rs.go:351-373
-        int idx[2 * kMaxVects];
-        for (int i = 0; i < d; ++i) idx[i] = i;
-        for (int i = 0; i < pn; ++i) idx[d + i] = pl.nr[pl.dn + i];
-        for (int i = 0; i < d + pn; ++i)
-            if (idx[i] >= n) return RS_ERR_INVAL;
-        RS_TRY(check_encode_idx(lens, idx, d + pn));
-        const size_t size = lens[0];
-        std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
-        if (!staged_data || rup(size, 256) != pitch) {
-            RS_TRY(ensure_stage(rs, rs->d + rs->p, size, &pitch));
-            for (int i = 0; i < d; ++i) RS_TRY(h2d(rs, slot(i), vects[i], size));
-        }
-        for (int i = 0; i < d; ++i) in[i] = slot(i);
-        for (int i = 0; i < pn; ++i) out[i] = slot(pl.nr[pl.dn + i]);
-        RS_TRY(matmul(rs, gm.data(), pn, d, in, 0, out, 0, 1, size, false, rs->stream));
-        for (int i = 0; i < pn; ++i) RS_TRY(d2h(rs, vects[pl.nr[pl.dn + i]], out[i], size));
+        for (int i = 0; i < rows; ++i) out[i] = rs->stage + static_cast<size_t>(d + i) * pitch;
+        std::vector<uint8_t> m;
+        RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
+        RS_TRY(matmul(rs, m.data(), rows, d, in, 0, out, 0, 1, size, false, rs->stream));
+        for (int i = 0; i < rows; ++i) RS_TRY(d2h(rs, vects[pl.nr[i]], out[i], size));
         RS_TRY(sync(rs));
     }
-    return RS_OK;
+    return parity_rc;
 }
 
 int rs_reconst_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
@@ -690,37 +723,24 @@ int rs_reconst_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, c
     if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
     if (rc) return rc;
     if (!vects || !lens) return RS_ERR_INVAL;
-    const int d = rs->d, pn = pl.nnr - pl.dn;
+    const int d = rs->d;
+    int parity_rc = RS_OK;
+    RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
-    if (pl.dn > 0) {
-        int idx[2 * kMaxVects];
-        for (int i = 0; i < d; ++i) idx[i] = pl.vs[i];
-        for (int i = 0; i < pl.dn; ++i) idx[d + i] = pl.nr[i];
-        for (int i = 0; i < d + pl.dn; ++i)
-            if (idx[i] >= n) return RS_ERR_INVAL;
-        RS_TRY(check_encode_idx(lens, idx, d + pl.dn));
-        std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
-        RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
-        for (int i = 0; i < d; ++i) in[i] = vects[pl.vs[i]];
-        for (int i = 0; i < pl.dn; ++i) out[i] = vects[pl.nr[i]];
-        RS_TRY(matmul(rs, gm.data(), pl.dn, d, in, 0, out, 0, 1, lens[idx[0]], false, as_stream(stream)));
+    for (int i = 0; i < d; ++i) in[i] = vects[pl.vs[i]];
+    // Parity pass would fail its checks: rebuild the data only, then report
+    // the parity-pass error (the reference's order).  Otherwise one pass.
+    const int rows = parity_rc ? pl.dn : pl.nnr;
+    if (rows > 0) {
+        std::vector<uint8_t> m;
+        RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
+        for (int i = 0; i < rows; ++i) out[i] = vects[pl.nr[i]];
+        RS_TRY(matmul(rs, m.data(), rows, d, in, 0, out, 0, 1, lens[pl.vs[0]], false, as_stream(stream)));
     }
-    if (pn > 0) {
-        int idx[2 * kMaxVects];
-        for (int i = 0; i < d; ++i) idx[i] = i;
-        for (int i = 0; i < pn; ++i) idx[d + i] = pl.nr[pl.dn + i];
-        for (int i = 0; i < d + pn; ++i)
-            if (idx[i] >= n) return RS_ERR_INVAL;
-        RS_TRY(check_encode_idx(lens, idx, d + pn));
-        std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
-        for (int i = 0; i < d; ++i) in[i] = vects[i];
-        for (int i = 0; i < pn; ++i) out[i] = vects[pl.nr[pl.dn + i]];
-        RS_TRY(matmul(rs, gm.data(), pn, d, in, 0, out, 0, 1, lens[0], false, as_stream(stream)));
-    }
-    return RS_OK;
+    return parity_rc;
 }
 
 int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const int* survived, int ns,
@@ -733,40 +753,26 @@ int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* L, int nstripes, size_t
     if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
     if (nstripes == 0) return RS_OK;
     if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
-    const int d = rs->d, pn = pl.nnr - pl.dn;
+    const int d = rs->d;
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
+    // One pass: every lost vector from the first d survivors (combined_matrix).
+    std::vector<uint8_t> m;
+    RS_TRY(combined_matrix(rs, pl.vs, pl.nr, pl.nnr, pl.dn, m));
     const LayoutAddr A{L, d};
     const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
     uint8_t isid[kMaxVects], osid[kMaxVects];  // stride selectors (copied into the dword kernel array)
-    if (pl.dn > 0) {  // reconstData rs.go:327-349: inputs = first d survivors (data or parity)
-        std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
-        RS_TRY(reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data()));
-        for (int i = 0; i < d; ++i) {
-            in[i] = A.ptr(pl.vs[i]);
-            isid[i] = A.sid(pl.vs[i]);
-        }
-        for (int i = 0; i < pl.dn; ++i) {
-            out[i] = A.ptr(pl.nr[i]);
-            osid[i] = A.sid(pl.nr[i]);
-        }
-        RS_TRY(matmul_ex(rs, gm.data(), pl.dn, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream)));
+    for (int i = 0; i < d; ++i) {
+        in[i] = A.ptr(pl.vs[i]);
+        isid[i] = A.sid(pl.vs[i]);
     }
-    if (pn > 0) {  // reconstParity rs.go:351-373: inputs = all data vectors
-        std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
-        for (int i = 0; i < d; ++i) {
-            in[i] = A.ptr(i);
-            isid[i] = 0;
-        }
-        for (int i = 0; i < pn; ++i) {
-            out[i] = A.ptr(pl.nr[pl.dn + i]);
-            osid[i] = 1;
-        }
-        RS_TRY(matmul_ex(rs, gm.data(), pn, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream)));
+    for (int i = 0; i < pl.nnr; ++i) {
+        out[i] = A.ptr(pl.nr[i]);
+        osid[i] = A.sid(pl.nr[i]);
     }
-    return RS_OK;
+    return matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream));
 }
 
 int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
@@ -828,40 +834,22 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
     uint8_t isid[kMaxVects], osid[kMaxVects];
-    for (const Group& gr : plan) {
+    for (const Group& gr : plan) {  // one launch per distinct pattern (combined_matrix)
         if (rc) break;
         const ReconstPlan& pl = gr.pl;
-        const int pn = pl.nnr - pl.dn;
-        const int32_t* gids = dids + gr.off;
-        if (pl.dn > 0) {
-            std::vector<uint8_t> gm(static_cast<size_t>(pl.dn) * d);
-            rc = reconst_matrix(rs, pl.vs, pl.nr, pl.dn, gm.data());
-            if (rc) break;
-            for (int i = 0; i < d; ++i) {
-                in[i] = A.ptr(pl.vs[i]);
-                isid[i] = A.sid(pl.vs[i]);
-            }
-            for (int i = 0; i < pl.dn; ++i) {
-                out[i] = A.ptr(pl.nr[i]);
-                osid[i] = A.sid(pl.nr[i]);
-            }
-            rc = matmul_ex(rs, gm.data(), pl.dn, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
-                           gids);
-            if (rc) break;
+        std::vector<uint8_t> m;
+        rc = combined_matrix(rs, pl.vs, pl.nr, pl.nnr, pl.dn, m);
+        if (rc) break;
+        for (int i = 0; i < d; ++i) {
+            in[i] = A.ptr(pl.vs[i]);
+            isid[i] = A.sid(pl.vs[i]);
         }
-        if (pn > 0) {
-            std::vector<uint8_t> gm = enc_rows(rs, pl.nr + pl.dn, pn);
-            for (int i = 0; i < d; ++i) {
-                in[i] = A.ptr(i);
-                isid[i] = 0;
-            }
-            for (int i = 0; i < pn; ++i) {
-                out[i] = A.ptr(pl.nr[pl.dn + i]);
-                osid[i] = 1;
-            }
-            rc = matmul_ex(rs, gm.data(), pn, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
-                           gids);
+        for (int i = 0; i < pl.nnr; ++i) {
+            out[i] = A.ptr(pl.nr[i]);
+            osid[i] = A.sid(pl.nr[i]);
         }
+        rc = matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
+                       dids + gr.off);
     }
     (void)hipFreeAsync(dids, st);
     return rc;
