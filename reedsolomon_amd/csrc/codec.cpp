@@ -147,6 +147,8 @@ struct rs_codec {
     std::mutex stage_mu;  // staging for the host-memory entry points
     uint8_t* stage = nullptr;
     size_t stage_bytes = 0;
+    uint8_t* hstage = nullptr;  // pinned host mirror of `stage` (small-vector fast path)
+    size_t hstage_bytes = 0;
     hipStream_t stream = nullptr;
 
     const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
@@ -158,6 +160,7 @@ struct rs_codec {
         (void)hipDeviceSynchronize();
         for (auto& kv : tables) (void)hipFree(kv.second);
         if (stage) (void)hipFree(stage);
+        if (hstage) (void)hipHostFree(hstage);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -465,6 +468,32 @@ int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
     return RS_OK;
 }
 
+// Vectors up to this size go through the pinned host mirror: the caller's
+// bytes are memcpy'd into pinned memory and each direction is ONE DMA over
+// contiguous slots, instead of one pageable copy (staged by the runtime) per
+// vector.  Larger vectors use the runtime's pipelined pageable copies.
+size_t g_pinned_max = 256 * 1024;
+
+bool use_pinned(rs_t* rs, int slots, size_t pitch) {
+    if (pitch > g_pinned_max) return false;
+    const size_t need = pitch * static_cast<size_t>(slots);
+    if (need <= rs->hstage_bytes) return true;
+    if (rs->hstage) {
+        (void)hipStreamSynchronize(rs->stream);
+        (void)hipHostFree(rs->hstage);
+        rs->hstage = nullptr;
+        rs->hstage_bytes = 0;
+    }
+    if (hipHostMalloc(reinterpret_cast<void**>(&rs->hstage), need, hipHostMallocDefault) != hipSuccess) return false;
+    rs->hstage_bytes = need;
+    return true;
+}
+
+// Host vectors src[0..n) (size bytes each) -> device staging slots
+// [first, first+n).  Caller holds stage_mu and called ensure_stage.
+int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots);
+int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots);
+
 int h2d(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
     return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
 }
@@ -472,6 +501,33 @@ int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
     return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
 }
 int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE; }
+
+int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots) {
+    if (n <= 0) return RS_OK;
+    uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
+    if (use_pinned(rs, total_slots, pitch)) {
+        uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
+        for (int i = 0; i < n; ++i) std::memcpy(h + static_cast<size_t>(i) * pitch, src[i], size);
+        return h2d(rs, dev, h, static_cast<size_t>(n - 1) * pitch + size);
+    }
+    for (int i = 0; i < n; ++i) RS_TRY(h2d(rs, dev + static_cast<size_t>(i) * pitch, src[i], size));
+    return RS_OK;
+}
+
+// Device staging slots [first, first+n) -> host vectors dst[0..n); synchronous.
+int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots) {
+    if (n <= 0) return sync(rs);
+    const uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
+    if (use_pinned(rs, total_slots, pitch)) {
+        uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
+        RS_TRY(d2h(rs, h, dev, static_cast<size_t>(n - 1) * pitch + size));
+        RS_TRY(sync(rs));
+        for (int i = 0; i < n; ++i) std::memcpy(dst[i], h + static_cast<size_t>(i) * pitch, size);
+        return RS_OK;
+    }
+    for (int i = 0; i < n; ++i) RS_TRY(d2h(rs, dst[i], dev + static_cast<size_t>(i) * pitch, size));
+    return sync(rs);
+}
 
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -593,6 +649,7 @@ int rs_tune(const char* name, int value) {
     else if (n == "nt_store") t.nt_store = value;
     else if (n == "var") t.var = value;
     else if (n == "lds_pad") t.lds_pad = value;
+    else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
     else return RS_ERR_INVAL;
     return RS_OK;
 }
@@ -638,14 +695,11 @@ int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
     RS_TRY(ensure_stage(rs, d + p, size, &pitch));
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
-    for (int i = 0; i < d; ++i) {
-        RS_TRY(h2d(rs, rs->stage + i * pitch, vects[i], size));
-        in[i] = rs->stage + i * pitch;
-    }
+    for (int i = 0; i < d; ++i) in[i] = rs->stage + i * pitch;
     for (int j = 0; j < p; ++j) out[j] = rs->stage + (d + j) * pitch;
+    RS_TRY(stage_in(rs, vects, d, size, pitch, 0, d + p));
     RS_TRY(matmul(rs, rs->gen(), p, d, in, 0, out, 0, 1, size, false, rs->stream));
-    for (int j = 0; j < p; ++j) RS_TRY(d2h(rs, vects[d + j], out[j], size));
-    return sync(rs);
+    return stage_out(rs, vects + d, p, size, pitch, d, d + p);
 }
 
 int rs_encode_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, void* stream) {
@@ -701,16 +755,21 @@ int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const
         RS_TRY(ensure_stage(rs, d + rows, size, &pitch));
         const uint8_t* in[kMaxVects];
         uint8_t* out[kMaxVects];
+        const uint8_t* src[kMaxVects];
+        uint8_t* dst[kMaxVects];
         for (int i = 0; i < d; ++i) {
             in[i] = rs->stage + static_cast<size_t>(i) * pitch;
-            RS_TRY(h2d(rs, rs->stage + static_cast<size_t>(i) * pitch, vects[pl.vs[i]], size));
+            src[i] = vects[pl.vs[i]];
         }
-        for (int i = 0; i < rows; ++i) out[i] = rs->stage + static_cast<size_t>(d + i) * pitch;
+        for (int i = 0; i < rows; ++i) {
+            out[i] = rs->stage + static_cast<size_t>(d + i) * pitch;
+            dst[i] = vects[pl.nr[i]];
+        }
         std::vector<uint8_t> m;
         RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
+        RS_TRY(stage_in(rs, src, d, size, pitch, 0, d + rows));
         RS_TRY(matmul(rs, m.data(), rows, d, in, 0, out, 0, 1, size, false, rs->stream));
-        for (int i = 0; i < rows; ++i) RS_TRY(d2h(rs, vects[pl.nr[i]], out[i], size));
-        RS_TRY(sync(rs));
+        RS_TRY(stage_out(rs, dst, rows, size, pitch, d, d + rows));
     }
     return parity_rc;
 }
@@ -871,16 +930,15 @@ int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* 
     RS_TRY(ensure_stage(rs, 2 + p, size, &pitch));
     const uint8_t* in[2] = {rs->stage, rs->stage + pitch};
     uint8_t* out[kMaxVects];
-    RS_TRY(h2d(rs, rs->stage, old_data, size));
-    RS_TRY(h2d(rs, rs->stage + pitch, new_data, size));
-    for (int j = 0; j < p; ++j) {
-        out[j] = rs->stage + (2 + j) * pitch;
-        RS_TRY(h2d(rs, out[j], parity[j], size));
-    }
+    for (int j = 0; j < p; ++j) out[j] = rs->stage + (2 + j) * pitch;
+    const uint8_t* src[kMaxVects + 2];
+    src[0] = old_data;
+    src[1] = new_data;
+    for (int j = 0; j < p; ++j) src[2 + j] = parity[j];
+    RS_TRY(stage_in(rs, src, 2 + p, size, pitch, 0, 2 + p));
     std::vector<uint8_t> gm = update_matrix(rs, row);
     RS_TRY(matmul(rs, gm.data(), p, 2, in, 0, out, 0, 1, size, true, rs->stream));
-    for (int j = 0; j < p; ++j) RS_TRY(d2h(rs, parity[j], out[j], size));
-    return sync(rs);
+    return stage_out(rs, parity, p, size, pitch, 2, 2 + p);
 }
 
 int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
@@ -935,18 +993,19 @@ int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, in
     RS_TRY(ensure_stage(rs, nd + p, size, &pitch));
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
+    const uint8_t* src[2 * kMaxVects];
     for (int i = 0; i < nd; ++i) {
         in[i] = rs->stage + i * pitch;
-        RS_TRY(h2d(rs, rs->stage + i * pitch, data[i], size));
+        src[i] = data[i];
     }
     for (int j = 0; j < p; ++j) {
         out[j] = rs->stage + (nd + j) * pitch;
-        RS_TRY(h2d(rs, out[j], parity[j], size));
+        src[nd + j] = parity[j];
     }
+    RS_TRY(stage_in(rs, src, nd + p, size, pitch, 0, nd + p));
     std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
     RS_TRY(matmul(rs, gm.data(), p, nr, in, 0, out, 0, 1, size, true, rs->stream));
-    for (int j = 0; j < p; ++j) RS_TRY(d2h(rs, parity[j], out[j], size));
-    return sync(rs);
+    return stage_out(rs, parity, p, size, pitch, nd, nd + p);
 }
 
 int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows,

@@ -132,18 +132,23 @@ def main():
     # ---- host-memory Go-API calls (pageable numpy buffers), per-call latency
     import numpy as np
 
-    for vec in (8 << 10, 1 << 20):
-        rng = np.random.default_rng(1)
-        v = [rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] + [np.zeros(vec, np.uint8)
-                                                                             for _ in range(m)]
-        for _ in range(5):
-            r.Encode(v)
-        n = 50 if vec > 65536 else 500
-        t0 = time.perf_counter()
-        for _ in range(n):
-            r.Encode(v)
-        t = (time.perf_counter() - t0) / n
-        rec(f"Encode() host API pageable 10+4 {vec >> 10}KiB", (k + m) * vec, t)
+    L = rs.lib()
+    for pinned_max in (256 << 10, 4 << 20, 0):
+        L.rs_tune(b"host_pinned_max", pinned_max)
+        for vec in (8 << 10, 64 << 10, 256 << 10, 1 << 20):
+            rng = np.random.default_rng(1)
+            v = [rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] + [np.zeros(vec, np.uint8)
+                                                                                 for _ in range(m)]
+            for _ in range(5):
+                r.Encode(v)
+            n = 50 if vec > 65536 else 500
+            t0 = time.perf_counter()
+            for _ in range(n):
+                r.Encode(v)
+            t = (time.perf_counter() - t0) / n
+            rec(f"Encode() host API 10+4 {vec >> 10}KiB (pinned staging <= {pinned_max >> 10}KiB)",
+                (k + m) * vec, t)
+    L.rs_tune(b"host_pinned_max", 256 << 10)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ops_bench.json"), "w"), indent=1)
 
