@@ -222,6 +222,16 @@ RS_API int rs_gf_matmul_batch(rs_t* rs, const uint8_t* mat, int rows, int cols,
                        const int* out_map,
                        int nstripes, size_t len, int accumulate, void* stream);
 
+/* XOR of vectors (templexxx/xorsimd xor.Encode(dst, src), used by Update
+ * rs.go:432-433 and by templexxx/xrs): dst = src[0] ^ src[1] ^ ... for every
+ * stripe.  Vector c of stripe s at src_base + s*src_stripe_stride +
+ * c*src_vect_stride; dst at dst_base + s*dst_stripe_stride.  Runs as the
+ * GF(2^8) product with an all-ones 1 x nsrc matrix (multiplication by 1 is the
+ * identity table), so it shares the tuned kernel. */
+RS_API int rs_xor_batch(rs_t* rs, const uint8_t* src_base, int64_t src_stripe_stride, int64_t src_vect_stride,
+                        int nsrc, uint8_t* dst_base, int64_t dst_stripe_stride, int nstripes, size_t len,
+                        void* stream);
+
 /* ------------------------------------------------------------------------
  * Host-side planning helpers (no device work; exported for tests and for
  * callers that batch many erasure patterns themselves).

@@ -68,6 +68,7 @@ SIGNATURES = {
     "rs_encode_host_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_int, c_int]),
     "rs_host_register": (c_int, [c_void, c_sz]),
     "rs_host_unregister": (c_int, [c_void]),
+    "rs_xor_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_void, c_i64, c_int, c_sz, c_void]),
     "rs_gf_matmul_batch": (c_int, [c_void, c_u8p, c_int, c_int, c_void, c_i64, c_i64, c_intp, c_void, c_i64,
                                    c_i64, c_intp, c_int, c_sz, c_int, c_void]),
     "rs_plan_reconst": (c_int, [c_void, c_intp, c_int, c_intp, c_int, c_intp, c_intp, c_intp, c_intp, c_intp]),

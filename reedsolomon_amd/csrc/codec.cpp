@@ -882,6 +882,69 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
     hipStream_t st = as_stream(stream);
+
+    // Single launch over all stripes when every pattern has <= 4 outputs and
+    // the layout takes the 16-byte vector path; otherwise one launch per
+    // pattern over a stripe-id list (below).
+    bool single = len % 16 == 0 && len < (size_t{1} << 31);
+    for (const Group& gr : plan) single = single && gr.pl.nnr <= 4;
+    for (int v = 0; v < d + p && single; ++v)
+        single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
+    single = single && (L->data_stripe_stride & 15) == 0 && (L->parity_stripe_stride & 15) == 0;
+    if (single) {
+        const int npat = static_cast<int>(plan.size());
+        const int tdw = multi_table_dwords(d);
+        const size_t tab_bytes = static_cast<size_t>(npat) * tdw * 4;
+        const size_t desc_bytes = static_cast<size_t>(npat) * sizeof(PatternDesc);
+        const size_t pat_bytes = static_cast<size_t>(nstripes) * 4;
+        std::vector<uint8_t> host(tab_bytes + desc_bytes + pat_bytes, 0);
+        uint32_t* tabs = reinterpret_cast<uint32_t*>(host.data());
+        PatternDesc* descs = reinterpret_cast<PatternDesc*>(host.data() + tab_bytes);
+        int32_t* spat = reinterpret_cast<int32_t*>(host.data() + tab_bytes + desc_bytes);
+        for (int s = 0; s < nstripes; ++s) spat[s] = -1;
+        for (int gi = 0; gi < npat; ++gi) {
+            const Group& gr = plan[gi];
+            std::vector<uint8_t> m;
+            RS_TRY(combined_matrix(rs, gr.pl.vs, gr.pl.nr, gr.pl.nnr, gr.pl.dn, m));
+            uint32_t* img = tabs + static_cast<size_t>(gi) * tdw;
+            for (int i = 0; i < d; ++i)
+                for (int r = 0; r < gr.pl.nnr; ++r) perm_table(m[static_cast<size_t>(r) * d + i], img + i * 20 + r * 5);
+            PatternDesc& pd = descs[gi];
+            pd.tab_off = static_cast<uint32_t>(gi * tdw);
+            pd.nout = static_cast<uint32_t>(gr.pl.nnr);
+            for (int i = 0; i < d; ++i) pd.in_idx[i] = static_cast<uint32_t>(gr.pl.vs[i]);
+            for (int r = 0; r < gr.pl.nnr; ++r) pd.out_idx[r] = static_cast<uint32_t>(gr.pl.nr[r]);
+            for (size_t t = 0; t < gr.n; ++t) spat[ids[gr.off + t]] = gi;
+        }
+        uint8_t* dev = nullptr;
+        if (hipMallocAsync(reinterpret_cast<void**>(&dev), host.size(), st) != hipSuccess) return RS_ERR_DEVICE;
+        int rc = hipMemcpyAsync(dev, host.data(), host.size(), hipMemcpyHostToDevice, st) == hipSuccess
+                     ? RS_OK
+                     : RS_ERR_DEVICE;
+        if (rc == RS_OK) {
+            MatmulArgs a;
+            std::memset(&a, 0, sizeof a);
+            a.tables = reinterpret_cast<const uint32_t*>(dev);
+            a.rows = 4;
+            a.cols = d;
+            a.nstripes = nstripes;
+            a.len = len;
+            a.ss[0] = L->data_stripe_stride;
+            a.ss[1] = L->parity_stripe_stride;
+            const LayoutAddr A{L, d};
+            for (int v = 0; v < d + p; ++v) {
+                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
+                a.sid[v] = A.sid(v);
+            }
+            rc = launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
+                                 reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st) == hipSuccess
+                     ? RS_OK
+                     : RS_ERR_DEVICE;
+        }
+        (void)hipFreeAsync(dev, st);
+        return rc;
+    }
+
     int32_t* dids = nullptr;
     if (hipMallocAsync(reinterpret_cast<void**>(&dids), ids.size() * sizeof(int32_t), st) != hipSuccess)
         return RS_ERR_DEVICE;
@@ -1142,6 +1205,24 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             if (e) (void)hipEventDestroy(e);
     (void)hipFree(ring);
     return rc;
+}
+
+// ---------------------------------------------------------------- XOR primitive
+
+int rs_xor_batch(rs_t* rs, const uint8_t* src_base, int64_t src_stripe_stride, int64_t src_vect_stride, int nsrc,
+                 uint8_t* dst_base, int64_t dst_stripe_stride, int nstripes, size_t len, void* stream) {
+    if (!rs || nsrc <= 0 || nsrc + 1 > kMaxPtrs || nstripes < 0) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (nstripes == 0) return RS_OK;
+    if (!src_base || !dst_base) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    std::vector<uint8_t> ones(static_cast<size_t>(nsrc), 1);
+    const uint8_t* in[kMaxPtrs];
+    for (int c = 0; c < nsrc; ++c) in[c] = src_base + c * src_vect_stride;
+    uint8_t* out[1] = {dst_base};
+    return matmul(rs, ones.data(), 1, nsrc, in, src_stripe_stride, out, dst_stripe_stride, nstripes, len, false,
+                  as_stream(stream));
 }
 
 // ---------------------------------------------------------------- generic product

@@ -142,13 +142,147 @@ __device__ __forceinline__ void store16(g_u8* base, uint64_t off, uint32_t nbyte
 // global_load/store nt on the 10+4 @ 1 MiB x 256 launch.
 constexpr int kAuxNt = 2;
 
+// One workgroup-chunk of the product: the lane's 16*VPT-byte slice of every
+// input column in, of every output row (up to MC) out.  `in_base(c)` /
+// `out_base(r)` give the stripe base address of input column c / output row
+// r (wave-uniform); the LDS holds this launch's (or this pattern's) tables.
 //   WIN  0: issue all KB column loads up front; >0: rolling window of WIN
 //        columns in flight per lane (fewer VGPRs, more resident waves)
+template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR, int LAUX, int SAUX, int WIN, class InBase,
+          class OutBase>
+__device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4* lds_tab, int cols, int ncols_pad,
+                                           int nrows, int64_t cb, uint64_t nunits, InBase in_base,
+                                           OutBase out_base) {
+    constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
+    constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
+    const int tid = threadIdx.x;
+    uint64_t off[VPT];
+    bool ok[VPT];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+        const uint64_t u = static_cast<uint64_t>(cb) * a.units_per_chunk + v * kBlock + tid;
+        ok[v] = u < nunits;
+        off[v] = (ok[v] ? u : 0) * 16;  // clamp: out-of-range lanes read unit 0, store nothing
+    }
+
+    uint32_t acc[MC][VPT][4];
+#pragma unroll
+    for (int r = 0; r < MC; ++r)
+#pragma unroll
+        for (int v = 0; v < VPT; ++v)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][v][q] = 0;
+    if (ACC) {
+#pragma unroll
+        for (int r = 0; r < MC; ++r)
+            if (r < nrows)
+#pragma unroll
+                for (int v = 0; v < VPT; ++v) {
+                    const u32x4 o = load16<LAUX>(out_base(r), off[v], static_cast<uint32_t>(a.body), false);
+                    acc[r][v][0] = o.x; acc[r][v][1] = o.y; acc[r][v][2] = o.z; acc[r][v][3] = o.w;
+                }
+    }
+
+    for (int i0 = 0; i0 < ncols_pad; i0 += KB) {
+        // Issue the column loads of this batch first (KB*16*VPT bytes in flight
+        // per lane), or the first WIN of them with the rest rolled in below.
+        constexpr int kFirst = (WIN > 0 && WIN < KB) ? WIN : KB;
+        u32x4 x[KB][VPT];
+        auto load_col = [&](int b) {
+            int c = i0 + b;
+            if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
+            const g_u8* p = in_base(c);
+#pragma unroll
+            for (int v = 0; v < VPT; ++v)
+                x[b][v] = load16<LAUX>(p, off[v], static_cast<uint32_t>(a.body), (VAR & kVarNtLoad) != 0);
+        };
+#pragma unroll
+        for (int b = 0; b < kFirst; ++b) load_col(b);
+        // Tables of column b+1 are read from LDS while column b is computed.
+        constexpr bool kPrefetchTab = !(VAR & kVarSingleTab);
+        u32x4 tv[2][COLW];
+        if (kPrefetchTab) {
+#pragma unroll
+            for (int w = 0; w < COLW; ++w) tv[0][w] = lds_tab[i0 * COLW + w];
+        }
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            // Scheduling fence: keeps each column's LDS reads next to its math
+            // (hoisted, all k*MC tables would pin ~200 VGPRs: one wave/SIMD).
+            __builtin_amdgcn_sched_barrier(0);
+            if (kPrefetchTab) {
+                if (b + 1 < KB) {
+#pragma unroll
+                    for (int w = 0; w < COLW; ++w) tv[(b + 1) & 1][w] = lds_tab[(i0 + b + 1) * COLW + w];
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < COLW; ++w) tv[b & 1][w] = lds_tab[(i0 + b) * COLW + w];
+            }
+            uint32_t t[COLD];
+#pragma unroll
+            for (int w = 0; w < COLW; ++w) {
+                t[4 * w + 0] = tv[b & 1][w].x; t[4 * w + 1] = tv[b & 1][w].y;
+                t[4 * w + 2] = tv[b & 1][w].z; t[4 * w + 3] = tv[b & 1][w].w;
+            }
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                const uint32_t xs[4] = {x[b][v].x, x[b][v].y, x[b][v].z, x[b][v].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (VAR & kVarXorOnly) {
+#pragma unroll
+                        for (int r = 0; r < MC; ++r) acc[r][v][q] ^= xs[q] ^ t[r * 5];
+                        continue;
+                    }
+                    uint32_t g0, g1, g2;
+                    split_groups(xs[q], g0, g1, g2);
+#pragma unroll
+                    for (int r = 0; r < MC; ++r) {
+                        const uint32_t* tr = &t[r * 5];
+                        if (VAR & kVarBitop3) {
+                            const uint32_t p0 = __builtin_amdgcn_perm(tr[1], tr[0], g0);
+                            const uint32_t p1 = __builtin_amdgcn_perm(tr[3], tr[2], g1);
+                            const uint32_t p2 = __builtin_amdgcn_perm(tr[4], tr[4], g2);
+                            acc[r][v][q] = xor3(xor3(acc[r][v][q], p0, p1), p2, 0);
+                        } else {
+                            acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, tr);
+                        }
+                    }
+                }
+            }
+            // Pin the running sums per column: stops LLVM from reassociating
+            // the XOR chains across columns (which keeps every column's
+            // partial products live and spills to AGPRs).
+#pragma unroll
+            for (int r = 0; r < MC; ++r)
+#pragma unroll
+                for (int v = 0; v < VPT; ++v)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(acc[r][v][q]));
+            if (b + kFirst < KB) load_col(b + kFirst);  // rolling window refill
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+#pragma unroll
+    for (int r = 0; r < MC; ++r) {
+        if (r < nrows) {
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+                if (!ok[v]) continue;
+                u32x4 val;
+                val.x = acc[r][v][0]; val.y = acc[r][v][1]; val.z = acc[r][v][2]; val.w = acc[r][v][3];
+                store16<SAUX>(out_base(r), off[v], static_cast<uint32_t>(a.body), val, a.nt_store != 0);
+            }
+        }
+    }
+}
+
 template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR = kVarDefault, int LAUX = kAuxNt, int SAUX = kAuxNt,
           int WIN = 0>
 __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
-    constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
-    constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
+    constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
     const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
 
@@ -176,131 +310,41 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
             const int si = static_cast<int>(chunk / a.chunks_per_stripe);
             const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
             const int s = a.stripe_ids ? a.stripe_ids[si] : si;  // uniform: scalar load
-            uint64_t off[VPT];
-            bool ok[VPT];
-#pragma unroll
-            for (int v = 0; v < VPT; ++v) {
-                const uint64_t u = static_cast<uint64_t>(cb) * a.units_per_chunk + v * kBlock + tid;
-                ok[v] = u < nunits;
-                off[v] = (ok[v] ? u : 0) * 16;  // clamp: out-of-range lanes read unit 0, store nothing
-            }
-
-            uint32_t acc[MC][VPT][4];
-#pragma unroll
-            for (int r = 0; r < MC; ++r)
-#pragma unroll
-                for (int v = 0; v < VPT; ++v)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[r][v][q] = 0;
-            if (ACC) {
-#pragma unroll
-                for (int r = 0; r < MC; ++r)
-                    if (r < nrows)
-#pragma unroll
-                        for (int v = 0; v < VPT; ++v) {
-                            const u32x4 o = load16<LAUX>(out_ptr(a, cols, rg + r, s), off[v],
-                                                         static_cast<uint32_t>(a.body), false);
-                            acc[r][v][0] = o.x; acc[r][v][1] = o.y; acc[r][v][2] = o.z; acc[r][v][3] = o.w;
-                        }
-            }
-
-            for (int i0 = 0; i0 < ncols_pad; i0 += KB) {
-                // Issue the column loads of this batch first (KB*16*VPT bytes in flight
-                // per lane), or the first WIN of them with the rest rolled in below.
-                constexpr int kFirst = (WIN > 0 && WIN < KB) ? WIN : KB;
-                u32x4 x[KB][VPT];
-                auto load_col = [&](int b) {
-                    int c = i0 + b;
-                    if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
-                    const g_u8* p = in_ptr(a, c, s);
-#pragma unroll
-                    for (int v = 0; v < VPT; ++v)
-                        x[b][v] = load16<LAUX>(p, off[v], static_cast<uint32_t>(a.body), (VAR & kVarNtLoad) != 0);
-                };
-#pragma unroll
-                for (int b = 0; b < kFirst; ++b) load_col(b);
-                // Tables of column b+1 are read from LDS while column b is computed.
-                constexpr bool kPrefetchTab = !(VAR & kVarSingleTab);
-                u32x4 tv[2][COLW];
-                if (kPrefetchTab) {
-#pragma unroll
-                    for (int w = 0; w < COLW; ++w) tv[0][w] = lds_tab[i0 * COLW + w];
-                }
-#pragma unroll
-                for (int b = 0; b < KB; ++b) {
-                    // Scheduling fence: keeps each column's LDS reads next to its math
-                    // (hoisted, all k*MC tables would pin ~200 VGPRs: one wave/SIMD).
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (kPrefetchTab) {
-                        if (b + 1 < KB) {
-#pragma unroll
-                            for (int w = 0; w < COLW; ++w) tv[(b + 1) & 1][w] = lds_tab[(i0 + b + 1) * COLW + w];
-                        }
-                    } else {
-#pragma unroll
-                        for (int w = 0; w < COLW; ++w) tv[b & 1][w] = lds_tab[(i0 + b) * COLW + w];
-                    }
-                    uint32_t t[COLD];
-#pragma unroll
-                    for (int w = 0; w < COLW; ++w) {
-                        t[4 * w + 0] = tv[b & 1][w].x; t[4 * w + 1] = tv[b & 1][w].y;
-                        t[4 * w + 2] = tv[b & 1][w].z; t[4 * w + 3] = tv[b & 1][w].w;
-                    }
-#pragma unroll
-                    for (int v = 0; v < VPT; ++v) {
-                        const uint32_t xs[4] = {x[b][v].x, x[b][v].y, x[b][v].z, x[b][v].w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            if (VAR & kVarXorOnly) {
-#pragma unroll
-                                for (int r = 0; r < MC; ++r) acc[r][v][q] ^= xs[q] ^ t[r * 5];
-                                continue;
-                            }
-                            uint32_t g0, g1, g2;
-                            split_groups(xs[q], g0, g1, g2);
-#pragma unroll
-                            for (int r = 0; r < MC; ++r) {
-                                const uint32_t* tr = &t[r * 5];
-                                if (VAR & kVarBitop3) {
-                                    const uint32_t p0 = __builtin_amdgcn_perm(tr[1], tr[0], g0);
-                                    const uint32_t p1 = __builtin_amdgcn_perm(tr[3], tr[2], g1);
-                                    const uint32_t p2 = __builtin_amdgcn_perm(tr[4], tr[4], g2);
-                                    acc[r][v][q] = xor3(xor3(acc[r][v][q], p0, p1), p2, 0);
-                                } else {
-                                    acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, tr);
-                                }
-                            }
-                        }
-                    }
-                    // Pin the running sums per column: stops LLVM from reassociating
-                    // the XOR chains across columns (which keeps every column's
-                    // partial products live and spills to AGPRs).
-#pragma unroll
-                    for (int r = 0; r < MC; ++r)
-#pragma unroll
-                        for (int v = 0; v < VPT; ++v)
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(acc[r][v][q]));
-                    if (b + kFirst < KB) load_col(b + kFirst);  // rolling window refill
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-
-#pragma unroll
-            for (int r = 0; r < MC; ++r) {
-                if (r < nrows) {
-#pragma unroll
-                    for (int v = 0; v < VPT; ++v) {
-                        if (!ok[v]) continue;
-                        u32x4 val;
-                        val.x = acc[r][v][0]; val.y = acc[r][v][1]; val.z = acc[r][v][2]; val.w = acc[r][v][3];
-                        store16<SAUX>(out_ptr(a, cols, rg + r, s), off[v], static_cast<uint32_t>(a.body), val,
-                                      a.nt_store != 0);
-                    }
-                }
-            }
+            chunk_body<KB, KFIX, MC, ACC, VPT, VAR, LAUX, SAUX, WIN>(
+                a, lds_tab, cols, ncols_pad, nrows, cb, nunits, [&](int c) { return in_ptr(a, c, s); },
+                [&](int r) { return out_ptr(a, cols, rg + r, s); });
         }
     }
+}
+
+// Multi-pattern mode (rs_reconst_batch_multi): every stripe names a pattern;
+// a pattern holds its input / output vector indexes and the offset of its
+// prepared LDS table image.  a.ptr / a.sid address ALL d+p vectors of
+// stripe 0.  One workgroup = one chunk of one stripe (grid = all chunks).
+template <int KB, bool KFIX, int MC>
+__global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
+                                                          const int32_t* __restrict__ stripe_pat) {
+    constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+    const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
+    const int64_t chunk = blockIdx.x;
+    const int s = static_cast<int>(chunk / a.chunks_per_stripe);
+    const int64_t cb = chunk - static_cast<int64_t>(s) * a.chunks_per_stripe;
+    const int pid = stripe_pat[s];
+    if (pid < 0) return;  // stripe not in the batch's work (uniform: whole workgroup)
+    const PatternDesc* P = pats + pid;
+    const int cols = KFIX ? KB : a.cols;
+    const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
+    const uint32_t* img = a.tables + P->tab_off;
+    for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) lds32[idx] = img[idx];
+    __syncthreads();
+    auto base = [&](uint32_t v) {
+        return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
+    };
+    chunk_body<KB, KFIX, MC, false, 1, kVarDefault, kAuxNt, kAuxNt, (KFIX ? 5 : 0)>(
+        a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body >> 4,
+        [&](int c) { return const_cast<const g_u8*>(base(P->in_idx[c])); },
+        [&](int r) { return base(P->out_idx[r]); });
 }
 
 // ---------------------------------------------------------------------------
@@ -456,6 +500,29 @@ const char* vector_kernel_name(int rows, int cols, int accumulate) {
 }
 
 static bool aligned16(uint64_t v) { return (v & 15u) == 0; }
+
+hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream) {
+    if (a.len == 0 || a.nstripes <= 0) return hipSuccess;
+    a.body = a.len;  // caller guarantees len % 16 == 0, aligned vectors, len < 2 GiB
+    a.tail_start = a.len;
+    a.units_per_chunk = kBlock;
+    a.nt_store = 1;
+    const uint64_t nunits = a.body >> 4;
+    a.chunks_per_stripe = static_cast<int64_t>((nunits + kBlock - 1) / kBlock);
+    a.total_chunks = a.chunks_per_stripe * a.nstripes;
+    const bool k10 = a.cols == 10;
+    const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
+    const size_t lds = static_cast<size_t>(ncols_pad) * 20 * 4;
+    if (k10)
+        hipLaunchKernelGGL((gf_matmul_multi<10, true, 4>), dim3(static_cast<unsigned>(a.total_chunks)), dim3(kBlock),
+                           lds, stream, a, pats, stripe_pat);
+    else
+        hipLaunchKernelGGL((gf_matmul_multi<4, false, 4>), dim3(static_cast<unsigned>(a.total_chunks)), dim3(kBlock),
+                           lds, stream, a, pats, stripe_pat);
+    return hipGetLastError();
+}
+
+int multi_table_dwords(int cols) { return (cols == 10 ? 10 : ((cols + 3) / 4) * 4) * 20; }
 
 hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     if (a.len == 0 || a.nstripes <= 0 || a.rows <= 0 || a.cols <= 0) return hipSuccess;

@@ -38,6 +38,19 @@ struct MatmulArgs {
                               // kernel reads them with scalar loads
 };
 
+// Multi-pattern mode: one pattern of rs_reconst_batch_multi.  tab_off is the
+// dword offset (in MatmulArgs::tables) of the pattern's LDS image:
+// multi_table_dwords(cols) dwords laid out [column][4 rows x 5 dwords], zero
+// padded (rows >= nout, columns >= cols).
+struct PatternDesc {
+    uint32_t tab_off;
+    uint32_t nout;        // <= 4 outputs
+    uint32_t in_idx[64];  // the d input vectors (indexes into MatmulArgs::ptr)
+    uint32_t out_idx[4];  // the output vectors
+};
+int multi_table_dwords(int cols);
+hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream);
+
 // Launch tuning knobs (read from the environment once).
 struct LaunchTuning {
     int max_grid;     // cap on workgroups of the vector kernel (0 = one per chunk)

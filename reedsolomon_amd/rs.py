@@ -347,6 +347,17 @@ class RS:
         _check(lib().rs_encode_host_batch(self._h, ctypes.c_void_p(ptr), ss, vs, S, n, int(stripes_per_chunk),
                                           int(streams)))
 
+    def xor_batch(self, src, dst, stream=None) -> None:
+        """dst[s] = src[s, 0] ^ src[s, 1] ^ ... (xorsimd xor.Encode) for [S, n, len] / [S, len] GPU tensors."""
+        _check_tensor_any(src)
+        _check_tensor_any(dst)
+        if src.dim() != 3 or dst.dim() != 2 or src.shape[0] != dst.shape[0] or src.shape[2] != dst.shape[1] or \
+                src.stride(2) != 1 or dst.stride(1) != 1:
+            raise TypeError("expected src [S, n, len] and dst [S, len] uint8 GPU tensors")
+        _check(lib().rs_xor_batch(self._h, ctypes.c_void_p(src.data_ptr()), src.stride(0), src.stride(1),
+                                  src.shape[1], ctypes.c_void_p(dst.data_ptr()), dst.stride(0), src.shape[0],
+                                  src.shape[2], _stream(stream)))
+
     def gf_matmul_batch(self, mat: np.ndarray, src, in_map, dst, out_map, accumulate=False, stream=None) -> None:
         """dst[:, out_map[r]] (=|^=) sum_c mat[r, c] x src[:, in_map[c]] for every stripe."""
         mat = np.ascontiguousarray(mat, dtype=np.uint8)

@@ -516,3 +516,44 @@ def test_reconst_batch_multi_pattern(rslib, torch_dev):
         r.reconst_batch_multi(work[:, :d], work[:, d:], bad)
     torch.cuda.synchronize()
     assert torch.equal(work, ref)
+
+
+def test_xor_batch(rslib, torch_dev):
+    """xorsimd xor.Encode restated on the device."""
+    torch = torch_dev
+    r = rslib.New(10, 4)
+    g = torch.Generator(device="cuda").manual_seed(14)
+    for S, n, L in ((1, 2, 1), (7, 3, 1000), (64, 5, 8192), (4, 16, 65536 + 7)):
+        src = torch.randint(0, 256, (S, n, L), dtype=torch.uint8, device="cuda", generator=g)
+        dst = torch.full((S, L), 0x33, dtype=torch.uint8, device="cuda")
+        r.xor_batch(src, dst)
+        exp = src[:, 0].clone()
+        for i in range(1, n):
+            exp ^= src[:, i]
+        torch.cuda.synchronize()
+        assert torch.equal(dst, exp), (S, n, L)
+
+
+@pytest.mark.parametrize("d,p,n", [(10, 4, 8192), (6, 3, 4096), (10, 4, 65536), (8, 6, 4096), (3, 2, 16)])
+def test_reconst_batch_multi_single_launch(rslib, torch_dev, d, p, n):
+    """Aligned lengths take the single-launch pattern kernel (nout <= 4);
+    8+6 also has patterns with 5-6 outputs (grouped fallback)."""
+    torch = torch_dev
+    S = 200
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(d * 100 + p)
+    data = torch.randint(0, 256, (S, d, n), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    ref_d, ref_p = data.clone(), parity.clone()
+    rng = np.random.default_rng(d + p)
+    masks = np.zeros(S, np.uint64)
+    for s in range(S):
+        lost = rng.choice(d + p, int(rng.integers(0, p + 1)), replace=False)
+        for v in lost:
+            v = int(v)
+            masks[s] |= np.uint64(1) << np.uint64(v)
+            (data[s, v] if v < d else parity[s, v - d]).fill_(0xE7)
+    r.reconst_batch_multi(data, parity, masks)
+    torch.cuda.synchronize()
+    assert torch.equal(data, ref_d) and torch.equal(parity, ref_p)
