@@ -317,6 +317,34 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
     }
 }
 
+// One chunk per workgroup, rows <= MC (grid = all chunks): the common case
+// without the row-group / grid-stride loops of gf_matmul_vec (less live state).
+template <int KB, bool KFIX, int MC, bool ACC, int WIN>
+__global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
+    constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+    const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
+    const int cols = KFIX ? KB : a.cols;
+    const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
+    for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
+        const int i = idx / COLD;
+        const int w = idx - i * COLD;
+        const int rr = w / 5;
+        uint32_t v = 0;
+        if (i < cols && rr < MC && rr < a.rows)
+            v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + rr) * 5 + (w - rr * 5)];
+        lds32[idx] = v;
+    }
+    __syncthreads();
+    const int64_t chunk = blockIdx.x;
+    const int si = static_cast<int>(chunk / a.chunks_per_stripe);
+    const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
+    const int s = a.stripe_ids ? a.stripe_ids[si] : si;
+    chunk_body<KB, KFIX, MC, ACC, 1, kVarDefault, kAuxNt, kAuxNt, WIN>(
+        a, lds_tab, cols, ncols_pad, a.rows, cb, a.body >> 4, [&](int c) { return in_ptr(a, c, s); },
+        [&](int r) { return out_ptr(a, cols, r, s); });
+}
+
 // Multi-pattern mode (rs_reconst_batch_multi): every stripe names a pattern;
 // a pattern holds its input / output vector indexes and the offset of its
 // prepared LDS table image.  a.ptr / a.sid address ALL d+p vectors of
@@ -391,6 +419,7 @@ struct Variant {
     int kb, mc, vpt;
     bool kfix;
     const char* name;
+    bool one_chunk = false;  // gf_matmul_vec1: needs grid == total chunks and rows <= mc
 };
 
 #define RSAMD_VARIANT(KB, KFIX, MC, ACC, VPT) \
@@ -440,6 +469,10 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
         case 125: *out = RSAMD_VARIANT_WIN(5); return true;
         case 126: *out = RSAMD_VARIANT_WIN(6); return true;
         case 128: *out = RSAMD_VARIANT_WIN(8); return true;
+        case 130: *out = Variant{gf_matmul_vec1<10, true, 4, false, 5>, 10, 4, 1, true, "vec1<10,w5>", true}; return true;
+        case 131: *out = Variant{gf_matmul_vec1<10, true, 4, false, 3>, 10, 4, 1, true, "vec1<10,w3>", true}; return true;
+        case 132: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0>, 10, 4, 1, true, "vec1<10,w0>", true}; return true;
+        case 133: *out = Variant{gf_matmul_vec1<10, true, 4, false, 4>, 10, 4, 1, true, "vec1<10,w4>", true}; return true;
         default: break;
     }
     switch (var) {
@@ -470,25 +503,49 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
     return RSAMD_VARIANT_G(4, false, 8, true);
 }
 
+#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN) \
+    Variant { gf_matmul_vec1<KB, KFIX, MC, ACC, WIN>, KB, MC, 1, KFIX, \
+              "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN ">", true }
+
+// Loop-free one-chunk-per-workgroup kernels (the default launch: grid = all
+// chunks, rows <= MC).  A/B on MI355X, 10+4 @ 1 MiB x 256 (tools/ab.py, 2 x 30
+// interleaved rounds): vec1 all-loads-up-front 0.589 ms, vec1 5-column window
+// 0.600, looped kernel with window 0.602, looped without 0.611; XOR-only
+// diagnostic 0.591 (the memory pattern's own ceiling).
+static bool pick_one_chunk(int rows, int cols, bool acc, Variant* out) {
+    if (!acc) {
+        if (cols == 10 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(10, true, 4, false, 0); return true; }
+        if (cols == 12 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(12, true, 4, false, 0); return true; }
+        if (cols == 10 && rows == 1) { *out = RSAMD_VARIANT1(10, true, 1, false, 0); return true; }
+        if (cols == 10 && rows == 2) { *out = RSAMD_VARIANT1(10, true, 2, false, 0); return true; }
+        if (rows == 1) { *out = RSAMD_VARIANT1(4, false, 1, false, 0); return true; }
+        if (rows == 2) { *out = RSAMD_VARIANT1(4, false, 2, false, 0); return true; }
+        if (rows <= 4) { *out = RSAMD_VARIANT1(4, false, 4, false, 0); return true; }
+        return false;
+    }
+    if (cols == 2 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(2, true, 4, true, 0); return true; }
+    if (rows == 1) { *out = RSAMD_VARIANT1(4, false, 1, true, 0); return true; }
+    if (rows == 2) { *out = RSAMD_VARIANT1(4, false, 2, true, 0); return true; }
+    if (rows <= 4) { *out = RSAMD_VARIANT1(4, false, 4, true, 0); return true; }
+    return false;
+}
+
 static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body) {
     if (body >= (uint64_t{1} << 31)) return pick_global(rows, acc);
     Variant ex;
     if (pick_experimental(rows, cols, acc, vpt, &ex)) return ex;
-    // Specialised shapes: the BASELINE configs (10+4, 12+4 encode; 10-column
-    // reconst with 1-4 outputs; 10+4 Update = 2 columns, accumulate).
+    if (vpt == 1 && tuning().max_grid <= 0 && pick_one_chunk(rows, cols, acc, &ex)) return ex;
+    // Looped kernels: row groups (rows > 4), grid caps, or VPT experiments.
     if (!acc) {
         if (cols == 10 && rows > 2 && rows <= 4)
             return vpt == 2 ? RSAMD_VARIANT(10, true, 4, false, 2) : RSAMD_VARIANT_W5(10);
         if (cols == 12 && rows > 2 && rows <= 4)
             return vpt == 2 ? RSAMD_VARIANT(12, true, 4, false, 2) : RSAMD_VARIANT_W5(12);
-        if (cols == 10 && rows == 1) return RSAMD_VARIANT(10, true, 1, false, 1);
-        if (cols == 10 && rows == 2) return RSAMD_VARIANT(10, true, 2, false, 1);
         if (rows == 1) return RSAMD_VARIANT(4, false, 1, false, 1);
         if (rows == 2) return RSAMD_VARIANT(4, false, 2, false, 1);
         if (rows <= 4) return RSAMD_VARIANT(4, false, 4, false, 1);
         return RSAMD_VARIANT(4, false, 8, false, 1);
     }
-    if (cols == 2 && rows > 2 && rows <= 4) return RSAMD_VARIANT(2, true, 4, true, 1);
     if (rows == 1) return RSAMD_VARIANT(4, false, 1, true, 1);
     if (rows == 2) return RSAMD_VARIANT(4, false, 2, true, 1);
     if (rows <= 4) return RSAMD_VARIANT(4, false, 4, true, 1);
@@ -536,14 +593,22 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
 
     if (a.body) {
         const LaunchTuning& tu = tuning();
-        const Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt, a.body);
+        Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt, a.body);
+        if (var.one_chunk) {  // one workgroup per chunk: the grid must fit a 31-bit dimension
+            const uint64_t chunks = ((a.body >> 4) + kBlock - 1) / kBlock * static_cast<uint64_t>(a.nstripes);
+            if (chunks > 0x7fffffffull)
+                var = a.accumulate ? RSAMD_VARIANT(4, false, 4, true, 1) : RSAMD_VARIANT(4, false, 4, false, 1);
+        }
         a.units_per_chunk = kBlock * var.vpt;
         a.nt_store = tu.nt_store;
         const uint64_t nunits = a.body >> 4;
         a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
         a.total_chunks = a.chunks_per_stripe * a.nstripes;
         int64_t grid = a.total_chunks;
-        if (tu.max_grid > 0 && grid > tu.max_grid) grid = tu.max_grid;
+        if (!var.one_chunk) {
+            if (tu.max_grid > 0 && grid > tu.max_grid) grid = tu.max_grid;
+            if (grid > 0x7fffffff) grid = 65536 * 8;  // looped kernels stride over the rest
+        }
         const int ncols_pad = var.kfix ? var.kb : ((a.cols + var.kb - 1) / var.kb) * var.kb;
         const int cold = ((var.mc * 5 + 3) / 4) * 4;
         size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
