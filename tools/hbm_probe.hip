@@ -95,7 +95,53 @@ __global__ __launch_bounds__(256) void k_pattern_sep(uint8_t* base, uint8_t* pba
     }
 }
 
+// Buffer-instruction (nt) variants of copy / read / write / 10+4 pattern.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(n), 0x00020000);
+}
+__global__ __launch_bounds__(256) void kb_copy(const uint8_t* src, uint8_t* dst, uint64_t chunk_bytes) {
+    const uint64_t base = (uint64_t)blockIdx.x * 4096;
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(src + base, 4096), threadIdx.x * 16, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(dst + base, 4096), threadIdx.x * 16, 0, 2);
+}
+__global__ __launch_bounds__(256) void kb_read(const uint8_t* src, uint8_t* dst) {
+    const uint64_t base = (uint64_t)blockIdx.x * 4096;
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(src + base, 4096), threadIdx.x * 16, 0, 2);
+    if (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u && v.z == 1u) *(u32x4*)dst = v;
+}
+__global__ __launch_bounds__(256) void kb_write(uint8_t* dst) {
+    const uint64_t base = (uint64_t)blockIdx.x * 4096;
+    u32x4 v = {blockIdx.x, threadIdx.x, 2u, 3u};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(dst + base, 4096), threadIdx.x * 16, 0, 2);
+}
+template <int K, int M>
+__global__ __launch_bounds__(256) void kb_pattern(const uint8_t* dbase, uint8_t* pbase, uint64_t vec, uint64_t dss,
+                                                  uint64_t pss, uint64_t cps) {
+    const uint64_t s = blockIdx.x / cps, cb = blockIdx.x % cps;
+    const uint32_t off = (uint32_t)(cb * 4096 + threadIdx.x * 16);
+    u32x4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(dbase + s * dss + i * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        u32x4 a = {(uint32_t)j, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < K; ++i) a ^= x[i];
+        __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(pbase + s * pss + j * vec, (uint32_t)vec), off, 0, 2);
+    }
+}
+
 extern "C" {
+int probe_buf(int kind, void* a, void* b, uint64_t bytes, uint64_t vec, int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (kind == 0) hipLaunchKernelGGL(kb_copy, dim3(bytes / 4096), dim3(256), 0, st, (const uint8_t*)a, (uint8_t*)b, 4096ull);
+    else if (kind == 1) hipLaunchKernelGGL(kb_read, dim3(bytes / 4096), dim3(256), 0, st, (const uint8_t*)a, (uint8_t*)b);
+    else if (kind == 2) hipLaunchKernelGGL(kb_write, dim3(bytes / 4096), dim3(256), 0, st, (uint8_t*)b);
+    else if (kind == 3) hipLaunchKernelGGL((kb_pattern<10, 4>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
+                                           (const uint8_t*)a, (uint8_t*)b, vec, 10 * vec, 4 * vec, vec / 4096);
+    else return -1;
+    return hipGetLastError();
+}
 int probe_pattern_sep(void* base, void* pbase, uint64_t vec, uint64_t dss, uint64_t pss, int nstripes, void* stream) {
     uint64_t cps = vec / 4096;
     hipLaunchKernelGGL((k_pattern_sep<10, 4>), dim3(cps * nstripes), dim3(256), 0, (hipStream_t)stream,

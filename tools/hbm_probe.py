@@ -70,6 +70,24 @@ def basic_probes(L, a, b, n, vp, sp, timeit):
 
 
 def pattern_probes(L, a, n, vp, sp, timeit):
+    if os.environ.get("PROBE_BUF", "0") == "1":
+        import torch
+        half = (n // 2) // 4096 * 4096
+        b = torch.empty(half, dtype=torch.uint8, device="cuda")
+        assert half <= n and half <= b.numel()
+        for _ in range(2):
+            timeit("buffer nt copy (read+write)", lambda: L.probe_buf(0, vp(a), vp(b), ctypes.c_uint64(half),
+                                                                       ctypes.c_uint64(0), 0, sp), 2 * half)
+            timeit("buffer nt read-only", lambda: L.probe_buf(1, vp(a), vp(b), ctypes.c_uint64(n // 4096 * 4096),
+                                                               ctypes.c_uint64(0), 0, sp), n // 4096 * 4096)
+            timeit("buffer nt write-only", lambda: L.probe_buf(2, vp(a), vp(b), ctypes.c_uint64(half),
+                                                                ctypes.c_uint64(0), 0, sp), half)
+            vec, S = 1 << 20, 240
+            assert S * 10 * vec <= n and S * 4 * vec <= b.numel()
+            timeit("buffer nt 10+4 pattern, split layout", lambda: L.probe_buf(3, vp(a), vp(b), ctypes.c_uint64(0),
+                                                                                ctypes.c_uint64(vec), S, sp),
+                   S * 14 * vec)
+        return
     if os.environ.get("PROBE_SEP", "0") == "1":
         vec = 1 << 20
         S = 240
