@@ -113,25 +113,66 @@ def timed_region(step_fn, steps: int, barrier, sync, max_over_ranks):
 
 def cpu_baseline(k, m, vec, seconds):
     """The oracle's AVX2 restatement of the reference's encode path
-    (gmu_amd64.s split-nibble + rs.go:141-203 chunking), one core."""
+    (gmu_amd64.s split-nibble + rs.go:141-203 chunking): one core (the
+    reference's published convention, README.md:129-138) and, beside it, all
+    cores of this process's CPU share with stripes partitioned over threads
+    (SURVEY.md 8d)."""
+    import concurrent.futures as cf
+    import threading
+
     import numpy as np
 
     from oracle import oracle
 
     oracle.build()
     rng = np.random.default_rng(0x5EED)
-    nstripes = 4
-    stripes = [[rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] +
-               [np.zeros(vec, np.uint8) for _ in range(m)] for _ in range(nstripes)]
+
+    def make(n):
+        return [[rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] +
+                [np.zeros(vec, np.uint8) for _ in range(m)] for _ in range(n)]
+
+    def run(stripes, deadline):
+        n = 0
+        while True:
+            oracle.encode_avx2(k, m, stripes[n % len(stripes)])  # ctypes drops the GIL
+            n += 1
+            if time.perf_counter() >= deadline:
+                return n
+
+    stripes = make(4)
     used_avx2 = oracle.has_avx2()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle.encode_avx2(k, m, stripes[n % nstripes])
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    t0 = time.perf_counter()
+    n = run(stripes, t0 + seconds)
+    el = time.perf_counter() - t0
     gibs = n * (k + m) * vec / el / 2 ** 30
+
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)), 64))
+    per = [make(2) for _ in range(threads)]
+    mt_seconds = max(1.0, seconds / 3)
+    start = threading.Barrier(threads + 1, timeout=120)
+    t1 = [0.0]
+
+    def worker(st):
+        for x in st:  # untimed: first touch of the parity pages happens here
+            oracle.encode_avx2(k, m, x)
+        start.wait()
+        start.wait()  # main thread has stamped t1
+        return run(st, t1[0] + mt_seconds)
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        futs = [ex.submit(worker, st) for st in per]
+        start.wait()
+        t1[0] = time.perf_counter()
+        start.wait()
+        counts = [f.result() for f in futs]
+        el_mt = time.perf_counter() - t1[0]
+    mt = sum(counts) * (k + m) * vec / el_mt / 2 ** 30
+    del per, stripes
+
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -140,11 +181,14 @@ def cpu_baseline(k, m, vec, seconds):
                 break
     except OSError:
         pass
+    kern = "AVX2 split-nibble" if used_avx2 else "scalar table"
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
         "sample": f"{n} encodes of {k}+{m} x {vec} B stripes (4 distinct, host memory) in {el:.1f} s, "
-                  f"{'AVX2 split-nibble' if used_avx2 else 'scalar table'} restatement of gmu_amd64.s, "
-                  f"1 thread on {cpu}",
+                  f"{kern} restatement of gmu_amd64.s, 1 thread on {cpu}",
+        "multi_thread": {"value": round(mt, 3), "unit": "GiB/s", "cores": threads,
+                         "sample": f"{sum(counts)} encodes over {threads} threads (2 stripes each) "
+                                   f"in {el_mt:.1f} s, same kernel"},
     }
 
 
