@@ -149,7 +149,26 @@ struct rs_codec {
     size_t stage_bytes = 0;
     uint8_t* hstage = nullptr;  // pinned host mirror of `stage` (small-vector fast path)
     size_t hstage_bytes = 0;
+    uint8_t* slots = nullptr;   // where this call's kernels read/write: `stage`, or `hstage` (zero-copy)
+    bool zc = false;            // zero-copy: kernels access the pinned mirror over PCIe directly
+    bool zc_pending = false;    // a zero-copy kernel may still be using hstage
     hipStream_t stream = nullptr;
+
+    // Upload ring for per-call device descriptors (multi-pattern Reconst):
+    // pinned host slot -> device slot on a private copy stream, so the copy
+    // for call n+1 overlaps call n's kernel instead of stalling the stream.
+    static constexpr int kUploadSlots = 4;
+    struct UploadSlot {
+        uint8_t* host = nullptr;
+        uint8_t* dev = nullptr;
+        size_t cap = 0;
+        hipEvent_t copied = nullptr, done = nullptr;
+        bool in_flight = false;
+    };
+    std::mutex up_mu;
+    UploadSlot up[kUploadSlots];
+    int up_next = 0;
+    hipStream_t up_stream = nullptr;
 
     const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
 
@@ -159,6 +178,13 @@ struct rs_codec {
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipDeviceSynchronize();
         for (auto& kv : tables) (void)hipFree(kv.second);
+        for (UploadSlot& u : up) {
+            if (u.host) (void)hipHostFree(u.host);
+            if (u.dev) (void)hipFree(u.dev);
+            if (u.copied) (void)hipEventDestroy(u.copied);
+            if (u.done) (void)hipEventDestroy(u.done);
+        }
+        if (up_stream) (void)hipStreamDestroy(up_stream);
         if (stage) (void)hipFree(stage);
         if (hstage) (void)hipHostFree(hstage);
         if (stream) (void)hipStreamDestroy(stream);
@@ -181,6 +207,76 @@ int ensure_device(rs_t* rs) {
     rs->device_ready = true;
     return RS_OK;
 }
+
+// One leased upload slot (see rs_codec::up).  Holds the ring lock from
+// acquire() until the consumer's kernels are enqueued; the destructor records
+// the slot's `done` event on the consumer stream.
+class UploadLease {
+public:
+    explicit UploadLease(rs_t* rs) : rs_(rs), lk_(rs->up_mu) {}
+    ~UploadLease() {
+        if (slot_ && st_) {
+            (void)hipEventRecord(slot_->done, st_);
+            slot_->in_flight = true;
+        }
+    }
+    // A pinned host buffer of `bytes` to fill (slot free for reuse on return).
+    int acquire(size_t bytes, uint8_t** host) {
+        rs_codec::UploadSlot& u = rs_->up[rs_->up_next];
+        rs_->up_next = (rs_->up_next + 1) % rs_codec::kUploadSlots;
+        if (!rs_->up_stream && hipStreamCreateWithFlags(&rs_->up_stream, hipStreamNonBlocking) != hipSuccess) {
+            rs_->up_stream = nullptr;
+            return RS_ERR_DEVICE;
+        }
+        if (u.in_flight) {  // the kernel that read this slot's device copy has finished
+            if (hipEventSynchronize(u.done) != hipSuccess) return RS_ERR_DEVICE;
+            u.in_flight = false;
+        }
+        if (!u.copied && (hipEventCreateWithFlags(&u.copied, hipEventDisableTiming) != hipSuccess ||
+                          hipEventCreateWithFlags(&u.done, hipEventDisableTiming) != hipSuccess))
+            return RS_ERR_DEVICE;
+        if (u.cap < bytes) {
+            if (u.host) (void)hipHostFree(u.host);
+            if (u.dev) (void)hipFree(u.dev);
+            u.host = nullptr;
+            u.dev = nullptr;
+            u.cap = 0;
+            size_t cap = (bytes + (size_t{64} << 10) - 1) & ~((size_t{64} << 10) - 1);
+            if (hipHostMalloc(reinterpret_cast<void**>(&u.host), cap, hipHostMallocDefault) != hipSuccess) {
+                u.host = nullptr;
+                return RS_ERR_NOMEM;
+            }
+            if (hipMalloc(reinterpret_cast<void**>(&u.dev), cap) != hipSuccess) {
+                (void)hipHostFree(u.host);
+                u.host = nullptr;
+                u.dev = nullptr;
+                return RS_ERR_NOMEM;
+            }
+            u.cap = cap;
+        }
+        slot_ = &u;
+        bytes_ = bytes;
+        *host = u.host;
+        return RS_OK;
+    }
+    // Copy the filled host buffer to the device and make `st` wait for it.
+    int upload(hipStream_t st, uint8_t** dev) {
+        st_ = st;
+        if (hipMemcpyAsync(slot_->dev, slot_->host, bytes_, hipMemcpyHostToDevice, rs_->up_stream) != hipSuccess ||
+            hipEventRecord(slot_->copied, rs_->up_stream) != hipSuccess ||
+            hipStreamWaitEvent(st, slot_->copied, 0) != hipSuccess)
+            return RS_ERR_DEVICE;
+        *dev = slot_->dev;
+        return RS_OK;
+    }
+
+private:
+    rs_t* rs_;
+    std::lock_guard<std::mutex> lk_;
+    rs_codec::UploadSlot* slot_ = nullptr;
+    hipStream_t st_ = nullptr;
+    size_t bytes_ = 0;
+};
 
 // Perm tables for a rows x cols coefficient matrix, laid out
 // [col][rows_pad][5] dwords (rows padded to a multiple of 8 so that every
@@ -447,32 +543,14 @@ std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr) {  
 
 // ---------------------------------------------------------------- host staging
 
-// Staging area for the host-memory entry points: `slots` vectors of `pitch`
-// bytes (pitch 256-aligned so every slot takes the vector kernel).  Caller
-// holds stage_mu.
-int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
-    *pitch = rup(size, 256);
-    const size_t need = *pitch * static_cast<size_t>(slots);
-    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-        return RS_ERR_DEVICE;
-    if (need > rs->stage_bytes) {
-        if (rs->stage) {
-            (void)hipStreamSynchronize(rs->stream);
-            (void)hipFree(rs->stage);
-            rs->stage = nullptr;
-            rs->stage_bytes = 0;
-        }
-        if (hipMalloc(&rs->stage, need) != hipSuccess) return RS_ERR_DEVICE;
-        rs->stage_bytes = need;
-    }
-    return RS_OK;
-}
-
 // Vectors up to this size go through the pinned host mirror: the caller's
 // bytes are memcpy'd into pinned memory and each direction is ONE DMA over
 // contiguous slots, instead of one pageable copy (staged by the runtime) per
 // vector.  Larger vectors use the runtime's pipelined pageable copies.
 size_t g_pinned_max = 256 * 1024;
+// Vectors up to this size skip the device staging copy altogether: the kernel
+// reads and writes the pinned mirror over PCIe (no DMA setup either way).
+size_t g_zc_max = 256 * 1024;
 
 bool use_pinned(rs_t* rs, int slots, size_t pitch) {
     if (pitch > g_pinned_max) return false;
@@ -483,10 +561,43 @@ bool use_pinned(rs_t* rs, int slots, size_t pitch) {
         (void)hipHostFree(rs->hstage);
         rs->hstage = nullptr;
         rs->hstage_bytes = 0;
+        rs->zc_pending = false;
     }
     if (hipHostMalloc(reinterpret_cast<void**>(&rs->hstage), need, hipHostMallocDefault) != hipSuccess) return false;
     rs->hstage_bytes = need;
     return true;
+}
+
+// Staging area for the host-memory entry points: `slots` vectors of `pitch`
+// bytes (pitch 256-aligned so every slot takes the vector kernel), at
+// rs->slots.  Small vectors (<= g_zc_max) are staged zero-copy in the pinned
+// mirror, the rest in device memory.  Caller holds stage_mu.
+int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
+    *pitch = rup(size, 256);
+    const size_t need = *pitch * static_cast<size_t>(slots);
+    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+        return RS_ERR_DEVICE;
+    rs->zc = false;
+    if (*pitch <= g_zc_max && *pitch <= g_pinned_max && use_pinned(rs, slots, *pitch)) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, rs->hstage, 0) == hipSuccess && dp) {
+            rs->zc = true;
+            rs->slots = static_cast<uint8_t*>(dp);
+            return RS_OK;
+        }
+    }
+    if (need > rs->stage_bytes) {
+        if (rs->stage) {
+            (void)hipStreamSynchronize(rs->stream);
+            (void)hipFree(rs->stage);
+            rs->stage = nullptr;
+            rs->stage_bytes = 0;
+        }
+        if (hipMalloc(&rs->stage, need) != hipSuccess) return RS_ERR_DEVICE;
+        rs->stage_bytes = need;
+    }
+    rs->slots = rs->stage;
+    return RS_OK;
 }
 
 // Host vectors src[0..n) (size bytes each) -> device staging slots
@@ -504,6 +615,13 @@ int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_
 
 int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots) {
     if (n <= 0) return RS_OK;
+    if (rs->zc) {  // the kernel reads the pinned mirror itself
+        if (rs->zc_pending) RS_TRY(sync(rs));
+        uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
+        for (int i = 0; i < n; ++i) std::memcpy(h + static_cast<size_t>(i) * pitch, src[i], size);
+        rs->zc_pending = true;
+        return RS_OK;
+    }
     uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
     if (use_pinned(rs, total_slots, pitch)) {
         uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
@@ -516,6 +634,13 @@ int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pit
 
 // Device staging slots [first, first+n) -> host vectors dst[0..n); synchronous.
 int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots) {
+    if (rs->zc) {
+        RS_TRY(sync(rs));
+        rs->zc_pending = false;
+        const uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
+        for (int i = 0; i < n; ++i) std::memcpy(dst[i], h + static_cast<size_t>(i) * pitch, size);
+        return RS_OK;
+    }
     if (n <= 0) return sync(rs);
     const uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
     if (use_pinned(rs, total_slots, pitch)) {
@@ -649,7 +774,9 @@ int rs_tune(const char* name, int value) {
     else if (n == "nt_store") t.nt_store = value;
     else if (n == "var") t.var = value;
     else if (n == "lds_pad") t.lds_pad = value;
+    else if (n == "stage_late") t.stage_late = value;
     else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
+    else if (n == "host_zc_max") g_zc_max = value < 0 ? 0 : static_cast<size_t>(value);
     else return RS_ERR_INVAL;
     return RS_OK;
 }
@@ -695,8 +822,8 @@ int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
     RS_TRY(ensure_stage(rs, d + p, size, &pitch));
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
-    for (int i = 0; i < d; ++i) in[i] = rs->stage + i * pitch;
-    for (int j = 0; j < p; ++j) out[j] = rs->stage + (d + j) * pitch;
+    for (int i = 0; i < d; ++i) in[i] = rs->slots + i * pitch;
+    for (int j = 0; j < p; ++j) out[j] = rs->slots + (d + j) * pitch;
     RS_TRY(stage_in(rs, vects, d, size, pitch, 0, d + p));
     RS_TRY(matmul(rs, rs->gen(), p, d, in, 0, out, 0, 1, size, false, rs->stream));
     return stage_out(rs, vects + d, p, size, pitch, d, d + p);
@@ -758,11 +885,11 @@ int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const
         const uint8_t* src[kMaxVects];
         uint8_t* dst[kMaxVects];
         for (int i = 0; i < d; ++i) {
-            in[i] = rs->stage + static_cast<size_t>(i) * pitch;
+            in[i] = rs->slots + static_cast<size_t>(i) * pitch;
             src[i] = vects[pl.vs[i]];
         }
         for (int i = 0; i < rows; ++i) {
-            out[i] = rs->stage + static_cast<size_t>(d + i) * pitch;
+            out[i] = rs->slots + static_cast<size_t>(d + i) * pitch;
             dst[i] = vects[pl.nr[i]];
         }
         std::vector<uint8_t> m;
@@ -897,10 +1024,15 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
         const size_t tab_bytes = static_cast<size_t>(npat) * tdw * 4;
         const size_t desc_bytes = static_cast<size_t>(npat) * sizeof(PatternDesc);
         const size_t pat_bytes = static_cast<size_t>(nstripes) * 4;
-        std::vector<uint8_t> host(tab_bytes + desc_bytes + pat_bytes, 0);
-        uint32_t* tabs = reinterpret_cast<uint32_t*>(host.data());
-        PatternDesc* descs = reinterpret_cast<PatternDesc*>(host.data() + tab_bytes);
-        int32_t* spat = reinterpret_cast<int32_t*>(host.data() + tab_bytes + desc_bytes);
+        int nout_max = 0;
+        for (const Group& gr : plan) nout_max = gr.pl.nnr > nout_max ? gr.pl.nnr : nout_max;
+        UploadLease lease(rs);
+        uint8_t* host = nullptr;
+        RS_TRY(lease.acquire(tab_bytes + desc_bytes + pat_bytes, &host));
+        std::memset(host, 0, tab_bytes + desc_bytes);
+        uint32_t* tabs = reinterpret_cast<uint32_t*>(host);
+        PatternDesc* descs = reinterpret_cast<PatternDesc*>(host + tab_bytes);
+        int32_t* spat = reinterpret_cast<int32_t*>(host + tab_bytes + desc_bytes);
         for (int s = 0; s < nstripes; ++s) spat[s] = -1;
         for (int gi = 0; gi < npat; ++gi) {
             const Group& gr = plan[gi];
@@ -917,40 +1049,35 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
             for (size_t t = 0; t < gr.n; ++t) spat[ids[gr.off + t]] = gi;
         }
         uint8_t* dev = nullptr;
-        if (hipMallocAsync(reinterpret_cast<void**>(&dev), host.size(), st) != hipSuccess) return RS_ERR_DEVICE;
-        int rc = hipMemcpyAsync(dev, host.data(), host.size(), hipMemcpyHostToDevice, st) == hipSuccess
-                     ? RS_OK
-                     : RS_ERR_DEVICE;
-        if (rc == RS_OK) {
-            MatmulArgs a;
-            std::memset(&a, 0, sizeof a);
-            a.tables = reinterpret_cast<const uint32_t*>(dev);
-            a.rows = 4;
-            a.cols = d;
-            a.nstripes = nstripes;
-            a.len = len;
-            a.ss[0] = L->data_stripe_stride;
-            a.ss[1] = L->parity_stripe_stride;
-            const LayoutAddr A{L, d};
-            for (int v = 0; v < d + p; ++v) {
-                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
-                a.sid[v] = A.sid(v);
-            }
-            rc = launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
-                                 reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st) == hipSuccess
-                     ? RS_OK
-                     : RS_ERR_DEVICE;
+        RS_TRY(lease.upload(st, &dev));
+        MatmulArgs a;
+        std::memset(&a, 0, sizeof a);
+        a.tables = reinterpret_cast<const uint32_t*>(dev);
+        a.rows = nout_max;
+        a.cols = d;
+        a.nstripes = nstripes;
+        a.len = len;
+        a.ss[0] = L->data_stripe_stride;
+        a.ss[1] = L->parity_stripe_stride;
+        const LayoutAddr A{L, d};
+        for (int v = 0; v < d + p; ++v) {
+            a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
+            a.sid[v] = A.sid(v);
         }
-        (void)hipFreeAsync(dev, st);
-        return rc;
+        return launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
+                               reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st) == hipSuccess
+                   ? RS_OK
+                   : RS_ERR_DEVICE;
     }
 
-    int32_t* dids = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&dids), ids.size() * sizeof(int32_t), st) != hipSuccess)
-        return RS_ERR_DEVICE;
-    int rc = hipMemcpyAsync(dids, ids.data(), ids.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) == hipSuccess
-                 ? RS_OK
-                 : RS_ERR_DEVICE;
+    UploadLease lease(rs);
+    uint8_t* hids = nullptr;
+    RS_TRY(lease.acquire(ids.size() * sizeof(int32_t), &hids));
+    std::memcpy(hids, ids.data(), ids.size() * sizeof(int32_t));
+    uint8_t* dev_ids = nullptr;
+    RS_TRY(lease.upload(st, &dev_ids));
+    const int32_t* dids = reinterpret_cast<const int32_t*>(dev_ids);
+    int rc = RS_OK;
     const LayoutAddr A{L, d};
     const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
     const uint8_t* in[kMaxVects];
@@ -973,7 +1100,6 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
         rc = matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
                        dids + gr.off);
     }
-    (void)hipFreeAsync(dids, st);
     return rc;
 }
 
@@ -991,9 +1117,9 @@ int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* 
     std::lock_guard<std::mutex> lk(rs->stage_mu);
     size_t pitch = 0;
     RS_TRY(ensure_stage(rs, 2 + p, size, &pitch));
-    const uint8_t* in[2] = {rs->stage, rs->stage + pitch};
+    const uint8_t* in[2] = {rs->slots, rs->slots + pitch};
     uint8_t* out[kMaxVects];
-    for (int j = 0; j < p; ++j) out[j] = rs->stage + (2 + j) * pitch;
+    for (int j = 0; j < p; ++j) out[j] = rs->slots + (2 + j) * pitch;
     const uint8_t* src[kMaxVects + 2];
     src[0] = old_data;
     src[1] = new_data;
@@ -1058,11 +1184,11 @@ int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, in
     uint8_t* out[kMaxVects];
     const uint8_t* src[2 * kMaxVects];
     for (int i = 0; i < nd; ++i) {
-        in[i] = rs->stage + i * pitch;
+        in[i] = rs->slots + i * pitch;
         src[i] = data[i];
     }
     for (int j = 0; j < p; ++j) {
-        out[j] = rs->stage + (nd + j) * pitch;
+        out[j] = rs->slots + (nd + j) * pitch;
         src[nd + j] = parity[j];
     }
     RS_TRY(stage_in(rs, src, nd + p, size, pitch, 0, nd + p));

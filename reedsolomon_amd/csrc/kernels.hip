@@ -53,6 +53,8 @@ LaunchTuning& tuning() {
         x.var = e ? std::atoi(e) : -1;
         const char* l = std::getenv("RSAMD_LDS_PAD");
         x.lds_pad = l ? std::atoi(l) : 0;
+        const char* sl = std::getenv("RSAMD_STAGE_LATE");
+        x.stage_late = sl ? std::atoi(sl) : 0;
         return x;
     }();
     return t;
@@ -148,11 +150,18 @@ constexpr int kAuxNt = 2;
 // r (wave-uniform); the LDS holds this launch's (or this pattern's) tables.
 //   WIN  0: issue all KB column loads up front; >0: rolling window of WIN
 //        columns in flight per lane (fewer VGPRs, more resident waves)
+struct NoStage {
+    __device__ void operator()() const {}
+};
+
+// `stage` runs once, after the first column batch's loads are issued and
+// before the first LDS table read: a kernel that stages its tables there
+// overlaps that global->LDS copy with its data loads.
 template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR, int LAUX, int SAUX, int WIN, class InBase,
-          class OutBase>
+          class OutBase, class Stage = NoStage>
 __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4* lds_tab, int cols, int ncols_pad,
                                            int nrows, int64_t cb, uint64_t nunits, InBase in_base,
-                                           OutBase out_base) {
+                                           OutBase out_base, Stage stage = Stage()) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
     constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
     const int tid = threadIdx.x;
@@ -198,6 +207,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
         };
 #pragma unroll
         for (int b = 0; b < kFirst; ++b) load_col(b);
+        if (i0 == 0) stage();
         // Tables of column b+1 are read from LDS while column b is computed.
         constexpr bool kPrefetchTab = !(VAR & kVarSingleTab);
         u32x4 tv[2][COLW];
@@ -319,37 +329,40 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
 
 // One chunk per workgroup, rows <= MC (grid = all chunks): the common case
 // without the row-group / grid-stride loops of gf_matmul_vec (less live state).
-template <int KB, bool KFIX, int MC, bool ACC, int WIN>
+template <int KB, bool KFIX, int MC, bool ACC, int WIN, bool STAGE_LATE = false>
 __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
     const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
     const int cols = KFIX ? KB : a.cols;
     const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
-    for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
-        const int i = idx / COLD;
-        const int w = idx - i * COLD;
-        const int rr = w / 5;
-        uint32_t v = 0;
-        if (i < cols && rr < MC && rr < a.rows)
-            v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + rr) * 5 + (w - rr * 5)];
-        lds32[idx] = v;
-    }
-    __syncthreads();
+    auto stage = [&]() {
+        for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
+            const int i = idx / COLD;
+            const int w = idx - i * COLD;
+            const int rr = w / 5;
+            uint32_t v = 0;
+            if (i < cols && rr < MC && rr < a.rows)
+                v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + rr) * 5 + (w - rr * 5)];
+            lds32[idx] = v;
+        }
+        __syncthreads();
+    };
     const int64_t chunk = blockIdx.x;
     const int si = static_cast<int>(chunk / a.chunks_per_stripe);
     const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
     const int s = a.stripe_ids ? a.stripe_ids[si] : si;
+    if (!STAGE_LATE) stage();
     chunk_body<KB, KFIX, MC, ACC, 1, kVarDefault, kAuxNt, kAuxNt, WIN>(
         a, lds_tab, cols, ncols_pad, a.rows, cb, a.body >> 4, [&](int c) { return in_ptr(a, c, s); },
-        [&](int r) { return out_ptr(a, cols, r, s); });
+        [&](int r) { return out_ptr(a, cols, r, s); }, [&]() { if (STAGE_LATE) stage(); });
 }
 
 // Multi-pattern mode (rs_reconst_batch_multi): every stripe names a pattern;
 // a pattern holds its input / output vector indexes and the offset of its
 // prepared LDS table image.  a.ptr / a.sid address ALL d+p vectors of
 // stripe 0.  One workgroup = one chunk of one stripe (grid = all chunks).
-template <int KB, bool KFIX, int MC>
+template <int KB, bool KFIX, int MC, bool STAGE_LATE = false>
 __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
                                                           const int32_t* __restrict__ stripe_pat) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
@@ -364,15 +377,22 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, co
     const int cols = KFIX ? KB : a.cols;
     const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
     const uint32_t* img = a.tables + P->tab_off;
-    for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) lds32[idx] = img[idx];
-    __syncthreads();
+    // image columns are 20 dwords (4 rows x 5); keep the first COLD of each
+    auto stage = [&]() {
+        for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
+            const int c = idx / COLD;
+            lds32[idx] = img[c * 20 + (idx - c * COLD)];
+        }
+        __syncthreads();
+    };
+    if (!STAGE_LATE) stage();
     auto base = [&](uint32_t v) {
         return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
     };
-    chunk_body<KB, KFIX, MC, false, 1, kVarDefault, kAuxNt, kAuxNt, (KFIX ? 5 : 0)>(
+    chunk_body<KB, KFIX, MC, false, 1, kVarDefault, kAuxNt, kAuxNt, 0>(
         a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body >> 4,
         [&](int c) { return const_cast<const g_u8*>(base(P->in_idx[c])); },
-        [&](int r) { return base(P->out_idx[r]); });
+        [&](int r) { return base(P->out_idx[r]); }, [&]() { if (STAGE_LATE) stage(); });
 }
 
 // ---------------------------------------------------------------------------
@@ -503,9 +523,12 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
     return RSAMD_VARIANT_G(4, false, 8, true);
 }
 
-#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN) \
-    Variant { gf_matmul_vec1<KB, KFIX, MC, ACC, WIN>, KB, MC, 1, KFIX, \
-              "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN ">", true }
+#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN)                                                         \
+    (tuning().stage_late                                                                              \
+         ? Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, true>, KB, MC, 1, KFIX,                     \
+                   "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN ",late>", true}          \
+         : Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, false>, KB, MC, 1, KFIX,                    \
+                   "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN ">", true})
 
 // Loop-free one-chunk-per-workgroup kernels (the default launch: grid = all
 // chunks, rows <= MC).  A/B on MI355X, 10+4 @ 1 MiB x 256 (tools/ab.py, 2 x 30
@@ -567,15 +590,31 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     const uint64_t nunits = a.body >> 4;
     a.chunks_per_stripe = static_cast<int64_t>((nunits + kBlock - 1) / kBlock);
     a.total_chunks = a.chunks_per_stripe * a.nstripes;
+    // a.rows = the largest output count over the batch's patterns (<= 4)
     const bool k10 = a.cols == 10;
+    const int mc = a.rows <= 1 ? 1 : (a.rows == 2 ? 2 : 4);
     const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
-    const size_t lds = static_cast<size_t>(ncols_pad) * 20 * 4;
-    if (k10)
-        hipLaunchKernelGGL((gf_matmul_multi<10, true, 4>), dim3(static_cast<unsigned>(a.total_chunks)), dim3(kBlock),
-                           lds, stream, a, pats, stripe_pat);
-    else
-        hipLaunchKernelGGL((gf_matmul_multi<4, false, 4>), dim3(static_cast<unsigned>(a.total_chunks)), dim3(kBlock),
-                           lds, stream, a, pats, stripe_pat);
+    const size_t lds = static_cast<size_t>(ncols_pad) * (((mc * 5 + 3) / 4) * 4) * 4;
+    const dim3 grid(static_cast<unsigned>(a.total_chunks));
+#define RSAMD_MULTI(KB, KFIX, MC)                                                                          \
+    do {                                                                                                  \
+        if (tuning().stage_late)                                                                          \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, true>), grid, dim3(kBlock), lds, stream, a, pats, \
+                               stripe_pat);                                                               \
+        else                                                                                              \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, false>), grid, dim3(kBlock), lds, stream, a, pats, \
+                               stripe_pat);                                                               \
+    } while (0)
+    if (k10) {
+        if (mc == 1) RSAMD_MULTI(10, true, 1);
+        else if (mc == 2) RSAMD_MULTI(10, true, 2);
+        else RSAMD_MULTI(10, true, 4);
+    } else {
+        if (mc == 1) RSAMD_MULTI(4, false, 1);
+        else if (mc == 2) RSAMD_MULTI(4, false, 2);
+        else RSAMD_MULTI(4, false, 4);
+    }
+#undef RSAMD_MULTI
     return hipGetLastError();
 }
 

@@ -58,6 +58,7 @@ struct LaunchTuning {
     int nt_store;     // non-temporal parity stores
     int var;          // experimental 10+4 code shape (RSAMD_VAR), -1 = default
     int lds_pad;      // minimum dynamic LDS per workgroup (caps occupancy; experiments)
+    int stage_late;   // one-chunk kernels: stage LDS tables after issuing the data loads
 };
 LaunchTuning& tuning();
 

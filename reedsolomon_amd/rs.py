@@ -21,7 +21,7 @@ from typing import Sequence
 
 import numpy as np
 
-from ._lib import RSLayout, c_u8p, lib
+from ._lib import RSLayout, c_u8p, c_u8pp, lib
 
 
 # ---------------------------------------------------------------- errors
@@ -108,14 +108,14 @@ def _check(rc: int) -> None:
 
 # ---------------------------------------------------------------- marshalling
 
+_U8 = np.dtype(np.uint8)
+
+
 def _host_array(buf, writable: bool) -> np.ndarray:
-    if isinstance(buf, np.ndarray):
-        a = buf
-    else:
-        a = np.frombuffer(buf, dtype=np.uint8)
-    if a.dtype != np.uint8 or a.ndim != 1 or not a.flags["C_CONTIGUOUS"]:
+    a = buf if type(buf) is np.ndarray else np.frombuffer(buf, dtype=np.uint8)
+    if a.dtype != _U8 or a.ndim != 1 or not a.flags.c_contiguous:
         raise TypeError("vectors must be 1-D contiguous uint8 buffers")
-    if writable and not a.flags["WRITEABLE"]:
+    if writable and not a.flags.writeable:
         raise TypeError("output vector is read-only")
     return a
 
@@ -123,12 +123,10 @@ def _host_array(buf, writable: bool) -> np.ndarray:
 def _host_vecs(bufs: Sequence, writable: bool):
     arrs = [_host_array(b, writable) for b in bufs]
     n = len(arrs)
-    ptrs = (c_u8p * max(n, 1))()
-    lens = (ctypes.c_size_t * max(n, 1))()
-    for i, a in enumerate(arrs):
-        ptrs[i] = a.ctypes.data_as(c_u8p)
-        lens[i] = a.size
-    return arrs, ptrs, lens, n
+    # one address read per vector (data_as() per vector costs ~2x more)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.__array_interface__["data"][0] for a in arrs])
+    lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
+    return arrs, ctypes.cast(ptrs, c_u8pp), lens, n
 
 
 def _dev_vecs(tensors: Sequence):

@@ -4,6 +4,10 @@ rule 24): variants are switched with rs_tune() and timed in interleaved
 rounds on the same device and buffers; reports median / min kernel time.
 
     python tools/ab.py "var=12" "var=14" "var=14,layout=inter" ...
+    python tools/ab.py "op=rec1" "op=rec1,stage_late=1" "op=multi16" ...
+
+op: enc (Encode, default) | rec1 / rec2 / rec4 (Reconst of 1 / 2 / 4 lost data
+vectors, split layout) | multi16 (rs_reconst_batch_multi, 16 patterns).
 """
 import os
 import statistics
@@ -19,13 +23,15 @@ import reedsolomon_amd as rs  # noqa: E402
 K, M, VEC, S = 10, 4, 1 << 20, 256
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
-DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0}
+DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0}
+LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9]}
 
 
 def parse(spec):
     kv = dict(x.split("=") for x in spec.split(",") if x)
     layout = kv.pop("layout", "split")
-    return layout, {k: int(v) for k, v in kv.items()}
+    op = kv.pop("op", "enc")
+    return layout, op, {k: int(v) for k, v in kv.items()}
 
 
 def main():
@@ -40,20 +46,37 @@ def main():
     st = torch.cuda.current_stream()
     times = {s: [] for s in specs}
 
+    import numpy as np
+
+    rng = np.random.default_rng(5)
+    pats = [sum(1 << int(v) for v in rng.choice(K + M, int(rng.integers(1, M + 1)), replace=False))
+            for _ in range(16)]
+    masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
+    nrec16 = sum(bin(int(x)).count("1") for x in masks)
+    r.encode_batch_split(data, par)
+
     def setup(spec):
-        layout, kv = parse(spec)
+        layout, op, kv = parse(spec)
         for k, v in {**DEFAULTS, **kv}.items():
             assert L.rs_tune(k.encode(), v) == 0, k
-        return (lambda: r.encode_batch(buf)) if layout == "inter" else (lambda: r.encode_batch_split(data, par))
+        if op in LOST:
+            lost = LOST[op]
+            return (lambda: r.reconst_batch_split(data, par, [], lost)), S * (K + len(lost)) * VEC
+        if op == "multi16":
+            return (lambda: r.reconst_batch_multi(data, par, masks)), (S * K + nrec16) * VEC
+        if layout == "inter":
+            return (lambda: r.encode_batch(buf)), S * (K + M) * VEC
+        return (lambda: r.encode_batch_split(data, par)), S * (K + M) * VEC
 
+    nbytes = {}
     for s in specs:  # warm every variant
-        f = setup(s)
+        f, nbytes[s] = setup(s)
         for _ in range(30):
             f()
     torch.cuda.synchronize()
     for _ in range(ROUNDS):
         for s in specs:
-            f = setup(s)
+            f, _ = setup(s)
             f()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
@@ -62,11 +85,10 @@ def main():
             b.record(st)
             torch.cuda.synchronize()
             times[s].append(a.elapsed_time(b) / ITERS)
-    nbytes = S * (K + M) * VEC
     for s in specs:
         med, mn = statistics.median(times[s]), min(times[s])
-        print(f"{s:40s} median {med:.4f} ms ({nbytes / med / 1e9:7.1f} TB/s)  min {mn:.4f} ms "
-              f"({nbytes / mn / 1e9:7.1f} TB/s)", flush=True)
+        print(f"{s:40s} median {med:.4f} ms ({nbytes[s] / med / 1e9:7.3f} TB/s)  min {mn:.4f} ms "
+              f"({nbytes[s] / mn / 1e9:7.3f} TB/s)", flush=True)
 
 
 if __name__ == "__main__":

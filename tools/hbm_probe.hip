@@ -139,6 +139,20 @@ int probe_buf(int kind, void* a, void* b, uint64_t bytes, uint64_t vec, int nstr
     else if (kind == 2) hipLaunchKernelGGL(kb_write, dim3(bytes / 4096), dim3(256), 0, st, (uint8_t*)b);
     else if (kind == 3) hipLaunchKernelGGL((kb_pattern<10, 4>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
                                            (const uint8_t*)a, (uint8_t*)b, vec, 10 * vec, 4 * vec, vec / 4096);
+    // 10 reads + 1..3 writes: the Reconst mixes (lost vectors written to their own region)
+    else if (kind == 4) hipLaunchKernelGGL((kb_pattern<10, 1>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
+                                           (const uint8_t*)a, (uint8_t*)b, vec, 10 * vec, 1 * vec, vec / 4096);
+    else if (kind == 5) hipLaunchKernelGGL((kb_pattern<10, 2>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
+                                           (const uint8_t*)a, (uint8_t*)b, vec, 10 * vec, 2 * vec, vec / 4096);
+    else if (kind == 6) hipLaunchKernelGGL((kb_pattern<10, 3>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
+                                           (const uint8_t*)a, (uint8_t*)b, vec, 10 * vec, 3 * vec, vec / 4096);
+    // in place, Reconst's real layout: stripe = 11 vectors in one region,
+    // vectors 1..10 read, vector 0 written (reads and write vec bytes apart)
+    else if (kind == 7) hipLaunchKernelGGL((kb_pattern<10, 1>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
+                                           (const uint8_t*)a + vec, (uint8_t*)a, vec, 11 * vec, 11 * vec, vec / 4096);
+    // in place, 14-vector stripes, data 4..9 + parity 10..13 read, 0..3 written (lost = 4 data)
+    else if (kind == 8) hipLaunchKernelGGL((kb_pattern<10, 4>), dim3(vec / 4096 * nstripes), dim3(256), 0, st,
+                                           (const uint8_t*)a + 4 * vec, (uint8_t*)a, vec, 14 * vec, 14 * vec, vec / 4096);
     else return -1;
     return hipGetLastError();
 }

@@ -70,6 +70,24 @@ def basic_probes(L, a, b, n, vp, sp, timeit):
 
 
 def pattern_probes(L, a, n, vp, sp, timeit):
+    if os.environ.get("PROBE_RECON", "0") == "1":
+        # Reconst ceilings: 10 reads + m writes per stripe, buffer nt, split regions.
+        import torch
+        b = torch.empty(n // 2, dtype=torch.uint8, device="cuda")
+        for vec, S in ((1 << 20, 240), (8 << 10, 30720)):
+            for m, kind in ((1, 4), (2, 5), (3, 6), (4, 3)):
+                assert S * 10 * vec <= n and S * m * vec <= b.numel(), "probe case out of bounds"
+                timeit(f"buffer nt 10+{m} pattern vec={vec >> 10}KiB",
+                       lambda: L.probe_buf(kind, vp(a), vp(b), ctypes.c_uint64(0), ctypes.c_uint64(vec), S, sp),
+                       S * (10 + m) * vec)
+            assert S * 14 * vec <= n, "probe case out of bounds"
+            timeit(f"buffer nt 10+1 in place (11-vector stripes) vec={vec >> 10}KiB",
+                   lambda: L.probe_buf(7, vp(a), vp(b), ctypes.c_uint64(0), ctypes.c_uint64(vec), S, sp),
+                   S * 11 * vec)
+            timeit(f"buffer nt 10+4 in place (lost 0-3 of 14) vec={vec >> 10}KiB",
+                   lambda: L.probe_buf(8, vp(a), vp(b), ctypes.c_uint64(0), ctypes.c_uint64(vec), S, sp),
+                   S * 14 * vec)
+        return
     if os.environ.get("PROBE_BUF", "0") == "1":
         import torch
         half = (n // 2) // 4096 * 4096

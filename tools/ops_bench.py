@@ -133,8 +133,14 @@ def main():
     import numpy as np
 
     L = rs.lib()
-    for pinned_max in (256 << 10, 4 << 20, 0):
+    modes = (("default: zero-copy <= 64KiB, pinned DMA <= 256KiB", 256 << 10, 64 << 10),
+             ("zero-copy <= 1MiB", 4 << 20, 1 << 20),
+             ("pinned DMA <= 256KiB, no zero-copy", 256 << 10, 0),
+             ("pinned DMA <= 4MiB", 4 << 20, 0),
+             ("pageable per-vector copies", 0, 0))
+    for label, pinned_max, zc_max in modes:
         L.rs_tune(b"host_pinned_max", pinned_max)
+        L.rs_tune(b"host_zc_max", zc_max)
         for vec in (8 << 10, 64 << 10, 256 << 10, 1 << 20):
             rng = np.random.default_rng(1)
             v = [rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] + [np.zeros(vec, np.uint8)
@@ -146,9 +152,21 @@ def main():
             for _ in range(n):
                 r.Encode(v)
             t = (time.perf_counter() - t0) / n
-            rec(f"Encode() host API 10+4 {vec >> 10}KiB (pinned staging <= {pinned_max >> 10}KiB)",
-                (k + m) * vec, t)
+            rec(f"Encode() host API 10+4 {vec >> 10}KiB ({label})", (k + m) * vec, t)
+            if vec == 8 << 10:
+                full = [x.copy() for x in v]
+                for lost in ([0], [0, 1, 2, 3]):
+                    w = [x.copy() for x in full]
+                    for _ in range(5):
+                        r.Reconst(w, [], lost)
+                    t0 = time.perf_counter()
+                    for _ in range(n):
+                        r.Reconst(w, [], lost)
+                    t = (time.perf_counter() - t0) / n
+                    assert all(np.array_equal(a, b) for a, b in zip(w, full))
+                    rec(f"Reconst() host API 10+4 8KiB lost={len(lost)} ({label})", (k + len(lost)) * vec, t)
     L.rs_tune(b"host_pinned_max", 256 << 10)
+    L.rs_tune(b"host_zc_max", 64 << 10)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ops_bench.json"), "w"), indent=1)
 
