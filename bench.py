@@ -52,6 +52,9 @@ def parse_args(argv=None):
                          "interleaved: one [S][k+m][vec] buffer")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--verify", type=int, default=1, help="encode->erase->reconst self-check of one stripe per rank")
+    ap.add_argument("--e2e-stripes", type=int, default=128,
+                    help="stripes per GPU for the host-resident end-to-end leg (0 = skip)")
+    ap.add_argument("--e2e-reps", type=int, default=10)
     return ap.parse_args(argv)
 
 
@@ -152,26 +155,42 @@ def cpu_baseline(k, m, vec, seconds):
         threads = os.cpu_count() or 1
     threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)), 64))
     per = [make(2) for _ in range(threads)]
-    mt_seconds = max(1.0, seconds / 3)
-    start = threading.Barrier(threads + 1, timeout=120)
-    t1 = [0.0]
+    mt_seconds = max(1.0, seconds / 6)
+    best = None
+    for _rep in range(2):  # best of two passes (the first can catch host-side noise)
+        start = threading.Barrier(threads + 1, timeout=120)
+        t1 = [0.0]
 
-    def worker(st):
-        for x in st:  # untimed: first touch of the parity pages happens here
-            oracle.encode_avx2(k, m, x)
-        start.wait()
-        start.wait()  # main thread has stamped t1
-        return run(st, t1[0] + mt_seconds)
+        def worker(st):
+            for x in st:  # untimed: first touch of the parity pages happens here
+                oracle.encode_avx2(k, m, x)
+            start.wait()
+            start.wait()  # main thread has stamped t1
+            return run(st, t1[0] + mt_seconds)
 
-    with cf.ThreadPoolExecutor(threads) as ex:
-        futs = [ex.submit(worker, st) for st in per]
-        start.wait()
-        t1[0] = time.perf_counter()
-        start.wait()
-        counts = [f.result() for f in futs]
-        el_mt = time.perf_counter() - t1[0]
+        with cf.ThreadPoolExecutor(threads) as ex:
+            futs = [ex.submit(worker, st) for st in per]
+            start.wait()
+            t1[0] = time.perf_counter()
+            start.wait()
+            c = [f.result() for f in futs]
+            e = time.perf_counter() - t1[0]
+        if best is None or sum(c) / e > sum(best[0]) / best[1]:
+            best = (c, e)
+    counts, el_mt = best
     mt = sum(counts) * (k + m) * vec / el_mt / 2 ** 30
     del per, stripes
+
+    # BASELINE.json config 1: 10+4 @ 8 KiB on the scalar table path
+    # (mulVectNoSIMD, gmu.go:11-23), the reference's no-SIMD row (README.md:135).
+    small = make(1)[0]
+    small = [x[:8192].copy() for x in small]
+    small = [x for x in small[:10]] + [np.zeros(8192, np.uint8) for _ in range(4)]
+    n_ns, t2 = 0, time.perf_counter()
+    while time.perf_counter() - t2 < max(0.5, seconds / 10):
+        oracle.encode(10, 4, small)
+        n_ns += 1
+    ns = n_ns * 14 * 8192 / (time.perf_counter() - t2) / 2 ** 30
 
     cpu = "unknown"
     try:
@@ -188,8 +207,39 @@ def cpu_baseline(k, m, vec, seconds):
                   f"{kern} restatement of gmu_amd64.s, 1 thread on {cpu}",
         "multi_thread": {"value": round(mt, 3), "unit": "GiB/s", "cores": threads,
                          "sample": f"{sum(counts)} encodes over {threads} threads (2 stripes each) "
-                                   f"in {el_mt:.1f} s, same kernel"},
+                                   f"in {el_mt:.1f} s (best of 2 passes), same kernel"},
+        "no_simd_10_4_8KiB": {"value": round(ns, 3), "unit": "GiB/s", "cores": 1,
+                              "sample": f"{n_ns} encodes of 10+4 x 8 KiB, scalar mulTbl path (gmu.go:11-23); "
+                                        "reference i7-12700K: 1.26 GiB/s (README.md:135)"},
     }
+
+
+def end_to_end(codec, data, parity, k, m, vec, S, reps, n_gpus, barrier, max_over, sync):
+    """Host-resident leg (north star: the path starts and ends in host memory):
+    S stripes per rank in pinned host memory, encoded by the H2D -> kernel ->
+    D2H pipeline (rs_encode_host_batch), all ranks at once; max over ranks.
+    The stripes are the first S of the device run, so the returned parity is
+    checked against the device-resident result."""
+    import torch
+
+    host = torch.empty((S, k + m, vec), dtype=torch.uint8, pin_memory=True)
+    host[:, :k].copy_(data[:S])
+    host[:, k:].fill_(0xA5)
+    codec.encode_host_batch(host, 4, 3)  # warm (and pins the slots)
+    if not torch.equal(host[:2, k:].cuda(), parity[:2]):
+        raise SystemExit("end-to-end parity differs from the device-resident encode")
+    sync()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        codec.encode_host_batch(host, 4, 3)
+    el = max_over(time.perf_counter() - t0)
+    barrier()
+    del host
+    return {"value": round(n_gpus * S * (k + m) * vec * reps / el / 2 ** 30, 2), "unit": "GiB/s",
+            "stripes_per_gpu": S, "reps": reps,
+            "path": "pinned host stripes -> H2D / encode / D2H pipeline (rs_encode_host_batch, 4 stripes "
+                    "per step, 3 streams) -> pinned host parity; all GPUs at once; wall clock, max over ranks"}
 
 
 def load_traffic(config: str):
@@ -308,6 +358,11 @@ def main(argv=None):
 
     bytes_per_step_rank = S * (k + m) * vec
     value = throughput(bytes_per_step_rank, n_gpus, args.steps, elapsed)
+
+    e2e = None
+    if args.e2e_stripes > 0:
+        e2e = end_to_end(codec, data, parity, k, m, vec, min(args.e2e_stripes, S), args.e2e_reps, n_gpus,
+                         barrier, max_over, lambda: torch.cuda.synchronize(dev))
     achieved = bytes_per_step_rank / kern_mean_s / 1e9
 
     result = None
@@ -348,6 +403,7 @@ def main(argv=None):
                 "kernel_timing": "HIP event pair on the launch stream around the K timed launches / K",
             },
         }
+        result["end_to_end"] = e2e
         if n_gpus == 1 and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(k, m, vec, args.cpu_seconds)
         else:
