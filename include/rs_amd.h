@@ -260,7 +260,8 @@ RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
 
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad", "stage_late",
- * "host_pinned_max", "host_zc_max" (bytes; host-memory call staging).  Returns
+ * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
+ * host-memory call staging).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name. */
 RS_API int rs_tune(const char* name, int value);
 

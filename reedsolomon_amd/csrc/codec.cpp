@@ -25,6 +25,7 @@
 
 #include "../../include/rs_amd.h"
 #include "gf256.hpp"
+#include "host_pool.hpp"
 #include "kernels.hpp"
 
 using namespace rsamd;
@@ -149,9 +150,9 @@ struct rs_codec {
     size_t stage_bytes = 0;
     uint8_t* hstage = nullptr;  // pinned host mirror of `stage` (small-vector fast path)
     size_t hstage_bytes = 0;
-    uint8_t* slots = nullptr;   // where this call's kernels read/write: `stage`, or `hstage` (zero-copy)
-    bool zc = false;            // zero-copy: kernels access the pinned mirror over PCIe directly
+    uint8_t* slots = nullptr;   // device staging slots of the staged (non-zero-copy) host path
     bool zc_pending = false;    // a zero-copy kernel may still be using hstage
+    hipEvent_t chunk_ev[3] = {nullptr, nullptr, nullptr};  // host-call chunk pipeline slots
     hipStream_t stream = nullptr;
 
     // Upload ring for per-call device descriptors (multi-pattern Reconst):
@@ -187,6 +188,8 @@ struct rs_codec {
         if (up_stream) (void)hipStreamDestroy(up_stream);
         if (stage) (void)hipFree(stage);
         if (hstage) (void)hipHostFree(hstage);
+        for (hipEvent_t e : chunk_ev)
+            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -548,9 +551,10 @@ std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr) {  
 // contiguous slots, instead of one pageable copy (staged by the runtime) per
 // vector.  Larger vectors use the runtime's pipelined pageable copies.
 size_t g_pinned_max = 256 * 1024;
-// Vectors up to this size skip the device staging copy altogether: the kernel
-// reads and writes the pinned mirror over PCIe (no DMA setup either way).
-size_t g_zc_max = 256 * 1024;
+// Host calls on vectors up to this size take the chunked zero-copy pipeline
+// (host_matmul: the kernel reads and writes the pinned mirror over PCIe, no
+// DMA set-up either way); larger ones the staged paths below.  Default: all.
+size_t g_zc_max = SIZE_MAX;
 
 bool use_pinned(rs_t* rs, int slots, size_t pitch) {
     if (pitch > g_pinned_max) return false;
@@ -568,24 +572,14 @@ bool use_pinned(rs_t* rs, int slots, size_t pitch) {
     return true;
 }
 
-// Staging area for the host-memory entry points: `slots` vectors of `pitch`
+// Device staging area of the staged host path: `slots` vectors of `pitch`
 // bytes (pitch 256-aligned so every slot takes the vector kernel), at
-// rs->slots.  Small vectors (<= g_zc_max) are staged zero-copy in the pinned
-// mirror, the rest in device memory.  Caller holds stage_mu.
+// rs->slots.  Caller holds stage_mu.
 int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
     *pitch = rup(size, 256);
     const size_t need = *pitch * static_cast<size_t>(slots);
     if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
         return RS_ERR_DEVICE;
-    rs->zc = false;
-    if (*pitch <= g_zc_max && *pitch <= g_pinned_max && use_pinned(rs, slots, *pitch)) {
-        void* dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, rs->hstage, 0) == hipSuccess && dp) {
-            rs->zc = true;
-            rs->slots = static_cast<uint8_t*>(dp);
-            return RS_OK;
-        }
-    }
     if (need > rs->stage_bytes) {
         if (rs->stage) {
             (void)hipStreamSynchronize(rs->stream);
@@ -615,13 +609,6 @@ int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_
 
 int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots) {
     if (n <= 0) return RS_OK;
-    if (rs->zc) {  // the kernel reads the pinned mirror itself
-        if (rs->zc_pending) RS_TRY(sync(rs));
-        uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
-        for (int i = 0; i < n; ++i) std::memcpy(h + static_cast<size_t>(i) * pitch, src[i], size);
-        rs->zc_pending = true;
-        return RS_OK;
-    }
     uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
     if (use_pinned(rs, total_slots, pitch)) {
         uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
@@ -634,13 +621,6 @@ int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pit
 
 // Device staging slots [first, first+n) -> host vectors dst[0..n); synchronous.
 int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots) {
-    if (rs->zc) {
-        RS_TRY(sync(rs));
-        rs->zc_pending = false;
-        const uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
-        for (int i = 0; i < n; ++i) std::memcpy(dst[i], h + static_cast<size_t>(i) * pitch, size);
-        return RS_OK;
-    }
     if (n <= 0) return sync(rs);
     const uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
     if (use_pinned(rs, total_slots, pitch)) {
@@ -654,6 +634,143 @@ int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, i
     return sync(rs);
 }
 
+
+// Column-chunk size of the host-call pipeline (bytes per vector per chunk).
+size_t g_chunk = 256 * 1024;
+// Total copy bytes of one chunk above which the staging copies are split
+// over the host copy pool.
+constexpr size_t kParallelCopyMin = 512 * 1024;
+
+// dst[i] <- src[i] (n vectors, len bytes each) on the copy pool, in
+// 64 KiB pieces so every thread gets work.
+void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t len) {
+    const size_t piece = 64 * 1024;
+    const size_t per = (len + piece - 1) / piece;
+    const size_t total = per * static_cast<size_t>(n);
+    if (len * static_cast<size_t>(n) < kParallelCopyMin || total <= 1) {
+        for (int i = 0; i < n; ++i) std::memcpy(dst[i], src[i], len);
+        return;
+    }
+    CopyPool::get().run(total, [&](size_t k) {
+        const size_t v = k / per, off = (k % per) * piece;
+        const size_t b = std::min(piece, len - off);
+        std::memcpy(dst[v] + off, src[v] + off, b);
+    });
+}
+
+// The synchronous host-memory product behind rs_encode / rs_reconst /
+// rs_update / rs_replace: dst[r] (=|^=) sum_c mat[r][c] x src[c], all host
+// pointers, `size` bytes each.  The vectors are cut into column chunks;
+// each chunk is copied into a slot of the pinned mirror (several host
+// threads), processed by the kernel straight out of the mirror over PCIe
+// (zero-copy: no DMA set-up), and copied back, with up to 3 chunks in
+// flight so copies overlap the GPU.  Caller holds stage_mu.
+int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+                size_t size, bool accumulate) {
+    const int nvec = rows + cols;
+    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+        return RS_ERR_DEVICE;
+    // chunk: <= g_chunk per vector and <= 8 MiB per slot, 4 KiB multiple
+    size_t C = rup(size, 256);
+    const size_t cap = std::max<size_t>(4096, std::min(g_chunk, (size_t{8} << 20) / nvec) & ~size_t{4095});
+    if (C > cap) C = cap;
+    const size_t nch = (size + C - 1) / C;
+    const int ns = nch > 1 ? 3 : 1;
+    const size_t slot = C * static_cast<size_t>(nvec);
+    if (rs->zc_pending) RS_TRY(sync(rs));
+    if (slot * ns > rs->hstage_bytes) {
+        if (rs->hstage) {
+            (void)hipHostFree(rs->hstage);
+            rs->hstage = nullptr;
+            rs->hstage_bytes = 0;
+        }
+        if (hipHostMalloc(reinterpret_cast<void**>(&rs->hstage), slot * ns, hipHostMallocDefault) != hipSuccess) {
+            rs->hstage = nullptr;
+            return RS_ERR_NOMEM;
+        }
+        rs->hstage_bytes = slot * ns;
+    }
+    void* dbase = nullptr;
+    if (hipHostGetDevicePointer(&dbase, rs->hstage, 0) != hipSuccess || !dbase) return RS_ERR_DEVICE;
+    for (int i = 0; i < ns; ++i)
+        if (!rs->chunk_ev[i] && hipEventCreateWithFlags(&rs->chunk_ev[i], hipEventDisableTiming) != hipSuccess) {
+            rs->chunk_ev[i] = nullptr;
+            return RS_ERR_DEVICE;
+        }
+    auto hslot = [&](size_t c, int v) { return rs->hstage + (c % ns) * slot + static_cast<size_t>(v) * C; };
+    auto dslot = [&](size_t c, int v) {
+        return static_cast<uint8_t*>(dbase) + (c % ns) * slot + static_cast<size_t>(v) * C;
+    };
+    auto clen = [&](size_t c) { return std::min(C, size - c * C); };
+    auto finish = [&](size_t c) -> int {  // wait for chunk c, copy its outputs back
+        if (hipEventSynchronize(rs->chunk_ev[c % ns]) != hipSuccess) return RS_ERR_DEVICE;
+        uint8_t* d[kMaxVects];
+        const uint8_t* h[kMaxVects];
+        for (int r = 0; r < rows; ++r) {
+            d[r] = dst[r] + c * C;
+            h[r] = hslot(c, cols + r);
+        }
+        parallel_copy(d, h, rows, clen(c));
+        return RS_OK;
+    };
+    int rc = RS_OK;
+    size_t done = 0;
+    for (size_t c = 0; c < nch && rc == RS_OK; ++c) {
+        if (c >= static_cast<size_t>(ns)) {
+            rc = finish(done++);
+            if (rc) break;
+        }
+        const size_t len = clen(c);
+        uint8_t* h[2 * kMaxVects];
+        const uint8_t* s_[2 * kMaxVects];
+        int n = 0;
+        for (int i = 0; i < cols; ++i, ++n) {
+            h[n] = hslot(c, i);
+            s_[n] = src[i] + c * C;
+        }
+        if (accumulate)
+            for (int r = 0; r < rows; ++r, ++n) {
+                h[n] = hslot(c, cols + r);
+                s_[n] = dst[r] + c * C;
+            }
+        parallel_copy(h, s_, n, len);
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        for (int i = 0; i < cols; ++i) in[i] = dslot(c, i);
+        for (int r = 0; r < rows; ++r) out[r] = dslot(c, cols + r);
+        rs->zc_pending = true;
+        rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, len, accumulate, rs->stream);
+        if (rc == RS_OK && hipEventRecord(rs->chunk_ev[c % ns], rs->stream) != hipSuccess) rc = RS_ERR_DEVICE;
+    }
+    while (rc == RS_OK && done < nch) rc = finish(done++);
+    if (rc) (void)hipStreamSynchronize(rs->stream);  // never leave a kernel on the mirror
+    rs->zc_pending = false;
+    return rc;
+}
+
+// Host-call dispatcher: the chunked zero-copy pipeline (default), or the
+// older staged paths (device staging + pinned DMA or pageable copies) for
+// vectors above host_zc_max (kept for A/B).
+int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+                 size_t size, bool accumulate) {
+    if (size <= g_zc_max) return host_matmul(rs, mat, rows, cols, src, dst, size, accumulate);
+    size_t pitch = 0;
+    RS_TRY(ensure_stage(rs, cols + rows, size, &pitch));
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    const uint8_t* s_[2 * kMaxVects];
+    for (int i = 0; i < cols; ++i) {
+        in[i] = rs->slots + static_cast<size_t>(i) * pitch;
+        s_[i] = src[i];
+    }
+    for (int r = 0; r < rows; ++r) {
+        out[r] = rs->slots + static_cast<size_t>(cols + r) * pitch;
+        s_[cols + r] = dst[r];
+    }
+    RS_TRY(stage_in(rs, s_, accumulate ? cols + rows : cols, size, pitch, 0, cols + rows));
+    RS_TRY(matmul(rs, mat, rows, cols, in, 0, out, 0, 1, size, accumulate, rs->stream));
+    return stage_out(rs, dst, rows, size, pitch, cols, cols + rows);
+}
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -776,7 +893,8 @@ int rs_tune(const char* name, int value) {
     else if (n == "lds_pad") t.lds_pad = value;
     else if (n == "stage_late") t.stage_late = value;
     else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
-    else if (n == "host_zc_max") g_zc_max = value < 0 ? 0 : static_cast<size_t>(value);
+    else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
+    else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
     else return RS_ERR_INVAL;
     return RS_OK;
 }
@@ -815,18 +933,8 @@ int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
     RS_TRY(check_encode(rs, lens, n));
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
-    const int d = rs->d, p = rs->p;
-    const size_t size = lens[0];
     std::lock_guard<std::mutex> lk(rs->stage_mu);
-    size_t pitch = 0;
-    RS_TRY(ensure_stage(rs, d + p, size, &pitch));
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    for (int i = 0; i < d; ++i) in[i] = rs->slots + i * pitch;
-    for (int j = 0; j < p; ++j) out[j] = rs->slots + (d + j) * pitch;
-    RS_TRY(stage_in(rs, vects, d, size, pitch, 0, d + p));
-    RS_TRY(matmul(rs, rs->gen(), p, d, in, 0, out, 0, 1, size, false, rs->stream));
-    return stage_out(rs, vects + d, p, size, pitch, d, d + p);
+    return host_product(rs, rs->gen(), rs->p, rs->d, vects, vects + rs->d, lens[0], false);
 }
 
 int rs_encode_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, void* stream) {
@@ -877,26 +985,13 @@ int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::lock_guard<std::mutex> lk(rs->stage_mu);
-        const size_t size = lens[pl.vs[0]];
-        size_t pitch = 0;
-        RS_TRY(ensure_stage(rs, d + rows, size, &pitch));
-        const uint8_t* in[kMaxVects];
-        uint8_t* out[kMaxVects];
         const uint8_t* src[kMaxVects];
         uint8_t* dst[kMaxVects];
-        for (int i = 0; i < d; ++i) {
-            in[i] = rs->slots + static_cast<size_t>(i) * pitch;
-            src[i] = vects[pl.vs[i]];
-        }
-        for (int i = 0; i < rows; ++i) {
-            out[i] = rs->slots + static_cast<size_t>(d + i) * pitch;
-            dst[i] = vects[pl.nr[i]];
-        }
+        for (int i = 0; i < d; ++i) src[i] = vects[pl.vs[i]];
+        for (int i = 0; i < rows; ++i) dst[i] = vects[pl.nr[i]];
         std::vector<uint8_t> m;
         RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
-        RS_TRY(stage_in(rs, src, d, size, pitch, 0, d + rows));
-        RS_TRY(matmul(rs, m.data(), rows, d, in, 0, out, 0, 1, size, false, rs->stream));
-        RS_TRY(stage_out(rs, dst, rows, size, pitch, d, d + rows));
+        RS_TRY(host_product(rs, m.data(), rows, d, src, dst, lens[pl.vs[0]], false));
     }
     return parity_rc;
 }
@@ -1112,22 +1207,10 @@ int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* 
     if (!old_data || !new_data) return RS_ERR_INVAL;
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
-    const int p = rs->p;
-    const size_t size = new_len;
     std::lock_guard<std::mutex> lk(rs->stage_mu);
-    size_t pitch = 0;
-    RS_TRY(ensure_stage(rs, 2 + p, size, &pitch));
-    const uint8_t* in[2] = {rs->slots, rs->slots + pitch};
-    uint8_t* out[kMaxVects];
-    for (int j = 0; j < p; ++j) out[j] = rs->slots + (2 + j) * pitch;
-    const uint8_t* src[kMaxVects + 2];
-    src[0] = old_data;
-    src[1] = new_data;
-    for (int j = 0; j < p; ++j) src[2 + j] = parity[j];
-    RS_TRY(stage_in(rs, src, 2 + p, size, pitch, 0, 2 + p));
+    const uint8_t* src[2] = {old_data, new_data};
     std::vector<uint8_t> gm = update_matrix(rs, row);
-    RS_TRY(matmul(rs, gm.data(), p, 2, in, 0, out, 0, 1, size, true, rs->stream));
-    return stage_out(rs, parity, p, size, pitch, 2, 2 + p);
+    return host_product(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
 }
 
 int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
@@ -1175,26 +1258,9 @@ int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, in
     RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
-    const int p = rs->p;
-    const size_t size = data_lens[0];
     std::lock_guard<std::mutex> lk(rs->stage_mu);
-    size_t pitch = 0;
-    RS_TRY(ensure_stage(rs, nd + p, size, &pitch));
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    const uint8_t* src[2 * kMaxVects];
-    for (int i = 0; i < nd; ++i) {
-        in[i] = rs->slots + i * pitch;
-        src[i] = data[i];
-    }
-    for (int j = 0; j < p; ++j) {
-        out[j] = rs->slots + (nd + j) * pitch;
-        src[nd + j] = parity[j];
-    }
-    RS_TRY(stage_in(rs, src, nd + p, size, pitch, 0, nd + p));
     std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-    RS_TRY(matmul(rs, gm.data(), p, nr, in, 0, out, 0, 1, size, true, rs->stream));
-    return stage_out(rs, parity, p, size, pitch, nd, nd + p);
+    return host_product(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
 }
 
 int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows,

@@ -557,3 +557,53 @@ def test_reconst_batch_multi_single_launch(rslib, torch_dev, d, p, n):
     r.reconst_batch_multi(data, parity, masks)
     torch.cuda.synchronize()
     assert torch.equal(data, ref_d) and torch.equal(parity, ref_p)
+
+
+# ---------------------------------------------------------------- host-call staging paths
+
+@pytest.mark.parametrize("mode", ["chunked", "small_chunks", "staged_pinned", "staged_pageable"])
+def test_host_calls_staging_paths(rslib, orc, torch_dev, mode):
+    """The synchronous host-memory calls through every staging path:
+    the chunked zero-copy pipeline (default; 1 MiB + 5 B = 5 ragged chunks),
+    4 KiB chunks (many trips around the 3-slot ring), and the older staged
+    paths (device staging with pinned DMA / pageable copies)."""
+    L = rslib.lib()
+    knobs = {"chunked": {}, "small_chunks": {"host_chunk": 4096},
+             "staged_pinned": {"host_zc_max": 0, "host_pinned_max": 4 << 20},
+             "staged_pageable": {"host_zc_max": 0, "host_pinned_max": 0}}[mode]
+    try:
+        for k, v in knobs.items():
+            assert L.rs_tune(k.encode(), v) == 0
+        d, p = 10, 4
+        r = rslib.New(d, p)
+        rng = np.random.default_rng(120)
+        for size in (1, 4099, 65536 * 3 + 7, (1 << 20) + 5):
+            data = [_rand(rng, size) for _ in range(d)]
+            exp = _oracle_encode(orc, d, p, data)
+            act = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
+            r.Encode(act)
+            for j in range(p):
+                assert np.array_equal(act[d + j], exp[j]), (size, j)
+            full = [x.copy() for x in act]
+            lost = [1, 4, 10, 13]
+            for i in lost:
+                act[i][:] = 0x77
+            r.Reconst(act, [], lost)
+            for i in range(d + p):
+                assert np.array_equal(act[i], full[i]), (size, i)
+            new = _rand(rng, size)
+            par = [x.copy() for x in full[d:]]
+            r.Update(full[2], new, 2, par)
+            ora = [x.copy() for x in full[d:]]
+            assert orc.update(d, p, full[2], new, 2, ora) == 0
+            for j in range(p):
+                assert np.array_equal(par[j], ora[j]), (size, j)
+            par = [x.copy() for x in full[d:]]
+            r.Replace([full[3], full[7]], [3, 7], par)
+            ora = [x.copy() for x in full[d:]]
+            assert orc.replace(d, p, [full[3], full[7]], [3, 7], ora) == 0
+            for j in range(p):
+                assert np.array_equal(par[j], ora[j]), (size, j)
+    finally:
+        for k, v in {"host_chunk": 256 << 10, "host_zc_max": -1, "host_pinned_max": 256 << 10}.items():
+            L.rs_tune(k.encode(), v)

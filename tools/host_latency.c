@@ -4,7 +4,8 @@
  *
  *   gcc -O2 -std=c99 -Iinclude tools/host_latency.c -Lreedsolomon_amd/_lib -lrsamd \
  *       -Wl,-rpath,$PWD/reedsolomon_amd/_lib -o tools/_build/host_latency
- *   tools/_build/host_latency [host_zc_max host_pinned_max]
+ *   tools/_build/host_latency [host_zc_max host_pinned_max [host_chunk]]
+ *   (host_zc_max -1 = default chunked zero-copy for every size, 0 = staged paths)
  *
  * Prints one JSON object per (op, size).
  */
@@ -43,20 +44,21 @@ static void report(const char* op, size_t vec, double bytes, int reps) {
 }
 
 int main(int argc, char** argv) {
-    static const size_t sizes[] = {4096, 8192, 65536, 262144, 1048576};
+    static const size_t sizes[] = {4096, 8192, 65536, 262144, 1048576, 4194304};
     rs_t* rs = NULL;
     size_t si;
-    if (argc == 3) {
+    if (argc >= 3) {
         rs_tune("host_zc_max", atoi(argv[1]));
         rs_tune("host_pinned_max", atoi(argv[2]));
     }
+    if (argc >= 4) rs_tune("host_chunk", atoi(argv[3]));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
     }
     for (si = 0; si < sizeof sizes / sizeof sizes[0]; ++si) {
         const size_t vec = sizes[si];
-        const int reps = vec >= 262144 ? REPS / 4 : REPS;
+        const int reps = vec >= 4194304 ? REPS / 8 : (vec >= 262144 ? REPS / 4 : REPS);
         uint8_t* v[N];
         size_t lens[N];
         int i, k;

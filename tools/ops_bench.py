@@ -133,11 +133,9 @@ def main():
     import numpy as np
 
     L = rs.lib()
-    modes = (("default: zero-copy <= 64KiB, pinned DMA <= 256KiB", 256 << 10, 64 << 10),
-             ("zero-copy <= 1MiB", 4 << 20, 1 << 20),
-             ("pinned DMA <= 256KiB, no zero-copy", 256 << 10, 0),
-             ("pinned DMA <= 4MiB", 4 << 20, 0),
-             ("pageable per-vector copies", 0, 0))
+    modes = (("default: chunked zero-copy pipeline", 256 << 10, -1),
+             ("staged: pinned mirror + DMA <= 4MiB", 4 << 20, 0),
+             ("staged: pageable per-vector copies", 0, 0))
     for label, pinned_max, zc_max in modes:
         L.rs_tune(b"host_pinned_max", pinned_max)
         L.rs_tune(b"host_zc_max", zc_max)
@@ -166,7 +164,7 @@ def main():
                     assert all(np.array_equal(a, b) for a, b in zip(w, full))
                     rec(f"Reconst() host API 10+4 8KiB lost={len(lost)} ({label})", (k + len(lost)) * vec, t)
     L.rs_tune(b"host_pinned_max", 256 << 10)
-    L.rs_tune(b"host_zc_max", 64 << 10)
+    L.rs_tune(b"host_zc_max", -1)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ops_bench.json"), "w"), indent=1)
 
