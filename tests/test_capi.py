@@ -199,3 +199,46 @@ def test_host_checks_before_device(rslib, orc):
         assert ei.value.code == code
     # nothing to rebuild: Reconst swallows ErrNoNeedReconst (rs.go:225-228)
     r.Reconst([_z(8)] * 14, [0, 1], [])
+
+
+def test_reconst_matrix_from_cache(rslib):  # TestRS_getReconstMatrixFromCache rs_test.go:355-404
+    """The reference force-enables the cache on 64+64 (white-box); here the
+    widest shape the cache serves by policy (d+p = 64, rs.go:70) with d = 60,
+    so the miss pays a 60x60 Gauss-Jordan."""
+    import time
+
+    r = rslib.New(60, 4)
+    surv = list(range(4, 64))  # data 0..3 lost
+    need = [0, 1, 2, 3]
+    t0 = time.perf_counter()
+    first = r.reconst_matrix(surv, need)
+    t1 = time.perf_counter()
+    second = r.reconst_matrix(surv, need)
+    t2 = time.perf_counter()
+    assert np.array_equal(first, second)
+    assert r.inverse_cache_size() == 1
+    assert (t2 - t1) < (t1 - t0)  # the hit skips the inverse
+
+
+def _gf_matmul(mul, a, b):
+    """a (n x k) * b (k x m) over GF(2^8) with the mulTbl (gmu.go:26-28)."""
+    out = np.zeros((a.shape[0], b.shape[1]), np.uint8)
+    for t in range(a.shape[1]):
+        out ^= mul[a[:, t][:, None], b[t][None, :]]
+    return out
+
+
+def test_enc_matrix_invertible_random(rslib, orc):  # TestEncMatrixInvertibleRandom matrix_test.go:202-241
+    """One random survivor subset for a spread of d+p <= 256 shapes: the
+    reconst matrix times the survivors' encoding rows is the identity."""
+    mul = orc.tables()["mul"]
+    rng = np.random.default_rng(14)
+    shapes = [(1, 1), (1, 255), (255, 1), (128, 128), (200, 56), (17, 3)]
+    shapes += [(int(d), int(rng.integers(1, 257 - d))) for d in rng.integers(1, 255, 24)]
+    for d, p in shapes:
+        r = rslib.New(d, p)
+        em = r.encMatrix.reshape(d + p, d)
+        surv = sorted(rng.choice(d + p, d, replace=False).tolist())
+        need = list(range(d))
+        inv = r.reconst_matrix(surv, need).reshape(d, d)
+        assert np.array_equal(_gf_matmul(mul, inv, em[surv]), np.eye(d, dtype=np.uint8)), (d, p)
