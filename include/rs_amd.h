@@ -204,6 +204,26 @@ RS_API int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_str
 RS_API int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                 int nstripes, size_t len, int stripes_per_chunk, int streams);
 
+/* ------------------------------------------------------------------------
+ * Several GPUs from one process: a group holds one codec per
+ * device.  Batched calls split the stripes into contiguous slices, one per
+ * device, and run the slices concurrently (one host thread per device); they
+ * return when every device is done, with the first error seen.  Stripes are
+ * independent, so there is no inter-GPU traffic.  A device may be listed
+ * more than once (two codecs sharing it).
+ * ------------------------------------------------------------------------ */
+typedef struct rs_group rs_group_t;
+RS_API int  rs_group_new(int data_num, int parity_num, const int* devices, int ndev, rs_group_t** out);
+RS_API void rs_group_free(rs_group_t* g);
+RS_API int  rs_group_size(const rs_group_t* g);
+/* The codec of member i (borrowed; valid until rs_group_free), for
+ * device-resident calls on that member's device. */
+RS_API rs_t* rs_group_codec(rs_group_t* g, int i);
+/* rs_encode_host_batch over the group: stripes [0, nstripes) of one host
+ * buffer split across the members. */
+RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                                      int nstripes, size_t len, int stripes_per_chunk, int streams);
+
 /* Page-lock / unlock caller memory for DMA (hipHostRegister). */
 RS_API int rs_host_register(void* ptr, size_t bytes);
 RS_API int rs_host_unregister(void* ptr);

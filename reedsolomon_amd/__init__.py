@@ -6,7 +6,7 @@ vector byte processed by hand-written CDNA4 HIP kernels (librsamd.so).
 See DESIGN.md and include/rs_amd.h.
 """
 from .rs import (  # noqa: F401
-    RS, New, RSError, ErrIllegalVects, ErrMismatchVects, ErrZeroVectSize, ErrMismatchVectSize,
+    RS, New, Group, NewGroup, RSError, ErrIllegalVects, ErrMismatchVects, ErrZeroVectSize, ErrMismatchVectSize,
     ErrNoNeedReconst, ErrTooManyLost, ErrMismatchParityNum, ErrIllegalVectIndex, ErrTooManyReplace,
     ErrMismatchReplace, ErrNotSquare, ErrSingularMatrix, ErrInvalidArgument, ErrDevice, ErrNoMemory,
     invert, inverse_cache_key, gf_mul, device_count, host_register, host_unregister,

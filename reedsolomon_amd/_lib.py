@@ -66,6 +66,11 @@ SIGNATURES = {
     "rs_replace_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_intp, c_int, c_void, c_i64, c_i64, c_int, c_sz,
                                  c_void]),
     "rs_encode_host_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_int, c_int]),
+    "rs_group_new": (c_int, [c_int, c_int, c_intp, c_int, ctypes.POINTER(c_void)]),
+    "rs_group_free": (None, [c_void]),
+    "rs_group_size": (c_int, [c_void]),
+    "rs_group_codec": (c_void, [c_void, c_int]),
+    "rs_group_encode_host_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_int, c_int]),
     "rs_host_register": (c_int, [c_void, c_sz]),
     "rs_host_unregister": (c_int, [c_void]),
     "rs_xor_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_void, c_i64, c_int, c_sz, c_void]),

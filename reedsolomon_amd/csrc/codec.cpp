@@ -20,6 +20,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1397,6 +1398,70 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             if (e) (void)hipEventDestroy(e);
     (void)hipFree(ring);
     return rc;
+}
+
+// ---------------------------------------------------------------- device groups
+
+struct rs_group {
+    std::vector<rs_t*> members;
+};
+
+int rs_group_new(int data_num, int parity_num, const int* devices, int ndev, rs_group_t** out) {
+    if (!out) return RS_ERR_INVAL;
+    *out = nullptr;
+    if (ndev <= 0 || ndev > 1024 || !devices) return RS_ERR_INVAL;
+    rs_group_t* g = new (std::nothrow) rs_group();
+    if (!g) return RS_ERR_NOMEM;
+    for (int i = 0; i < ndev; ++i) {
+        rs_t* r = nullptr;
+        int rc = devices[i] < 0 ? RS_ERR_INVAL : rs_new(data_num, parity_num, devices[i], &r);
+        if (rc) {
+            rs_group_free(g);
+            return rc;
+        }
+        g->members.push_back(r);
+    }
+    *out = g;
+    return RS_OK;
+}
+
+void rs_group_free(rs_group_t* g) {
+    if (!g) return;
+    for (rs_t* r : g->members) rs_free(r);
+    delete g;
+}
+
+int rs_group_size(const rs_group_t* g) { return g ? static_cast<int>(g->members.size()) : 0; }
+
+rs_t* rs_group_codec(rs_group_t* g, int i) {
+    return g && i >= 0 && i < static_cast<int>(g->members.size()) ? g->members[i] : nullptr;
+}
+
+int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                               int nstripes, size_t len, int stripes_per_chunk, int streams) {
+    if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    const int n = static_cast<int>(g->members.size());
+    std::vector<int> rc(n, RS_OK);
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; ++i) {
+        const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
+        const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+        if (hi <= lo) continue;
+        auto job = [&, i, lo, hi] {
+            rc[i] = rs_encode_host_batch(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
+                                         stripe_stride, vect_stride, hi - lo, len, stripes_per_chunk, streams);
+        };
+        try {
+            th.emplace_back(job);
+        } catch (...) {
+            job();  // no thread available: run this slice here
+        }
+    }
+    for (std::thread& t : th) t.join();
+    for (int r : rc)
+        if (r) return r;
+    return RS_OK;
 }
 
 // ---------------------------------------------------------------- XOR primitive

@@ -169,9 +169,10 @@ def _stream(stream) -> ctypes.c_void_p:
 class RS:
     """Reed-Solomon encoder/decoder (rs.go:22-42).  Create with :func:`New`."""
 
-    def __init__(self, handle: ctypes.c_void_p, device: int):
+    def __init__(self, handle: ctypes.c_void_p, device: int, owner=None):
         self._h = handle
         self.device = device
+        self._owner = owner  # a Group keeps borrowed member handles alive
         L = lib()
         self.DataNum = L.rs_data_num(handle)
         self.ParityNum = L.rs_parity_num(handle)
@@ -185,7 +186,7 @@ class RS:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and getattr(self, "_owner", None) is None:
             try:
                 lib().rs_free(h)
             except Exception:
@@ -330,18 +331,7 @@ class RS:
         """Encode stripes held in HOST memory: buf is a [S, d+p, len] uint8
         numpy array or CPU torch tensor (pin it for full PCIe rate).  Pipelined
         H2D -> encode -> D2H; returns when parity is back in host memory."""
-        import numpy as _np
-
-        if isinstance(buf, _np.ndarray):
-            if buf.dtype != _np.uint8 or buf.ndim != 3 or buf.strides[2] != 1:
-                raise TypeError("expected a [stripes, d+p, len] uint8 array with unit inner stride")
-            ptr, ss, vs, S, n = buf.ctypes.data, buf.strides[0], buf.strides[1], buf.shape[0], buf.shape[2]
-        else:
-            if buf.dtype.__str__() != "torch.uint8" or buf.is_cuda or buf.dim() != 3 or buf.stride(2) != 1:
-                raise TypeError("expected a [stripes, d+p, len] uint8 CPU tensor with unit inner stride")
-            ptr, ss, vs, S, n = buf.data_ptr(), buf.stride(0), buf.stride(1), buf.shape[0], buf.shape[2]
-        if buf.shape[1] < self.DataNum + self.ParityNum:
-            raise TypeError("buffer holds fewer than d+p vectors per stripe")
+        ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
         _check(lib().rs_encode_host_batch(self._h, ctypes.c_void_p(ptr), ss, vs, S, n, int(stripes_per_chunk),
                                           int(streams)))
 
@@ -401,6 +391,63 @@ def _check_tensor_any(t) -> None:
 
     if not isinstance(t, torch.Tensor) or t.dtype != torch.uint8 or not t.is_cuda:
         raise TypeError("expected a torch.uint8 tensor on a GPU")
+
+
+def _host_batch(buf, nvec: int):
+    """(address, stripe stride, vector stride, stripes, len) of a [S, >=nvec, len]
+    uint8 host array (numpy, or a CPU torch tensor)."""
+    if isinstance(buf, np.ndarray):
+        if buf.dtype != np.uint8 or buf.ndim != 3 or buf.strides[2] != 1:
+            raise TypeError("expected a [stripes, d+p, len] uint8 array with unit inner stride")
+        ptr, ss, vs, S, n = buf.ctypes.data, buf.strides[0], buf.strides[1], buf.shape[0], buf.shape[2]
+    else:
+        if str(buf.dtype) != "torch.uint8" or buf.is_cuda or buf.dim() != 3 or buf.stride(2) != 1:
+            raise TypeError("expected a [stripes, d+p, len] uint8 CPU tensor with unit inner stride")
+        ptr, ss, vs, S, n = buf.data_ptr(), buf.stride(0), buf.stride(1), buf.shape[0], buf.shape[2]
+    if buf.shape[1] < nvec:
+        raise TypeError("buffer holds fewer than d+p vectors per stripe")
+    return ptr, ss, vs, S, n
+
+
+class Group:
+    """One codec per device for a process that drives several GPUs
+    (rs_group_*).  Create with :func:`NewGroup`."""
+
+    def __init__(self, handle: ctypes.c_void_p, devices):
+        self._g = handle
+        self.devices = list(devices)
+        L = lib()
+        self.members = [RS(ctypes.c_void_p(L.rs_group_codec(handle, i)), dv, owner=self)
+                        for i, dv in enumerate(self.devices)]
+        self.DataNum, self.ParityNum = self.members[0].DataNum, self.members[0].ParityNum
+
+    def __len__(self) -> int:
+        return lib().rs_group_size(self._g)
+
+    def encode_host_batch(self, buf, stripes_per_chunk: int = 4, streams: int = 3) -> None:
+        """RS.encode_host_batch with the stripes split across the group's devices."""
+        ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
+        _check(lib().rs_group_encode_host_batch(self._g, ctypes.c_void_p(ptr), ss, vs, S, n,
+                                                int(stripes_per_chunk), int(streams)))
+
+    def __del__(self):
+        g = getattr(self, "_g", None)
+        if g:
+            for m in getattr(self, "members", []):
+                m._h = None
+            try:
+                lib().rs_group_free(g)
+            except Exception:
+                pass
+            self._g = None
+
+
+def NewGroup(dataNum: int, parityNum: int, devices) -> Group:
+    devs = [int(x) for x in devices]
+    arr = (ctypes.c_int * max(len(devs), 1))(*devs)
+    h = ctypes.c_void_p()
+    _check(lib().rs_group_new(int(dataNum), int(parityNum), arr, len(devs), ctypes.byref(h)))
+    return Group(h, devs)
 
 
 def New(dataNum: int, parityNum: int, device: int = -1) -> RS:

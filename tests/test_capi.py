@@ -242,3 +242,17 @@ def test_enc_matrix_invertible_random(rslib, orc):  # TestEncMatrixInvertibleRan
         need = list(range(d))
         inv = r.reconst_matrix(surv, need).reshape(d, d)
         assert np.array_equal(_gf_matmul(mul, inv, em[surv]), np.eye(d, dtype=np.uint8)), (d, p)
+
+
+def test_group_handles(rslib):
+    """rs_group_* (one codec per device) needs no GPU until a call runs."""
+    g = rslib.NewGroup(10, 4, [0, 0, 3])
+    assert len(g) == 3 and [m.device for m in g.members] == [0, 0, 3]
+    assert all(np.array_equal(m.GenMatrix, g.members[0].GenMatrix) for m in g.members)
+    for bad in ([], [-1]):
+        with pytest.raises(rslib.ErrInvalidArgument):
+            rslib.NewGroup(10, 4, bad)
+    with pytest.raises(rslib.ErrIllegalVects):
+        rslib.NewGroup(200, 57, [0])
+    L = rslib.lib()
+    assert L.rs_group_codec(g._g, 3) is None and L.rs_group_codec(g._g, -1) is None

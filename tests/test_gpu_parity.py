@@ -607,3 +607,22 @@ def test_host_calls_staging_paths(rslib, orc, torch_dev, mode):
     finally:
         for k, v in {"host_chunk": 256 << 10, "host_zc_max": -1, "host_pinned_max": 256 << 10}.items():
             L.rs_tune(k.encode(), v)
+
+
+def test_group_encode_host_batch(rslib, torch_dev):
+    """rs_group_encode_host_batch: stripes split over the members (here two
+    codecs sharing cuda:0, plus a ragged split), parity identical to one
+    device-resident encode."""
+    torch = torch_dev
+    d, p, S, n = 10, 4, 37, 65536 + 256
+    g = torch.Generator(device="cuda").manual_seed(21)
+    ref = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
+    host = ref.cpu()
+    host[:, d:] = 0xA5
+    rslib.New(d, p).encode_batch(ref)
+    torch.cuda.synchronize()
+    for devs in ([0], [0, 0], [0, 0, 0]):
+        h = host.clone()
+        grp = rslib.NewGroup(d, p, devs)
+        grp.encode_host_batch(h, 4, 3)
+        assert torch.equal(h, ref.cpu()), devs
