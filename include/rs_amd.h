@@ -224,9 +224,28 @@ RS_API rs_t* rs_group_codec(rs_group_t* g, int i);
 RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                       int nstripes, size_t len, int stripes_per_chunk, int streams);
 
-/* Page-lock / unlock caller memory for DMA (hipHostRegister). */
+/* Page-lock / unlock caller memory (hipHostRegister, mapped + portable).
+ * Registered (or hipHostMalloc'd) memory is device-addressable: the host
+ * batch entry points then run their kernels straight over it (zero-copy,
+ * no staging): 72 GiB/s for 10+4 encode on one MI355X vs 57 GiB/s through
+ * the DMA pipeline used for pageable memory. */
 RS_API int rs_host_register(void* ptr, size_t bytes);
 RS_API int rs_host_unregister(void* ptr);
+/* Device address of host range [host_ptr, host_ptr+bytes) if all of it is
+ * pinned / registered and device-mapped; RS_ERR_INVAL for pageable memory.
+ * The result may be passed to every device / batch entry point above. */
+RS_API int rs_host_device_pointer(const void* host_ptr, size_t bytes, void** dev_ptr);
+
+/* Reconst of a host-resident batch, a different erasure set per stripe
+ * (need_masks as in rs_reconst_batch_multi): stripe s, vector v at
+ * base + s*stripe_stride + v*vect_stride (data 0..d-1, then parity).  The
+ * memory must be pinned / registered (zero-copy; RS_ERR_INVAL otherwise).
+ * Synchronous. */
+RS_API int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                                       int nstripes, size_t len, const uint64_t* need_masks);
+RS_API int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stripe_stride,
+                                             int64_t vect_stride, int nstripes, size_t len,
+                                             const uint64_t* need_masks);
 
 /* ------------------------------------------------------------------------
  * Generic GF(2^8) matrix product over device vectors — the primitive all of
@@ -281,7 +300,7 @@ RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad", "stage_late",
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
- * host-memory call staging).  Returns
+ * host-memory call staging), "host_batch_zc" (0/1).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name. */
 RS_API int rs_tune(const char* name, int value);
 

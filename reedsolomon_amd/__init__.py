@@ -9,7 +9,7 @@ from .rs import (  # noqa: F401
     RS, New, Group, NewGroup, RSError, ErrIllegalVects, ErrMismatchVects, ErrZeroVectSize, ErrMismatchVectSize,
     ErrNoNeedReconst, ErrTooManyLost, ErrMismatchParityNum, ErrIllegalVectIndex, ErrTooManyReplace,
     ErrMismatchReplace, ErrNotSquare, ErrSingularMatrix, ErrInvalidArgument, ErrDevice, ErrNoMemory,
-    invert, inverse_cache_key, gf_mul, device_count, host_register, host_unregister,
+    invert, inverse_cache_key, gf_mul, device_count, host_register, host_unregister, host_device_pointer,
 )
 from ._lib import lib, LIB_PATH  # noqa: F401
 

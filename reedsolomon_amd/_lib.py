@@ -71,6 +71,11 @@ SIGNATURES = {
     "rs_group_size": (c_int, [c_void]),
     "rs_group_codec": (c_void, [c_void, c_int]),
     "rs_group_encode_host_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_int, c_int]),
+    "rs_group_reconst_host_batch_multi": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
+                                                  ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_reconst_host_batch_multi": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
+                                            ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_host_device_pointer": (c_int, [c_void, c_sz, ctypes.POINTER(c_void)]),
     "rs_host_register": (c_int, [c_void, c_sz]),
     "rs_host_unregister": (c_int, [c_void]),
     "rs_xor_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_void, c_i64, c_int, c_sz, c_void]),

@@ -292,9 +292,7 @@ class RS:
         (data in [S, d, len], parity in [S, p, len]; the interleaved buffer can be passed as
         data=buf[:, :d], parity=buf[:, d:])."""
         L, S, n = self._split_layout(data, parity)
-        masks = np.ascontiguousarray(np.asarray(need_masks, dtype=np.uint64))
-        if masks.shape != (S,):
-            raise TypeError("need_masks must hold one mask per stripe")
+        masks = _masks(need_masks, S)
         _check(lib().rs_reconst_batch_multi(self._h, ctypes.byref(L), S, n,
                                             masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _stream(stream)))
 
@@ -334,6 +332,14 @@ class RS:
         ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
         _check(lib().rs_encode_host_batch(self._h, ctypes.c_void_p(ptr), ss, vs, S, n, int(stripes_per_chunk),
                                           int(streams)))
+
+    def reconst_host_batch_multi(self, buf, need_masks) -> None:
+        """Reconst a pinned host batch [S, d+p, len] in place, need_masks[s] =
+        bitmap of the vectors of stripe s to rebuild (zero-copy kernels)."""
+        ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
+        masks = _masks(need_masks, S)
+        _check(lib().rs_reconst_host_batch_multi(self._h, ctypes.c_void_p(ptr), ss, vs, S, n,
+                                                 masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
 
     def xor_batch(self, src, dst, stream=None) -> None:
         """dst[s] = src[s, 0] ^ src[s, 1] ^ ... (xorsimd xor.Encode) for [S, n, len] / [S, len] GPU tensors."""
@@ -409,6 +415,20 @@ def _host_batch(buf, nvec: int):
     return ptr, ss, vs, S, n
 
 
+def _masks(need_masks, S: int) -> np.ndarray:
+    masks = np.ascontiguousarray(np.asarray(need_masks, dtype=np.uint64))
+    if masks.shape != (S,):
+        raise TypeError("need_masks must hold one mask per stripe")
+    return masks
+
+
+def host_device_pointer(ptr: int, nbytes: int) -> int:
+    """Device address of a pinned / registered host range (rs_host_device_pointer)."""
+    d = ctypes.c_void_p()
+    _check(lib().rs_host_device_pointer(ctypes.c_void_p(int(ptr)), int(nbytes), ctypes.byref(d)))
+    return int(d.value)
+
+
 class Group:
     """One codec per device for a process that drives several GPUs
     (rs_group_*).  Create with :func:`NewGroup`."""
@@ -429,6 +449,13 @@ class Group:
         ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
         _check(lib().rs_group_encode_host_batch(self._g, ctypes.c_void_p(ptr), ss, vs, S, n,
                                                 int(stripes_per_chunk), int(streams)))
+
+    def reconst_host_batch_multi(self, buf, need_masks) -> None:
+        """RS.reconst_host_batch_multi with the stripes split across the group's devices."""
+        ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
+        masks = _masks(need_masks, S)
+        _check(lib().rs_group_reconst_host_batch_multi(self._g, ctypes.c_void_p(ptr), ss, vs, S, n,
+                                                       masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
 
     def __del__(self):
         g = getattr(self, "_g", None)

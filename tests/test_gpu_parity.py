@@ -443,8 +443,61 @@ def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
         assert np.array_equal(a[:, d:], exp)
         assert np.array_equal(a[:, :d], host[:, :d])
         pinned = torch.from_numpy(host.copy()).pin_memory()
-        r.encode_host_batch(pinned, spc, st)
+        r.encode_host_batch(pinned, spc, st)  # zero-copy: kernels straight over pinned memory
         assert np.array_equal(pinned.numpy()[:, d:], exp)
+        L = rslib.lib()
+        assert L.rs_tune(b"host_batch_zc", 0) == 0
+        try:
+            pinned = torch.from_numpy(host.copy()).pin_memory()
+            r.encode_host_batch(pinned, spc, st)  # DMA pipeline over pinned memory
+            assert np.array_equal(pinned.numpy()[:, d:], exp)
+        finally:
+            L.rs_tune(b"host_batch_zc", 1)
+
+
+def test_host_batch_zero_copy(rslib, orc, torch_dev):
+    """Zero-copy host batches: registered numpy memory (rs_host_register),
+    multi-pattern Reconst in place on pinned memory (single and group), and
+    a clean RS_ERR_INVAL (no kernel) for pageable memory."""
+    torch = torch_dev
+    d, p, S, n = 10, 4, 33, 8192 + 16
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(122)
+    host = _rand(rng, S, d + p, n)
+    exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
+    # registered pageable numpy buffer -> device-mapped
+    reg = host.copy()
+    rslib.host_register(reg.ctypes.data, reg.nbytes)
+    try:
+        dp = rslib.host_device_pointer(reg.ctypes.data, reg.nbytes)
+        assert dp != 0
+        r.encode_host_batch(reg)
+        assert np.array_equal(reg[:, d:], exp)
+    finally:
+        rslib.host_unregister(reg.ctypes.data)
+    full = host.copy()
+    full[:, d:] = exp
+    masks = np.zeros(S, np.uint64)
+    for s in range(S):
+        for v in rng.choice(d + p, int(rng.integers(0, p + 1)), replace=False):
+            masks[s] |= np.uint64(1) << np.uint64(int(v))
+    broken = full.copy()
+    for s in range(S):
+        for v in range(d + p):
+            if int(masks[s]) >> v & 1:
+                broken[s, v] = 0xEE
+    pinned = torch.from_numpy(broken.copy()).pin_memory()
+    r.reconst_host_batch_multi(pinned, masks)
+    assert np.array_equal(pinned.numpy(), full)
+    pinned = torch.from_numpy(broken.copy()).pin_memory()
+    rslib.NewGroup(d, p, [0, 0]).reconst_host_batch_multi(pinned, masks)
+    assert np.array_equal(pinned.numpy(), full)
+    pageable = broken.copy()
+    with pytest.raises(rslib.ErrInvalidArgument):
+        r.reconst_host_batch_multi(pageable, masks)
+    with pytest.raises(rslib.ErrInvalidArgument):
+        rslib.host_device_pointer(pageable.ctypes.data, pageable.nbytes)
+    assert np.array_equal(pageable, broken)
 
 
 def test_split_layout_encode_reconst(rslib, orc, torch_dev):
