@@ -9,12 +9,12 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
-    python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 > "$OUT/kt_bench.log" 2>&1
+    python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --e2e-stripes 0 > "$OUT/kt_bench.log" 2>&1
 tail -1 "$OUT/kt_bench.log"
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C"
   timeout -k 10 400 rocprofv3 --pmc "$C" -d "$OUT/pmc_$C" -o pmc --output-format csv -- \
-      python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --steps 5 --warmup 1 --verify 0 > "$OUT/pmc_$C.log" 2>&1
+      python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --e2e-stripes 0 --steps 5 --warmup 1 --verify 0 > "$OUT/pmc_$C.log" 2>&1
   tail -1 "$OUT/pmc_$C.log" | cut -c1-200
 done
 find "$OUT" -name "*.csv" | head -20
