@@ -131,7 +131,57 @@ __global__ __launch_bounds__(256) void kb_pattern(const uint8_t* dbase, uint8_t*
     }
 }
 
+// 10+4 split pattern with UPL 4 KiB units per vector per workgroup (UPL=2:
+// 8 KiB, 4: 16 KiB) and an optional XCD-aware block order (XCD=1: the 8
+// round-robin XCDs each walk one contiguous eighth of the chunks).
+template <int K, int M, int UPL, int XCD>
+__global__ __launch_bounds__(256) void kb_pattern_u(const uint8_t* dbase, uint8_t* pbase, uint64_t vec, uint64_t dss,
+                                                    uint64_t pss, uint64_t cps, uint32_t nblocks) {
+    uint32_t b = blockIdx.x;
+    if (XCD) b = (b % 8) * (nblocks / 8) + b / 8;  // nblocks % 8 == 0 (host checks)
+    const uint64_t s = b / cps, cb = b % cps;
+    u32x4 x[K][UPL];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int u = 0; u < UPL; ++u)
+            x[i][u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(dbase + s * dss + i * vec, (uint32_t)vec),
+                                                            (uint32_t)((cb * UPL + u) * 4096 + threadIdx.x * 16), 0, 2);
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int u = 0; u < UPL; ++u) {
+            u32x4 a = {(uint32_t)j, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < K; ++i) a ^= x[i][u];
+            __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(pbase + s * pss + j * vec, (uint32_t)vec),
+                                                   (uint32_t)((cb * UPL + u) * 4096 + threadIdx.x * 16), 0, 2);
+        }
+}
+
 extern "C" {
+// kind: 0 UPL1, 1 UPL2, 2 UPL4, +4 = XCD-aware order.  10+4 split layout.
+int probe_buf_u(int kind, void* a, void* b, uint64_t vec, int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int upl = 1 << (kind & 3);
+    const uint64_t cps = vec / (4096ull * upl);
+    const uint32_t nb = (uint32_t)(cps * nstripes);
+    if (nb % 8) return -2;
+#define KU(U, X) hipLaunchKernelGGL((kb_pattern_u<10, 4, U, X>), dim3(nb), dim3(256), 0, st, (const uint8_t*)a, \
+                                    (uint8_t*)b, vec, 10 * vec, 4 * vec, cps, nb)
+    switch (kind) {
+        case 0: KU(1, 0); break;
+        case 1: KU(2, 0); break;
+        case 2: KU(4, 0); break;
+        case 4: KU(1, 1); break;
+        case 5: KU(2, 1); break;
+        case 6: KU(4, 1); break;
+        default: return -1;
+    }
+#undef KU
+    return hipGetLastError();
+}
+
 int probe_buf(int kind, void* a, void* b, uint64_t bytes, uint64_t vec, int nstripes, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (kind == 0) hipLaunchKernelGGL(kb_copy, dim3(bytes / 4096), dim3(256), 0, st, (const uint8_t*)a, (uint8_t*)b, 4096ull);

@@ -70,6 +70,18 @@ def basic_probes(L, a, b, n, vp, sp, timeit):
 
 
 def pattern_probes(L, a, n, vp, sp, timeit):
+    if os.environ.get("PROBE_UPL", "0") == "1":
+        # 10+4 split pattern: 4/8/16 KiB per vector per workgroup, natural vs XCD-aware order
+        import torch
+        vec, S = 1 << 20, 240
+        b = torch.empty(S * 4 * vec, dtype=torch.uint8, device="cuda")
+        assert S * 10 * vec <= n, "probe case out of bounds"
+        for _ in range(2):
+            for kind, name in ((0, "4KiB"), (1, "8KiB"), (2, "16KiB"), (4, "4KiB xcd"), (5, "8KiB xcd"),
+                               (6, "16KiB xcd")):
+                timeit(f"buffer nt 10+4 pattern {name}/vector/WG",
+                       lambda: L.probe_buf_u(kind, vp(a), vp(b), ctypes.c_uint64(vec), S, sp), S * 14 * vec)
+        return
     if os.environ.get("PROBE_RECON", "0") == "1":
         # Reconst ceilings: 10 reads + m writes per stripe, buffer nt, split regions.
         import torch
