@@ -1,0 +1,265 @@
+// codec_internal.hpp — internals shared by librsamd's host-side sources:
+//   codec.cpp         handle, matrices, inverse cache, checks, planning, small ABI
+//   host_calls.cpp    the synchronous host-memory calls (rs_encode ... rs_replace)
+//   batches.cpp       device-resident single-stripe and batched calls
+//   host_batches.cpp  host-resident batches, zero-copy, device groups
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rs_amd.h"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+#define RS_TRY(x)                 \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
+    } while (0)
+
+namespace rsamd {
+namespace detail {
+
+constexpr int kMaxVects = 256;                              // rs.go:47
+constexpr uint64_t kMaxInverseCacheBytes = 16ull << 20;     // rs.go:50
+constexpr size_t kMaxRegistryEntries = 1 << 14;
+
+// ---------------------------------------------------------------- device helpers
+
+struct DeviceGuard {  // switch to the handle's device, restore the caller's on exit
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) return;
+        ok = (prev == dev) || hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (ok && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline uint64_t rup(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+
+}  // namespace detail
+}  // namespace rsamd
+
+// ---------------------------------------------------------------- the handle
+
+struct rs_codec {
+    int d = 0, p = 0;
+    std::vector<uint8_t> enc;  // (d+p) x d; GenMatrix = enc[d*d:]   rs.go:30-31,65-68
+
+    // inverse cache rs.go:33-39,70-74
+    bool cache_enabled = false;
+    uint64_t cache_max = 0;
+    std::atomic<uint64_t> cache_n{0};
+    std::mutex cache_mu;
+    std::unordered_map<uint64_t, std::vector<uint8_t>> cache;
+
+    // device state (created lazily; the handle works on a GPU-less host)
+    std::mutex dev_mu;
+    int device = -1;
+    bool device_ready = false;
+
+    std::mutex tab_mu;  // coefficient-table registry: matrix bytes -> device perm tables
+    std::map<std::string, uint32_t*> tables;
+
+    std::mutex stage_mu;  // staging for the host-memory entry points
+    uint8_t* stage = nullptr;
+    size_t stage_bytes = 0;
+    uint8_t* hstage = nullptr;  // pinned host mirror of `stage` (small-vector fast path)
+    size_t hstage_bytes = 0;
+    uint8_t* slots = nullptr;   // device staging slots of the staged (non-zero-copy) host path
+    bool zc_pending = false;    // a zero-copy kernel may still be using hstage
+    hipEvent_t chunk_ev[3] = {nullptr, nullptr, nullptr};  // host-call chunk pipeline slots
+    hipStream_t stream = nullptr;
+
+    // Upload ring for per-call device descriptors (multi-pattern Reconst):
+    // pinned host slot -> device slot on a private copy stream, so the copy
+    // for call n+1 overlaps call n's kernel instead of stalling the stream.
+    static constexpr int kUploadSlots = 4;
+    struct UploadSlot {
+        uint8_t* host = nullptr;
+        uint8_t* dev = nullptr;
+        size_t cap = 0;
+        hipEvent_t copied = nullptr, done = nullptr;
+        bool in_flight = false;
+    };
+    std::mutex up_mu;
+    UploadSlot up[kUploadSlots];
+    int up_next = 0;
+    hipStream_t up_stream = nullptr;
+
+    const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
+
+    ~rs_codec() {
+        if (!device_ready) return;
+        rsamd::detail::DeviceGuard g(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        (void)hipDeviceSynchronize();
+        for (auto& kv : tables) (void)hipFree(kv.second);
+        for (UploadSlot& u : up) {
+            if (u.host) (void)hipHostFree(u.host);
+            if (u.dev) (void)hipFree(u.dev);
+            if (u.copied) (void)hipEventDestroy(u.copied);
+            if (u.done) (void)hipEventDestroy(u.done);
+        }
+        if (up_stream) (void)hipStreamDestroy(up_stream);
+        if (stage) (void)hipFree(stage);
+        if (hstage) (void)hipHostFree(hstage);
+        for (hipEvent_t e : chunk_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace rsamd {
+namespace detail {
+
+// ---------------------------------------------------------------- matrix.go (codec.cpp)
+std::vector<uint8_t> make_encode_matrix(int d, int p);              // matrix.go:37-54
+int invert(const uint8_t* src, size_t len, int n, uint8_t* out);    // matrix.go:85-147
+uint64_t cache_key(const int* survived, int ns);                    // rs.go:414-420
+
+// ---------------------------------------------------------------- device product (codec.cpp)
+int ensure_device(rs_t* rs);
+int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t** out, int* rows_pad_out);
+int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs,
+              const uint8_t* in_sid, uint8_t* const* out_ptrs, const uint8_t* out_sid, const int64_t ss[4],
+              int nstripes, uint64_t len, bool accumulate, hipStream_t stream, const int32_t* stripe_ids = nullptr);
+int matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs, int64_t in_ss,
+           uint8_t* const* out_ptrs, int64_t out_ss, int nstripes, uint64_t len, bool accumulate,
+           hipStream_t stream);
+
+// One leased upload slot (see rs_codec::up).  Holds the ring lock from
+// acquire() until the consumer's kernels are enqueued; the destructor records
+// the slot's `done` event on the consumer stream.
+class UploadLease {
+public:
+    explicit UploadLease(rs_t* rs) : rs_(rs), lk_(rs->up_mu) {}
+    ~UploadLease() {
+        if (slot_ && st_) {
+            (void)hipEventRecord(slot_->done, st_);
+            slot_->in_flight = true;
+        }
+    }
+    // A pinned host buffer of `bytes` to fill (slot free for reuse on return).
+    int acquire(size_t bytes, uint8_t** host) {
+        rs_codec::UploadSlot& u = rs_->up[rs_->up_next];
+        rs_->up_next = (rs_->up_next + 1) % rs_codec::kUploadSlots;
+        if (!rs_->up_stream && hipStreamCreateWithFlags(&rs_->up_stream, hipStreamNonBlocking) != hipSuccess) {
+            rs_->up_stream = nullptr;
+            return RS_ERR_DEVICE;
+        }
+        if (u.in_flight) {  // the kernel that read this slot's device copy has finished
+            if (hipEventSynchronize(u.done) != hipSuccess) return RS_ERR_DEVICE;
+            u.in_flight = false;
+        }
+        if (!u.copied && (hipEventCreateWithFlags(&u.copied, hipEventDisableTiming) != hipSuccess ||
+                          hipEventCreateWithFlags(&u.done, hipEventDisableTiming) != hipSuccess))
+            return RS_ERR_DEVICE;
+        if (u.cap < bytes) {
+            if (u.host) (void)hipHostFree(u.host);
+            if (u.dev) (void)hipFree(u.dev);
+            u.host = nullptr;
+            u.dev = nullptr;
+            u.cap = 0;
+            size_t cap = (bytes + (size_t{64} << 10) - 1) & ~((size_t{64} << 10) - 1);
+            if (hipHostMalloc(reinterpret_cast<void**>(&u.host), cap, hipHostMallocDefault) != hipSuccess) {
+                u.host = nullptr;
+                return RS_ERR_NOMEM;
+            }
+            if (hipMalloc(reinterpret_cast<void**>(&u.dev), cap) != hipSuccess) {
+                (void)hipHostFree(u.host);
+                u.host = nullptr;
+                u.dev = nullptr;
+                return RS_ERR_NOMEM;
+            }
+            u.cap = cap;
+        }
+        slot_ = &u;
+        bytes_ = bytes;
+        *host = u.host;
+        return RS_OK;
+    }
+    // Copy the filled host buffer to the device and make `st` wait for it.
+    int upload(hipStream_t st, uint8_t** dev) {
+        st_ = st;
+        if (hipMemcpyAsync(slot_->dev, slot_->host, bytes_, hipMemcpyHostToDevice, rs_->up_stream) != hipSuccess ||
+            hipEventRecord(slot_->copied, rs_->up_stream) != hipSuccess ||
+            hipStreamWaitEvent(st, slot_->copied, 0) != hipSuccess)
+            return RS_ERR_DEVICE;
+        *dev = slot_->dev;
+        return RS_OK;
+    }
+
+private:
+    rs_t* rs_;
+    std::lock_guard<std::mutex> lk_;
+    rs_codec::UploadSlot* slot_ = nullptr;
+    hipStream_t st_ = nullptr;
+    size_t bytes_ = 0;
+};
+
+// Address of vector v (0..d+p) of stripe 0 and its stride selector under a layout.
+struct LayoutAddr {
+    const rs_layout_t* L;
+    int d;
+    uint8_t* ptr(int v) const {
+        return v < d ? L->data_base + v * L->data_vect_stride : L->parity_base + (v - d) * L->parity_vect_stride;
+    }
+    uint8_t sid(int v) const { return v < d ? 0 : 1; }
+};
+
+// ---------------------------------------------------------------- reference checks (codec.cpp)
+int check_encode(const rs_t* rs, const size_t* lens, int n);
+int check_encode_idx(const size_t* lens, const int* idx, int cnt);
+int check_vect_idx(const int* idx, int cnt, int n);
+int plan_reconst(const rs_t* rs, const int* survived, int ns, const int* need, int nn, int* vs, int* nvs,
+                 int* nr, int* nnr, int* dn);
+int get_inverse(rs_t* rs, const int* survived_d, std::vector<uint8_t>& inv);
+int reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out);
+int combined_matrix(rs_t* rs, const int* vs, const int* nr, int nnr, int dn, std::vector<uint8_t>& m);
+int check_update(const rs_t* rs, size_t old_len, size_t new_len, int row, const size_t* plens, int np);
+int check_replace(const rs_t* rs, const size_t* dlens, int nd, const int* rows, int nr, const size_t* plens,
+                  int np);
+std::vector<uint8_t> update_matrix(const rs_t* rs, int row);
+std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr);
+
+// Reconst on one stripe whose vectors are addressed by `ptr` (host staging
+// slots or caller device pointers).  Shared by rs_reconst / rs_reconst_dev /
+// rs_reconst_batch.  `before_parity` lets the host path copy the rebuilt data
+// back before the parity check runs (the reference returns the parity-pass
+// error with the data already rebuilt).
+struct ReconstPlan {
+    int vs[kMaxVects], nr[kMaxVects];
+    int nvs = 0, nnr = 0, dn = 0;
+};
+
+int check_reconst_passes(const rs_t* rs, const ReconstPlan& pl, const size_t* lens, int n, int* parity_rc);
+
+// ---------------------------------------------------------------- host calls (host_calls.cpp)
+extern size_t g_pinned_max, g_zc_max, g_chunk;
+int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+                 size_t size, bool accumulate);
+
+// ---------------------------------------------------------------- host batches (host_batches.cpp)
+extern int g_host_batch_zc;
+int host_device_range(const void* p, size_t bytes, uint8_t** dev);
+size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace detail
+}  // namespace rsamd

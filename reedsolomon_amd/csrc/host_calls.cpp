@@ -1,0 +1,312 @@
+// host_calls.cpp — the synchronous host-memory entry points (the Go API's
+// shape: rs_encode / rs_reconst / rs_update / rs_replace on caller vectors
+// in pageable host memory): column-chunked zero-copy staging through a
+// pinned mirror, or the staged DMA paths for large vectors.
+#include <algorithm>
+
+#include "host_pool.hpp"
+#include "codec_internal.hpp"
+
+using namespace rsamd;
+using namespace rsamd::detail;
+
+namespace rsamd {
+namespace detail {
+
+// ---------------------------------------------------------------- host staging
+
+// Vectors up to this size go through the pinned host mirror: the caller's
+// bytes are memcpy'd into pinned memory and each direction is ONE DMA over
+// contiguous slots, instead of one pageable copy (staged by the runtime) per
+// vector.  Larger vectors use the runtime's pipelined pageable copies.
+size_t g_pinned_max = 256 * 1024;
+// Host calls on vectors up to this size take the chunked zero-copy pipeline
+// (host_matmul: the kernel reads and writes the pinned mirror over PCIe, no
+// DMA set-up either way); larger ones the runtime's pageable copies, which
+// measured 7 % faster at 4 MiB (profiles/r01/host_latency.log).
+size_t g_zc_max = 2 * 1024 * 1024;
+
+bool use_pinned(rs_t* rs, int slots, size_t pitch) {
+    if (pitch > g_pinned_max) return false;
+    const size_t need = pitch * static_cast<size_t>(slots);
+    if (need <= rs->hstage_bytes) return true;
+    if (rs->hstage) {
+        (void)hipStreamSynchronize(rs->stream);
+        (void)hipHostFree(rs->hstage);
+        rs->hstage = nullptr;
+        rs->hstage_bytes = 0;
+        rs->zc_pending = false;
+    }
+    if (hipHostMalloc(reinterpret_cast<void**>(&rs->hstage), need, hipHostMallocDefault) != hipSuccess) return false;
+    rs->hstage_bytes = need;
+    return true;
+}
+
+// Device staging area of the staged host path: `slots` vectors of `pitch`
+// bytes (pitch 256-aligned so every slot takes the vector kernel), at
+// rs->slots.  Caller holds stage_mu.
+int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
+    *pitch = rup(size, 256);
+    const size_t need = *pitch * static_cast<size_t>(slots);
+    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+        return RS_ERR_DEVICE;
+    if (need > rs->stage_bytes) {
+        if (rs->stage) {
+            (void)hipStreamSynchronize(rs->stream);
+            (void)hipFree(rs->stage);
+            rs->stage = nullptr;
+            rs->stage_bytes = 0;
+        }
+        if (hipMalloc(&rs->stage, need) != hipSuccess) return RS_ERR_DEVICE;
+        rs->stage_bytes = need;
+    }
+    rs->slots = rs->stage;
+    return RS_OK;
+}
+
+// Host vectors src[0..n) (size bytes each) -> device staging slots
+// [first, first+n).  Caller holds stage_mu and called ensure_stage.
+int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots);
+int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots);
+
+int h2d(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
+    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
+    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+}
+int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE; }
+
+int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots) {
+    if (n <= 0) return RS_OK;
+    uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
+    if (use_pinned(rs, total_slots, pitch)) {
+        uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
+        for (int i = 0; i < n; ++i) std::memcpy(h + static_cast<size_t>(i) * pitch, src[i], size);
+        return h2d(rs, dev, h, static_cast<size_t>(n - 1) * pitch + size);
+    }
+    for (int i = 0; i < n; ++i) RS_TRY(h2d(rs, dev + static_cast<size_t>(i) * pitch, src[i], size));
+    return RS_OK;
+}
+
+// Device staging slots [first, first+n) -> host vectors dst[0..n); synchronous.
+int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots) {
+    if (n <= 0) return sync(rs);
+    const uint8_t* dev = rs->stage + static_cast<size_t>(first) * pitch;
+    if (use_pinned(rs, total_slots, pitch)) {
+        uint8_t* h = rs->hstage + static_cast<size_t>(first) * pitch;
+        RS_TRY(d2h(rs, h, dev, static_cast<size_t>(n - 1) * pitch + size));
+        RS_TRY(sync(rs));
+        for (int i = 0; i < n; ++i) std::memcpy(dst[i], h + static_cast<size_t>(i) * pitch, size);
+        return RS_OK;
+    }
+    for (int i = 0; i < n; ++i) RS_TRY(d2h(rs, dst[i], dev + static_cast<size_t>(i) * pitch, size));
+    return sync(rs);
+}
+
+
+// Column-chunk size of the host-call pipeline (bytes per vector per chunk).
+size_t g_chunk = 128 * 1024;
+// Total copy bytes of one chunk above which the staging copies are split
+// over the host copy pool.
+constexpr size_t kParallelCopyMin = 512 * 1024;
+
+// dst[i] <- src[i] (n vectors, len bytes each) on the copy pool, in
+// 64 KiB pieces so every thread gets work.
+void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t len) {
+    const size_t piece = 64 * 1024;
+    const size_t per = (len + piece - 1) / piece;
+    const size_t total = per * static_cast<size_t>(n);
+    if (len * static_cast<size_t>(n) < kParallelCopyMin || total <= 1) {
+        for (int i = 0; i < n; ++i) std::memcpy(dst[i], src[i], len);
+        return;
+    }
+    CopyPool::get().run(total, [&](size_t k) {
+        const size_t v = k / per, off = (k % per) * piece;
+        const size_t b = std::min(piece, len - off);
+        std::memcpy(dst[v] + off, src[v] + off, b);
+    });
+}
+
+// The synchronous host-memory product behind rs_encode / rs_reconst /
+// rs_update / rs_replace: dst[r] (=|^=) sum_c mat[r][c] x src[c], all host
+// pointers, `size` bytes each.  The vectors are cut into column chunks;
+// each chunk is copied into a slot of the pinned mirror (several host
+// threads), processed by the kernel straight out of the mirror over PCIe
+// (zero-copy: no DMA set-up), and copied back, with up to 3 chunks in
+// flight so copies overlap the GPU.  Caller holds stage_mu.
+int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+                size_t size, bool accumulate) {
+    const int nvec = rows + cols;
+    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+        return RS_ERR_DEVICE;
+    // chunk: <= g_chunk per vector and <= 8 MiB per slot, 4 KiB multiple
+    size_t C = rup(size, 256);
+    const size_t cap = std::max<size_t>(4096, std::min(g_chunk, (size_t{8} << 20) / nvec) & ~size_t{4095});
+    if (C > cap) C = cap;
+    const size_t nch = (size + C - 1) / C;
+    const int ns = nch > 1 ? 3 : 1;
+    const size_t slot = C * static_cast<size_t>(nvec);
+    if (rs->zc_pending) RS_TRY(sync(rs));
+    if (slot * ns > rs->hstage_bytes) {
+        if (rs->hstage) {
+            (void)hipHostFree(rs->hstage);
+            rs->hstage = nullptr;
+            rs->hstage_bytes = 0;
+        }
+        if (hipHostMalloc(reinterpret_cast<void**>(&rs->hstage), slot * ns, hipHostMallocDefault) != hipSuccess) {
+            rs->hstage = nullptr;
+            return RS_ERR_NOMEM;
+        }
+        rs->hstage_bytes = slot * ns;
+    }
+    void* dbase = nullptr;
+    if (hipHostGetDevicePointer(&dbase, rs->hstage, 0) != hipSuccess || !dbase) return RS_ERR_DEVICE;
+    for (int i = 0; i < ns; ++i)
+        if (!rs->chunk_ev[i] && hipEventCreateWithFlags(&rs->chunk_ev[i], hipEventDisableTiming) != hipSuccess) {
+            rs->chunk_ev[i] = nullptr;
+            return RS_ERR_DEVICE;
+        }
+    auto hslot = [&](size_t c, int v) { return rs->hstage + (c % ns) * slot + static_cast<size_t>(v) * C; };
+    auto dslot = [&](size_t c, int v) {
+        return static_cast<uint8_t*>(dbase) + (c % ns) * slot + static_cast<size_t>(v) * C;
+    };
+    auto clen = [&](size_t c) { return std::min(C, size - c * C); };
+    auto finish = [&](size_t c) -> int {  // wait for chunk c, copy its outputs back
+        if (hipEventSynchronize(rs->chunk_ev[c % ns]) != hipSuccess) return RS_ERR_DEVICE;
+        uint8_t* d[kMaxVects];
+        const uint8_t* h[kMaxVects];
+        for (int r = 0; r < rows; ++r) {
+            d[r] = dst[r] + c * C;
+            h[r] = hslot(c, cols + r);
+        }
+        parallel_copy(d, h, rows, clen(c));
+        return RS_OK;
+    };
+    int rc = RS_OK;
+    size_t done = 0;
+    for (size_t c = 0; c < nch && rc == RS_OK; ++c) {
+        if (c >= static_cast<size_t>(ns)) {
+            rc = finish(done++);
+            if (rc) break;
+        }
+        const size_t len = clen(c);
+        uint8_t* h[2 * kMaxVects];
+        const uint8_t* s_[2 * kMaxVects];
+        int n = 0;
+        for (int i = 0; i < cols; ++i, ++n) {
+            h[n] = hslot(c, i);
+            s_[n] = src[i] + c * C;
+        }
+        if (accumulate)
+            for (int r = 0; r < rows; ++r, ++n) {
+                h[n] = hslot(c, cols + r);
+                s_[n] = dst[r] + c * C;
+            }
+        parallel_copy(h, s_, n, len);
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        for (int i = 0; i < cols; ++i) in[i] = dslot(c, i);
+        for (int r = 0; r < rows; ++r) out[r] = dslot(c, cols + r);
+        rs->zc_pending = true;
+        rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, len, accumulate, rs->stream);
+        if (rc == RS_OK && hipEventRecord(rs->chunk_ev[c % ns], rs->stream) != hipSuccess) rc = RS_ERR_DEVICE;
+    }
+    while (rc == RS_OK && done < nch) rc = finish(done++);
+    if (rc) (void)hipStreamSynchronize(rs->stream);  // never leave a kernel on the mirror
+    rs->zc_pending = false;
+    return rc;
+}
+
+// Host-call dispatcher: the chunked zero-copy pipeline (default), or the
+// older staged paths (device staging + pinned DMA or pageable copies) for
+// vectors above host_zc_max (kept for A/B).
+int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+                 size_t size, bool accumulate) {
+    if (size <= g_zc_max) return host_matmul(rs, mat, rows, cols, src, dst, size, accumulate);
+    size_t pitch = 0;
+    RS_TRY(ensure_stage(rs, cols + rows, size, &pitch));
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    const uint8_t* s_[2 * kMaxVects];
+    for (int i = 0; i < cols; ++i) {
+        in[i] = rs->slots + static_cast<size_t>(i) * pitch;
+        s_[i] = src[i];
+    }
+    for (int r = 0; r < rows; ++r) {
+        out[r] = rs->slots + static_cast<size_t>(cols + r) * pitch;
+        s_[cols + r] = dst[r];
+    }
+    RS_TRY(stage_in(rs, s_, accumulate ? cols + rows : cols, size, pitch, 0, cols + rows));
+    RS_TRY(matmul(rs, mat, rows, cols, in, 0, out, 0, 1, size, accumulate, rs->stream));
+    return stage_out(rs, dst, rows, size, pitch, cols, cols + rows);
+}
+
+}  // namespace detail
+}  // namespace rsamd
+
+extern "C" {
+
+int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
+    if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
+    RS_TRY(check_encode(rs, lens, n));
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    return host_product(rs, rs->gen(), rs->p, rs->d, vects, vects + rs->d, lens[0], false);
+}
+
+int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
+               const int* need, int nn) {
+    if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+    ReconstPlan pl;
+    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;  // rs.go:225-228
+    if (rc) return rc;
+    if (!vects || !lens) return RS_ERR_INVAL;
+    const int d = rs->d;
+    int parity_rc = RS_OK;
+    RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
+    const int rows = parity_rc ? pl.dn : pl.nnr;  // see rs_reconst_dev
+    if (rows > 0) {
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        std::lock_guard<std::mutex> lk(rs->stage_mu);
+        const uint8_t* src[kMaxVects];
+        uint8_t* dst[kMaxVects];
+        for (int i = 0; i < d; ++i) src[i] = vects[pl.vs[i]];
+        for (int i = 0; i < rows; ++i) dst[i] = vects[pl.nr[i]];
+        std::vector<uint8_t> m;
+        RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
+        RS_TRY(host_product(rs, m.data(), rows, d, src, dst, lens[pl.vs[0]], false));
+    }
+    return parity_rc;
+}
+
+int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
+              uint8_t* const* parity, const size_t* parity_lens, int np) {
+    if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
+    RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
+    if (!old_data || !new_data) return RS_ERR_INVAL;
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    const uint8_t* src[2] = {old_data, new_data};
+    std::vector<uint8_t> gm = update_matrix(rs, row);
+    return host_product(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
+}
+
+int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows, int nr,
+               uint8_t* const* parity, const size_t* parity_lens, int np) {
+    if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
+        (np > 0 && (!parity || !parity_lens)))
+        return RS_ERR_INVAL;
+    RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+    return host_product(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
+}
+
+}  // extern "C"
