@@ -36,6 +36,7 @@ namespace rsamd {
 
 constexpr int kBlock = 256;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;        // global (HBM) 16-byte word
 typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;  // LDS 16-byte word
 
@@ -55,6 +56,11 @@ LaunchTuning& tuning() {
         x.lds_pad = l ? std::atoi(l) : 0;
         const char* sl = std::getenv("RSAMD_STAGE_LATE");
         x.stage_late = sl ? std::atoi(sl) : 0;
+        const char* lb = std::getenv("RSAMD_LANE_BYTES");
+        x.lane_bytes = lb ? std::atoi(lb) : 0;  // 0: per launch (lane16_for)
+        const char* v1 = std::getenv("RSAMD_VPT1");
+        x.vpt1 = (v1 && std::atoi(v1) == 2) ? 2 : 1;
+
         return x;
     }();
     return t;
@@ -114,26 +120,44 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // on gfx950); -1 keeps global_load/store (nt per VAR / nt_store).  The buffer
 // descriptor is built from wave-uniform values (kernarg pointer + stripe
 // base), so no waterfall loop is generated (cdna_hip_programming.md T20).
-template <int AUX>
-__device__ __forceinline__ u32x4 load16(const g_u8* base, uint64_t off, uint32_t nbytes, bool nt) {
+template <int LQ> struct LaneWord;
+template <> struct LaneWord<4> { typedef u32x4 type; };
+template <> struct LaneWord<2> { typedef u32x2 type; };
+
+// 4*LQ-byte load / store of vector data (LQ = 4: dwordx4, LQ = 2: dwordx2).
+// AUX >= 0 selects buffer instructions with that cache-policy immediate (bit0
+// sc0, bit1 nt, bit4 sc1 on gfx950); -1 keeps global_load/store (nt per VAR /
+// nt_store).  The buffer descriptor is built from wave-uniform values
+// (kernarg pointer + stripe base), so no waterfall loop is generated
+// (cdna_hip_programming.md T20).
+template <int AUX, int LQ = 4>
+__device__ __forceinline__ typename LaneWord<LQ>::type load16(const g_u8* base, uint64_t off, uint32_t nbytes,
+                                                              bool nt) {
+    typedef typename LaneWord<LQ>::type W;
     if constexpr (AUX >= 0) {
         __amdgpu_buffer_rsrc_t r =
             __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, static_cast<int>(nbytes), 0x00020000);
-        return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, AUX);
+        if constexpr (LQ == 4) return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, AUX);
+        else return __builtin_amdgcn_raw_buffer_load_b64(r, static_cast<int>(off), 0, AUX);
     } else {
-        const g_u32x4* src = reinterpret_cast<const g_u32x4*>(base + off);
+        typedef __attribute__((address_space(1))) W gW;
+        const gW* src = reinterpret_cast<const gW*>(base + off);
         return nt ? __builtin_nontemporal_load(src) : *src;
     }
 }
 
-template <int AUX>
-__device__ __forceinline__ void store16(g_u8* base, uint64_t off, uint32_t nbytes, u32x4 val, bool nt) {
+template <int AUX, int LQ = 4>
+__device__ __forceinline__ void store16(g_u8* base, uint64_t off, uint32_t nbytes, typename LaneWord<LQ>::type val,
+                                        bool nt) {
+    typedef typename LaneWord<LQ>::type W;
     if constexpr (AUX >= 0) {
         __amdgpu_buffer_rsrc_t r =
             __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, static_cast<int>(nbytes), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(val, r, static_cast<int>(off), 0, AUX);
+        if constexpr (LQ == 4) __builtin_amdgcn_raw_buffer_store_b128(val, r, static_cast<int>(off), 0, AUX);
+        else __builtin_amdgcn_raw_buffer_store_b64(val, r, static_cast<int>(off), 0, AUX);
     } else {
-        g_u32x4* o = reinterpret_cast<g_u32x4*>(base + off);
+        typedef __attribute__((address_space(1))) W gW;
+        gW* o = reinterpret_cast<gW*>(base + off);
         if (nt) __builtin_nontemporal_store(val, o);
         else *o = val;
     }
@@ -157,13 +181,14 @@ struct NoStage {
 // `stage` runs once, after the first column batch's loads are issued and
 // before the first LDS table read: a kernel that stages its tables there
 // overlaps that global->LDS copy with its data loads.
-template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR, int LAUX, int SAUX, int WIN, class InBase,
+template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR, int LAUX, int SAUX, int WIN, int LQ, class InBase,
           class OutBase, class Stage = NoStage>
 __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4* lds_tab, int cols, int ncols_pad,
                                            int nrows, int64_t cb, uint64_t nunits, InBase in_base,
                                            OutBase out_base, Stage stage = Stage()) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
     constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
+    typedef typename LaneWord<LQ>::type W;  // the lane's unit: 4*LQ bytes of one vector
     const int tid = threadIdx.x;
     uint64_t off[VPT];
     bool ok[VPT];
@@ -171,24 +196,25 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
     for (int v = 0; v < VPT; ++v) {
         const uint64_t u = static_cast<uint64_t>(cb) * a.units_per_chunk + v * kBlock + tid;
         ok[v] = u < nunits;
-        off[v] = (ok[v] ? u : 0) * 16;  // clamp: out-of-range lanes read unit 0, store nothing
+        off[v] = (ok[v] ? u : 0) * (4 * LQ);  // clamp: out-of-range lanes read unit 0, store nothing
     }
 
-    uint32_t acc[MC][VPT][4];
+    uint32_t acc[MC][VPT][LQ];
 #pragma unroll
     for (int r = 0; r < MC; ++r)
 #pragma unroll
         for (int v = 0; v < VPT; ++v)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[r][v][q] = 0;
+            for (int q = 0; q < LQ; ++q) acc[r][v][q] = 0;
     if (ACC) {
 #pragma unroll
         for (int r = 0; r < MC; ++r)
             if (r < nrows)
 #pragma unroll
                 for (int v = 0; v < VPT; ++v) {
-                    const u32x4 o = load16<LAUX>(out_base(r), off[v], static_cast<uint32_t>(a.body), false);
-                    acc[r][v][0] = o.x; acc[r][v][1] = o.y; acc[r][v][2] = o.z; acc[r][v][3] = o.w;
+                    const W o = load16<LAUX, LQ>(out_base(r), off[v], static_cast<uint32_t>(a.body), false);
+#pragma unroll
+                    for (int q = 0; q < LQ; ++q) acc[r][v][q] = o[q];
                 }
     }
 
@@ -196,14 +222,14 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
         // Issue the column loads of this batch first (KB*16*VPT bytes in flight
         // per lane), or the first WIN of them with the rest rolled in below.
         constexpr int kFirst = (WIN > 0 && WIN < KB) ? WIN : KB;
-        u32x4 x[KB][VPT];
+        W x[KB][VPT];
         auto load_col = [&](int b) {
             int c = i0 + b;
             if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
             const g_u8* p = in_base(c);
 #pragma unroll
             for (int v = 0; v < VPT; ++v)
-                x[b][v] = load16<LAUX>(p, off[v], static_cast<uint32_t>(a.body), (VAR & kVarNtLoad) != 0);
+                x[b][v] = load16<LAUX, LQ>(p, off[v], static_cast<uint32_t>(a.body), (VAR & kVarNtLoad) != 0);
         };
 #pragma unroll
         for (int b = 0; b < kFirst; ++b) load_col(b);
@@ -237,16 +263,16 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
             }
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
-                const uint32_t xs[4] = {x[b][v].x, x[b][v].y, x[b][v].z, x[b][v].w};
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < LQ; ++q) {
+                    const uint32_t xq = x[b][v][q];
                     if (VAR & kVarXorOnly) {
 #pragma unroll
-                        for (int r = 0; r < MC; ++r) acc[r][v][q] ^= xs[q] ^ t[r * 5];
+                        for (int r = 0; r < MC; ++r) acc[r][v][q] ^= xq ^ t[r * 5];
                         continue;
                     }
                     uint32_t g0, g1, g2;
-                    split_groups(xs[q], g0, g1, g2);
+                    split_groups(xq, g0, g1, g2);
 #pragma unroll
                     for (int r = 0; r < MC; ++r) {
                         const uint32_t* tr = &t[r * 5];
@@ -269,7 +295,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
 #pragma unroll
                 for (int v = 0; v < VPT; ++v)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(acc[r][v][q]));
+                    for (int q = 0; q < LQ; ++q) asm volatile("" : "+v"(acc[r][v][q]));
             if (b + kFirst < KB) load_col(b + kFirst);  // rolling window refill
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -281,9 +307,10 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
                 if (!ok[v]) continue;
-                u32x4 val;
-                val.x = acc[r][v][0]; val.y = acc[r][v][1]; val.z = acc[r][v][2]; val.w = acc[r][v][3];
-                store16<SAUX>(out_base(r), off[v], static_cast<uint32_t>(a.body), val, a.nt_store != 0);
+                W val;
+#pragma unroll
+                for (int q = 0; q < LQ; ++q) val[q] = acc[r][v][q];
+                store16<SAUX, LQ>(out_base(r), off[v], static_cast<uint32_t>(a.body), val, a.nt_store != 0);
             }
         }
     }
@@ -320,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
             const int si = static_cast<int>(chunk / a.chunks_per_stripe);
             const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
             const int s = a.stripe_ids ? a.stripe_ids[si] : si;  // uniform: scalar load
-            chunk_body<KB, KFIX, MC, ACC, VPT, VAR, LAUX, SAUX, WIN>(
+            chunk_body<KB, KFIX, MC, ACC, VPT, VAR, LAUX, SAUX, WIN, 4>(
                 a, lds_tab, cols, ncols_pad, nrows, cb, nunits, [&](int c) { return in_ptr(a, c, s); },
                 [&](int r) { return out_ptr(a, cols, rg + r, s); });
         }
@@ -329,7 +356,8 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
 
 // One chunk per workgroup, rows <= MC (grid = all chunks): the common case
 // without the row-group / grid-stride loops of gf_matmul_vec (less live state).
-template <int KB, bool KFIX, int MC, bool ACC, int WIN, bool STAGE_LATE = false>
+template <int KB, bool KFIX, int MC, bool ACC, int WIN, bool STAGE_LATE = false, int LQ = 4, int VPT = 1,
+          int VAR = kVarDefault>
 __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
@@ -353,8 +381,8 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
     const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
     const int s = a.stripe_ids ? a.stripe_ids[si] : si;
     if (!STAGE_LATE) stage();
-    chunk_body<KB, KFIX, MC, ACC, 1, kVarDefault, kAuxNt, kAuxNt, WIN>(
-        a, lds_tab, cols, ncols_pad, a.rows, cb, a.body >> 4, [&](int c) { return in_ptr(a, c, s); },
+    chunk_body<KB, KFIX, MC, ACC, VPT, VAR, kAuxNt, kAuxNt, WIN, LQ>(
+        a, lds_tab, cols, ncols_pad, a.rows, cb, a.body / (4 * LQ), [&](int c) { return in_ptr(a, c, s); },
         [&](int r) { return out_ptr(a, cols, r, s); }, [&]() { if (STAGE_LATE) stage(); });
 }
 
@@ -362,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
 // a pattern holds its input / output vector indexes and the offset of its
 // prepared LDS table image.  a.ptr / a.sid address ALL d+p vectors of
 // stripe 0.  One workgroup = one chunk of one stripe (grid = all chunks).
-template <int KB, bool KFIX, int MC, bool STAGE_LATE = false>
+template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4>
 __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
                                                           const int32_t* __restrict__ stripe_pat) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
@@ -389,8 +417,8 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, co
     auto base = [&](uint32_t v) {
         return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
     };
-    chunk_body<KB, KFIX, MC, false, 1, kVarDefault, kAuxNt, kAuxNt, 0>(
-        a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body >> 4,
+    chunk_body<KB, KFIX, MC, false, 1, kVarDefault, kAuxNt, kAuxNt, 0, LQ>(
+        a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body / (4 * LQ),
         [&](int c) { return const_cast<const g_u8*>(base(P->in_idx[c])); },
         [&](int r) { return base(P->out_idx[r]); }, [&]() { if (STAGE_LATE) stage(); });
 }
@@ -440,6 +468,7 @@ struct Variant {
     bool kfix;
     const char* name;
     bool one_chunk = false;  // gf_matmul_vec1: needs grid == total chunks and rows <= mc
+    int lq = 4;              // dwords per lane unit (4: 16-byte units, 2: 8-byte units)
 };
 
 #define RSAMD_VARIANT(KB, KFIX, MC, ACC, VPT) \
@@ -493,6 +522,13 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
         case 131: *out = Variant{gf_matmul_vec1<10, true, 4, false, 3>, 10, 4, 1, true, "vec1<10,w3>", true}; return true;
         case 132: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0>, 10, 4, 1, true, "vec1<10,w0>", true}; return true;
         case 133: *out = Variant{gf_matmul_vec1<10, true, 4, false, 4>, 10, 4, 1, true, "vec1<10,w4>", true}; return true;
+        // DIAGNOSTIC xor-only one-chunk kernels (the memory ceiling of each lane width)
+        case 140: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 4, 1, kVarDefault | kVarXorOnly>, 10, 4, 1,
+                                 true, "vec1<10,16B,xor>", true, 4}; return true;
+        case 141: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 2, 1, kVarDefault | kVarXorOnly>, 10, 4, 1,
+                                 true, "vec1<10,8B,xor>", true, 2}; return true;
+        case 142: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, true, 2, 1, kVarDefault | kVarXorOnly>, 10, 4, 1,
+                                 true, "vec1<10,8B,late,xor>", true, 2}; return true;
         default: break;
     }
     switch (var) {
@@ -523,19 +559,26 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
     return RSAMD_VARIANT_G(4, false, 8, true);
 }
 
-#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN)                                                         \
-    (tuning().stage_late                                                                              \
-         ? Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, true>, KB, MC, 1, KFIX,                     \
-                   "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN ",late>", true}          \
-         : Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, false>, KB, MC, 1, KFIX,                    \
-                   "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN ">", true})
+// One-chunk kernels come in six builds: LDS tables staged before / after the
+// data loads (stage_late) x 16-byte lane units, 8-byte units, or two 8-byte
+// units per lane (lane16, vpt1 = 1 | 2).
+#define RSAMD_V1(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, TAG)                                     \
+    Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT>, KB, MC, VPT, KFIX,             \
+            "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN "," TAG ">", true, LQ}
+#define RSAMD_V1L(KB, KFIX, MC, ACC, WIN, LQ, VPT, TAG)                                             \
+    (tuning().stage_late ? RSAMD_V1(KB, KFIX, MC, ACC, WIN, true, LQ, VPT, "late," TAG)            \
+                         : RSAMD_V1(KB, KFIX, MC, ACC, WIN, false, LQ, VPT, TAG))
+#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN)                                                   \
+    (lane16                    ? RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 4, 1, "16B")                  \
+     : tuning().vpt1 == 2      ? RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 2, 2, "8Bx2")                 \
+                               : RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 2, 1, "8B"))
 
 // Loop-free one-chunk-per-workgroup kernels (the default launch: grid = all
 // chunks, rows <= MC).  A/B on MI355X, 10+4 @ 1 MiB x 256 (tools/ab.py, 2 x 30
 // interleaved rounds): vec1 all-loads-up-front 0.589 ms, vec1 5-column window
 // 0.600, looped kernel with window 0.602, looped without 0.611; XOR-only
 // diagnostic 0.591 (the memory pattern's own ceiling).
-static bool pick_one_chunk(int rows, int cols, bool acc, Variant* out) {
+static bool pick_one_chunk(int rows, int cols, bool acc, bool lane16, Variant* out) {
     if (!acc) {
         if (cols == 10 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(10, true, 4, false, 0); return true; }
         if (cols == 12 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(12, true, 4, false, 0); return true; }
@@ -553,11 +596,11 @@ static bool pick_one_chunk(int rows, int cols, bool acc, Variant* out) {
     return false;
 }
 
-static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body) {
+static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body, bool lane16) {
     if (body >= (uint64_t{1} << 31)) return pick_global(rows, acc);
     Variant ex;
     if (pick_experimental(rows, cols, acc, vpt, &ex)) return ex;
-    if (vpt == 1 && tuning().max_grid <= 0 && pick_one_chunk(rows, cols, acc, &ex)) return ex;
+    if (vpt == 1 && tuning().max_grid <= 0 && pick_one_chunk(rows, cols, acc, lane16, &ex)) return ex;
     // Looped kernels: row groups (rows > 4), grid caps, or VPT experiments.
     if (!acc) {
         if (cols == 10 && rows > 2 && rows <= 4)
@@ -575,8 +618,27 @@ static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body) {
     return RSAMD_VARIANT(4, false, 8, true, 1);
 }
 
+// Lane width of the one-chunk kernels.  A/B on MI355X (tools/ab.py, same
+// process): Encode with parity in its own region (split layout) runs at
+// 6.30-6.41 TB/s with 16-byte lane units vs 6.14-6.32 with 8-byte units;
+// every pattern whose outputs sit among its inputs (interleaved Encode,
+// in-place Reconst, Update, Replace) is faster with 8-byte units (Reconst of
+// one lost vector 5.75 -> 6.36-6.41 TB/s, interleaved Encode 5.85-5.97 ->
+// 6.00-6.12).  XOR-only diagnostics of the same kernel: 8-byte 6.63, 16-byte
+// 6.27 TB/s.
+static bool lane16_for(const MatmulArgs& a) {
+    if (tuning().lane_bytes == 16) return true;
+    if (tuning().lane_bytes == 8) return false;
+    if (a.accumulate || a.rows < 3 || a.nstripes == 1) return false;
+    for (int r = 0; r < a.rows; ++r)
+        for (int c = 0; c < a.cols; ++c)
+            if ((a.sid[a.cols + r] & 3) == (a.sid[c] & 3)) return false;
+    return true;
+}
+
 const char* vector_kernel_name(int rows, int cols, int accumulate) {
-    return pick(rows, cols, accumulate != 0, tuning().vpt, 0).name;
+    // the name for a split-layout batch (outputs in their own region)
+    return pick(rows, cols, accumulate != 0, tuning().vpt, 0, accumulate == 0 && rows >= 3).name;
 }
 
 static bool aligned16(uint64_t v) { return (v & 15u) == 0; }
@@ -587,7 +649,8 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     a.tail_start = a.len;
     a.units_per_chunk = kBlock;
     a.nt_store = 1;
-    const uint64_t nunits = a.body >> 4;
+    const int lq = tuning().lane_bytes == 16 ? 4 : 2;
+    const uint64_t nunits = a.body / (4 * lq);
     a.chunks_per_stripe = static_cast<int64_t>((nunits + kBlock - 1) / kBlock);
     a.total_chunks = a.chunks_per_stripe * a.nstripes;
     // a.rows = the largest output count over the batch's patterns (<= 4)
@@ -596,14 +659,19 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
     const size_t lds = static_cast<size_t>(ncols_pad) * (((mc * 5 + 3) / 4) * 4) * 4;
     const dim3 grid(static_cast<unsigned>(a.total_chunks));
-#define RSAMD_MULTI(KB, KFIX, MC)                                                                          \
+#define RSAMD_MULTI_L(KB, KFIX, MC, LATE)                                                                    \
     do {                                                                                                  \
-        if (tuning().stage_late)                                                                          \
-            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, true>), grid, dim3(kBlock), lds, stream, a, pats, \
+        if (lq == 4)                                                                                      \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 4>), grid, dim3(kBlock), lds, stream, a, pats, \
                                stripe_pat);                                                               \
         else                                                                                              \
-            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, false>), grid, dim3(kBlock), lds, stream, a, pats, \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 2>), grid, dim3(kBlock), lds, stream, a, pats, \
                                stripe_pat);                                                               \
+    } while (0)
+#define RSAMD_MULTI(KB, KFIX, MC)                                                                          \
+    do {                                                                                                  \
+        if (tuning().stage_late) RSAMD_MULTI_L(KB, KFIX, MC, true);                                       \
+        else RSAMD_MULTI_L(KB, KFIX, MC, false);                                                          \
     } while (0)
     if (k10) {
         if (mc == 1) RSAMD_MULTI(10, true, 1);
@@ -615,6 +683,7 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
         else RSAMD_MULTI(4, false, 4);
     }
 #undef RSAMD_MULTI
+#undef RSAMD_MULTI_L
     return hipGetLastError();
 }
 
@@ -632,15 +701,15 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
 
     if (a.body) {
         const LaunchTuning& tu = tuning();
-        Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt, a.body);
+        Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt, a.body, lane16_for(a));
         if (var.one_chunk) {  // one workgroup per chunk: the grid must fit a 31-bit dimension
-            const uint64_t chunks = ((a.body >> 4) + kBlock - 1) / kBlock * static_cast<uint64_t>(a.nstripes);
+            const uint64_t chunks = (a.body / (4 * var.lq) + kBlock - 1) / kBlock * static_cast<uint64_t>(a.nstripes);
             if (chunks > 0x7fffffffull)
                 var = a.accumulate ? RSAMD_VARIANT(4, false, 4, true, 1) : RSAMD_VARIANT(4, false, 4, false, 1);
         }
         a.units_per_chunk = kBlock * var.vpt;
         a.nt_store = tu.nt_store;
-        const uint64_t nunits = a.body >> 4;
+        const uint64_t nunits = a.body / (4 * var.lq);
         a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
         a.total_chunks = a.chunks_per_stripe * a.nstripes;
         int64_t grid = a.total_chunks;
@@ -652,6 +721,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         const int cold = ((var.mc * 5 + 3) / 4) * 4;
         size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
         if (tu.lds_pad > 0 && static_cast<size_t>(tu.lds_pad) > lds) lds = tu.lds_pad;  // occupancy experiments
+
         hipLaunchKernelGGL(var.fn, dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds, stream, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

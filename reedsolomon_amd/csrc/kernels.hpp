@@ -24,7 +24,7 @@ struct MatmulArgs {
     int rows, cols, rows_pad;
     int nstripes;
     int accumulate;           // 0: overwrite (Encode), 1: XOR into out (updateOnly)
-    int units_per_chunk;      // 16-byte units per workgroup-chunk (block * vpt)
+    int units_per_chunk;      // lane units (16 or 8 bytes) per workgroup-chunk (block * vpt)
     int nt_store;             // non-temporal output stores (overwrite mode)
     uint64_t len;             // bytes per vector
     uint64_t body;            // bytes handled by the vector kernel (multiple of 16)
@@ -59,6 +59,8 @@ struct LaunchTuning {
     int var;          // experimental 10+4 code shape (RSAMD_VAR), -1 = default
     int lds_pad;      // minimum dynamic LDS per workgroup (caps occupancy; experiments)
     int stage_late;   // one-chunk kernels: stage LDS tables after issuing the data loads
+    int lane_bytes;   // one-chunk / multi-pattern kernels: bytes per lane unit (16, 8; 0 = per launch)
+    int vpt1;         // one-chunk kernels with 8-byte units: units per lane (1 or 2)
 };
 LaunchTuning& tuning();
 

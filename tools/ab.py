@@ -7,7 +7,9 @@ rounds on the same device and buffers; reports median / min kernel time.
     python tools/ab.py "op=rec1" "op=rec1,stage_late=1" "op=multi16" ...
 
 op: enc (Encode, default) | rec1 / rec2 / rec4 (Reconst of 1 / 2 / 4 lost data
-vectors, split layout) | multi16 (rs_reconst_batch_multi, 16 patterns).
+vectors, split layout) | multi16 (rs_reconst_batch_multi, 16 patterns) |
+upd (Update of one row) | rep3 (Replace of 3 rows), both on the interleaved
+[S][d+p][len] buffer.
 """
 import os
 import statistics
@@ -23,7 +25,7 @@ import reedsolomon_amd as rs  # noqa: E402
 K, M, VEC, S = 10, 4, 1 << 20, 256
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
-DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0}
+DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0, "lane_bytes": 0, "vpt1": 1}
 LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9]}
 
 
@@ -62,6 +64,10 @@ def main():
         if op in LOST:
             lost = LOST[op]
             return (lambda: r.reconst_batch_split(data, par, [], lost)), S * (K + len(lost)) * VEC
+        if op == "upd":  # Update row 3 of every stripe: reads old, new, 4 parity; writes 4 parity
+            return (lambda: r.update_batch(data[:, 0], data[:, 1], 3, buf)), S * (2 + 2 * M) * VEC
+        if op == "rep3":  # Replace rows 1, 4, 7: reads 3 data + 4 parity, writes 4 parity
+            return (lambda: r.replace_batch(data[:, :3], [1, 4, 7], buf)), S * (3 + 2 * M) * VEC
         if op == "multi16":
             return (lambda: r.reconst_batch_multi(data, par, masks)), (S * K + nrec16) * VEC
         if layout == "inter":

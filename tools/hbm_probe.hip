@@ -254,3 +254,56 @@ int probe_pattern_km(void* base, uint64_t vec, uint64_t pitch, uint64_t stripe_s
     return -1;
 }
 }
+
+// Granularity sweep of the 10+4 split pattern: BS lanes per workgroup, BPL
+// bytes per lane (16: dwordx4, 8: dwordx2) -> BS*BPL bytes per vector per WG.
+template <int K, int M, int BS, int BPL>
+__global__ __launch_bounds__(BS) void kb_pattern_g(const uint8_t* dbase, uint8_t* pbase, uint64_t vec, uint64_t dss,
+                                                   uint64_t pss, uint64_t cps) {
+    const uint64_t s = blockIdx.x / cps, cb = blockIdx.x % cps;
+    const uint32_t off = (uint32_t)(cb * (BS * BPL) + threadIdx.x * BPL);
+    if constexpr (BPL == 16) {
+        u32x4 x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(dbase + s * dss + i * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            u32x4 a = {(uint32_t)j, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < K; ++i) a ^= x[i];
+            __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(pbase + s * pss + j * vec, (uint32_t)vec), off, 0, 2);
+        }
+    } else {
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b64(rsrc(dbase + s * dss + i * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            u32x2 a = {(uint32_t)j, 0u};
+#pragma unroll
+            for (int i = 0; i < K; ++i) a ^= x[i];
+            __builtin_amdgcn_raw_buffer_store_b64(a, rsrc(pbase + s * pss + j * vec, (uint32_t)vec), off, 0, 2);
+        }
+    }
+}
+
+extern "C" int probe_buf_g(int kind, void* a, void* b, uint64_t vec, int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+#define KG(BS, BPL) do { const uint64_t cps = vec / (BS * BPL); \
+    hipLaunchKernelGGL((kb_pattern_g<10, 4, BS, BPL>), dim3(cps * nstripes), dim3(BS), 0, st, (const uint8_t*)a, \
+                       (uint8_t*)b, vec, 10 * vec, 4 * vec, cps); } while (0)
+    switch (kind) {
+        case 0: KG(64, 16); break;
+        case 1: KG(128, 16); break;
+        case 2: KG(256, 16); break;
+        case 3: KG(512, 16); break;
+        case 4: KG(1024, 16); break;
+        case 5: KG(256, 8); break;
+        case 6: KG(128, 8); break;
+        case 7: KG(512, 8); break;
+        default: return -1;
+    }
+#undef KG
+    return hipGetLastError();
+}

@@ -70,6 +70,19 @@ def basic_probes(L, a, b, n, vp, sp, timeit):
 
 
 def pattern_probes(L, a, n, vp, sp, timeit):
+    if os.environ.get("PROBE_GRAN", "0") == "1":
+        # 10+4 split pattern: bytes per vector per workgroup = lanes x bytes/lane
+        import torch
+        vec, S = 1 << 20, 240
+        b = torch.empty(S * 4 * vec, dtype=torch.uint8, device="cuda")
+        assert S * 10 * vec <= n, "probe case out of bounds"
+        L.probe_buf_g.restype = ctypes.c_int
+        for _ in range(3):
+            for kind, name in ((0, "64x16B"), (1, "128x16B"), (2, "256x16B"), (3, "512x16B"), (4, "1024x16B"),
+                               (5, "256x8B"), (6, "128x8B"), (7, "512x8B")):
+                timeit(f"buffer nt 10+4 pattern {name}/vector/WG",
+                       lambda: L.probe_buf_g(kind, vp(a), vp(b), ctypes.c_uint64(vec), S, sp), S * 14 * vec)
+        return
     if os.environ.get("PROBE_UPL", "0") == "1":
         # 10+4 split pattern: 4/8/16 KiB per vector per workgroup, natural vs XCD-aware order
         import torch
