@@ -61,6 +61,7 @@ LaunchTuning& tuning() {
         const char* v1 = std::getenv("RSAMD_VPT1");
         x.vpt1 = (v1 && std::atoi(v1) == 2) ? 2 : 1;
 
+
         return x;
     }();
     return t;
@@ -108,8 +109,12 @@ enum : int {
     kVarNtLoad = 2,      // non-temporal input loads
     kVarSingleTab = 4,   // no LDS table prefetch across columns (fewer VGPRs)
     kVarBitop3 = 8,      // explicit v_bitop3 (xor3) accumulation
+    kVarCarry = 16,      // with kVarBitop3: pair columns through a carried term (1.5 xor3 per product, not 2)
 };
-constexpr int kVarDefault = kVarBitop3 | kVarSingleTab | kVarNtLoad;
+// kVarCarry: A/B on MI355X (tools/ab.py, profiles/r01/ab_carry.log): split
+// Encode +0.3-2.6 %, interleaved Encode +2 %, Reconst of 4 +2.4 %, 16-pattern
+// Reconst +1.6 %, the rest within noise; 8 % fewer VALU instructions.
+constexpr int kVarDefault = kVarBitop3 | kVarSingleTab | kVarNtLoad | kVarCarry;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -206,6 +211,15 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
         for (int v = 0; v < VPT; ++v)
 #pragma unroll
             for (int q = 0; q < LQ; ++q) acc[r][v][q] = 0;
+    uint32_t carry[MC][VPT][LQ];  // kVarCarry: third partial product of an even column
+    if (VAR & kVarCarry) {
+#pragma unroll
+        for (int r = 0; r < MC; ++r)
+#pragma unroll
+            for (int v = 0; v < VPT; ++v)
+#pragma unroll
+                for (int q = 0; q < LQ; ++q) carry[r][v][q] = 0;
+    }
     if (ACC) {
 #pragma unroll
         for (int r = 0; r < MC; ++r)
@@ -280,7 +294,16 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
                             const uint32_t p0 = __builtin_amdgcn_perm(tr[1], tr[0], g0);
                             const uint32_t p1 = __builtin_amdgcn_perm(tr[3], tr[2], g1);
                             const uint32_t p2 = __builtin_amdgcn_perm(tr[4], tr[4], g2);
-                            acc[r][v][q] = xor3(xor3(acc[r][v][q], p0, p1), p2, 0);
+                            if (VAR & kVarCarry) {
+                                if ((b & 1) == 0) {
+                                    acc[r][v][q] = xor3(acc[r][v][q], p0, p1);
+                                    carry[r][v][q] = p2;
+                                } else {
+                                    acc[r][v][q] = xor3(xor3(acc[r][v][q], carry[r][v][q], p0), p1, p2);
+                                }
+                            } else {
+                                acc[r][v][q] = xor3(xor3(acc[r][v][q], p0, p1), p2, 0);
+                            }
                         } else {
                             acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, tr);
                         }
@@ -295,8 +318,19 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
 #pragma unroll
                 for (int v = 0; v < VPT; ++v)
 #pragma unroll
-                    for (int q = 0; q < LQ; ++q) asm volatile("" : "+v"(acc[r][v][q]));
+                    for (int q = 0; q < LQ; ++q) {
+                        asm volatile("" : "+v"(acc[r][v][q]));
+                        if ((VAR & kVarCarry) && (b & 1) == 0) asm volatile("" : "+v"(carry[r][v][q]));
+                    }
             if (b + kFirst < KB) load_col(b + kFirst);  // rolling window refill
+        }
+        if ((VAR & kVarCarry) && (KB & 1)) {  // odd batch width: fold the last carry
+#pragma unroll
+            for (int r = 0; r < MC; ++r)
+#pragma unroll
+                for (int v = 0; v < VPT; ++v)
+#pragma unroll
+                    for (int q = 0; q < LQ; ++q) acc[r][v][q] ^= carry[r][v][q];
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -390,7 +424,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
 // a pattern holds its input / output vector indexes and the offset of its
 // prepared LDS table image.  a.ptr / a.sid address ALL d+p vectors of
 // stripe 0.  One workgroup = one chunk of one stripe (grid = all chunks).
-template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4>
+template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4, int VAR = kVarDefault>
 __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
                                                           const int32_t* __restrict__ stripe_pat) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
@@ -417,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, co
     auto base = [&](uint32_t v) {
         return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
     };
-    chunk_body<KB, KFIX, MC, false, 1, kVarDefault, kAuxNt, kAuxNt, 0, LQ>(
+    chunk_body<KB, KFIX, MC, false, 1, VAR, kAuxNt, kAuxNt, 0, LQ>(
         a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body / (4 * LQ),
         [&](int c) { return const_cast<const g_u8*>(base(P->in_idx[c])); },
         [&](int r) { return base(P->out_idx[r]); }, [&]() { if (STAGE_LATE) stage(); });
@@ -529,6 +563,11 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
                                  true, "vec1<10,8B,xor>", true, 2}; return true;
         case 142: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, true, 2, 1, kVarDefault | kVarXorOnly>, 10, 4, 1,
                                  true, "vec1<10,8B,late,xor>", true, 2}; return true;
+        // without the paired-column XOR accumulation (kVarCarry)
+        case 143: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 2, 1, kVarDefault & ~kVarCarry>, 10, 4, 1,
+                                 true, "vec1<10,8B,nocarry>", true, 2}; return true;
+        case 144: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 4, 1, kVarDefault & ~kVarCarry>, 10, 4, 1,
+                                 true, "vec1<10,16B,nocarry>", true, 4}; return true;
         default: break;
     }
     switch (var) {
@@ -562,12 +601,14 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
 // One-chunk kernels come in six builds: LDS tables staged before / after the
 // data loads (stage_late) x 16-byte lane units, 8-byte units, or two 8-byte
 // units per lane (lane16, vpt1 = 1 | 2).
-#define RSAMD_V1(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, TAG)                                     \
-    Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT>, KB, MC, VPT, KFIX,             \
+#define RSAMD_V1(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, VAR, TAG)                                \
+    Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, VAR>, KB, MC, VPT, KFIX,        \
             "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN "," TAG ">", true, LQ}
+#define RSAMD_V1C(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, TAG) \
+    RSAMD_V1(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, kVarDefault, TAG)
 #define RSAMD_V1L(KB, KFIX, MC, ACC, WIN, LQ, VPT, TAG)                                             \
-    (tuning().stage_late ? RSAMD_V1(KB, KFIX, MC, ACC, WIN, true, LQ, VPT, "late," TAG)            \
-                         : RSAMD_V1(KB, KFIX, MC, ACC, WIN, false, LQ, VPT, TAG))
+    (tuning().stage_late ? RSAMD_V1C(KB, KFIX, MC, ACC, WIN, true, LQ, VPT, "late," TAG)           \
+                         : RSAMD_V1C(KB, KFIX, MC, ACC, WIN, false, LQ, VPT, TAG))
 #define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN)                                                   \
     (lane16                    ? RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 4, 1, "16B")                  \
      : tuning().vpt1 == 2      ? RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 2, 2, "8Bx2")                 \
@@ -659,19 +700,19 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
     const size_t lds = static_cast<size_t>(ncols_pad) * (((mc * 5 + 3) / 4) * 4) * 4;
     const dim3 grid(static_cast<unsigned>(a.total_chunks));
-#define RSAMD_MULTI_L(KB, KFIX, MC, LATE)                                                                    \
+#define RSAMD_MULTI_L(KB, KFIX, MC, LATE, VAR)                                                                    \
     do {                                                                                                  \
         if (lq == 4)                                                                                      \
-            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 4>), grid, dim3(kBlock), lds, stream, a, pats, \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 4, VAR>), grid, dim3(kBlock), lds, stream, a, pats, \
                                stripe_pat);                                                               \
         else                                                                                              \
-            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 2>), grid, dim3(kBlock), lds, stream, a, pats, \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 2, VAR>), grid, dim3(kBlock), lds, stream, a, pats, \
                                stripe_pat);                                                               \
     } while (0)
 #define RSAMD_MULTI(KB, KFIX, MC)                                                                          \
     do {                                                                                                  \
-        if (tuning().stage_late) RSAMD_MULTI_L(KB, KFIX, MC, true);                                       \
-        else RSAMD_MULTI_L(KB, KFIX, MC, false);                                                          \
+        if (tuning().stage_late) RSAMD_MULTI_L(KB, KFIX, MC, true, kVarDefault);                          \
+        else RSAMD_MULTI_L(KB, KFIX, MC, false, kVarDefault);                                             \
     } while (0)
     if (k10) {
         if (mc == 1) RSAMD_MULTI(10, true, 1);
