@@ -186,7 +186,7 @@ struct NoStage {
 // `stage` runs once, after the first column batch's loads are issued and
 // before the first LDS table read: a kernel that stages its tables there
 // overlaps that global->LDS copy with its data loads.
-template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR, int LAUX, int SAUX, int WIN, int LQ, class InBase,
+template <int KB, bool KFIX, int MC, bool ACC, int VPT, int VAR, int LAUX, int SAUX, int WIN, int LQ, int BS, class InBase,
           class OutBase, class Stage = NoStage>
 __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4* lds_tab, int cols, int ncols_pad,
                                            int nrows, int64_t cb, uint64_t nunits, InBase in_base,
@@ -199,7 +199,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
     bool ok[VPT];
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-        const uint64_t u = static_cast<uint64_t>(cb) * a.units_per_chunk + v * kBlock + tid;
+        const uint64_t u = static_cast<uint64_t>(cb) * a.units_per_chunk + v * BS + tid;
         ok[v] = u < nunits;
         off[v] = (ok[v] ? u : 0) * (4 * LQ);  // clamp: out-of-range lanes read unit 0, store nothing
     }
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
             const int si = static_cast<int>(chunk / a.chunks_per_stripe);
             const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
             const int s = a.stripe_ids ? a.stripe_ids[si] : si;  // uniform: scalar load
-            chunk_body<KB, KFIX, MC, ACC, VPT, VAR, LAUX, SAUX, WIN, 4>(
+            chunk_body<KB, KFIX, MC, ACC, VPT, VAR, LAUX, SAUX, WIN, 4, kBlock>(
                 a, lds_tab, cols, ncols_pad, nrows, cb, nunits, [&](int c) { return in_ptr(a, c, s); },
                 [&](int r) { return out_ptr(a, cols, rg + r, s); });
         }
@@ -391,15 +391,15 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
 // One chunk per workgroup, rows <= MC (grid = all chunks): the common case
 // without the row-group / grid-stride loops of gf_matmul_vec (less live state).
 template <int KB, bool KFIX, int MC, bool ACC, int WIN, bool STAGE_LATE = false, int LQ = 4, int VPT = 1,
-          int VAR = kVarDefault>
-__global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
+          int VAR = kVarDefault, int BS = kBlock>
+__global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
     const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
     const int cols = KFIX ? KB : a.cols;
     const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
     auto stage = [&]() {
-        for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
+        for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) {
             const int i = idx / COLD;
             const int w = idx - i * COLD;
             const int rr = w / 5;
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
     const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
     const int s = a.stripe_ids ? a.stripe_ids[si] : si;
     if (!STAGE_LATE) stage();
-    chunk_body<KB, KFIX, MC, ACC, VPT, VAR, kAuxNt, kAuxNt, WIN, LQ>(
+    chunk_body<KB, KFIX, MC, ACC, VPT, VAR, kAuxNt, kAuxNt, WIN, LQ, BS>(
         a, lds_tab, cols, ncols_pad, a.rows, cb, a.body / (4 * LQ), [&](int c) { return in_ptr(a, c, s); },
         [&](int r) { return out_ptr(a, cols, r, s); }, [&]() { if (STAGE_LATE) stage(); });
 }
@@ -424,18 +424,14 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec1(const MatmulArgs a) {
 // a pattern holds its input / output vector indexes and the offset of its
 // prepared LDS table image.  a.ptr / a.sid address ALL d+p vectors of
 // stripe 0.  One workgroup = one chunk of one stripe (grid = all chunks).
-template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4, int VAR = kVarDefault>
-__global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
-                                                          const int32_t* __restrict__ stripe_pat) {
+// The workgroup runs the body built for its own pattern's output count
+// (1, 2 or up to MC rows): a uniform branch, so a stripe that lost one vector
+// does not pay the VALU work of the batch's widest pattern.
+template <int MC, int KB, bool KFIX, bool STAGE_LATE, int LQ, int VAR>
+__device__ __forceinline__ void multi_chunk(const MatmulArgs& a, const PatternDesc* P, int s, int64_t cb,
+                                            uint32_t* lds32) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
     const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
-    const int64_t chunk = blockIdx.x;
-    const int s = static_cast<int>(chunk / a.chunks_per_stripe);
-    const int64_t cb = chunk - static_cast<int64_t>(s) * a.chunks_per_stripe;
-    const int pid = stripe_pat[s];
-    if (pid < 0) return;  // stripe not in the batch's work (uniform: whole workgroup)
-    const PatternDesc* P = pats + pid;
     const int cols = KFIX ? KB : a.cols;
     const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
     const uint32_t* img = a.tables + P->tab_off;
@@ -451,10 +447,30 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, co
     auto base = [&](uint32_t v) {
         return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
     };
-    chunk_body<KB, KFIX, MC, false, 1, VAR, kAuxNt, kAuxNt, 0, LQ>(
+    chunk_body<KB, KFIX, MC, false, 1, VAR, kAuxNt, kAuxNt, 0, LQ, kBlock>(
         a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body / (4 * LQ),
         [&](int c) { return const_cast<const g_u8*>(base(P->in_idx[c])); },
         [&](int r) { return base(P->out_idx[r]); }, [&]() { if (STAGE_LATE) stage(); });
+}
+
+template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4, int VAR = kVarDefault>
+__global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
+                                                          const int32_t* __restrict__ stripe_pat) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+    const int64_t chunk = blockIdx.x;
+    const int s = static_cast<int>(chunk / a.chunks_per_stripe);
+    const int64_t cb = chunk - static_cast<int64_t>(s) * a.chunks_per_stripe;
+    const int pid = stripe_pat[s];
+    if (pid < 0) return;  // stripe not in the batch's work (uniform: whole workgroup)
+    const PatternDesc* P = pats + pid;
+    const uint32_t nout = P->nout;
+    if constexpr (MC > 2) {
+        if (nout > 2) return multi_chunk<MC, KB, KFIX, STAGE_LATE, LQ, VAR>(a, P, s, cb, lds32);
+    }
+    if constexpr (MC > 1) {
+        if (nout == 2) return multi_chunk<2, KB, KFIX, STAGE_LATE, LQ, VAR>(a, P, s, cb, lds32);
+    }
+    multi_chunk<1, KB, KFIX, STAGE_LATE, LQ, VAR>(a, P, s, cb, lds32);
 }
 
 // ---------------------------------------------------------------------------
@@ -503,6 +519,7 @@ struct Variant {
     const char* name;
     bool one_chunk = false;  // gf_matmul_vec1: needs grid == total chunks and rows <= mc
     int lq = 4;              // dwords per lane unit (4: 16-byte units, 2: 8-byte units)
+    int bs = kBlock;         // lanes per workgroup
 };
 
 #define RSAMD_VARIANT(KB, KFIX, MC, ACC, VPT) \
@@ -568,6 +585,17 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
                                  true, "vec1<10,8B,nocarry>", true, 2}; return true;
         case 144: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 4, 1, kVarDefault & ~kVarCarry>, 10, 4, 1,
                                  true, "vec1<10,16B,nocarry>", true, 4}; return true;
+        // workgroup size: 64 / 128 lanes (one / two waves), 16- or 8-byte units, tables staged early / late
+#define RSAMD_BSV(LATE, LQ, BS, TAG) \
+    Variant{gf_matmul_vec1<10, true, 4, false, 0, LATE, LQ, 1, kVarDefault, BS>, 10, 4, 1, true, TAG, true, LQ, BS}
+        case 150: *out = RSAMD_BSV(false, 4, 64, "vec1<10,16B,bs64>"); return true;
+        case 151: *out = RSAMD_BSV(false, 4, 128, "vec1<10,16B,bs128>"); return true;
+        case 152: *out = RSAMD_BSV(false, 2, 64, "vec1<10,8B,bs64>"); return true;
+        case 153: *out = RSAMD_BSV(false, 2, 128, "vec1<10,8B,bs128>"); return true;
+        case 154: *out = RSAMD_BSV(true, 4, 64, "vec1<10,16B,bs64,late>"); return true;
+        case 155: *out = RSAMD_BSV(true, 4, 128, "vec1<10,16B,bs128,late>"); return true;
+        case 156: *out = RSAMD_BSV(true, 2, 128, "vec1<10,8B,bs128,late>"); return true;
+#undef RSAMD_BSV
         default: break;
     }
     switch (var) {
@@ -744,11 +772,11 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         const LaunchTuning& tu = tuning();
         Variant var = pick(a.rows, a.cols, a.accumulate != 0, tu.vpt, a.body, lane16_for(a));
         if (var.one_chunk) {  // one workgroup per chunk: the grid must fit a 31-bit dimension
-            const uint64_t chunks = (a.body / (4 * var.lq) + kBlock - 1) / kBlock * static_cast<uint64_t>(a.nstripes);
+            const uint64_t chunks = (a.body / (4 * var.lq) + var.bs - 1) / var.bs * static_cast<uint64_t>(a.nstripes);
             if (chunks > 0x7fffffffull)
                 var = a.accumulate ? RSAMD_VARIANT(4, false, 4, true, 1) : RSAMD_VARIANT(4, false, 4, false, 1);
         }
-        a.units_per_chunk = kBlock * var.vpt;
+        a.units_per_chunk = var.bs * var.vpt;
         a.nt_store = tu.nt_store;
         const uint64_t nunits = a.body / (4 * var.lq);
         a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
@@ -763,7 +791,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
         if (tu.lds_pad > 0 && static_cast<size_t>(tu.lds_pad) > lds) lds = tu.lds_pad;  // occupancy experiments
 
-        hipLaunchKernelGGL(var.fn, dim3(static_cast<unsigned>(grid)), dim3(kBlock), lds, stream, a);
+        hipLaunchKernelGGL(var.fn, dim3(static_cast<unsigned>(grid)), dim3(var.bs), lds, stream, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
