@@ -141,6 +141,31 @@ def test_encode_dev_single_stripe(rslib, orc, torch_dev):
             assert np.array_equal(vecs[d + j].cpu().numpy(), exp[j]), (size, j)
 
 
+def test_vectors_over_2GiB(rslib, orc, torch_dev):
+    """Vectors past the 2 GiB buffer-descriptor range take the global-load
+    kernel (body >= 2^31) plus the byte kernel for the 37-byte tail; encode
+    then rebuild a lost data vector (rs.go accepts any length >= 1)."""
+    torch = torch_dev
+    d, p, n = 2, 1, (1 << 31) + 37
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(77)
+    vecs = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(d)]
+    vecs.append(torch.full((n,), 7, dtype=torch.uint8, device="cuda"))
+    r.encode_dev(vecs)
+    torch.cuda.synchronize()
+    for lo, hi in ((0, 4096), (1 << 30, (1 << 30) + 4096), ((1 << 31) - 4096, n)):
+        data = [v[lo:hi].cpu().numpy() for v in vecs[:d]]
+        exp = _oracle_encode(orc, d, p, data)
+        assert np.array_equal(vecs[d][lo:hi].cpu().numpy(), exp[0]), (lo, hi)
+    keep = vecs[0].clone()
+    vecs[0].zero_()
+    r.reconst_dev(vecs, [1, 2], [0])
+    torch.cuda.synchronize()
+    assert torch.equal(vecs[0], keep)
+    del vecs, keep
+    torch.cuda.empty_cache()
+
+
 def test_unaligned_device_vectors(rslib, orc, torch_dev):
     """Go slices can start anywhere: odd offsets take the byte-granular kernel."""
     torch = torch_dev
