@@ -236,10 +236,13 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
         // Issue the column loads of this batch first (KB*16*VPT bytes in flight
         // per lane), or the first WIN of them with the rest rolled in below.
         constexpr int kFirst = (WIN > 0 && WIN < KB) ? WIN : KB;
+        // Columns of this batch (uniform): a batch past `cols` skips its
+        // padding columns' loads and math with a scalar branch.
+        const int nb = KFIX ? KB : ((cols - i0) < KB ? (cols - i0) : KB);
         W x[KB][VPT];
         auto load_col = [&](int b) {
-            int c = i0 + b;
-            if (!KFIX) c = c < cols ? c : cols - 1;  // padded columns re-read a real one (zero table)
+            if (!KFIX && b >= nb) return;
+            const int c = i0 + b;
             const g_u8* p = in_base(c);
 #pragma unroll
             for (int v = 0; v < VPT; ++v)
@@ -257,6 +260,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
         }
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
+            if (!KFIX && b >= nb) break;
             // Scheduling fence: keeps each column's LDS reads next to its math
             // (hoisted, all k*MC tables would pin ~200 VGPRs: one wave/SIMD).
             __builtin_amdgcn_sched_barrier(0);
@@ -324,7 +328,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
                     }
             if (b + kFirst < KB) load_col(b + kFirst);  // rolling window refill
         }
-        if ((VAR & kVarCarry) && (KB & 1)) {  // odd batch width: fold the last carry
+        if ((VAR & kVarCarry) && (nb & 1)) {  // odd column count: fold the last carry
 #pragma unroll
             for (int r = 0; r < MC; ++r)
 #pragma unroll
