@@ -299,9 +299,11 @@ RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
 
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad", "stage_late",
+ * "lane_bytes" (16 | 8, 0 = per launch), "vpt1",
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
- * host-memory call staging), "host_batch_zc" (0/1).  Returns
- * RS_OK, or RS_ERR_INVAL for an unknown name. */
+ * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
+ * concurrent host calls of one shape share a launch; 0 = off),
+ * "host_batch_zc" (0/1).  Returns RS_OK, or RS_ERR_INVAL for an unknown name. */
 RS_API int rs_tune(const char* name, int value);
 
 /* GF(2^8) multiply (gmu.go:26-28) — for tests. */

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -85,6 +86,32 @@ struct rs_codec {
     hipEvent_t chunk_ev[3] = {nullptr, nullptr, nullptr};  // host-call chunk pipeline slots
     hipStream_t stream = nullptr;
 
+    // Host-call coalescing: concurrent small host calls of one shape (matrix,
+    // size, mode) join a shared batch in a pinned buffer, each caller copying
+    // its own vectors in and out on its own thread; the batch runs as ONE
+    // multi-stripe zero-copy launch.  Two batches: one fills while the other
+    // runs (host_calls.cpp host_call).
+    struct CoBatch {
+        enum State { kIdle, kFilling, kRunning, kDone } state = kIdle;
+        std::vector<uint8_t> mat;  // the shape: matrix bytes, rows, cols, size, mode
+        int rows = 0, cols = 0;
+        size_t size = 0;
+        bool accumulate = false;
+        size_t pitch = 0, stride = 0;
+        int cap = 0;               // stripes this batch may take
+        uint8_t* host = nullptr;   // pinned [cap][cols + rows][pitch]
+        uint8_t* dev = nullptr;    // its device-mapped address
+        size_t host_bytes = 0;
+        int joined = 0, ready = 0, released = 0;
+        int rc = 0;
+    };
+    std::mutex co_mu;
+    std::condition_variable co_cv;
+    CoBatch co[2];
+    bool co_gpu_busy = false;
+    int co_active = 0;             // callers inside host_call
+    hipStream_t co_stream = nullptr;
+
     // Upload ring for per-call device descriptors (multi-pattern Reconst):
     // pinned host slot -> device slot on a private copy stream, so the copy
     // for call n+1 overlaps call n's kernel instead of stalling the stream.
@@ -118,6 +145,9 @@ struct rs_codec {
         if (up_stream) (void)hipStreamDestroy(up_stream);
         if (stage) (void)hipFree(stage);
         if (hstage) (void)hipHostFree(hstage);
+        for (CoBatch& b : co)
+            if (b.host) (void)hipHostFree(b.host);
+        if (co_stream) (void)hipStreamDestroy(co_stream);
         for (hipEvent_t e : chunk_ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -250,9 +280,13 @@ struct ReconstPlan {
 int check_reconst_passes(const rs_t* rs, const ReconstPlan& pl, const size_t* lens, int n, int* parity_rc);
 
 // ---------------------------------------------------------------- host calls (host_calls.cpp)
-extern size_t g_pinned_max, g_zc_max, g_chunk;
+extern size_t g_pinned_max, g_zc_max, g_chunk, g_coalesce_max;
 int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
                  size_t size, bool accumulate);
+// host_product for a synchronous host call, coalesced with concurrent calls
+// of the same shape (takes stage_mu itself).
+int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+              size_t size, bool accumulate);
 
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
 extern int g_host_batch_zc;

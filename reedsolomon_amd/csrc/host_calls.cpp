@@ -242,6 +242,177 @@ int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t
     return stage_out(rs, dst, rows, size, pitch, cols, cols + rows);
 }
 
+// ---------------------------------------------------------------- coalescing
+
+// Vectors up to this size take part in host-call coalescing (0 = off).
+size_t g_coalesce_max = 128 * 1024;
+// Upper bound on one coalesced batch's pinned bytes and stripe count.
+constexpr size_t kCoalesceBytes = size_t{32} << 20;
+constexpr int kCoalesceStripes = 256;
+
+using CoBatch = rs_codec::CoBatch;
+
+static bool same_shape(const CoBatch& b, const uint8_t* mat, int rows, int cols, size_t size, bool acc) {
+    return b.rows == rows && b.cols == cols && b.size == size && b.accumulate == acc &&
+           std::memcmp(b.mat.data(), mat, static_cast<size_t>(rows) * cols) == 0;
+}
+
+// (Re)shape an idle batch for calls of this shape.  Caller holds co_mu.
+static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t size, bool acc) {
+    b.mat.assign(mat, mat + static_cast<size_t>(rows) * cols);
+    b.rows = rows;
+    b.cols = cols;
+    b.size = size;
+    b.accumulate = acc;
+    b.pitch = rup(size, 256);
+    b.stride = b.pitch * static_cast<size_t>(rows + cols);
+    b.cap = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kCoalesceStripes, kCoalesceBytes / b.stride)));
+    const size_t need = b.stride * static_cast<size_t>(b.cap);
+    if (need > b.host_bytes) {
+        if (b.host) (void)hipHostFree(b.host);
+        b.host = nullptr;
+        b.dev = nullptr;
+        b.host_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&b.host), need, hipHostMallocDefault) != hipSuccess) {
+            b.host = nullptr;
+            return RS_ERR_NOMEM;
+        }
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, b.host, 0) != hipSuccess || !dp) {
+            (void)hipHostFree(b.host);
+            b.host = nullptr;
+            return RS_ERR_DEVICE;
+        }
+        b.dev = static_cast<uint8_t*>(dp);
+        b.host_bytes = need;
+    }
+    b.joined = b.ready = b.released = 0;
+    b.rc = RS_OK;
+    b.state = CoBatch::kFilling;
+    return RS_OK;
+}
+
+// One launch over the batch's n stripes, straight out of the pinned buffer
+// (zero-copy), then wait for it.
+static int run_batch(rs_t* rs, const CoBatch& b, int n) {
+    const uint8_t* in[kMaxVects];
+    uint8_t* out[kMaxVects];
+    for (int i = 0; i < b.cols; ++i) in[i] = b.dev + static_cast<size_t>(i) * b.pitch;
+    for (int r = 0; r < b.rows; ++r) out[r] = b.dev + static_cast<size_t>(b.cols + r) * b.pitch;
+    const int rc = matmul(rs, b.mat.data(), b.rows, b.cols, in, static_cast<int64_t>(b.stride), out,
+                          static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
+    const bool ok = hipStreamSynchronize(rs->co_stream) == hipSuccess;  // never leave a kernel on the buffer
+    return rc ? rc : (ok ? RS_OK : RS_ERR_DEVICE);
+}
+
+// The synchronous host calls' entry (rs_encode / rs_reconst / rs_update /
+// rs_replace).  Vectors up to g_coalesce_max join a batch of concurrent
+// calls of the same shape:
+//   join (or open) a filling batch -> copy own inputs into own stripe slot
+//   -> the last ready member launches the batch once the GPU is free (one
+//   launch for every stripe that joined) -> each member copies its own
+//   outputs back and leaves; the batch is reused when all have left.
+// Copies run on the callers' own threads, in parallel; two batches let one
+// fill while the other runs.  A lone caller's call is one launch, as before.
+int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
+              size_t size, bool accumulate) {
+    if (size > g_coalesce_max || size == 0) {
+        std::lock_guard<std::mutex> lk(rs->stage_mu);
+        return host_product(rs, mat, rows, cols, src, dst, size, accumulate);
+    }
+    std::unique_lock<std::mutex> lk(rs->co_mu);
+    if (!rs->co_stream && hipStreamCreateWithFlags(&rs->co_stream, hipStreamNonBlocking) != hipSuccess) {
+        rs->co_stream = nullptr;
+        return RS_ERR_DEVICE;
+    }
+    ++rs->co_active;
+    CoBatch* b = nullptr;
+    int idx = -1;
+    while (!b) {
+        for (CoBatch& c : rs->co)
+            if (c.state == CoBatch::kFilling && c.joined < c.cap && same_shape(c, mat, rows, cols, size, accumulate)) {
+                b = &c;
+                break;
+            }
+        if (!b)
+            for (CoBatch& c : rs->co)
+                if (c.state == CoBatch::kIdle) {
+                    const int rc = init_batch(c, mat, rows, cols, size, accumulate);
+                    if (rc) {
+                        --rs->co_active;
+                        return rc;
+                    }
+                    b = &c;
+                    break;
+                }
+        if (!b) rs->co_cv.wait(lk);
+    }
+    idx = b->joined++;
+    const bool alone = rs->co_active == 1;
+    lk.unlock();
+
+    // copy in: own stripe slot [cols inputs | rows outputs (accumulate)]
+    uint8_t* slot = b->host + static_cast<size_t>(idx) * b->stride;
+    {
+        uint8_t* cd[2 * kMaxVects];
+        const uint8_t* cs[2 * kMaxVects];
+        int n = 0;
+        for (int i = 0; i < cols; ++i, ++n) {
+            cd[n] = slot + static_cast<size_t>(i) * b->pitch;
+            cs[n] = src[i];
+        }
+        if (accumulate)
+            for (int r = 0; r < rows; ++r, ++n) {
+                cd[n] = slot + static_cast<size_t>(cols + r) * b->pitch;
+                cs[n] = dst[r];
+            }
+        if (alone) parallel_copy(cd, cs, n, size);  // the copy pool serves one call at a time
+        else
+            for (int i = 0; i < n; ++i) std::memcpy(cd[i], cs[i], size);
+    }
+
+    lk.lock();
+    ++b->ready;
+    while (b->state != CoBatch::kDone) {
+        if (b->state == CoBatch::kFilling && !rs->co_gpu_busy && b->ready == b->joined) {
+            b->state = CoBatch::kRunning;
+            rs->co_gpu_busy = true;
+            const int n = b->joined;
+            lk.unlock();
+            const int rc = run_batch(rs, *b, n);
+            lk.lock();
+            b->rc = rc;
+            b->state = CoBatch::kDone;
+            rs->co_gpu_busy = false;
+            rs->co_cv.notify_all();
+            break;
+        }
+        rs->co_cv.wait(lk);
+    }
+    const int rc = b->rc;
+    lk.unlock();
+
+    if (rc == RS_OK) {  // copy out: own output rows
+        uint8_t* cd[kMaxVects];
+        const uint8_t* cs[kMaxVects];
+        for (int r = 0; r < rows; ++r) {
+            cd[r] = dst[r];
+            cs[r] = slot + static_cast<size_t>(cols + r) * b->pitch;
+        }
+        if (alone) parallel_copy(cd, cs, rows, size);
+        else
+            for (int r = 0; r < rows; ++r) std::memcpy(cd[r], cs[r], size);
+    }
+
+    lk.lock();
+    if (++b->released == b->joined) {
+        b->state = CoBatch::kIdle;
+        rs->co_cv.notify_all();
+    }
+    --rs->co_active;
+    return rc;
+}
+
 }  // namespace detail
 }  // namespace rsamd
 
@@ -252,8 +423,7 @@ int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
     RS_TRY(check_encode(rs, lens, n));
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
-    std::lock_guard<std::mutex> lk(rs->stage_mu);
-    return host_product(rs, rs->gen(), rs->p, rs->d, vects, vects + rs->d, lens[0], false);
+    return host_call(rs, rs->gen(), rs->p, rs->d, vects, vects + rs->d, lens[0], false);
 }
 
 int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
@@ -271,14 +441,13 @@ int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const
     if (rows > 0) {
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
-        std::lock_guard<std::mutex> lk(rs->stage_mu);
         const uint8_t* src[kMaxVects];
         uint8_t* dst[kMaxVects];
         for (int i = 0; i < d; ++i) src[i] = vects[pl.vs[i]];
         for (int i = 0; i < rows; ++i) dst[i] = vects[pl.nr[i]];
         std::vector<uint8_t> m;
         RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
-        RS_TRY(host_product(rs, m.data(), rows, d, src, dst, lens[pl.vs[0]], false));
+        RS_TRY(host_call(rs, m.data(), rows, d, src, dst, lens[pl.vs[0]], false));
     }
     return parity_rc;
 }
@@ -290,10 +459,9 @@ int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* 
     if (!old_data || !new_data) return RS_ERR_INVAL;
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
-    std::lock_guard<std::mutex> lk(rs->stage_mu);
     const uint8_t* src[2] = {old_data, new_data};
     std::vector<uint8_t> gm = update_matrix(rs, row);
-    return host_product(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
+    return host_call(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
 }
 
 int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows, int nr,
@@ -304,9 +472,8 @@ int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, in
     RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
     RS_TRY(ensure_device(rs));
     DeviceGuard g(rs->device);
-    std::lock_guard<std::mutex> lk(rs->stage_mu);
     std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-    return host_product(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
+    return host_call(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
 }
 
 }  // extern "C"

@@ -1,0 +1,144 @@
+/* Concurrent synchronous host calls (what a Go storage server does: many
+ * goroutines, one rs_encode / rs_reconst per stripe).  T threads share one
+ * handle; each encodes (even threads) or rebuilds two lost vectors (odd
+ * threads, mixed mode) of its own 10+4 stripe in a loop.  Every result is
+ * checked against the same call made alone before the timed phase.
+ *
+ *   gcc -O2 -std=c99 -pthread -Iinclude tools/host_concurrency.c -Lreedsolomon_amd/_lib -lrsamd \
+ *       -Wl,-rpath,$PWD/reedsolomon_amd/_lib -o tools/_build/host_concurrency
+ *   tools/_build/host_concurrency <vec bytes> <calls per thread> <coalesce_max> <mixed 0/1> T1 T2 ...
+ *
+ * Prints one JSON object per thread count.
+ */
+#define _POSIX_C_SOURCE 200112L
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "rs_amd.h"
+
+enum { D = 10, P = 4, N = D + P, MAXT = 256, MAXCALLS = 4096 };
+
+static rs_t* g_rs;
+static size_t g_vec;
+static int g_calls, g_mixed;
+
+typedef struct {
+    int id;
+    uint8_t* v[N];      /* working stripe */
+    uint8_t* want[N];   /* expected stripe after the call */
+    size_t lens[N];
+    double lat[MAXCALLS];
+    int bad;
+} Worker;
+
+static Worker g_w[MAXT];
+static pthread_barrier_t g_bar;
+
+static double now_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec / 1e3;
+}
+
+static int cmpd(const void* a, const void* b) {
+    double x = *(const double*)a, y = *(const double*)b;
+    return x < y ? -1 : x > y;
+}
+
+static const int kLost[2] = {0, 11};
+
+static int one_call(Worker* w) {
+    if (g_mixed && (w->id & 1)) {
+        memset(w->v[kLost[0]], 0, g_vec);
+        memset(w->v[kLost[1]], 0, g_vec);
+        return rs_reconst(g_rs, w->v, w->lens, N, NULL, 0, kLost, 2);
+    }
+    return rs_encode(g_rs, w->v, w->lens, N);
+}
+
+static void* run(void* arg) {
+    Worker* w = (Worker*)arg;
+    int i, j;
+    pthread_barrier_wait(&g_bar);
+    for (i = 0; i < g_calls; ++i) {
+        double t0 = now_us();
+        int rc = one_call(w);
+        w->lat[i] = now_us() - t0;
+        if (rc) w->bad++;
+    }
+    for (j = 0; j < N; ++j)
+        if (memcmp(w->v[j], w->want[j], g_vec)) w->bad++;
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    int a, t, j, nt;
+    uint32_t seed = 12345;
+    if (argc < 6) {
+        fprintf(stderr, "usage: %s vec calls coalesce_max mixed T...\n", argv[0]);
+        return 2;
+    }
+    g_vec = (size_t)atol(argv[1]);
+    g_calls = atoi(argv[2]);
+    if (g_calls > MAXCALLS) g_calls = MAXCALLS;
+    rs_tune("host_coalesce_max", atoi(argv[3]));
+    g_mixed = atoi(argv[4]);
+    if (rs_device_count() < 1 || rs_new(D, P, -1, &g_rs) != RS_OK) {
+        fprintf(stderr, "no device\n");
+        return 1;
+    }
+    for (t = 0; t < MAXT; ++t) {
+        Worker* w = &g_w[t];
+        w->id = t;
+        for (j = 0; j < N; ++j) {
+            size_t b;
+            w->v[j] = (uint8_t*)malloc(g_vec);
+            w->want[j] = (uint8_t*)malloc(g_vec);
+            w->lens[j] = g_vec;
+            for (b = 0; b < g_vec; ++b) {
+                seed = seed * 1664525u + 1013904223u;
+                w->v[j][b] = (uint8_t)(seed >> 24);
+            }
+        }
+        /* expected result: the same call made alone (also leaves v in its final state) */
+        if (rs_encode(g_rs, w->v, w->lens, N) != RS_OK) return 1;
+        for (j = 0; j < N; ++j) memcpy(w->want[j], w->v[j], g_vec);
+    }
+    for (a = 5; a < argc; ++a) {
+        pthread_t th[MAXT];
+        double t0, t1, all_lat[MAXT * 16], med, p90;
+        int bad = 0, k = 0;
+        nt = atoi(argv[a]);
+        if (nt < 1 || nt > MAXT) continue;
+        pthread_barrier_init(&g_bar, NULL, (unsigned)nt + 1);
+        for (t = 0; t < nt; ++t) {
+            g_w[t].bad = 0;
+            pthread_create(&th[t], NULL, run, &g_w[t]);
+        }
+        pthread_barrier_wait(&g_bar);
+        t0 = now_us();
+        for (t = 0; t < nt; ++t) pthread_join(th[t], NULL);
+        t1 = now_us();
+        pthread_barrier_destroy(&g_bar);
+        for (t = 0; t < nt; ++t) {
+            int i;
+            bad += g_w[t].bad;
+            for (i = 0; i < g_calls && k < MAXT * 16; i += (g_calls + 15) / 16) all_lat[k++] = g_w[t].lat[i];
+        }
+        qsort(all_lat, (size_t)k, sizeof(double), cmpd);
+        med = all_lat[k / 2];
+        p90 = all_lat[k * 9 / 10];
+        printf("{\"threads\": %d, \"vec\": %zu, \"calls\": %d, \"mixed\": %d, \"coalesce_max\": %s, "
+               "\"calls_per_s\": %.0f, \"GiBps\": %.3f, \"median_us\": %.1f, \"p90_us\": %.1f, \"errors\": %d}\n",
+               nt, g_vec, nt * g_calls, g_mixed, argv[3], nt * g_calls / ((t1 - t0) * 1e-6),
+               (double)nt * g_calls * N * g_vec / ((t1 - t0) * 1e-6) / 1073741824.0, med, p90, bad);
+        fflush(stdout);
+        if (bad) return 3;
+    }
+    rs_free(g_rs);
+    return 0;
+}
