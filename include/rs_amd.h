@@ -297,6 +297,11 @@ RS_API uint64_t rs_inverse_cache_key(const int* survived, int ns);
 /* Number of inverse matrices currently cached (rs.go:33-39). */
 RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
 
+/* Host-call coalescing counters since rs_new: kernel launches made for
+ * coalesced batches, and the host calls they carried (calls > launches
+ * when concurrent calls shared a launch).  Either pointer may be NULL. */
+RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls);
+
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad", "stage_late",
  * "lane_bytes" (16 | 8, 0 = per launch), "vpt1",

@@ -483,6 +483,13 @@ int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out) {
 
 uint64_t rs_inverse_cache_key(const int* survived, int ns) { return cache_key(survived, ns); }
 
+int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls) {
+    if (!rs) return RS_ERR_INVAL;
+    if (launches) *launches = rs->co_launches.load(std::memory_order_relaxed);
+    if (calls) *calls = rs->co_calls.load(std::memory_order_relaxed);
+    return RS_OK;
+}
+
 int64_t rs_inverse_cache_size(const rs_t* rs) {
     if (!rs) return -1;
     std::lock_guard<std::mutex> lk(const_cast<rs_t*>(rs)->cache_mu);

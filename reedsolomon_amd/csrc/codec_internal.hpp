@@ -110,6 +110,7 @@ struct rs_codec {
     CoBatch co[2];
     bool co_gpu_busy = false;
     int co_active = 0;             // callers inside host_call
+    std::atomic<uint64_t> co_launches{0}, co_calls{0};
     hipStream_t co_stream = nullptr;
 
     // Upload ring for per-call device descriptors (multi-pattern Reconst):

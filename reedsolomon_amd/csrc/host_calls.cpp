@@ -379,6 +379,8 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
             rs->co_gpu_busy = true;
             const int n = b->joined;
             lk.unlock();
+            rs->co_launches.fetch_add(1, std::memory_order_relaxed);
+            rs->co_calls.fetch_add(static_cast<uint64_t>(n), std::memory_order_relaxed);
             const int rc = run_batch(rs, *b, n);
             lk.lock();
             b->rc = rc;

@@ -454,6 +454,66 @@ def test_concurrent_host_calls(rslib, orc, torch_dev):
     assert not errors, errors
 
 
+def test_coalesced_host_calls(rslib, orc, torch_dev):
+    """Concurrent host calls of several shapes (Encode at two sizes, Update,
+    Replace, Reconst) from 16 threads share launches; every result must equal
+    the oracle's for that call alone."""
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    errors = []
+    barrier = threading.Barrier(16)
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(1000 + t)
+            size = 8192 if t % 2 == 0 else 8197
+            barrier.wait()
+            for it in range(12):
+                data = [_rand(rng, size) for _ in range(d)]
+                v = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
+                r.Encode(v)
+                exp = _oracle_encode(orc, d, p, data)
+                if any(not np.array_equal(v[d + j], exp[j]) for j in range(p)):
+                    errors.append((t, it, "encode"))
+                if t % 4 == 1:  # Update one row
+                    row = (t + it) % d
+                    new = _rand(rng, size)
+                    par = [x.copy() for x in v[d:]]
+                    r.Update(v[row], new, row, par)
+                    data2 = [x.copy() for x in data]
+                    data2[row] = new
+                    exp2 = _oracle_encode(orc, d, p, data2)
+                    if any(not np.array_equal(par[j], exp2[j]) for j in range(p)):
+                        errors.append((t, it, "update"))
+                elif t % 4 == 3:  # Replace rows 2, 5 from zero
+                    zdata = [x.copy() for x in data]
+                    zdata[2][:] = 0
+                    zdata[5][:] = 0
+                    par = _oracle_encode(orc, d, p, zdata)
+                    r.Replace([data[2], data[5]], [2, 5], par)
+                    if any(not np.array_equal(par[j], exp[j]) for j in range(p)):
+                        errors.append((t, it, "replace"))
+                lost = [0, 11] if t % 3 else [3, 7, 12]
+                w = [x.copy() for x in v]
+                for i in lost:
+                    w[i][:] = 0
+                r.Reconst(w, [], lost)
+                if any(not np.array_equal(w[i], v[i]) for i in lost):
+                    errors.append((t, it, "reconst"))
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:10]
+    launches, calls = r.host_call_stats()
+    assert calls >= 16 * 12 * 2  # every Encode and Reconst went through the coalescer
+    assert launches < calls, (launches, calls)  # concurrent calls shared launches
+
+
 def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
     """Host-resident stripes: pinned and pageable, ragged chunking."""
     torch = torch_dev
