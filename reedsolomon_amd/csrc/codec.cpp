@@ -470,6 +470,7 @@ int rs_tune(const char* name, int value) {
     else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
     else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
     else if (n == "host_batch_zc") g_host_batch_zc = value;
+    else if (n == "host_dma_1d") g_host_dma_1d = value;
     else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
     else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
     else return RS_ERR_INVAL;

@@ -111,6 +111,15 @@ struct rs_codec {
     bool co_gpu_busy = false;
     int co_active = 0;             // callers inside host_call
     std::atomic<uint64_t> co_launches{0}, co_calls{0};
+
+    // DMA pipeline of rs_encode_host_batch (host_batches.cpp): device ring,
+    // copy-in / compute / copy-out streams and per-slot events, kept across
+    // calls (a per-call hipMalloc / hipFree of the ring cost ~25 % of a
+    // 128-stripe call).  Guarded by stage_mu.
+    uint8_t* dma_ring = nullptr;
+    size_t dma_ring_bytes = 0;
+    hipStream_t dma_stream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t dma_ev[3][8] = {};
     hipStream_t co_stream = nullptr;
 
     // Upload ring for per-call device descriptors (multi-pattern Reconst):
@@ -148,6 +157,14 @@ struct rs_codec {
         if (hstage) (void)hipHostFree(hstage);
         for (CoBatch& b : co)
             if (b.host) (void)hipHostFree(b.host);
+        for (hipStream_t s : dma_stream)
+            if (s) (void)hipStreamSynchronize(s);
+        if (dma_ring) (void)hipFree(dma_ring);
+        for (auto& row : dma_ev)
+            for (hipEvent_t e : row)
+                if (e) (void)hipEventDestroy(e);
+        for (hipStream_t s : dma_stream)
+            if (s) (void)hipStreamDestroy(s);
         if (co_stream) (void)hipStreamDestroy(co_stream);
         for (hipEvent_t e : chunk_ev)
             if (e) (void)hipEventDestroy(e);
@@ -290,7 +307,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
               size_t size, bool accumulate);
 
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
-extern int g_host_batch_zc;
+extern int g_host_batch_zc, g_host_dma_1d;
 int host_device_range(const void* p, size_t bytes, uint8_t** dev);
 size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
 

@@ -48,6 +48,10 @@ size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len) 
 // memory over PCIe directly.  Measured on MI355X: 72 GiB/s of (k+m)*vec for
 // 10+4 encode at 8 KiB-1 MiB vectors vs 13-57 GiB/s for the DMA pipeline.
 int g_host_batch_zc = 1;
+// DMA pipeline copies of a dense layout: 0 = one 2-D copy per chunk (default:
+// 70.4-70.7 GiB/s for 10+4 @ 1 MiB x 128 vs 66.8-67.1 with 1-D copies,
+// tools/dma_ab.py), 1 = one 1-D hipMemcpyAsync per stripe.
+int g_host_dma_1d = 0;
 
 }  // namespace detail
 }  // namespace rsamd
@@ -115,20 +119,37 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
     const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);
     const size_t slot_bytes = static_cast<size_t>(dstripe) * stripes_per_chunk;
     std::lock_guard<std::mutex> lk(rs->stage_mu);
-    uint8_t* ring = nullptr;
-    if (hipMalloc(&ring, slot_bytes * slots) != hipSuccess) return RS_ERR_DEVICE;
-    hipStream_t sh = nullptr, sc = nullptr, sd = nullptr;
-    std::vector<hipEvent_t> ev_in(slots), ev_enc(slots), ev_free(slots);
     int rc = RS_OK;
-    if (hipStreamCreateWithFlags(&sh, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&sc, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&sd, hipStreamNonBlocking) != hipSuccess)
-        rc = RS_ERR_DEVICE;
-    for (int i = 0; i < slots && rc == RS_OK; ++i)
-        if (hipEventCreateWithFlags(&ev_in[i], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ev_enc[i], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ev_free[i], hipEventDisableTiming) != hipSuccess)
-            rc = RS_ERR_DEVICE;
+    if (slot_bytes * slots > rs->dma_ring_bytes) {
+        if (rs->dma_ring) {
+            for (hipStream_t s : rs->dma_stream)
+                if (s) (void)hipStreamSynchronize(s);
+            (void)hipFree(rs->dma_ring);
+        }
+        rs->dma_ring = nullptr;
+        rs->dma_ring_bytes = 0;
+        if (hipMalloc(&rs->dma_ring, slot_bytes * slots) != hipSuccess) {
+            rs->dma_ring = nullptr;
+            return RS_ERR_DEVICE;
+        }
+        rs->dma_ring_bytes = slot_bytes * slots;
+    }
+    uint8_t* ring = rs->dma_ring;
+    for (hipStream_t& s : rs->dma_stream)
+        if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            s = nullptr;
+            return RS_ERR_DEVICE;
+        }
+    for (auto& row : rs->dma_ev)
+        for (int i = 0; i < slots; ++i)
+            if (!row[i] && hipEventCreateWithFlags(&row[i], hipEventDisableTiming) != hipSuccess) {
+                row[i] = nullptr;
+                return RS_ERR_DEVICE;
+            }
+    hipStream_t sh = rs->dma_stream[0], sc = rs->dma_stream[1], sd = rs->dma_stream[2];
+    hipEvent_t* ev_in = rs->dma_ev[0];
+    hipEvent_t* ev_enc = rs->dma_ev[1];
+    hipEvent_t* ev_free = rs->dma_ev[2];
     auto ok = [&](hipError_t e) {
         if (e != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
         return rc == RS_OK;
@@ -142,7 +163,13 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
         uint8_t* dev = ring + static_cast<size_t>(slot) * slot_bytes;
         uint8_t* hb = base + static_cast<int64_t>(c0) * stripe_stride;
         if (chunk >= slots && !ok(hipStreamWaitEvent(sh, ev_free[slot], 0))) break;
-        if (dense) {  // one 2-D copy: cn rows of d*len bytes
+        if (dense && g_host_dma_1d) {  // cn 1-D copies of d*len bytes
+            bool good = true;
+            for (int s = 0; s < cn && good; ++s)
+                good = ok(hipMemcpyAsync(dev + static_cast<int64_t>(s) * dstripe, hb + s * stripe_stride,
+                                         static_cast<size_t>(d) * len, hipMemcpyHostToDevice, sh));
+            if (!good) break;
+        } else if (dense) {  // one 2-D copy: cn rows of d*len bytes
             if (!ok(hipMemcpy2DAsync(dev, dstripe, hb, stripe_stride, static_cast<size_t>(d) * len, cn,
                                      hipMemcpyHostToDevice, sh)))
                 break;
@@ -158,7 +185,14 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
         rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, sc);
         if (rc) break;
         if (!ok(hipEventRecord(ev_enc[slot], sc)) || !ok(hipStreamWaitEvent(sd, ev_enc[slot], 0))) break;
-        if (dense) {
+        if (dense && g_host_dma_1d) {
+            bool good = true;
+            for (int s = 0; s < cn && good; ++s)
+                good = ok(hipMemcpyAsync(hb + s * stripe_stride + d * vect_stride,
+                                         dev + static_cast<int64_t>(s) * dstripe + d * pitch,
+                                         static_cast<size_t>(p) * len, hipMemcpyDeviceToHost, sd));
+            if (!good) break;
+        } else if (dense) {
             if (!ok(hipMemcpy2DAsync(hb + d * vect_stride, stripe_stride, dev + d * pitch, dstripe,
                                      static_cast<size_t>(p) * len, cn, hipMemcpyDeviceToHost, sd)))
                 break;
@@ -171,14 +205,7 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
         if (!ok(hipEventRecord(ev_free[slot], sd))) break;
     }
     for (hipStream_t s : {sh, sc, sd})
-        if (s) {
-            if (hipStreamSynchronize(s) != hipSuccess) rc = RS_ERR_DEVICE;
-            (void)hipStreamDestroy(s);
-        }
-    for (int i = 0; i < slots; ++i)
-        for (hipEvent_t e : {ev_in[i], ev_enc[i], ev_free[i]})
-            if (e) (void)hipEventDestroy(e);
-    (void)hipFree(ring);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = RS_ERR_DEVICE;
     return rc;
 }
 
