@@ -57,7 +57,7 @@ LaunchTuning& tuning() {
         const char* sl = std::getenv("RSAMD_STAGE_LATE");
         x.stage_late = sl ? std::atoi(sl) : 0;
         const char* lb = std::getenv("RSAMD_LANE_BYTES");
-        x.lane_bytes = lb ? std::atoi(lb) : 0;  // 0: per launch (lane16_for)
+        x.lane_bytes = lb ? std::atoi(lb) : 8;
         const char* v1 = std::getenv("RSAMD_VPT1");
         x.vpt1 = (v1 && std::atoi(v1) == 2) ? 2 : 1;
 
@@ -110,11 +110,15 @@ enum : int {
     kVarSingleTab = 4,   // no LDS table prefetch across columns (fewer VGPRs)
     kVarBitop3 = 8,      // explicit v_bitop3 (xor3) accumulation
     kVarCarry = 16,      // with kVarBitop3: pair columns through a carried term (1.5 xor3 per product, not 2)
+    kVarShift64 = 32,    // bit groups of dword pairs via v_lshrrev_b64 (4 VALU per dword, not 5)
 };
 // kVarCarry: A/B on MI355X (tools/ab.py, profiles/r01/ab_carry.log): split
 // Encode +0.3-2.6 %, interleaved Encode +2 %, Reconst of 4 +2.4 %, 16-pattern
 // Reconst +1.6 %, the rest within noise; 8 % fewer VALU instructions.
-constexpr int kVarDefault = kVarBitop3 | kVarSingleTab | kVarNtLoad | kVarCarry;
+// kVarShift64: in-process A/B on two boxes (profiles/r01/ab_shift64.log):
+// +0.5-1.1 % with 16-byte lane units, +0.5-0.4 % with 8-byte units; VALU per
+// wave 959 -> 919 (16 B), 499 -> 479 (8 B).
+constexpr int kVarDefault = kVarBitop3 | kVarSingleTab | kVarNtLoad | kVarCarry | kVarShift64;
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -281,16 +285,37 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
             }
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
+                // kVarShift64: bit groups of a dword pair from two 64-bit shifts
+                constexpr int QS = ((VAR & kVarShift64) && LQ % 2 == 0) ? 2 : 1;
 #pragma unroll
-                for (int q = 0; q < LQ; ++q) {
+                for (int qp = 0; qp < LQ; qp += QS) {
+                uint32_t G0[QS], G1[QS], G2[QS];
+                if (!(VAR & kVarXorOnly)) {
+                    if constexpr (QS == 2) {
+                        const uint64_t X = (static_cast<uint64_t>(x[b][v][qp + 1]) << 32) | x[b][v][qp];
+                        uint64_t Y3, Y6;
+                        asm volatile("v_lshrrev_b64 %0, 3, %1" : "=v"(Y3) : "v"(X));
+                        asm volatile("v_lshrrev_b64 %0, 6, %1" : "=v"(Y6) : "v"(X));
+                        G0[0] = x[b][v][qp] & 0x07070707u;
+                        G0[1] = x[b][v][qp + 1] & 0x07070707u;
+                        G1[0] = static_cast<uint32_t>(Y3) & 0x07070707u;
+                        G1[1] = static_cast<uint32_t>(Y3 >> 32) & 0x07070707u;
+                        G2[0] = static_cast<uint32_t>(Y6) & 0x03030303u;
+                        G2[1] = static_cast<uint32_t>(Y6 >> 32) & 0x03030303u;
+                    } else {
+                        split_groups(x[b][v][qp], G0[0], G1[0], G2[0]);
+                    }
+                }
+#pragma unroll
+                for (int qq = 0; qq < QS; ++qq) {
+                    const int q = qp + qq;
                     const uint32_t xq = x[b][v][q];
                     if (VAR & kVarXorOnly) {
 #pragma unroll
                         for (int r = 0; r < MC; ++r) acc[r][v][q] ^= xq ^ t[r * 5];
                         continue;
                     }
-                    uint32_t g0, g1, g2;
-                    split_groups(xq, g0, g1, g2);
+                    const uint32_t g0 = G0[qq], g1 = G1[qq], g2 = G2[qq];
 #pragma unroll
                     for (int r = 0; r < MC; ++r) {
                         const uint32_t* tr = &t[r * 5];
@@ -312,6 +337,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
                             acc[r][v][q] ^= gf_mul_packed(g0, g1, g2, tr);
                         }
                     }
+                }
                 }
             }
             // Pin the running sums per column: stops LLVM from reassociating
@@ -589,6 +615,11 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
                                  true, "vec1<10,8B,nocarry>", true, 2}; return true;
         case 144: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 4, 1, kVarDefault & ~kVarCarry>, 10, 4, 1,
                                  true, "vec1<10,16B,nocarry>", true, 4}; return true;
+        // without the 64-bit-shift bit-group split (kVarShift64)
+        case 146: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 4, 1, kVarDefault & ~kVarShift64>, 10, 4,
+                                 1, true, "vec1<10,16B,noshift64>", true, 4}; return true;
+        case 147: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 2, 1, kVarDefault & ~kVarShift64>, 10, 4,
+                                 1, true, "vec1<10,8B,noshift64>", true, 2}; return true;
         // workgroup size: 64 / 128 lanes (one / two waves), 16- or 8-byte units, tables staged early / late
 #define RSAMD_BSV(LATE, LQ, BS, TAG) \
     Variant{gf_matmul_vec1<10, true, 4, false, 0, LATE, LQ, 1, kVarDefault, BS>, 10, 4, 1, true, TAG, true, LQ, BS}
@@ -691,27 +722,19 @@ static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body, bool l
     return RSAMD_VARIANT(4, false, 8, true, 1);
 }
 
-// Lane width of the one-chunk kernels.  A/B on MI355X (tools/ab.py, same
-// process): Encode with parity in its own region (split layout) runs at
-// 6.30-6.41 TB/s with 16-byte lane units vs 6.14-6.32 with 8-byte units;
-// every pattern whose outputs sit among its inputs (interleaved Encode,
-// in-place Reconst, Update, Replace) is faster with 8-byte units (Reconst of
-// one lost vector 5.75 -> 6.36-6.41 TB/s, interleaved Encode 5.85-5.97 ->
-// 6.00-6.12).  XOR-only diagnostics of the same kernel: 8-byte 6.63, 16-byte
-// 6.27 TB/s.
-static bool lane16_for(const MatmulArgs& a) {
-    if (tuning().lane_bytes == 16) return true;
-    if (tuning().lane_bytes == 8) return false;
-    if (a.accumulate || a.rows < 3 || a.nstripes == 1) return false;
-    for (int r = 0; r < a.rows; ++r)
-        for (int c = 0; c < a.cols; ++c)
-            if ((a.sid[a.cols + r] & 3) == (a.sid[c] & 3)) return false;
-    return true;
-}
+// Lane width of the one-chunk kernels: 8-byte units (dwordx2, 512 B per wave
+// instruction) unless rs_tune("lane_bytes", 16) forces 16-byte units.  A/B on
+// MI355X (tools/ab.py, same process, profiles/r01/ab_lane_width.log and
+// ab_shift64.log): with the paired / 64-bit-shift arithmetic, split-layout
+// Encode runs 6.43-6.53 TB/s with 8-byte units vs 6.34-6.49 with 16-byte
+// units, and every in-place pattern gains more (Reconst of one lost vector
+// 5.75 -> 6.41, Update 5.78 -> 6.34).  (Before the arithmetic was trimmed,
+// split-layout Encode was 2-4 % faster with 16-byte units.)  XOR-only
+// diagnostics of the same kernel: 8-byte 6.63, 16-byte 6.27 TB/s.
+static bool lane16_for(const MatmulArgs&) { return tuning().lane_bytes == 16; }
 
 const char* vector_kernel_name(int rows, int cols, int accumulate) {
-    // the name for a split-layout batch (outputs in their own region)
-    return pick(rows, cols, accumulate != 0, tuning().vpt, 0, accumulate == 0 && rows >= 3).name;
+    return pick(rows, cols, accumulate != 0, tuning().vpt, 0, tuning().lane_bytes == 16).name;
 }
 
 static bool aligned16(uint64_t v) { return (v & 15u) == 0; }
