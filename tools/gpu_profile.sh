@@ -17,4 +17,10 @@ for C in FETCH_SIZE WRITE_SIZE; do
       python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --e2e-stripes 0 --steps 5 --warmup 1 --verify 0 > "$OUT/pmc_$C.log" 2>&1
   tail -1 "$OUT/pmc_$C.log" | cut -c1-200
 done
+for C in FETCH_SIZE WRITE_SIZE; do
+  echo "== calibration pmc $C (known bytes, 16- and 8-byte lanes)"
+  timeout -k 10 200 rocprofv3 --pmc "$C" -d "$OUT/calib_$C" -o pmc --output-format csv -- \
+      python3 "$REPO/tools/fetch_calib.py" > "$OUT/calib_$C.log" 2>&1
+  tail -1 "$OUT/calib_$C.log" | cut -c1-200
+done
 find "$OUT" -name "*.csv" | head -20

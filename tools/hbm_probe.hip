@@ -307,3 +307,41 @@ extern "C" int probe_buf_g(int kind, void* a, void* b, uint64_t vec, int nstripe
 #undef KG
     return hipGetLastError();
 }
+
+// Counter calibration (MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are
+// calibrated only for 16-B-per-lane streams): one pass over `bytes` with each
+// access width, buffer nt like the codec kernels.  Distinct kernel names so
+// rocprofv3 attributes the counters per width (tools/fetch_calib.py).
+__global__ __launch_bounds__(256) void kc_read16(const uint8_t* src, uint8_t* sink) {
+    const uint64_t base = (uint64_t)blockIdx.x * 4096;
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(src + base, 4096), threadIdx.x * 16, 0, 2);
+    if (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u && v.z == 1u) *(u32x4*)sink = v;
+}
+__global__ __launch_bounds__(256) void kc_read8(const uint8_t* src, uint8_t* sink) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const uint64_t base = (uint64_t)blockIdx.x * 2048;
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rsrc(src + base, 2048), threadIdx.x * 8, 0, 2);
+    if (v.x == 0x9e3779b9u && v.y == 0x7f4a7c15u) *(u32x2*)sink = v;
+}
+__global__ __launch_bounds__(256) void kc_write16(uint8_t* dst) {
+    const uint64_t base = (uint64_t)blockIdx.x * 4096;
+    u32x4 v = {blockIdx.x, threadIdx.x, 2u, 3u};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(dst + base, 4096), threadIdx.x * 16, 0, 2);
+}
+__global__ __launch_bounds__(256) void kc_write8(uint8_t* dst) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const uint64_t base = (uint64_t)blockIdx.x * 2048;
+    u32x2 v = {blockIdx.x, threadIdx.x};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rsrc(dst + base, 2048), threadIdx.x * 8, 0, 2);
+}
+extern "C" int probe_calib(int kind, void* a, uint64_t bytes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* p = (uint8_t*)a;
+    if (bytes % 4096) return -1;
+    if (kind == 0) hipLaunchKernelGGL(kc_read16, dim3(bytes / 4096), dim3(256), 0, st, p, p);
+    else if (kind == 1) hipLaunchKernelGGL(kc_read8, dim3(bytes / 2048), dim3(256), 0, st, p, p);
+    else if (kind == 2) hipLaunchKernelGGL(kc_write16, dim3(bytes / 4096), dim3(256), 0, st, p);
+    else if (kind == 3) hipLaunchKernelGGL(kc_write8, dim3(bytes / 2048), dim3(256), 0, st, p);
+    else return -1;
+    return hipGetLastError();
+}

@@ -5,8 +5,12 @@
   profiles/traffic.json                  HBM bytes per launch, read by bench.py
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half
-the bytes of a wide 16-B/lane streaming read -> doubled; WRITE_SIZE (KiB) is
-exact for 16-B/lane stores."""
+the bytes of a wide 16-B/lane streaming read and WRITE_SIZE is exact for
+16-B/lane stores; other widths are uncalibrated there.  The codec kernel uses
+8-byte lanes, so gpu_profile.sh also runs tools/fetch_calib.py (one pass over
+a known 2 GiB with 16- and 8-byte buffer loads / stores) under the same
+counters, and the factor measured for the kernel's width (bytes per counted
+byte) converts its counts."""
 import csv
 import json
 import os
@@ -33,8 +37,24 @@ def per_launch(counter):
 
 fetch = per_launch("FETCH_SIZE")
 write = per_launch("WRITE_SIZE")
-f_b = statistics.median(fetch) * 1024 * 2
-w_b = statistics.median(write) * 1024
+
+
+def calib(counter, kernel, nbytes=2 << 30):
+    """bytes per counted byte for one calibration kernel (median over its launches)."""
+    path = os.path.join(src, f"calib_{counter}", "pmc_counter_collection.csv")
+    if not os.path.exists(path):
+        return None
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    return nbytes / (statistics.median(vals) * 1024) if vals else None
+
+
+lane = 8 if os.environ.get("RSAMD_LANE_BYTES", "8") != "16" else 16
+cal = {f"read{w}": calib("FETCH_SIZE", f"kc_read{w}") for w in (16, 8)}
+cal.update({f"write{w}": calib("WRITE_SIZE", f"kc_write{w}") for w in (16, 8)})
+f_fac = cal[f"read{lane}"] or 2.0
+w_fac = cal[f"write{lane}"] or 1.0
+f_b = statistics.median(fetch) * 1024 * f_fac
+w_b = statistics.median(write) * 1024 * w_fac
 trace_all = [r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv")))
              if "gf_matmul_vec" in r["Kernel_Name"]]
 dominant = statistics.mode([r["Kernel_Name"] for r in trace_all])
@@ -51,8 +71,10 @@ summary = {
                          "and warm-up, which include the post-idle power transient)",
     "FETCH_SIZE_KiB_median": statistics.median(fetch),
     "WRITE_SIZE_KiB_median": statistics.median(write),
-    "hbm_read_bytes_per_launch (FETCH_SIZE*1024*2)": f_b,
-    "hbm_write_bytes_per_launch (WRITE_SIZE*1024)": w_b,
+    "lane_bytes": lane,
+    "counter_calibration_bytes_per_counted_byte": cal,
+    "hbm_read_bytes_per_launch (FETCH_SIZE*1024*factor)": f_b,
+    "hbm_write_bytes_per_launch (WRITE_SIZE*1024*factor)": w_b,
     "hbm_bytes_per_launch": f_b + w_b,
 }
 json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
