@@ -13,6 +13,7 @@ counters, and the factor measured for the kernel's width (bytes per counted
 byte) converts its counts."""
 import csv
 import json
+import math
 import os
 import shutil
 import statistics
@@ -40,19 +41,25 @@ write = per_launch("WRITE_SIZE")
 
 
 def calib(counter, kernel, nbytes=2 << 30):
-    """bytes per counted byte for one calibration kernel (median over its launches)."""
+    """Bytes per counted byte for one calibration kernel (median over its
+    launches), as measured and rounded to the counter's unit (a power of two:
+    the measured 1.99998 / 0.9989-0.9993 are 2 and 1 plus ~0.1 % of unrelated
+    traffic counted during the calibration launch)."""
     path = os.path.join(src, f"calib_{counter}", "pmc_counter_collection.csv")
     if not os.path.exists(path):
         return None
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
-    return nbytes / (statistics.median(vals) * 1024) if vals else None
+    if not vals:
+        return None
+    raw = nbytes / (statistics.median(vals) * 1024)
+    return {"measured": raw, "unit": 2.0 ** round(math.log2(raw))}
 
 
 lane = 8 if os.environ.get("RSAMD_LANE_BYTES", "8") != "16" else 16
 cal = {f"read{w}": calib("FETCH_SIZE", f"kc_read{w}") for w in (16, 8)}
 cal.update({f"write{w}": calib("WRITE_SIZE", f"kc_write{w}") for w in (16, 8)})
-f_fac = cal[f"read{lane}"] or 2.0
-w_fac = cal[f"write{lane}"] or 1.0
+f_fac = cal[f"read{lane}"]["unit"] if cal[f"read{lane}"] else 2.0
+w_fac = cal[f"write{lane}"]["unit"] if cal[f"write{lane}"] else 1.0
 f_b = statistics.median(fetch) * 1024 * f_fac
 w_b = statistics.median(write) * 1024 * w_fac
 trace_all = [r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv")))
