@@ -104,8 +104,10 @@ int ensure_device(rs_t* rs) {
 
 // Perm tables for a rows x cols coefficient matrix, laid out
 // [col][rows_pad][5] dwords (rows padded to a multiple of 8 so that every
-// kernel row group reads inside the allocation).  Uploaded once per distinct
-// matrix and reused by every later launch.
+// kernel row group reads inside the allocation), followed - for rows <= 4 -
+// by the same tables as the 4-row kernels' LDS image [rup(cols, 4)][20]
+// (zero rows and columns as padding), which those kernels stage with a plain
+// copy.  Uploaded once per distinct matrix and reused by every later launch.
 int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t** out, int* rows_pad_out) {
     const int rows_pad = static_cast<int>(rup(rows, 8));
     std::string key(reinterpret_cast<const char*>(&rows), sizeof rows);
@@ -124,10 +126,14 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
         for (auto& kv : rs->tables) (void)hipFree(kv.second);
         rs->tables.clear();
     }
-    std::vector<uint32_t> host(static_cast<size_t>(cols) * rows_pad * 5, 0);
+    const size_t main_dw = static_cast<size_t>(cols) * rows_pad * 5;
+    const size_t img_dw = rows <= 4 ? rup(cols, 4) * 20 : 0;
+    std::vector<uint32_t> host(main_dw + img_dw, 0);
     for (int c = 0; c < cols; ++c)
-        for (int r = 0; r < rows; ++r)
+        for (int r = 0; r < rows; ++r) {
             perm_table(mat[static_cast<size_t>(r) * cols + c], &host[(static_cast<size_t>(c) * rows_pad + r) * 5]);
+            if (img_dw) perm_table(mat[static_cast<size_t>(r) * cols + c], &host[main_dw + static_cast<size_t>(c) * 20 + r * 5]);
+        }
     uint32_t* dptr = nullptr;
     if (hipMalloc(&dptr, host.size() * 4) != hipSuccess) return RS_ERR_DEVICE;
     if (hipMemcpy(dptr, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -152,6 +158,7 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     std::memset(&a, 0, sizeof a);
     int rc = get_tables(rs, mat, rows, cols, &a.tables, &a.rows_pad);
     if (rc) return rc;
+    a.img4 = rows <= 4 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
     a.rows = rows;
     a.cols = cols;
     a.nstripes = nstripes;

@@ -429,20 +429,28 @@ __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
     const int cols = KFIX ? KB : a.cols;
     const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
     auto stage = [&]() {
-        for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) {
-            const int i = idx / COLD;
-            const int w = idx - i * COLD;
-            const int rr = w / 5;
-            uint32_t v = 0;
-            if (i < cols && rr < MC && rr < a.rows)
-                v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + rr) * 5 + (w - rr * 5)];
-            lds32[idx] = v;
+        if (MC == 4 && a.img4) {  // prepared image (get_tables): a plain copy
+            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) lds32[idx] = a.img4[idx];
+        } else {
+            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) {
+                const int i = idx / COLD;
+                const int w = idx - i * COLD;
+                const int rr = w / 5;
+                uint32_t v = 0;
+                if (i < cols && rr < MC && rr < a.rows)
+                    v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + rr) * 5 + (w - rr * 5)];
+                lds32[idx] = v;
+            }
         }
         __syncthreads();
     };
-    const int64_t chunk = blockIdx.x;
-    const int si = static_cast<int>(chunk / a.chunks_per_stripe);
-    const int64_t cb = chunk - static_cast<int64_t>(si) * a.chunks_per_stripe;
+    // stripe and chunk of this workgroup: a scalar shift when the chunk count
+    // per stripe is a power of two (the grid is < 2^31 chunks)
+    const uint32_t chunk = blockIdx.x;
+    const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
+    const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
+    const int si = static_cast<int>(su);
+    const int64_t cb = static_cast<int64_t>(chunk - su * cps);
     const int s = a.stripe_ids ? a.stripe_ids[si] : si;
     if (!STAGE_LATE) stage();
     chunk_body<KB, KFIX, MC, ACC, VPT, VAR, kAuxNt, kAuxNt, WIN, LQ, BS>(
@@ -808,6 +816,9 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         const uint64_t nunits = a.body / (4 * var.lq);
         a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
         a.total_chunks = a.chunks_per_stripe * a.nstripes;
+        a.cps_shift = -1;
+        for (int sh = 0; sh < 31; ++sh)
+            if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
         int64_t grid = a.total_chunks;
         if (!var.one_chunk) {
             if (tu.max_grid > 0 && grid > tu.max_grid) grid = tu.max_grid;

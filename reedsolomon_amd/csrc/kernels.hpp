@@ -21,6 +21,7 @@ constexpr int kMaxPtrs = 260;  // inputs + outputs of one launch (d+p <= 256, Up
 // regions (e.g. data and parity in separate buffers).
 struct MatmulArgs {
     const uint32_t* tables;   // device perm tables, [cols][rows_pad][5] dwords
+    const uint32_t* img4;     // the same as a 4-row LDS image [rup(cols, 4)][20] (rows <= 4), or null
     int rows, cols, rows_pad;
     int nstripes;
     int accumulate;           // 0: overwrite (Encode), 1: XOR into out (updateOnly)
@@ -33,6 +34,7 @@ struct MatmulArgs {
     const int32_t* stripe_ids;  // optional device list: launch stripe i is stripe stripe_ids[i]
     int64_t chunks_per_stripe;
     int64_t total_chunks;
+    int cps_shift;            // log2(chunks_per_stripe) when a power of two, else -1
     uint64_t ptr[kMaxPtrs];   // inputs [0, cols), outputs [cols, cols+rows)
     uint32_t sid[kMaxPtrs];   // stride selector of each vector (0..3); dwords so the
                               // kernel reads them with scalar loads
