@@ -475,9 +475,13 @@ __device__ __forceinline__ void multi_chunk(const MatmulArgs& a, const PatternDe
     const uint32_t* img = a.tables + P->tab_off;
     // image columns are 20 dwords (4 rows x 5); keep the first COLD of each
     auto stage = [&]() {
-        for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
-            const int c = idx / COLD;
-            lds32[idx] = img[c * 20 + (idx - c * COLD)];
+        if (COLD == 20) {  // 4-row body: the image is the LDS layout
+            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) lds32[idx] = img[idx];
+        } else {
+            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
+                const int c = idx / COLD;
+                lds32[idx] = img[c * 20 + (idx - c * COLD)];
+            }
         }
         __syncthreads();
     };
@@ -495,9 +499,11 @@ template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4, int VA
 __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
                                                           const int32_t* __restrict__ stripe_pat) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
-    const int64_t chunk = blockIdx.x;
-    const int s = static_cast<int>(chunk / a.chunks_per_stripe);
-    const int64_t cb = chunk - static_cast<int64_t>(s) * a.chunks_per_stripe;
+    const uint32_t chunk = blockIdx.x;
+    const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
+    const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
+    const int s = static_cast<int>(su);
+    const int64_t cb = static_cast<int64_t>(chunk - su * cps);
     const int pid = stripe_pat[s];
     if (pid < 0) return;  // stripe not in the batch's work (uniform: whole workgroup)
     const PatternDesc* P = pats + pid;
@@ -757,6 +763,9 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     const uint64_t nunits = a.body / (4 * lq);
     a.chunks_per_stripe = static_cast<int64_t>((nunits + kBlock - 1) / kBlock);
     a.total_chunks = a.chunks_per_stripe * a.nstripes;
+    a.cps_shift = -1;
+    for (int sh = 0; sh < 31; ++sh)
+        if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
     // a.rows = the largest output count over the batch's patterns (<= 4)
     const bool k10 = a.cols == 10;
     const int mc = a.rows <= 1 ? 1 : (a.rows == 2 ? 2 : 4);
