@@ -8,8 +8,10 @@ CFG="${1:-10+4@1MiB}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 echo "== kernel trace"
+# 1000 timed steps, so the 50 warm-up launches (and the post-idle clock
+# ramp in them) move the --stats average by well under 1 %
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
-    python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --e2e-stripes 0 > "$OUT/kt_bench.log" 2>&1
+    python3 "$REPO/bench.py" --config "$CFG" --cpu-seconds 0 --e2e-stripes 0 --steps 1000 > "$OUT/kt_bench.log" 2>&1
 tail -1 "$OUT/kt_bench.log"
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C"

@@ -67,7 +67,7 @@ trace_all = [r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_t
 dominant = statistics.mode([r["Kernel_Name"] for r in trace_all])
 trace = [r for r in trace_all if r["Kernel_Name"] == dominant]
 durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
-steps = int(os.environ.get("BENCH_STEPS", "100"))
+steps = int(os.environ.get("BENCH_STEPS", "1000"))  # tools/gpu_profile.sh runs --steps 1000
 summary = {
     "config": cfg,
     "kernel": trace[0]["Kernel_Name"] if trace else None,
