@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 import reedsolomon_amd as rs  # noqa: E402
 
-K, M, VEC, S = 10, 4, 1 << 20, 256
+K, M, VEC, S = int(os.environ.get("AB_K", "10")), 4, 1 << 20, 256
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
 DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0, "lane_bytes": 8, "vpt1": 1}
