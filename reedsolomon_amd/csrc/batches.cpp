@@ -13,224 +13,93 @@ using namespace rsamd::detail;
 extern "C" {
 
 int rs_encode_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, void* stream) {
-    if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
-    RS_TRY(check_encode(rs, lens, n));
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    return matmul(rs, rs->gen(), rs->p, rs->d, vects, 0, vects + rs->d, 0, 1, lens[0], false, as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
+        RS_TRY(check_encode(rs, lens, n));
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        return matmul(rs, rs->gen(), rs->p, rs->d, vects, 0, vects + rs->d, 0, 1, lens[0], false, as_stream(stream));
+    });
 }
 
 int rs_encode_batch_layout(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, void* stream) {
-    if (!rs || !L || nstripes < 0 || (nstripes > 0 && (!L->data_base || !L->parity_base))) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (nstripes == 0) return RS_OK;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const LayoutAddr A{L, rs->d};
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    for (int i = 0; i < rs->d; ++i) in[i] = A.ptr(i);
-    for (int j = 0; j < rs->p; ++j) out[j] = A.ptr(rs->d + j);
-    return matmul(rs, rs->gen(), rs->p, rs->d, in, L->data_stripe_stride, out, L->parity_stripe_stride, nstripes,
-                  len, false, as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || !L || nstripes < 0 || (nstripes > 0 && (!L->data_base || !L->parity_base))) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (nstripes == 0) return RS_OK;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const LayoutAddr A{L, rs->d};
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        for (int i = 0; i < rs->d; ++i) in[i] = A.ptr(i);
+        for (int j = 0; j < rs->p; ++j) out[j] = A.ptr(rs->d + j);
+        return matmul(rs, rs->gen(), rs->p, rs->d, in, L->data_stripe_stride, out, L->parity_stripe_stride, nstripes,
+                      len, false, as_stream(stream));
+    });
 }
 
 int rs_encode_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
                     void* stream) {
-    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
-    const rs_layout_t L{base, stripe_stride, vect_stride, base + rs->d * vect_stride, stripe_stride, vect_stride};
-    return rs_encode_batch_layout(rs, &L, nstripes, len, stream);
+    return abi_guard([&]() -> int {
+        if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+        const rs_layout_t L{base, stripe_stride, vect_stride, base + rs->d * vect_stride, stripe_stride, vect_stride};
+        return rs_encode_batch_layout(rs, &L, nstripes, len, stream);
+    });
 }
 
 int rs_reconst_dev(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
                    const int* need, int nn, void* stream) {
-    if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
-    ReconstPlan pl;
-    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
-    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
-    if (rc) return rc;
-    if (!vects || !lens) return RS_ERR_INVAL;
-    const int d = rs->d;
-    int parity_rc = RS_OK;
-    RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    for (int i = 0; i < d; ++i) in[i] = vects[pl.vs[i]];
-    // Parity pass would fail its checks: rebuild the data only, then report
-    // the parity-pass error (the reference's order).  Otherwise one pass.
-    const int rows = parity_rc ? pl.dn : pl.nnr;
-    if (rows > 0) {
-        std::vector<uint8_t> m;
-        RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
-        for (int i = 0; i < rows; ++i) out[i] = vects[pl.nr[i]];
-        RS_TRY(matmul(rs, m.data(), rows, d, in, 0, out, 0, 1, lens[pl.vs[0]], false, as_stream(stream)));
-    }
-    return parity_rc;
+    return abi_guard([&]() -> int {
+        if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+        ReconstPlan pl;
+        int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+        if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
+        if (rc) return rc;
+        if (!vects || !lens) return RS_ERR_INVAL;
+        const int d = rs->d;
+        int parity_rc = RS_OK;
+        RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        for (int i = 0; i < d; ++i) in[i] = vects[pl.vs[i]];
+        // Parity pass would fail its checks: rebuild the data only, then report
+        // the parity-pass error (the reference's order).  Otherwise one pass.
+        const int rows = parity_rc ? pl.dn : pl.nnr;
+        if (rows > 0) {
+            std::vector<uint8_t> m;
+            RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
+            for (int i = 0; i < rows; ++i) out[i] = vects[pl.nr[i]];
+            RS_TRY(matmul(rs, m.data(), rows, d, in, 0, out, 0, 1, lens[pl.vs[0]], false, as_stream(stream)));
+        }
+        return parity_rc;
+    });
 }
 
 int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const int* survived, int ns,
                             const int* need, int nn, void* stream) {
-    if (!rs || !L || nstripes < 0 || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
-    ReconstPlan pl;
-    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
-    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
-    if (rc) return rc;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (nstripes == 0) return RS_OK;
-    if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
-    const int d = rs->d;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    // One pass: every lost vector from the first d survivors (combined_matrix).
-    std::vector<uint8_t> m;
-    RS_TRY(combined_matrix(rs, pl.vs, pl.nr, pl.nnr, pl.dn, m));
-    const LayoutAddr A{L, d};
-    const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    uint8_t isid[kMaxVects], osid[kMaxVects];  // stride selectors (copied into the dword kernel array)
-    for (int i = 0; i < d; ++i) {
-        in[i] = A.ptr(pl.vs[i]);
-        isid[i] = A.sid(pl.vs[i]);
-    }
-    for (int i = 0; i < pl.nnr; ++i) {
-        out[i] = A.ptr(pl.nr[i]);
-        osid[i] = A.sid(pl.nr[i]);
-    }
-    return matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream));
-}
-
-int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
-                     const int* survived, int ns, const int* need, int nn, void* stream) {
-    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
-    const rs_layout_t L{base, stripe_stride, vect_stride, base + rs->d * vect_stride, stripe_stride, vect_stride};
-    return rs_reconst_batch_layout(rs, &L, nstripes, len, survived, ns, need, nn, stream);
-}
-
-int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const uint64_t* need_masks,
-                           void* stream) {
-    if (!rs || !L || nstripes < 0 || (nstripes > 0 && !need_masks)) return RS_ERR_INVAL;
-    const int d = rs->d, p = rs->p;
-    if (d + p > 64) return RS_ERR_INVAL;  // masks are 64-bit survivor bitmaps, like the cache key
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    const uint64_t valid = (d + p == 64) ? ~uint64_t{0} : ((uint64_t{1} << (d + p)) - 1);
-    // Group stripes by erasure pattern (host, O(S)); validate every pattern before any launch.
-    std::unordered_map<uint64_t, std::vector<int32_t>> groups;
-    for (int s = 0; s < nstripes; ++s) {
-        const uint64_t m = need_masks[s];
-        if (!m) continue;
-        if (m & ~valid) return RS_ERR_ILLEGAL_VECTS;
-        groups[m].push_back(s);
-    }
-    if (groups.empty()) return RS_OK;
-    struct Group {
-        uint64_t mask;
+    return abi_guard([&]() -> int {
+        if (!rs || !L || nstripes < 0 || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
         ReconstPlan pl;
-        size_t off, n;
-    };
-    std::vector<Group> plan;
-    std::vector<int32_t> ids;
-    ids.reserve(nstripes);
-    for (auto& kv : groups) {
-        Group gr;
-        gr.mask = kv.first;
-        int need[64], nn = 0;
-        for (int v = 0; v < d + p; ++v)
-            if (kv.first >> v & 1) need[nn++] = v;
-        int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
-        if (rc) return rc;  // RS_ERR_TOO_MANY_LOST for a pattern beyond p erasures
-        gr.off = ids.size();
-        gr.n = kv.second.size();
-        ids.insert(ids.end(), kv.second.begin(), kv.second.end());
-        plan.push_back(gr);
-    }
-    if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    hipStream_t st = as_stream(stream);
-
-    // Single launch over all stripes when every pattern has <= 4 outputs and
-    // the layout takes the 16-byte vector path; otherwise one launch per
-    // pattern over a stripe-id list (below).
-    bool single = len % 16 == 0 && len < (size_t{1} << 31) &&
-                  (len / 2048 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
-    for (const Group& gr : plan) single = single && gr.pl.nnr <= 4;
-    for (int v = 0; v < d + p && single; ++v)
-        single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
-    single = single && (L->data_stripe_stride & 15) == 0 && (L->parity_stripe_stride & 15) == 0;
-    if (single) {
-        const int npat = static_cast<int>(plan.size());
-        const int tdw = multi_table_dwords(d);
-        const size_t tab_bytes = static_cast<size_t>(npat) * tdw * 4;
-        const size_t desc_bytes = static_cast<size_t>(npat) * sizeof(PatternDesc);
-        const size_t pat_bytes = static_cast<size_t>(nstripes) * 4;
-        int nout_max = 0;
-        for (const Group& gr : plan) nout_max = gr.pl.nnr > nout_max ? gr.pl.nnr : nout_max;
-        UploadLease lease(rs);
-        uint8_t* host = nullptr;
-        RS_TRY(lease.acquire(tab_bytes + desc_bytes + pat_bytes, &host));
-        std::memset(host, 0, tab_bytes + desc_bytes);
-        uint32_t* tabs = reinterpret_cast<uint32_t*>(host);
-        PatternDesc* descs = reinterpret_cast<PatternDesc*>(host + tab_bytes);
-        int32_t* spat = reinterpret_cast<int32_t*>(host + tab_bytes + desc_bytes);
-        for (int s = 0; s < nstripes; ++s) spat[s] = -1;
-        for (int gi = 0; gi < npat; ++gi) {
-            const Group& gr = plan[gi];
-            std::vector<uint8_t> m;
-            RS_TRY(combined_matrix(rs, gr.pl.vs, gr.pl.nr, gr.pl.nnr, gr.pl.dn, m));
-            uint32_t* img = tabs + static_cast<size_t>(gi) * tdw;
-            for (int i = 0; i < d; ++i)
-                for (int r = 0; r < gr.pl.nnr; ++r) perm_table(m[static_cast<size_t>(r) * d + i], img + i * 20 + r * 5);
-            PatternDesc& pd = descs[gi];
-            pd.tab_off = static_cast<uint32_t>(gi * tdw);
-            pd.nout = static_cast<uint32_t>(gr.pl.nnr);
-            for (int i = 0; i < d; ++i) pd.in_idx[i] = static_cast<uint32_t>(gr.pl.vs[i]);
-            for (int r = 0; r < gr.pl.nnr; ++r) pd.out_idx[r] = static_cast<uint32_t>(gr.pl.nr[r]);
-            for (size_t t = 0; t < gr.n; ++t) spat[ids[gr.off + t]] = gi;
-        }
-        uint8_t* dev = nullptr;
-        RS_TRY(lease.upload(st, &dev));
-        MatmulArgs a;
-        std::memset(&a, 0, sizeof a);
-        a.tables = reinterpret_cast<const uint32_t*>(dev);
-        a.rows = nout_max;
-        a.cols = d;
-        a.nstripes = nstripes;
-        a.len = len;
-        a.ss[0] = L->data_stripe_stride;
-        a.ss[1] = L->parity_stripe_stride;
-        const LayoutAddr A{L, d};
-        for (int v = 0; v < d + p; ++v) {
-            a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
-            a.sid[v] = A.sid(v);
-        }
-        return launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
-                               reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st) == hipSuccess
-                   ? RS_OK
-                   : RS_ERR_DEVICE;
-    }
-
-    UploadLease lease(rs);
-    uint8_t* hids = nullptr;
-    RS_TRY(lease.acquire(ids.size() * sizeof(int32_t), &hids));
-    std::memcpy(hids, ids.data(), ids.size() * sizeof(int32_t));
-    uint8_t* dev_ids = nullptr;
-    RS_TRY(lease.upload(st, &dev_ids));
-    const int32_t* dids = reinterpret_cast<const int32_t*>(dev_ids);
-    int rc = RS_OK;
-    const LayoutAddr A{L, d};
-    const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    uint8_t isid[kMaxVects], osid[kMaxVects];
-    for (const Group& gr : plan) {  // one launch per distinct pattern (combined_matrix)
-        if (rc) break;
-        const ReconstPlan& pl = gr.pl;
+        int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+        if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;
+        if (rc) return rc;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (nstripes == 0) return RS_OK;
+        if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
+        const int d = rs->d;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        // One pass: every lost vector from the first d survivors (combined_matrix).
         std::vector<uint8_t> m;
-        rc = combined_matrix(rs, pl.vs, pl.nr, pl.nnr, pl.dn, m);
-        if (rc) break;
+        RS_TRY(combined_matrix(rs, pl.vs, pl.nr, pl.nnr, pl.dn, m));
+        const LayoutAddr A{L, d};
+        const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        uint8_t isid[kMaxVects], osid[kMaxVects];  // stride selectors (copied into the dword kernel array)
         for (int i = 0; i < d; ++i) {
             in[i] = A.ptr(pl.vs[i]);
             isid[i] = A.sid(pl.vs[i]);
@@ -239,113 +108,270 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
             out[i] = A.ptr(pl.nr[i]);
             osid[i] = A.sid(pl.nr[i]);
         }
-        rc = matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
-                       dids + gr.off);
-    }
-    return rc;
+        return matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, nstripes, len, false, as_stream(stream));
+    });
+}
+
+int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes, size_t len,
+                     const int* survived, int ns, const int* need, int nn, void* stream) {
+    return abi_guard([&]() -> int {
+        if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+        const rs_layout_t L{base, stripe_stride, vect_stride, base + rs->d * vect_stride, stripe_stride, vect_stride};
+        return rs_reconst_batch_layout(rs, &L, nstripes, len, survived, ns, need, nn, stream);
+    });
+}
+
+int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const uint64_t* need_masks,
+                           void* stream) {
+    return abi_guard([&]() -> int {
+        if (!rs || !L || nstripes < 0 || (nstripes > 0 && !need_masks)) return RS_ERR_INVAL;
+        const int d = rs->d, p = rs->p;
+        if (d + p > 64) return RS_ERR_INVAL;  // masks are 64-bit survivor bitmaps, like the cache key
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        const uint64_t valid = (d + p == 64) ? ~uint64_t{0} : ((uint64_t{1} << (d + p)) - 1);
+        // Group stripes by erasure pattern (host, O(S)); validate every pattern before any launch.
+        std::unordered_map<uint64_t, std::vector<int32_t>> groups;
+        for (int s = 0; s < nstripes; ++s) {
+            const uint64_t m = need_masks[s];
+            if (!m) continue;
+            if (m & ~valid) return RS_ERR_ILLEGAL_VECTS;
+            groups[m].push_back(s);
+        }
+        if (groups.empty()) return RS_OK;
+        struct Group {
+            uint64_t mask;
+            ReconstPlan pl;
+            size_t off, n;
+        };
+        std::vector<Group> plan;
+        std::vector<int32_t> ids;
+        ids.reserve(nstripes);
+        for (auto& kv : groups) {
+            Group gr;
+            gr.mask = kv.first;
+            int need[64], nn = 0;
+            for (int v = 0; v < d + p; ++v)
+                if (kv.first >> v & 1) need[nn++] = v;
+            int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
+            if (rc) return rc;  // RS_ERR_TOO_MANY_LOST for a pattern beyond p erasures
+            gr.off = ids.size();
+            gr.n = kv.second.size();
+            ids.insert(ids.end(), kv.second.begin(), kv.second.end());
+            plan.push_back(gr);
+        }
+        if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        hipStream_t st = as_stream(stream);
+
+        // Single launch over all stripes when every pattern has <= 4 outputs and
+        // the layout takes the 16-byte vector path; otherwise one launch per
+        // pattern over a stripe-id list (below).
+        bool single = len % 16 == 0 && len < (size_t{1} << 31) &&
+                      (len / 2048 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
+        for (const Group& gr : plan) single = single && gr.pl.nnr <= 4;
+        for (int v = 0; v < d + p && single; ++v)
+            single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
+        single = single && (L->data_stripe_stride & 15) == 0 && (L->parity_stripe_stride & 15) == 0;
+        if (single) {
+            const int npat = static_cast<int>(plan.size());
+            const int tdw = multi_table_dwords(d);
+            const size_t tab_bytes = static_cast<size_t>(npat) * tdw * 4;
+            const size_t desc_bytes = static_cast<size_t>(npat) * sizeof(PatternDesc);
+            const size_t pat_bytes = static_cast<size_t>(nstripes) * 4;
+            int nout_max = 0;
+            for (const Group& gr : plan) nout_max = gr.pl.nnr > nout_max ? gr.pl.nnr : nout_max;
+            UploadLease lease(rs);
+            uint8_t* host = nullptr;
+            RS_TRY(lease.acquire(tab_bytes + desc_bytes + pat_bytes, &host));
+            std::memset(host, 0, tab_bytes + desc_bytes);
+            uint32_t* tabs = reinterpret_cast<uint32_t*>(host);
+            PatternDesc* descs = reinterpret_cast<PatternDesc*>(host + tab_bytes);
+            int32_t* spat = reinterpret_cast<int32_t*>(host + tab_bytes + desc_bytes);
+            for (int s = 0; s < nstripes; ++s) spat[s] = -1;
+            for (int gi = 0; gi < npat; ++gi) {
+                const Group& gr = plan[gi];
+                std::vector<uint8_t> m;
+                RS_TRY(combined_matrix(rs, gr.pl.vs, gr.pl.nr, gr.pl.nnr, gr.pl.dn, m));
+                uint32_t* img = tabs + static_cast<size_t>(gi) * tdw;
+                for (int i = 0; i < d; ++i)
+                    for (int r = 0; r < gr.pl.nnr; ++r) perm_table(m[static_cast<size_t>(r) * d + i], img + i * 20 + r * 5);
+                PatternDesc& pd = descs[gi];
+                pd.tab_off = static_cast<uint32_t>(gi * tdw);
+                pd.nout = static_cast<uint32_t>(gr.pl.nnr);
+                for (int i = 0; i < d; ++i) pd.in_idx[i] = static_cast<uint32_t>(gr.pl.vs[i]);
+                for (int r = 0; r < gr.pl.nnr; ++r) pd.out_idx[r] = static_cast<uint32_t>(gr.pl.nr[r]);
+                for (size_t t = 0; t < gr.n; ++t) spat[ids[gr.off + t]] = gi;
+            }
+            uint8_t* dev = nullptr;
+            RS_TRY(lease.upload(st, &dev));
+            MatmulArgs a;
+            std::memset(&a, 0, sizeof a);
+            a.tables = reinterpret_cast<const uint32_t*>(dev);
+            a.rows = nout_max;
+            a.cols = d;
+            a.nstripes = nstripes;
+            a.len = len;
+            a.ss[0] = L->data_stripe_stride;
+            a.ss[1] = L->parity_stripe_stride;
+            const LayoutAddr A{L, d};
+            for (int v = 0; v < d + p; ++v) {
+                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
+                a.sid[v] = A.sid(v);
+            }
+            return launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
+                                   reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st) == hipSuccess
+                       ? RS_OK
+                       : RS_ERR_DEVICE;
+        }
+
+        UploadLease lease(rs);
+        uint8_t* hids = nullptr;
+        RS_TRY(lease.acquire(ids.size() * sizeof(int32_t), &hids));
+        std::memcpy(hids, ids.data(), ids.size() * sizeof(int32_t));
+        uint8_t* dev_ids = nullptr;
+        RS_TRY(lease.upload(st, &dev_ids));
+        const int32_t* dids = reinterpret_cast<const int32_t*>(dev_ids);
+        int rc = RS_OK;
+        const LayoutAddr A{L, d};
+        const int64_t ss[4] = {L->data_stripe_stride, L->parity_stripe_stride, 0, 0};
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        uint8_t isid[kMaxVects], osid[kMaxVects];
+        for (const Group& gr : plan) {  // one launch per distinct pattern (combined_matrix)
+            if (rc) break;
+            const ReconstPlan& pl = gr.pl;
+            std::vector<uint8_t> m;
+            rc = combined_matrix(rs, pl.vs, pl.nr, pl.nnr, pl.dn, m);
+            if (rc) break;
+            for (int i = 0; i < d; ++i) {
+                in[i] = A.ptr(pl.vs[i]);
+                isid[i] = A.sid(pl.vs[i]);
+            }
+            for (int i = 0; i < pl.nnr; ++i) {
+                out[i] = A.ptr(pl.nr[i]);
+                osid[i] = A.sid(pl.nr[i]);
+            }
+            rc = matmul_ex(rs, m.data(), pl.nnr, d, in, isid, out, osid, ss, static_cast<int>(gr.n), len, false, st,
+                           dids + gr.off);
+        }
+        return rc;
+    });
 }
 
 int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
                   uint8_t* const* parity, const size_t* parity_lens, int np, void* stream) {
-    if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
-    RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
-    if (!old_data || !new_data) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const uint8_t* in[2] = {old_data, new_data};
-    std::vector<uint8_t> gm = update_matrix(rs, row);
-    return matmul(rs, gm.data(), rs->p, 2, in, 0, parity, 0, 1, new_len, true, as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
+        RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
+        if (!old_data || !new_data) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const uint8_t* in[2] = {old_data, new_data};
+        std::vector<uint8_t> gm = update_matrix(rs, row);
+        return matmul(rs, gm.data(), rs->p, 2, in, 0, parity, 0, 1, new_len, true, as_stream(stream));
+    });
 }
 
 int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride, const uint8_t* new_base,
                     int64_t new_stride, int row, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                     int nstripes, size_t len, void* stream) {
-    if (!rs || nstripes < 0) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (row >= rs->d || row < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
-    if (nstripes == 0) return RS_OK;
-    if (!old_base || !new_base || !base) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const uint8_t* in[2] = {old_base, new_base};
-    const uint8_t isid[2] = {0, 1};
-    uint8_t* out[kMaxVects];
-    uint8_t osid[kMaxVects];
-    for (int j = 0; j < rs->p; ++j) {
-        out[j] = base + (rs->d + j) * vect_stride;
-        osid[j] = 2;
-    }
-    const int64_t ss[4] = {old_stride, new_stride, stripe_stride, 0};
-    std::vector<uint8_t> gm = update_matrix(rs, row);
-    return matmul_ex(rs, gm.data(), rs->p, 2, in, isid, out, osid, ss, nstripes, len, true, as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || nstripes < 0) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (row >= rs->d || row < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
+        if (nstripes == 0) return RS_OK;
+        if (!old_base || !new_base || !base) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const uint8_t* in[2] = {old_base, new_base};
+        const uint8_t isid[2] = {0, 1};
+        uint8_t* out[kMaxVects];
+        uint8_t osid[kMaxVects];
+        for (int j = 0; j < rs->p; ++j) {
+            out[j] = base + (rs->d + j) * vect_stride;
+            osid[j] = 2;
+        }
+        const int64_t ss[4] = {old_stride, new_stride, stripe_stride, 0};
+        std::vector<uint8_t> gm = update_matrix(rs, row);
+        return matmul_ex(rs, gm.data(), rs->p, 2, in, isid, out, osid, ss, nstripes, len, true, as_stream(stream));
+    });
 }
 
 int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows,
                    int nr, uint8_t* const* parity, const size_t* parity_lens, int np, void* stream) {
-    if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
-        (np > 0 && (!parity || !parity_lens)))
-        return RS_ERR_INVAL;
-    RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-    return matmul(rs, gm.data(), rs->p, nr, data, 0, parity, 0, 1, data_lens[0], true, as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
+            (np > 0 && (!parity || !parity_lens)))
+            return RS_ERR_INVAL;
+        RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+        return matmul(rs, gm.data(), rs->p, nr, data, 0, parity, 0, 1, data_lens[0], true, as_stream(stream));
+    });
 }
 
 int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_stripe_stride, int64_t data_vect_stride,
                      const int* replace_rows, int nr, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                      int nstripes, size_t len, void* stream) {
-    if (!rs || nstripes < 0 || (nr > 0 && !replace_rows)) return RS_ERR_INVAL;
-    if (nr > rs->d) return RS_ERR_TOO_MANY_REPLACE;
-    if (nr <= 0) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    for (int i = 0; i < nr; ++i)
-        if (replace_rows[i] >= rs->d || replace_rows[i] < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
-    if (nstripes == 0) return RS_OK;
-    if (!data_base || !base) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    for (int i = 0; i < nr; ++i) in[i] = data_base + i * data_vect_stride;
-    for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
-    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-    return matmul(rs, gm.data(), rs->p, nr, in, data_stripe_stride, out, stripe_stride, nstripes, len, true,
-                  as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || nstripes < 0 || (nr > 0 && !replace_rows)) return RS_ERR_INVAL;
+        if (nr > rs->d) return RS_ERR_TOO_MANY_REPLACE;
+        if (nr <= 0) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        for (int i = 0; i < nr; ++i)
+            if (replace_rows[i] >= rs->d || replace_rows[i] < 0) return RS_ERR_ILLEGAL_VECT_INDEX;
+        if (nstripes == 0) return RS_OK;
+        if (!data_base || !base) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        for (int i = 0; i < nr; ++i) in[i] = data_base + i * data_vect_stride;
+        for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
+        std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+        return matmul(rs, gm.data(), rs->p, nr, in, data_stripe_stride, out, stripe_stride, nstripes, len, true,
+                      as_stream(stream));
+    });
 }
 
 int rs_xor_batch(rs_t* rs, const uint8_t* src_base, int64_t src_stripe_stride, int64_t src_vect_stride, int nsrc,
                  uint8_t* dst_base, int64_t dst_stripe_stride, int nstripes, size_t len, void* stream) {
-    if (!rs || nsrc <= 0 || nsrc + 1 > kMaxPtrs || nstripes < 0) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (nstripes == 0) return RS_OK;
-    if (!src_base || !dst_base) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    std::vector<uint8_t> ones(static_cast<size_t>(nsrc), 1);
-    const uint8_t* in[kMaxPtrs];
-    for (int c = 0; c < nsrc; ++c) in[c] = src_base + c * src_vect_stride;
-    uint8_t* out[1] = {dst_base};
-    return matmul(rs, ones.data(), 1, nsrc, in, src_stripe_stride, out, dst_stripe_stride, nstripes, len, false,
-                  as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || nsrc <= 0 || nsrc + 1 > kMaxPtrs || nstripes < 0) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (nstripes == 0) return RS_OK;
+        if (!src_base || !dst_base) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        std::vector<uint8_t> ones(static_cast<size_t>(nsrc), 1);
+        const uint8_t* in[kMaxPtrs];
+        for (int c = 0; c < nsrc; ++c) in[c] = src_base + c * src_vect_stride;
+        uint8_t* out[1] = {dst_base};
+        return matmul(rs, ones.data(), 1, nsrc, in, src_stripe_stride, out, dst_stripe_stride, nstripes, len, false,
+                      as_stream(stream));
+    });
 }
 
 int rs_gf_matmul_batch(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* in_base,
                        int64_t in_stripe_stride, int64_t in_vect_stride, const int* in_map, uint8_t* out_base,
                        int64_t out_stripe_stride, int64_t out_vect_stride, const int* out_map, int nstripes,
                        size_t len, int accumulate, void* stream) {
-    if (!rs || !mat || rows <= 0 || cols <= 0 || rows + cols > kMaxPtrs || nstripes < 0) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (nstripes == 0) return RS_OK;
-    if (!in_base || !out_base) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const uint8_t* in[kMaxPtrs];
-    uint8_t* out[kMaxPtrs];
-    for (int c = 0; c < cols; ++c) in[c] = in_base + (in_map ? in_map[c] : c) * in_vect_stride;
-    for (int r = 0; r < rows; ++r) out[r] = out_base + (out_map ? out_map[r] : r) * out_vect_stride;
-    return matmul(rs, mat, rows, cols, in, in_stripe_stride, out, out_stripe_stride, nstripes, len, accumulate != 0,
-                  as_stream(stream));
+    return abi_guard([&]() -> int {
+        if (!rs || !mat || rows <= 0 || cols <= 0 || rows + cols > kMaxPtrs || nstripes < 0) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (nstripes == 0) return RS_OK;
+        if (!in_base || !out_base) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const uint8_t* in[kMaxPtrs];
+        uint8_t* out[kMaxPtrs];
+        for (int c = 0; c < cols; ++c) in[c] = in_base + (in_map ? in_map[c] : c) * in_vect_stride;
+        for (int r = 0; r < rows; ++r) out[r] = out_base + (out_map ? out_map[r] : r) * out_vect_stride;
+        return matmul(rs, mat, rows, cols, in, in_stripe_stride, out, out_stripe_stride, nstripes, len, accumulate != 0,
+                      as_stream(stream));
+    });
 }
 
 }  // extern "C"

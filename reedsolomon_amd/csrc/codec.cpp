@@ -424,22 +424,24 @@ int rs_device_count(void) {
 }
 
 int rs_new(int data_num, int parity_num, int device, rs_t** out) {
-    if (!out) return RS_ERR_INVAL;
-    *out = nullptr;
-    const int d = data_num, p = parity_num;
-    if (d <= 0 || p <= 0 || d + p > kMaxVects) return RS_ERR_ILLEGAL_VECTS;  // rs.go:61-63
-    rs_t* rs = new (std::nothrow) rs_codec();
-    if (!rs) return RS_ERR_NOMEM;
-    rs->d = d;
-    rs->p = p;
-    rs->enc = make_encode_matrix(d, p);
-    if (d + p <= 64) {  // rs.go:70-74 (the cache key is a 64-bit bitmap)
-        rs->cache_enabled = true;
-        rs->cache_max = kMaxInverseCacheBytes / static_cast<uint64_t>(d) / static_cast<uint64_t>(d);
-    }
-    rs->device = device;
-    *out = rs;
-    return RS_OK;
+    return abi_guard([&]() -> int {
+        if (!out) return RS_ERR_INVAL;
+        *out = nullptr;
+        const int d = data_num, p = parity_num;
+        if (d <= 0 || p <= 0 || d + p > kMaxVects) return RS_ERR_ILLEGAL_VECTS;  // rs.go:61-63
+        rs_t* rs = new (std::nothrow) rs_codec();
+        if (!rs) return RS_ERR_NOMEM;
+        rs->d = d;
+        rs->p = p;
+        rs->enc = make_encode_matrix(d, p);
+        if (d + p <= 64) {  // rs.go:70-74 (the cache key is a 64-bit bitmap)
+            rs->cache_enabled = true;
+            rs->cache_max = kMaxInverseCacheBytes / static_cast<uint64_t>(d) / static_cast<uint64_t>(d);
+        }
+        rs->device = device;
+        *out = rs;
+        return RS_OK;
+    });
 }
 
 void rs_free(rs_t* rs) { delete rs; }
@@ -449,53 +451,63 @@ int rs_data_num(const rs_t* rs) { return rs ? rs->d : 0; }
 int rs_parity_num(const rs_t* rs) { return rs ? rs->p : 0; }
 
 int rs_gen_matrix(const rs_t* rs, uint8_t* out) {
-    if (!rs || !out) return RS_ERR_INVAL;
-    std::memcpy(out, rs->gen(), static_cast<size_t>(rs->p) * rs->d);
-    return RS_OK;
+    return abi_guard([&]() -> int {
+        if (!rs || !out) return RS_ERR_INVAL;
+        std::memcpy(out, rs->gen(), static_cast<size_t>(rs->p) * rs->d);
+        return RS_OK;
+    });
 }
 
 int rs_enc_matrix(const rs_t* rs, uint8_t* out) {
-    if (!rs || !out) return RS_ERR_INVAL;
-    std::memcpy(out, rs->enc.data(), rs->enc.size());
-    return RS_OK;
+    return abi_guard([&]() -> int {
+        if (!rs || !out) return RS_ERR_INVAL;
+        std::memcpy(out, rs->enc.data(), rs->enc.size());
+        return RS_OK;
+    });
 }
 
 uint8_t rs_gf_mul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
 
 int rs_tune(const char* name, int value) {
-    if (!name) return RS_ERR_INVAL;
-    LaunchTuning& t = tuning();
-    const std::string n(name);
-    if (n == "max_grid") t.max_grid = value;
-    else if (n == "vpt") t.vpt = value == 2 ? 2 : 1;
-    else if (n == "nt_store") t.nt_store = value;
-    else if (n == "var") t.var = value;
-    else if (n == "lds_pad") t.lds_pad = value;
-    else if (n == "stage_late") t.stage_late = value;
-    else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
-    else if (n == "vpt1") t.vpt1 = value == 2 ? 2 : 1;
-    else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
-    else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
-    else if (n == "host_batch_zc") g_host_batch_zc = value;
-    else if (n == "host_dma_1d") g_host_dma_1d = value;
-    else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
-    else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
-    else return RS_ERR_INVAL;
-    return RS_OK;
+    return abi_guard([&]() -> int {
+        if (!name) return RS_ERR_INVAL;
+        LaunchTuning& t = tuning();
+        const std::string n(name);
+        if (n == "max_grid") t.max_grid = value;
+        else if (n == "vpt") t.vpt = value == 2 ? 2 : 1;
+        else if (n == "nt_store") t.nt_store = value;
+        else if (n == "var") t.var = value;
+        else if (n == "lds_pad") t.lds_pad = value;
+        else if (n == "stage_late") t.stage_late = value;
+        else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
+        else if (n == "vpt1") t.vpt1 = value == 2 ? 2 : 1;
+        else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
+        else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
+        else if (n == "host_batch_zc") g_host_batch_zc = value;
+        else if (n == "host_dma_1d") g_host_dma_1d = value;
+        else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
+        else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
+        else return RS_ERR_INVAL;
+        return RS_OK;
+    });
 }
 
 int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out) {
-    if (n < 0 || (!m && m_len) || !out) return RS_ERR_INVAL;
-    return invert(m, m_len, n, out);
+    return abi_guard([&]() -> int {
+        if (n < 0 || (!m && m_len) || !out) return RS_ERR_INVAL;
+        return invert(m, m_len, n, out);
+    });
 }
 
 uint64_t rs_inverse_cache_key(const int* survived, int ns) { return cache_key(survived, ns); }
 
 int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls) {
-    if (!rs) return RS_ERR_INVAL;
-    if (launches) *launches = rs->co_launches.load(std::memory_order_relaxed);
-    if (calls) *calls = rs->co_calls.load(std::memory_order_relaxed);
-    return RS_OK;
+    return abi_guard([&]() -> int {
+        if (!rs) return RS_ERR_INVAL;
+        if (launches) *launches = rs->co_launches.load(std::memory_order_relaxed);
+        if (calls) *calls = rs->co_calls.load(std::memory_order_relaxed);
+        return RS_OK;
+    });
 }
 
 int64_t rs_inverse_cache_size(const rs_t* rs) {
@@ -506,16 +518,20 @@ int64_t rs_inverse_cache_size(const rs_t* rs) {
 
 int rs_plan_reconst(const rs_t* rs, const int* survived, int ns, const int* need, int nn, int* vs, int* nvs,
                     int* nr, int* nnr, int* dn) {
-    if (!rs || !vs || !nvs || !nr || !nnr || !dn) return RS_ERR_INVAL;
-    return plan_reconst(rs, survived, ns, need, nn, vs, nvs, nr, nnr, dn);
+    return abi_guard([&]() -> int {
+        if (!rs || !vs || !nvs || !nr || !nnr || !dn) return RS_ERR_INVAL;
+        return plan_reconst(rs, survived, ns, need, nn, vs, nvs, nr, nnr, dn);
+    });
 }
 
 int rs_reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, uint8_t* out) {
-    if (!rs || !survived_d || (nn && (!need || !out))) return RS_ERR_INVAL;
-    RS_TRY(check_vect_idx(survived_d, rs->d, rs->d + rs->p));
-    for (int i = 0; i < nn; ++i)
-        if (need[i] < 0 || need[i] >= rs->d) return RS_ERR_INVAL;
-    return reconst_matrix(rs, survived_d, need, nn, out);
+    return abi_guard([&]() -> int {
+        if (!rs || !survived_d || (nn && (!need || !out))) return RS_ERR_INVAL;
+        RS_TRY(check_vect_idx(survived_d, rs->d, rs->d + rs->p));
+        for (int i = 0; i < nn; ++i)
+            if (need[i] < 0 || need[i] >= rs->d) return RS_ERR_INVAL;
+        return reconst_matrix(rs, survived_d, need, nn, out);
+    });
 }
 
 }  // extern "C"

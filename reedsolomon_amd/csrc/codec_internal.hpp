@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <new>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -312,6 +313,20 @@ int host_device_range(const void* p, size_t bytes, uint8_t** dev);
 size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Every int-returning C ABI entry point runs its body through this guard, so
+// no C++ exception (an allocation failure in a std:: container, a thread
+// that cannot start) ever unwinds into a C or cgo caller.
+template <class F>
+int abi_guard(F&& body) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return RS_ERR_NOMEM;
+    } catch (...) {
+        return RS_ERR_DEVICE;
+    }
+}
 
 }  // namespace detail
 }  // namespace rsamd

@@ -59,25 +59,31 @@ int g_host_dma_1d = 0;
 extern "C" {
 
 int rs_host_register(void* ptr, size_t bytes) {
-    if (!ptr || !bytes) return RS_ERR_INVAL;
-    // mapped: kernels may address it directly (zero-copy host batches)
-    return hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess
-               ? RS_OK
-               : RS_ERR_DEVICE;
+    return abi_guard([&]() -> int {
+        if (!ptr || !bytes) return RS_ERR_INVAL;
+        // mapped: kernels may address it directly (zero-copy host batches)
+        return hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess
+                   ? RS_OK
+                   : RS_ERR_DEVICE;
+    });
 }
 
 int rs_host_device_pointer(const void* host_ptr, size_t bytes, void** dev_ptr) {
-    if (!host_ptr || !bytes || !dev_ptr) return RS_ERR_INVAL;
-    *dev_ptr = nullptr;
-    uint8_t* d = nullptr;
-    RS_TRY(host_device_range(host_ptr, bytes, &d));
-    *dev_ptr = d;
-    return RS_OK;
+    return abi_guard([&]() -> int {
+        if (!host_ptr || !bytes || !dev_ptr) return RS_ERR_INVAL;
+        *dev_ptr = nullptr;
+        uint8_t* d = nullptr;
+        RS_TRY(host_device_range(host_ptr, bytes, &d));
+        *dev_ptr = d;
+        return RS_OK;
+    });
 }
 
 int rs_host_unregister(void* ptr) {
-    if (!ptr) return RS_ERR_INVAL;
-    return hipHostUnregister(ptr) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+    return abi_guard([&]() -> int {
+        if (!ptr) return RS_ERR_INVAL;
+        return hipHostUnregister(ptr) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+    });
 }
 
 // Host-resident encode: a three-stage pipeline over a ring of `streams`
@@ -89,124 +95,126 @@ int rs_host_unregister(void* ptr) {
 //     d2h:  [wait ev_enc]    copy parity(c)-> ev_free[slot]
 int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
                          size_t len, int stripes_per_chunk, int streams) {
-    if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (nstripes == 0) return RS_OK;
-    if (stripes_per_chunk <= 0) stripes_per_chunk = 8;
-    int slots = streams <= 0 ? 3 : std::min(streams, 8);
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const int d = rs->d, p = rs->p;
-    uint8_t* zc = nullptr;
-    if (g_host_batch_zc && stripe_stride >= 0 && vect_stride >= 0 &&
-        host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) == RS_OK) {
-        // pinned / registered caller memory: one launch straight over it
+    return abi_guard([&]() -> int {
+        if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (nstripes == 0) return RS_OK;
+        if (stripes_per_chunk <= 0) stripes_per_chunk = 8;
+        int slots = streams <= 0 ? 3 : std::min(streams, 8);
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const int d = rs->d, p = rs->p;
+        uint8_t* zc = nullptr;
+        if (g_host_batch_zc && stripe_stride >= 0 && vect_stride >= 0 &&
+            host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) == RS_OK) {
+            // pinned / registered caller memory: one launch straight over it
+            std::lock_guard<std::mutex> lk(rs->stage_mu);
+            if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+                return RS_ERR_DEVICE;
+            const uint8_t* in[kMaxVects];
+            uint8_t* out[kMaxVects];
+            for (int i = 0; i < d; ++i) in[i] = zc + i * vect_stride;
+            for (int j = 0; j < p; ++j) out[j] = zc + (d + j) * vect_stride;
+            int rc = matmul(rs, rs->gen(), p, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
+                            rs->stream);
+            if (hipStreamSynchronize(rs->stream) != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
+            return rc;
+        }
+        // [S][d+p][len] with 256-B-multiple len: data and parity of a stripe are contiguous rows
+        const bool dense = vect_stride == static_cast<int64_t>(len) && len % 256 == 0;
+        const size_t pitch = dense ? len : rup(len, 256);
+        const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);
+        const size_t slot_bytes = static_cast<size_t>(dstripe) * stripes_per_chunk;
         std::lock_guard<std::mutex> lk(rs->stage_mu);
-        if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-            return RS_ERR_DEVICE;
-        const uint8_t* in[kMaxVects];
-        uint8_t* out[kMaxVects];
-        for (int i = 0; i < d; ++i) in[i] = zc + i * vect_stride;
-        for (int j = 0; j < p; ++j) out[j] = zc + (d + j) * vect_stride;
-        int rc = matmul(rs, rs->gen(), p, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
-                        rs->stream);
-        if (hipStreamSynchronize(rs->stream) != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
-        return rc;
-    }
-    // [S][d+p][len] with 256-B-multiple len: data and parity of a stripe are contiguous rows
-    const bool dense = vect_stride == static_cast<int64_t>(len) && len % 256 == 0;
-    const size_t pitch = dense ? len : rup(len, 256);
-    const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);
-    const size_t slot_bytes = static_cast<size_t>(dstripe) * stripes_per_chunk;
-    std::lock_guard<std::mutex> lk(rs->stage_mu);
-    int rc = RS_OK;
-    if (slot_bytes * slots > rs->dma_ring_bytes) {
-        if (rs->dma_ring) {
-            for (hipStream_t s : rs->dma_stream)
-                if (s) (void)hipStreamSynchronize(s);
-            (void)hipFree(rs->dma_ring);
-        }
-        rs->dma_ring = nullptr;
-        rs->dma_ring_bytes = 0;
-        if (hipMalloc(&rs->dma_ring, slot_bytes * slots) != hipSuccess) {
+        int rc = RS_OK;
+        if (slot_bytes * slots > rs->dma_ring_bytes) {
+            if (rs->dma_ring) {
+                for (hipStream_t s : rs->dma_stream)
+                    if (s) (void)hipStreamSynchronize(s);
+                (void)hipFree(rs->dma_ring);
+            }
             rs->dma_ring = nullptr;
-            return RS_ERR_DEVICE;
-        }
-        rs->dma_ring_bytes = slot_bytes * slots;
-    }
-    uint8_t* ring = rs->dma_ring;
-    for (hipStream_t& s : rs->dma_stream)
-        if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-            s = nullptr;
-            return RS_ERR_DEVICE;
-        }
-    for (auto& row : rs->dma_ev)
-        for (int i = 0; i < slots; ++i)
-            if (!row[i] && hipEventCreateWithFlags(&row[i], hipEventDisableTiming) != hipSuccess) {
-                row[i] = nullptr;
+            rs->dma_ring_bytes = 0;
+            if (hipMalloc(&rs->dma_ring, slot_bytes * slots) != hipSuccess) {
+                rs->dma_ring = nullptr;
                 return RS_ERR_DEVICE;
             }
-    hipStream_t sh = rs->dma_stream[0], sc = rs->dma_stream[1], sd = rs->dma_stream[2];
-    hipEvent_t* ev_in = rs->dma_ev[0];
-    hipEvent_t* ev_enc = rs->dma_ev[1];
-    hipEvent_t* ev_free = rs->dma_ev[2];
-    auto ok = [&](hipError_t e) {
-        if (e != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
-        return rc == RS_OK;
-    };
-    const uint8_t* in[kMaxVects];
-    uint8_t* out[kMaxVects];
-    int chunk = 0;
-    for (int c0 = 0; c0 < nstripes && rc == RS_OK; c0 += stripes_per_chunk, ++chunk) {
-        const int cn = std::min(stripes_per_chunk, nstripes - c0);
-        const int slot = chunk % slots;
-        uint8_t* dev = ring + static_cast<size_t>(slot) * slot_bytes;
-        uint8_t* hb = base + static_cast<int64_t>(c0) * stripe_stride;
-        if (chunk >= slots && !ok(hipStreamWaitEvent(sh, ev_free[slot], 0))) break;
-        if (dense && g_host_dma_1d) {  // cn 1-D copies of d*len bytes
-            bool good = true;
-            for (int s = 0; s < cn && good; ++s)
-                good = ok(hipMemcpyAsync(dev + static_cast<int64_t>(s) * dstripe, hb + s * stripe_stride,
-                                         static_cast<size_t>(d) * len, hipMemcpyHostToDevice, sh));
-            if (!good) break;
-        } else if (dense) {  // one 2-D copy: cn rows of d*len bytes
-            if (!ok(hipMemcpy2DAsync(dev, dstripe, hb, stripe_stride, static_cast<size_t>(d) * len, cn,
-                                     hipMemcpyHostToDevice, sh)))
-                break;
-        } else {
-            for (int i = 0; i < d; ++i)
-                if (!ok(hipMemcpy2DAsync(dev + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len, cn,
+            rs->dma_ring_bytes = slot_bytes * slots;
+        }
+        uint8_t* ring = rs->dma_ring;
+        for (hipStream_t& s : rs->dma_stream)
+            if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+                s = nullptr;
+                return RS_ERR_DEVICE;
+            }
+        for (auto& row : rs->dma_ev)
+            for (int i = 0; i < slots; ++i)
+                if (!row[i] && hipEventCreateWithFlags(&row[i], hipEventDisableTiming) != hipSuccess) {
+                    row[i] = nullptr;
+                    return RS_ERR_DEVICE;
+                }
+        hipStream_t sh = rs->dma_stream[0], sc = rs->dma_stream[1], sd = rs->dma_stream[2];
+        hipEvent_t* ev_in = rs->dma_ev[0];
+        hipEvent_t* ev_enc = rs->dma_ev[1];
+        hipEvent_t* ev_free = rs->dma_ev[2];
+        auto ok = [&](hipError_t e) {
+            if (e != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
+            return rc == RS_OK;
+        };
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        int chunk = 0;
+        for (int c0 = 0; c0 < nstripes && rc == RS_OK; c0 += stripes_per_chunk, ++chunk) {
+            const int cn = std::min(stripes_per_chunk, nstripes - c0);
+            const int slot = chunk % slots;
+            uint8_t* dev = ring + static_cast<size_t>(slot) * slot_bytes;
+            uint8_t* hb = base + static_cast<int64_t>(c0) * stripe_stride;
+            if (chunk >= slots && !ok(hipStreamWaitEvent(sh, ev_free[slot], 0))) break;
+            if (dense && g_host_dma_1d) {  // cn 1-D copies of d*len bytes
+                bool good = true;
+                for (int s = 0; s < cn && good; ++s)
+                    good = ok(hipMemcpyAsync(dev + static_cast<int64_t>(s) * dstripe, hb + s * stripe_stride,
+                                             static_cast<size_t>(d) * len, hipMemcpyHostToDevice, sh));
+                if (!good) break;
+            } else if (dense) {  // one 2-D copy: cn rows of d*len bytes
+                if (!ok(hipMemcpy2DAsync(dev, dstripe, hb, stripe_stride, static_cast<size_t>(d) * len, cn,
                                          hipMemcpyHostToDevice, sh)))
                     break;
-        }
-        if (!ok(hipEventRecord(ev_in[slot], sh)) || !ok(hipStreamWaitEvent(sc, ev_in[slot], 0))) break;
-        for (int i = 0; i < d; ++i) in[i] = dev + i * pitch;
-        for (int j = 0; j < p; ++j) out[j] = dev + (d + j) * pitch;
-        rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, sc);
-        if (rc) break;
-        if (!ok(hipEventRecord(ev_enc[slot], sc)) || !ok(hipStreamWaitEvent(sd, ev_enc[slot], 0))) break;
-        if (dense && g_host_dma_1d) {
-            bool good = true;
-            for (int s = 0; s < cn && good; ++s)
-                good = ok(hipMemcpyAsync(hb + s * stripe_stride + d * vect_stride,
-                                         dev + static_cast<int64_t>(s) * dstripe + d * pitch,
-                                         static_cast<size_t>(p) * len, hipMemcpyDeviceToHost, sd));
-            if (!good) break;
-        } else if (dense) {
-            if (!ok(hipMemcpy2DAsync(hb + d * vect_stride, stripe_stride, dev + d * pitch, dstripe,
-                                     static_cast<size_t>(p) * len, cn, hipMemcpyDeviceToHost, sd)))
-                break;
-        } else {
-            for (int j = 0; j < p; ++j)
-                if (!ok(hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, dev + (d + j) * pitch, dstripe,
-                                         len, cn, hipMemcpyDeviceToHost, sd)))
+            } else {
+                for (int i = 0; i < d; ++i)
+                    if (!ok(hipMemcpy2DAsync(dev + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len, cn,
+                                             hipMemcpyHostToDevice, sh)))
+                        break;
+            }
+            if (!ok(hipEventRecord(ev_in[slot], sh)) || !ok(hipStreamWaitEvent(sc, ev_in[slot], 0))) break;
+            for (int i = 0; i < d; ++i) in[i] = dev + i * pitch;
+            for (int j = 0; j < p; ++j) out[j] = dev + (d + j) * pitch;
+            rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, sc);
+            if (rc) break;
+            if (!ok(hipEventRecord(ev_enc[slot], sc)) || !ok(hipStreamWaitEvent(sd, ev_enc[slot], 0))) break;
+            if (dense && g_host_dma_1d) {
+                bool good = true;
+                for (int s = 0; s < cn && good; ++s)
+                    good = ok(hipMemcpyAsync(hb + s * stripe_stride + d * vect_stride,
+                                             dev + static_cast<int64_t>(s) * dstripe + d * pitch,
+                                             static_cast<size_t>(p) * len, hipMemcpyDeviceToHost, sd));
+                if (!good) break;
+            } else if (dense) {
+                if (!ok(hipMemcpy2DAsync(hb + d * vect_stride, stripe_stride, dev + d * pitch, dstripe,
+                                         static_cast<size_t>(p) * len, cn, hipMemcpyDeviceToHost, sd)))
                     break;
+            } else {
+                for (int j = 0; j < p; ++j)
+                    if (!ok(hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, dev + (d + j) * pitch, dstripe,
+                                             len, cn, hipMemcpyDeviceToHost, sd)))
+                        break;
+            }
+            if (!ok(hipEventRecord(ev_free[slot], sd))) break;
         }
-        if (!ok(hipEventRecord(ev_free[slot], sd))) break;
-    }
-    for (hipStream_t s : {sh, sc, sd})
-        if (hipStreamSynchronize(s) != hipSuccess) rc = RS_ERR_DEVICE;
-    return rc;
+        for (hipStream_t s : {sh, sc, sd})
+            if (hipStreamSynchronize(s) != hipSuccess) rc = RS_ERR_DEVICE;
+        return rc;
+    });
 }
 
 // ---------------------------------------------------------------- device groups
@@ -216,22 +224,24 @@ struct rs_group {
 };
 
 int rs_group_new(int data_num, int parity_num, const int* devices, int ndev, rs_group_t** out) {
-    if (!out) return RS_ERR_INVAL;
-    *out = nullptr;
-    if (ndev <= 0 || ndev > 1024 || !devices) return RS_ERR_INVAL;
-    rs_group_t* g = new (std::nothrow) rs_group();
-    if (!g) return RS_ERR_NOMEM;
-    for (int i = 0; i < ndev; ++i) {
-        rs_t* r = nullptr;
-        int rc = devices[i] < 0 ? RS_ERR_INVAL : rs_new(data_num, parity_num, devices[i], &r);
-        if (rc) {
-            rs_group_free(g);
-            return rc;
+    return abi_guard([&]() -> int {
+        if (!out) return RS_ERR_INVAL;
+        *out = nullptr;
+        if (ndev <= 0 || ndev > 1024 || !devices) return RS_ERR_INVAL;
+        rs_group_t* g = new (std::nothrow) rs_group();
+        if (!g) return RS_ERR_NOMEM;
+        for (int i = 0; i < ndev; ++i) {
+            rs_t* r = nullptr;
+            int rc = devices[i] < 0 ? RS_ERR_INVAL : rs_new(data_num, parity_num, devices[i], &r);
+            if (rc) {
+                rs_group_free(g);
+                return rc;
+            }
+            g->members.push_back(r);
         }
-        g->members.push_back(r);
-    }
-    *out = g;
-    return RS_OK;
+        *out = g;
+        return RS_OK;
+    });
 }
 
 void rs_group_free(rs_group_t* g) {
@@ -248,77 +258,83 @@ rs_t* rs_group_codec(rs_group_t* g, int i) {
 
 int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                int nstripes, size_t len, int stripes_per_chunk, int streams) {
-    if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    const int n = static_cast<int>(g->members.size());
-    std::vector<int> rc(n, RS_OK);
-    std::vector<std::thread> th;
-    for (int i = 0; i < n; ++i) {
-        const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
-        const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
-        if (hi <= lo) continue;
-        auto job = [&, i, lo, hi] {
-            rc[i] = rs_encode_host_batch(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
-                                         stripe_stride, vect_stride, hi - lo, len, stripes_per_chunk, streams);
-        };
-        try {
-            th.emplace_back(job);
-        } catch (...) {
-            job();  // no thread available: run this slice here
+    return abi_guard([&]() -> int {
+        if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        const int n = static_cast<int>(g->members.size());
+        std::vector<int> rc(n, RS_OK);
+        std::vector<std::thread> th;
+        for (int i = 0; i < n; ++i) {
+            const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
+            const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+            if (hi <= lo) continue;
+            auto job = [&, i, lo, hi] {
+                rc[i] = rs_encode_host_batch(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
+                                             stripe_stride, vect_stride, hi - lo, len, stripes_per_chunk, streams);
+            };
+            try {
+                th.emplace_back(job);
+            } catch (...) {
+                job();  // no thread available: run this slice here
+            }
         }
-    }
-    for (std::thread& t : th) t.join();
-    for (int r : rc)
-        if (r) return r;
-    return RS_OK;
+        for (std::thread& t : th) t.join();
+        for (int r : rc)
+            if (r) return r;
+        return RS_OK;
+    });
 }
 
 int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
                                 size_t len, const uint64_t* need_masks) {
-    if (!rs || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    if (nstripes == 0) return RS_OK;
-    if (stripe_stride < 0 || vect_stride < 0) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const int d = rs->d, p = rs->p;
-    uint8_t* zc = nullptr;
-    RS_TRY(host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc));
-    rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
-                  vect_stride};
-    std::lock_guard<std::mutex> lk(rs->stage_mu);
-    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-        return RS_ERR_DEVICE;
-    int rc = rs_reconst_batch_multi(rs, &L, nstripes, len, need_masks, rs->stream);
-    if (hipStreamSynchronize(rs->stream) != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
-    return rc;
+    return abi_guard([&]() -> int {
+        if (!rs || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        if (nstripes == 0) return RS_OK;
+        if (stripe_stride < 0 || vect_stride < 0) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const int d = rs->d, p = rs->p;
+        uint8_t* zc = nullptr;
+        RS_TRY(host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc));
+        rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
+                      vect_stride};
+        std::lock_guard<std::mutex> lk(rs->stage_mu);
+        if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+            return RS_ERR_DEVICE;
+        int rc = rs_reconst_batch_multi(rs, &L, nstripes, len, need_masks, rs->stream);
+        if (hipStreamSynchronize(rs->stream) != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
+        return rc;
+    });
 }
 
 int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                       int nstripes, size_t len, const uint64_t* need_masks) {
-    if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
-    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-    const int n = static_cast<int>(g->members.size());
-    std::vector<int> rc(n, RS_OK);
-    std::vector<std::thread> th;
-    for (int i = 0; i < n; ++i) {
-        const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
-        const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
-        if (hi <= lo) continue;
-        auto job = [&, i, lo, hi] {
-            rc[i] = rs_reconst_host_batch_multi(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
-                                                stripe_stride, vect_stride, hi - lo, len, need_masks + lo);
-        };
-        try {
-            th.emplace_back(job);
-        } catch (...) {
-            job();
+    return abi_guard([&]() -> int {
+        if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
+        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        const int n = static_cast<int>(g->members.size());
+        std::vector<int> rc(n, RS_OK);
+        std::vector<std::thread> th;
+        for (int i = 0; i < n; ++i) {
+            const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
+            const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+            if (hi <= lo) continue;
+            auto job = [&, i, lo, hi] {
+                rc[i] = rs_reconst_host_batch_multi(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
+                                                    stripe_stride, vect_stride, hi - lo, len, need_masks + lo);
+            };
+            try {
+                th.emplace_back(job);
+            } catch (...) {
+                job();
+            }
         }
-    }
-    for (std::thread& t : th) t.join();
-    for (int r : rc)
-        if (r) return r;
-    return RS_OK;
+        for (std::thread& t : th) t.join();
+        for (int r : rc)
+            if (r) return r;
+        return RS_OK;
+    });
 }
 
 }  // extern "C"

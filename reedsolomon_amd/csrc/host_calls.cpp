@@ -421,61 +421,69 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
 extern "C" {
 
 int rs_encode(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n) {
-    if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
-    RS_TRY(check_encode(rs, lens, n));
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    return host_call(rs, rs->gen(), rs->p, rs->d, vects, vects + rs->d, lens[0], false);
+    return abi_guard([&]() -> int {
+        if (!rs || (n > 0 && (!vects || !lens))) return RS_ERR_INVAL;
+        RS_TRY(check_encode(rs, lens, n));
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        return host_call(rs, rs->gen(), rs->p, rs->d, vects, vects + rs->d, lens[0], false);
+    });
 }
 
 int rs_reconst(rs_t* rs, uint8_t* const* vects, const size_t* lens, int n, const int* survived, int ns,
                const int* need, int nn) {
-    if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
-    ReconstPlan pl;
-    int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
-    if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;  // rs.go:225-228
-    if (rc) return rc;
-    if (!vects || !lens) return RS_ERR_INVAL;
-    const int d = rs->d;
-    int parity_rc = RS_OK;
-    RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
-    const int rows = parity_rc ? pl.dn : pl.nnr;  // see rs_reconst_dev
-    if (rows > 0) {
-        RS_TRY(ensure_device(rs));
-        DeviceGuard g(rs->device);
-        const uint8_t* src[kMaxVects];
-        uint8_t* dst[kMaxVects];
-        for (int i = 0; i < d; ++i) src[i] = vects[pl.vs[i]];
-        for (int i = 0; i < rows; ++i) dst[i] = vects[pl.nr[i]];
-        std::vector<uint8_t> m;
-        RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
-        RS_TRY(host_call(rs, m.data(), rows, d, src, dst, lens[pl.vs[0]], false));
-    }
-    return parity_rc;
+    return abi_guard([&]() -> int {
+        if (!rs || (nn > 0 && !need) || (ns > 0 && !survived)) return RS_ERR_INVAL;
+        ReconstPlan pl;
+        int rc = plan_reconst(rs, survived, ns, need, nn, pl.vs, &pl.nvs, pl.nr, &pl.nnr, &pl.dn);
+        if (rc == RS_ERR_NO_NEED_RECONST) return RS_OK;  // rs.go:225-228
+        if (rc) return rc;
+        if (!vects || !lens) return RS_ERR_INVAL;
+        const int d = rs->d;
+        int parity_rc = RS_OK;
+        RS_TRY(check_reconst_passes(rs, pl, lens, n, &parity_rc));
+        const int rows = parity_rc ? pl.dn : pl.nnr;  // see rs_reconst_dev
+        if (rows > 0) {
+            RS_TRY(ensure_device(rs));
+            DeviceGuard g(rs->device);
+            const uint8_t* src[kMaxVects];
+            uint8_t* dst[kMaxVects];
+            for (int i = 0; i < d; ++i) src[i] = vects[pl.vs[i]];
+            for (int i = 0; i < rows; ++i) dst[i] = vects[pl.nr[i]];
+            std::vector<uint8_t> m;
+            RS_TRY(combined_matrix(rs, pl.vs, pl.nr, rows, pl.dn, m));
+            RS_TRY(host_call(rs, m.data(), rows, d, src, dst, lens[pl.vs[0]], false));
+        }
+        return parity_rc;
+    });
 }
 
 int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,
               uint8_t* const* parity, const size_t* parity_lens, int np) {
-    if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
-    RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
-    if (!old_data || !new_data) return RS_ERR_INVAL;
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    const uint8_t* src[2] = {old_data, new_data};
-    std::vector<uint8_t> gm = update_matrix(rs, row);
-    return host_call(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
+    return abi_guard([&]() -> int {
+        if (!rs || (np > 0 && (!parity || !parity_lens))) return RS_ERR_INVAL;
+        RS_TRY(check_update(rs, old_len, new_len, row, parity_lens, np));
+        if (!old_data || !new_data) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        const uint8_t* src[2] = {old_data, new_data};
+        std::vector<uint8_t> gm = update_matrix(rs, row);
+        return host_call(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
+    });
 }
 
 int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, int nd, const int* replace_rows, int nr,
                uint8_t* const* parity, const size_t* parity_lens, int np) {
-    if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
-        (np > 0 && (!parity || !parity_lens)))
-        return RS_ERR_INVAL;
-    RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
-    RS_TRY(ensure_device(rs));
-    DeviceGuard g(rs->device);
-    std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-    return host_call(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
+    return abi_guard([&]() -> int {
+        if (!rs || (nd > 0 && (!data || !data_lens)) || (nr > 0 && !replace_rows) ||
+            (np > 0 && (!parity || !parity_lens)))
+            return RS_ERR_INVAL;
+        RS_TRY(check_replace(rs, data_lens, nd, replace_rows, nr, parity_lens, np));
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
+        return host_call(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
+    });
 }
 
 }  // extern "C"
