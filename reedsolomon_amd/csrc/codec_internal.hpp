@@ -310,6 +310,10 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
 extern int g_host_batch_zc, g_host_dma_1d;
 int host_device_range(const void* p, size_t bytes, uint8_t** dev);
+// Device address of [p, p+bytes) inside a range registered with
+// rs_host_register, or nullptr.
+uint8_t* registered_device_ptr(const void* p, size_t bytes);
+extern std::atomic<int> g_reg_count;
 size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -38,6 +38,30 @@ int host_device_range(const void* p, size_t bytes, uint8_t** dev) {
     return RS_OK;
 }
 
+// Ranges registered through rs_host_register: host base -> (bytes, device
+// address).  Host calls look their vectors up here (registered_device_ptr)
+// and, when every vector is registered, run the kernel straight over the
+// caller's memory.
+namespace {
+struct RegRange {
+    size_t bytes;
+    uint8_t* dev;
+};
+std::mutex g_reg_mu;
+std::map<uintptr_t, RegRange> g_reg;
+}  // namespace
+std::atomic<int> g_reg_count{0};
+
+uint8_t* registered_device_ptr(const void* p, size_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(a);
+    if (it == g_reg.begin()) return nullptr;
+    --it;
+    if (a + bytes > it->first + it->second.bytes) return nullptr;
+    return it->second.dev + (a - it->first);
+}
+
 // Bytes spanned by a [S][nvec][len] batch with non-negative strides.
 size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len) {
     return static_cast<size_t>(nstripes - 1) * static_cast<size_t>(ss) +
@@ -61,10 +85,16 @@ extern "C" {
 int rs_host_register(void* ptr, size_t bytes) {
     return abi_guard([&]() -> int {
         if (!ptr || !bytes) return RS_ERR_INVAL;
-        // mapped: kernels may address it directly (zero-copy host batches)
-        return hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess
-                   ? RS_OK
-                   : RS_ERR_DEVICE;
+        // mapped: kernels may address it directly (zero-copy host batches and calls)
+        if (hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess)
+            return RS_ERR_DEVICE;
+        void* dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, ptr, 0) == hipSuccess && dev) {
+            std::lock_guard<std::mutex> lk(g_reg_mu);
+            g_reg[reinterpret_cast<uintptr_t>(ptr)] = RegRange{bytes, static_cast<uint8_t*>(dev)};
+            g_reg_count.store(static_cast<int>(g_reg.size()));
+        }
+        return RS_OK;
     });
 }
 
@@ -82,6 +112,11 @@ int rs_host_device_pointer(const void* host_ptr, size_t bytes, void** dev_ptr) {
 int rs_host_unregister(void* ptr) {
     return abi_guard([&]() -> int {
         if (!ptr) return RS_ERR_INVAL;
+        {
+            std::lock_guard<std::mutex> lk(g_reg_mu);
+            g_reg.erase(reinterpret_cast<uintptr_t>(ptr));
+            g_reg_count.store(static_cast<int>(g_reg.size()));
+        }
         return hipHostUnregister(ptr) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
     });
 }

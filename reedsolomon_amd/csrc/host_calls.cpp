@@ -316,6 +316,26 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
 // fill while the other runs.  A lone caller's call is one launch, as before.
 int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
               size_t size, bool accumulate) {
+    if (size > 0 && g_reg_count.load(std::memory_order_relaxed) > 0) {
+        // every vector in memory the caller registered (rs_host_register) and
+        // 16-byte aligned: one zero-copy launch over the caller's own bytes
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        bool direct = true;
+        for (int i = 0; i < cols && direct; ++i)
+            direct = (in[i] = registered_device_ptr(src[i], size)) && (reinterpret_cast<uintptr_t>(src[i]) & 15) == 0;
+        for (int r = 0; r < rows && direct; ++r)
+            direct = (out[r] = registered_device_ptr(dst[r], size)) && (reinterpret_cast<uintptr_t>(dst[r]) & 15) == 0;
+        if (direct) {
+            std::lock_guard<std::mutex> lk(rs->stage_mu);
+            if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
+                return RS_ERR_DEVICE;
+            if (rs->zc_pending) RS_TRY(sync(rs));
+            const int rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, size, accumulate, rs->stream);
+            const int src_rc = sync(rs);
+            return rc ? rc : src_rc;
+        }
+    }
     if (size > g_coalesce_max || size == 0) {
         std::lock_guard<std::mutex> lk(rs->stage_mu);
         return host_product(rs, mat, rows, cols, src, dst, size, accumulate);

@@ -514,6 +514,49 @@ def test_coalesced_host_calls(rslib, orc, torch_dev):
     assert launches < calls, (launches, calls)  # concurrent calls shared launches
 
 
+def test_host_calls_on_registered_memory(rslib, orc, torch_dev):
+    """Host calls whose vectors all lie in rs_host_register'ed memory run the
+    kernel straight over them; a vector outside it (or misaligned) takes the
+    staged path.  Results equal the oracle's either way."""
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(404)
+    for size in (4096, 65536, 1 << 20, 1000):
+        pitch = (size + 4095) // 4096 * 4096
+        arena = np.zeros((d + p + 1) * pitch + 4096, np.uint8)
+        off = (-arena.ctypes.data) % 4096
+        base = arena[off: off + (d + p + 1) * pitch]
+        rslib.host_register(base.ctypes.data, base.nbytes)
+        try:
+            v = [base[i * pitch: i * pitch + size] for i in range(d + p)]
+            data = [_rand(rng, size) for _ in range(d)]
+            for i in range(d):
+                v[i][:] = data[i]
+            r.Encode(v)
+            exp = _oracle_encode(orc, d, p, data)
+            for j in range(p):
+                assert np.array_equal(v[d + j], exp[j]), (size, j)
+            keep = [x.copy() for x in v]
+            for i in (1, 12):
+                v[i][:] = 0
+            r.Reconst(v, [], [1, 12])
+            for i in (1, 12):
+                assert np.array_equal(v[i], keep[i]), (size, i)
+            new = _rand(rng, size)
+            r.Update(v[4], new, 4, v[d:])
+            data[4] = new
+            v[4][:] = new
+            exp = _oracle_encode(orc, d, p, data)
+            for j in range(p):
+                assert np.array_equal(v[d + j], exp[j]), (size, "update", j)
+            # one vector outside the registered range: staged path, same bytes
+            mixed = v[:d] + [np.zeros(size, np.uint8)] + v[d + 1:]
+            r.Encode(mixed)
+            assert np.array_equal(mixed[d], exp[0]), (size, "mixed")
+        finally:
+            rslib.host_unregister(base.ctypes.data)
+
+
 def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
     """Host-resident stripes: pinned and pageable, ragged chunking."""
     torch = torch_dev

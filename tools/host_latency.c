@@ -6,10 +6,12 @@
  *       -Wl,-rpath,$PWD/reedsolomon_amd/_lib -o tools/_build/host_latency
  *   tools/_build/host_latency [host_zc_max host_pinned_max [host_chunk]]
  *   (host_zc_max -1 = default chunked zero-copy for every size, 0 = staged paths)
+ *   HL_REGISTER=1: page-aligned vectors registered with rs_host_register (the
+ *   calls then run zero-copy over the caller's memory)
  *
  * Prints one JSON object per (op, size).
  */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200112L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -62,10 +64,14 @@ int main(int argc, char** argv) {
         uint8_t* v[N];
         size_t lens[N];
         int i, k;
+        const char* reg = getenv("HL_REGISTER");
         for (i = 0; i < N; ++i) {
-            v[i] = (uint8_t*)malloc(vec);
+            void* mem = NULL;
+            if (posix_memalign(&mem, 4096, vec)) return 7;
+            v[i] = (uint8_t*)mem;
             lens[i] = vec;
             for (k = 0; k < (int)vec; ++k) v[i][k] = (uint8_t)(k * 31 + i * 7);
+            if (reg && atoi(reg) && rs_host_register(v[i], vec) != RS_OK) return 8;
         }
         for (k = 0; k < 10; ++k) rs_encode(rs, v, lens, N);
         for (k = 0; k < reps; ++k) {
@@ -108,7 +114,10 @@ int main(int argc, char** argv) {
             }
             report("Replace rn=1", vec, (double)(1 + 2 * P) * vec, reps);
         }
-        for (i = 0; i < N; ++i) free(v[i]);
+        for (i = 0; i < N; ++i) {
+            if (reg && atoi(reg)) rs_host_unregister(v[i]);
+            free(v[i]);
+        }
     }
     rs_free(rs);
     return 0;

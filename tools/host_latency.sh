@@ -13,6 +13,7 @@ run() { echo "# $1"; shift; timeout -k 10 200 "$@"; }
   run "chunk 1 MiB" tools/_build/host_latency -1 262144 1048576
   run "1 copy thread" env RSAMD_HOST_THREADS=1 tools/_build/host_latency
   run "8 copy threads" env RSAMD_HOST_THREADS=8 tools/_build/host_latency
+  run "registered caller vectors (rs_host_register): zero-copy over them" env HL_REGISTER=1 tools/_build/host_latency
   run "staged: pinned mirror + DMA <= 4 MiB" tools/_build/host_latency 0 4194304
   run "staged: pageable per-vector copies" tools/_build/host_latency 0 0
 } > gpurun_out/host_latency.log 2>&1
