@@ -308,7 +308,9 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
  * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),
- * "host_batch_zc" (0/1).  Returns RS_OK, or RS_ERR_INVAL for an unknown name. */
+ * "host_batch_zc" (0/1), "table_registry_max" (distinct coefficient matrices
+ * kept on the device per handle before the registry is recycled).  Returns
+ * RS_OK, or RS_ERR_INVAL for an unknown name. */
 RS_API int rs_tune(const char* name, int value);
 
 /* GF(2^8) multiply (gmu.go:26-28) — for tests. */

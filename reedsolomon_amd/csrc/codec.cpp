@@ -102,25 +102,29 @@ int ensure_device(rs_t* rs) {
     return RS_OK;
 }
 
+size_t g_registry_max = size_t{1} << 14;
+
 // Perm tables for a rows x cols coefficient matrix, laid out
 // [col][rows_pad][5] dwords (rows padded to a multiple of 8 so that every
 // kernel row group reads inside the allocation), followed - for rows <= 4 -
 // by the same tables as the 4-row kernels' LDS image [rup(cols, 4)][20]
 // (zero rows and columns as padding), which those kernels stage with a plain
 // copy.  Uploaded once per distinct matrix and reused by every later launch.
+// Caller holds tab_mu until its launch is enqueued: a full registry is
+// recycled after a device sync, so no table may be handed out and launched
+// across a recycle.
 int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t** out, int* rows_pad_out) {
     const int rows_pad = static_cast<int>(rup(rows, 8));
     std::string key(reinterpret_cast<const char*>(&rows), sizeof rows);
     key.append(reinterpret_cast<const char*>(&cols), sizeof cols);
     key.append(reinterpret_cast<const char*>(mat), static_cast<size_t>(rows) * cols);
-    std::lock_guard<std::mutex> lk(rs->tab_mu);
     auto it = rs->tables.find(key);
     if (it != rs->tables.end()) {
         *out = it->second;
         *rows_pad_out = rows_pad;
         return RS_OK;
     }
-    if (rs->tables.size() >= kMaxRegistryEntries) {
+    if (rs->tables.size() >= g_registry_max) {
         // Bounded registry: drain the device before recycling table memory.
         if (hipDeviceSynchronize() != hipSuccess) return RS_ERR_DEVICE;
         for (auto& kv : rs->tables) (void)hipFree(kv.second);
@@ -156,6 +160,7 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     if (rows + cols > kMaxPtrs) return RS_ERR_INVAL;
     MatmulArgs a;
     std::memset(&a, 0, sizeof a);
+    std::lock_guard<std::mutex> lk(rs->tab_mu);  // table lookup through launch (get_tables)
     int rc = get_tables(rs, mat, rows, cols, &a.tables, &a.rows_pad);
     if (rc) return rc;
     a.img4 = rows <= 4 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
@@ -485,7 +490,8 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;
         else if (n == "host_dma_1d") g_host_dma_1d = value;
-        else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
+        else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
+    else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
         else return RS_ERR_INVAL;
         return RS_OK;

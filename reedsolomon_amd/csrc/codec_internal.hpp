@@ -33,7 +33,7 @@ namespace detail {
 
 constexpr int kMaxVects = 256;                              // rs.go:47
 constexpr uint64_t kMaxInverseCacheBytes = 16ull << 20;     // rs.go:50
-constexpr size_t kMaxRegistryEntries = 1 << 14;
+extern size_t g_registry_max;  // coefficient-table registry cap (distinct matrices per handle)
 
 // ---------------------------------------------------------------- device helpers
 

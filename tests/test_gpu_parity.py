@@ -418,6 +418,44 @@ def test_gf_matmul_batch(rslib, orc, torch_dev, rows, cols, acc):
     assert np.array_equal(ddst.cpu().numpy(), exp)
 
 
+def test_table_registry_recycling_under_threads(rslib, orc, torch_dev):
+    """The per-handle table registry is recycled (device sync + free) when
+    full; with a cap of 3 and 4 threads launching 12 distinct matrices each,
+    every product must still be right (no table freed under a launch)."""
+    torch = torch_dev
+    L = rslib.lib()
+    assert L.rs_tune(b"table_registry_max", 3) == 0
+    try:
+        r = rslib.New(10, 4)
+        errors = []
+
+        def worker(t):
+            try:
+                rng = np.random.default_rng(900 + t)
+                for i in range(12):
+                    mat = _rand(rng, 3, 5)
+                    src = _rand(rng, 2, 5, 4096)
+                    dsrc = torch.from_numpy(src).cuda()
+                    ddst = torch.zeros((2, 3, 4096), dtype=torch.uint8, device="cuda")
+                    st = torch.cuda.Stream()
+                    with torch.cuda.stream(st):
+                        r.gf_matmul_batch(mat, dsrc, None, ddst, None, stream=st)
+                    st.synchronize()
+                    if not np.array_equal(ddst.cpu().numpy(), orc.encode_numpy(mat, src)):
+                        errors.append((t, i))
+            except Exception as e:  # pragma: no cover
+                errors.append(repr(e))
+
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors
+    finally:
+        assert L.rs_tune(b"table_registry_max", 1 << 14) == 0
+
+
 def test_concurrent_host_calls(rslib, orc, torch_dev):
     """*RS is safe for concurrent use (rs.go: immutable but for the cache)."""
     d, p, size = 10, 4, 20000
