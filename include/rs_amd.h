@@ -304,10 +304,12 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
 
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad", "stage_late",
- * "lane_bytes" (8 default | 16), "vpt1",
+ * "lane_bytes" (8 | 16; 0 = chosen per launch, the default), "vpt1",
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
  * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),
+ * "host_coalesce_linger_us" (a ready shared batch waits this long for more
+ * callers before it launches; default 0),
  * "host_batch_zc" (0/1), "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name. */

@@ -484,13 +484,14 @@ int rs_tune(const char* name, int value) {
         else if (n == "var") t.var = value;
         else if (n == "lds_pad") t.lds_pad = value;
         else if (n == "stage_late") t.stage_late = value;
-        else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
+        else if (n == "lane_bytes") t.lane_bytes = (value == 16 || value == 8) ? value : 0;
         else if (n == "vpt1") t.vpt1 = value == 2 ? 2 : 1;
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;
         else if (n == "host_dma_1d") g_host_dma_1d = value;
         else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
+    else if (n == "host_coalesce_linger_us") g_coalesce_linger_us = value < 0 ? 0 : value;
     else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
         else return RS_ERR_INVAL;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -105,6 +106,8 @@ struct rs_codec {
         size_t host_bytes = 0;
         int joined = 0, ready = 0, released = 0;
         int rc = 0;
+        bool launchable = false;   // linger window started (host_coalesce_linger_us)
+        std::chrono::steady_clock::time_point deadline;
     };
     std::mutex co_mu;
     std::condition_variable co_cv;
@@ -300,6 +303,7 @@ int check_reconst_passes(const rs_t* rs, const ReconstPlan& pl, const size_t* le
 
 // ---------------------------------------------------------------- host calls (host_calls.cpp)
 extern size_t g_pinned_max, g_zc_max, g_chunk, g_coalesce_max;
+extern int g_coalesce_linger_us;
 int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
                  size_t size, bool accumulate);
 // host_product for a synchronous host call, coalesced with concurrent calls

@@ -3,6 +3,7 @@
 // in pageable host memory): column-chunked zero-copy staging through a
 // pinned mirror, or the staged DMA paths for large vectors.
 #include <algorithm>
+#include <chrono>
 
 #include "host_pool.hpp"
 #include "codec_internal.hpp"
@@ -246,6 +247,9 @@ int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t
 
 // Vectors up to this size take part in host-call coalescing (0 = off).
 size_t g_coalesce_max = 128 * 1024;
+// Group-commit window: a ready batch waits up to this long for more callers
+// before it launches (0 = launch as soon as the GPU is free; the default).
+int g_coalesce_linger_us = 0;
 // Upper bound on one coalesced batch's pinned bytes and stripe count.
 constexpr size_t kCoalesceBytes = size_t{32} << 20;
 constexpr int kCoalesceStripes = 256;
@@ -287,6 +291,7 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
         b.host_bytes = need;
     }
     b.joined = b.ready = b.released = 0;
+    b.launchable = false;
     b.rc = RS_OK;
     b.state = CoBatch::kFilling;
     return RS_OK;
@@ -395,6 +400,18 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     ++b->ready;
     while (b->state != CoBatch::kDone) {
         if (b->state == CoBatch::kFilling && !rs->co_gpu_busy && b->ready == b->joined) {
+            if (g_coalesce_linger_us > 0 && b->joined < b->cap) {
+                // group-commit window: give other callers until the deadline to join
+                const auto now = std::chrono::steady_clock::now();
+                if (!b->launchable) {
+                    b->launchable = true;
+                    b->deadline = now + std::chrono::microseconds(g_coalesce_linger_us);
+                }
+                if (now < b->deadline) {
+                    rs->co_cv.wait_until(lk, b->deadline);
+                    continue;
+                }
+            }
             b->state = CoBatch::kRunning;
             rs->co_gpu_busy = true;
             const int n = b->joined;

@@ -57,7 +57,7 @@ LaunchTuning& tuning() {
         const char* sl = std::getenv("RSAMD_STAGE_LATE");
         x.stage_late = sl ? std::atoi(sl) : 0;
         const char* lb = std::getenv("RSAMD_LANE_BYTES");
-        x.lane_bytes = lb ? std::atoi(lb) : 8;
+        x.lane_bytes = lb ? std::atoi(lb) : 0;  // 0: per launch (lane16_for)
         const char* v1 = std::getenv("RSAMD_VPT1");
         x.vpt1 = (v1 && std::atoi(v1) == 2) ? 2 : 1;
 
@@ -737,15 +737,41 @@ static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body, bool l
 }
 
 // Lane width of the one-chunk kernels: 8-byte units (dwordx2, 512 B per wave
-// instruction) unless rs_tune("lane_bytes", 16) forces 16-byte units.  A/B on
-// MI355X (tools/ab.py, same process, profiles/r01/ab_lane_width.log and
-// ab_shift64.log): with the paired / 64-bit-shift arithmetic, split-layout
-// Encode runs 6.43-6.53 TB/s with 8-byte units vs 6.34-6.49 with 16-byte
-// units, and every in-place pattern gains more (Reconst of one lost vector
-// 5.75 -> 6.41, Update 5.78 -> 6.34).  (Before the arithmetic was trimmed,
-// split-layout Encode was 2-4 % faster with 16-byte units.)  XOR-only
-// diagnostics of the same kernel: 8-byte 6.63, 16-byte 6.27 TB/s.
-static bool lane16_for(const MatmulArgs&) { return tuning().lane_bytes == 16; }
+// instruction) or 16-byte units (dwordx4, 1 KiB); rs_tune("lane_bytes", 8 |
+// 16) forces one.  Chosen per launch from same-process A/B on MI355X
+// (tools/ab.py AB_VEC=..., profiles/r01/ab_lane_width.log and ab_shift64.log):
+//   * accumulate (Update / Replace) or < 3 outputs (Reconst of 1-2): 8-byte
+//     units at every size (Reconst of 1 at 8 KiB 5.87 vs 5.54 TB/s, at 1 MiB
+//     6.41 vs 5.75; Update 5.95 vs 5.61 at 8 KiB);
+//   * 3-4 outputs with vectors <= 32 KiB: 16-byte units (Encode 8 KiB split
+//     6.35 vs 6.28, interleaved 5.77 vs 5.43; 32 KiB interleaved 6.48 vs 5.97,
+//     Reconst of 4 6.38 vs 6.20);
+//   * Encode-shaped launches (outputs after all inputs in the same stripe
+//     pitch: the interleaved [S][d+p][len] layout) up to 256 KiB: 16-byte
+//     units (64 KiB 6.34 vs 6.13, 128 KiB 5.88 vs 5.50, 256 KiB 6.02 vs 5.93);
+//   * everything else, i.e. larger vectors: 8-byte units (1 MiB split Encode
+//     6.54 vs 6.40, interleaved 6.51 vs 5.95; 256 KiB split 6.61 vs 6.37,
+//     Reconst of 4 6.45 vs 6.10).
+// XOR-only diagnostics of the 1 MiB split Encode: 8-byte 6.63, 16-byte 6.27.
+static bool lane16_for(const MatmulArgs& a) {
+    if (tuning().lane_bytes == 16) return true;
+    if (tuning().lane_bytes == 8) return false;
+    if (a.accumulate || a.rows < 3) return false;
+    if (a.len <= (32u << 10)) return true;
+    if (a.len > (256u << 10) || a.nstripes < 2) return false;
+    const int64_t pitch = a.ss[a.sid[0] & 3];
+    uint64_t max_in = 0, min_out = ~uint64_t{0};
+    for (int c = 0; c < a.cols; ++c) {
+        if (a.ss[a.sid[c] & 3] != pitch) return false;
+        max_in = a.ptr[c] > max_in ? a.ptr[c] : max_in;
+    }
+    for (int r = 0; r < a.rows; ++r) {
+        const uint64_t o = a.ptr[a.cols + r];
+        if (a.ss[a.sid[a.cols + r] & 3] != pitch) return false;
+        min_out = o < min_out ? o : min_out;
+    }
+    return min_out > max_in && static_cast<int64_t>(min_out - max_in) < pitch;
+}
 
 const char* vector_kernel_name(int rows, int cols, int accumulate) {
     return pick(rows, cols, accumulate != 0, tuning().vpt, 0, tuning().lane_bytes == 16).name;

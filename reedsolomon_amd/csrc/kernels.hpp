@@ -61,7 +61,7 @@ struct LaunchTuning {
     int var;          // experimental 10+4 code shape (RSAMD_VAR), -1 = default
     int lds_pad;      // minimum dynamic LDS per workgroup (caps occupancy; experiments)
     int stage_late;   // one-chunk kernels: stage LDS tables after issuing the data loads
-    int lane_bytes;   // one-chunk / multi-pattern kernels: bytes per lane unit (8 default, or 16)
+    int lane_bytes;   // one-chunk kernels: bytes per lane unit (8 | 16; 0 = per launch); multi-pattern: 16 or 8
     int vpt1;         // one-chunk kernels with 8-byte units: units per lane (1 or 2)
 };
 LaunchTuning& tuning();

@@ -500,6 +500,10 @@ def test_coalesced_host_calls(rslib, orc, torch_dev):
     r = rslib.New(d, p)
     errors = []
     barrier = threading.Barrier(16)
+    L = rslib.lib()
+    # a 2 ms group-commit window: concurrent calls reliably share launches
+    # even when Python threads arrive staggered (GIL)
+    assert L.rs_tune(b"host_coalesce_linger_us", 2000) == 0
 
     def worker(t):
         try:
@@ -542,10 +546,13 @@ def test_coalesced_host_calls(rslib, orc, torch_dev):
             errors.append(repr(e))
 
     ts = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
+    try:
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        assert L.rs_tune(b"host_coalesce_linger_us", 0) == 0
     assert not errors, errors[:10]
     launches, calls = r.host_call_stats()
     assert calls >= 16 * 12 * 2  # every Encode and Reconst went through the coalescer

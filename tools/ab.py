@@ -22,10 +22,12 @@ import torch  # noqa: E402
 
 import reedsolomon_amd as rs  # noqa: E402
 
-K, M, VEC, S = int(os.environ.get("AB_K", "10")), 4, 1 << 20, 256
+K, M = int(os.environ.get("AB_K", "10")), 4
+VEC = int(os.environ.get("AB_VEC", str(1 << 20)))  # bytes per vector; stripes keep ~3.5 GiB per launch
+S = 256 * (1 << 20) // VEC
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
-DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0, "lane_bytes": 8, "vpt1": 1}
+DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0, "lane_bytes": 0, "vpt1": 1}
 LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9]}
 
 
