@@ -56,6 +56,7 @@ def main():
     pats = [sum(1 << int(v) for v in rng.choice(K + M, int(rng.integers(1, M + 1)), replace=False))
             for _ in range(16)]
     masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
+    masks_sorted = np.array([pats[i * 16 // S] for i in range(S)], dtype=np.uint64)  # runs of one pattern
     nrec16 = sum(bin(int(x)).count("1") for x in masks)
     r.encode_batch_split(data, par)
 
@@ -70,6 +71,8 @@ def main():
             return (lambda: r.update_batch(data[:, 0], data[:, 1], 3, buf)), S * (2 + 2 * M) * VEC
         if op == "rep3":  # Replace rows 1, 4, 7: reads 3 data + 4 parity, writes 4 parity
             return (lambda: r.replace_batch(data[:, :3], [1, 4, 7], buf)), S * (3 + 2 * M) * VEC
+        if op == "multi16s":
+            return (lambda: r.reconst_batch_multi(data, par, masks_sorted)), (S * K + nrec16) * VEC
         if op == "multi16":
             return (lambda: r.reconst_batch_multi(data, par, masks)), (S * K + nrec16) * VEC
         if layout == "inter":
