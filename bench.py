@@ -427,8 +427,8 @@ def main(argv=None):
 
 
 def _kernel_name(k, m):
-    return f"gf_matmul_vec1<{k},true,4,false,0,8B> (buffer nt dwordx2 loads/stores, paired-column xor3, " \
-        "64-bit-shift bit groups)" if (k, m) in ((10, 4), (12, 4)) else "gf_matmul_vec1"
+    return f"gf_matmul_vec1<{k},true,4,false,0,8B,128 lanes> (buffer nt dwordx2 loads/stores, paired-column " \
+        "xor3, 64-bit-shift bit groups)" if (k, m) in ((10, 4), (12, 4)) else "gf_matmul_vec1"
 
 
 if __name__ == "__main__":

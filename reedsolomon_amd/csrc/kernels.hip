@@ -58,8 +58,8 @@ LaunchTuning& tuning() {
         x.stage_late = sl ? std::atoi(sl) : 0;
         const char* lb = std::getenv("RSAMD_LANE_BYTES");
         x.lane_bytes = lb ? std::atoi(lb) : 0;  // 0: per launch (lane16_for)
-        const char* v1 = std::getenv("RSAMD_VPT1");
-        x.vpt1 = (v1 && std::atoi(v1) == 2) ? 2 : 1;
+        const char* b8 = std::getenv("RSAMD_BLOCK8");
+        x.block8 = (b8 && std::atoi(b8) == 256) ? 256 : 128;
 
 
         return x;
@@ -644,6 +644,8 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
         case 154: *out = RSAMD_BSV(true, 4, 64, "vec1<10,16B,bs64,late>"); return true;
         case 155: *out = RSAMD_BSV(true, 4, 128, "vec1<10,16B,bs128,late>"); return true;
         case 156: *out = RSAMD_BSV(true, 2, 128, "vec1<10,8B,bs128,late>"); return true;
+        case 157: *out = RSAMD_BSV(false, 2, 512, "vec1<10,8B,bs512>"); return true;
+        case 158: *out = RSAMD_BSV(false, 2, 1024, "vec1<10,8B,bs1024>"); return true;
 #undef RSAMD_BSV
         default: break;
     }
@@ -675,21 +677,21 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
     return RSAMD_VARIANT_G(4, false, 8, true);
 }
 
-// One-chunk kernels come in six builds: LDS tables staged before / after the
-// data loads (stage_late) x 16-byte lane units, 8-byte units, or two 8-byte
-// units per lane (lane16, vpt1 = 1 | 2).
-#define RSAMD_V1(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, VAR, TAG)                                \
-    Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, VAR>, KB, MC, VPT, KFIX,        \
-            "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN "," TAG ">", true, LQ}
-#define RSAMD_V1C(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, TAG) \
-    RSAMD_V1(KB, KFIX, MC, ACC, WIN, LATE, LQ, VPT, kVarDefault, TAG)
-#define RSAMD_V1L(KB, KFIX, MC, ACC, WIN, LQ, VPT, TAG)                                             \
-    (tuning().stage_late ? RSAMD_V1C(KB, KFIX, MC, ACC, WIN, true, LQ, VPT, "late," TAG)           \
-                         : RSAMD_V1C(KB, KFIX, MC, ACC, WIN, false, LQ, VPT, TAG))
-#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN)                                                   \
-    (lane16                    ? RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 4, 1, "16B")                  \
-     : tuning().vpt1 == 2      ? RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 2, 2, "8Bx2")                 \
-                               : RSAMD_V1L(KB, KFIX, MC, ACC, WIN, 2, 1, "8B"))
+// One-chunk kernels come in three builds: 16-byte lane units on 256-lane
+// workgroups, and 8-byte units on 128-lane (default) or 256-lane workgroups
+// (rs_tune("block8", 128 | 256)).  A/B (tools/ab.py, same process,
+// profiles/r01/ab_block8.log): 128 lanes (1 KiB per vector per workgroup)
+// win or tie at 8 KiB-1 MiB: 1 MiB split Encode 6.59-6.64 vs 6.56-6.57 TB/s,
+// 128 KiB Update 6.16 vs 5.62, Reconst of 4 6.53 vs 6.20.  (Staging the
+// tables after the data loads and two 8-byte units per lane were measured
+// and dropped: both slower.)
+#define RSAMD_V1(KB, KFIX, MC, ACC, WIN, LQ, BS, TAG)                                                  \
+    Variant{gf_matmul_vec1<KB, KFIX, MC, ACC, WIN, false, LQ, 1, kVarDefault, BS>, KB, MC, 1, KFIX,       \
+            "gf_matmul_vec1<" #KB "," #KFIX "," #MC "," #ACC "," #WIN "," TAG ">", true, LQ, BS}
+#define RSAMD_VARIANT1(KB, KFIX, MC, ACC, WIN)                                                         \
+    (lane16                      ? RSAMD_V1(KB, KFIX, MC, ACC, WIN, 4, 256, "16B")                      \
+     : tuning().block8 == 128 ? RSAMD_V1(KB, KFIX, MC, ACC, WIN, 2, 128, "8B,128 lanes")             \
+                                 : RSAMD_V1(KB, KFIX, MC, ACC, WIN, 2, 256, "8B"))
 
 // Loop-free one-chunk-per-workgroup kernels (the default launch: grid = all
 // chunks, rows <= MC).  A/B on MI355X, 10+4 @ 1 MiB x 256 (tools/ab.py, 2 x 30
