@@ -303,8 +303,8 @@ RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
 RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls);
 
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
- * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad", "stage_late",
- * "lane_bytes" (8 | 16; 0 = chosen per launch, the default), "block8" (lanes
+ * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad",
+ * "lane_bytes" (8 default | 16), "block8" (lanes
  * per workgroup of the 8-byte-lane kernels: 128 default | 256),
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
  * host-memory call staging), "host_coalesce_max" (bytes per vector up to which

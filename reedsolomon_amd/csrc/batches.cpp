@@ -168,7 +168,7 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
         // the layout takes the 16-byte vector path; otherwise one launch per
         // pattern over a stripe-id list (below).
         bool single = len % 16 == 0 && len < (size_t{1} << 31) &&
-                      (len / 2048 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
+                      (len / 1024 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
         for (const Group& gr : plan) single = single && gr.pl.nnr <= 4;
         for (int v = 0; v < d + p && single; ++v)
             single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;

@@ -483,8 +483,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "nt_store") t.nt_store = value;
         else if (n == "var") t.var = value;
         else if (n == "lds_pad") t.lds_pad = value;
-        else if (n == "stage_late") t.stage_late = value;
-        else if (n == "lane_bytes") t.lane_bytes = (value == 16 || value == 8) ? value : 0;
+            else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
         else if (n == "block8") t.block8 = value == 128 ? 128 : 256;
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);

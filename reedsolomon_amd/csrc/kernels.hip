@@ -54,10 +54,8 @@ LaunchTuning& tuning() {
         x.var = e ? std::atoi(e) : -1;
         const char* l = std::getenv("RSAMD_LDS_PAD");
         x.lds_pad = l ? std::atoi(l) : 0;
-        const char* sl = std::getenv("RSAMD_STAGE_LATE");
-        x.stage_late = sl ? std::atoi(sl) : 0;
         const char* lb = std::getenv("RSAMD_LANE_BYTES");
-        x.lane_bytes = lb ? std::atoi(lb) : 0;  // 0: per launch (lane16_for)
+        x.lane_bytes = (lb && std::atoi(lb) == 16) ? 16 : 8;
         const char* b8 = std::getenv("RSAMD_BLOCK8");
         x.block8 = (b8 && std::atoi(b8) == 256) ? 256 : 128;
 
@@ -465,7 +463,7 @@ __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
 // The workgroup runs the body built for its own pattern's output count
 // (1, 2 or up to MC rows): a uniform branch, so a stripe that lost one vector
 // does not pay the VALU work of the batch's widest pattern.
-template <int MC, int KB, bool KFIX, bool STAGE_LATE, int LQ, int VAR>
+template <int MC, int KB, bool KFIX, int BS, int LQ, int VAR>
 __device__ __forceinline__ void multi_chunk(const MatmulArgs& a, const PatternDesc* P, int s, int64_t cb,
                                             uint32_t* lds32) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
@@ -476,27 +474,27 @@ __device__ __forceinline__ void multi_chunk(const MatmulArgs& a, const PatternDe
     // image columns are 20 dwords (4 rows x 5); keep the first COLD of each
     auto stage = [&]() {
         if (COLD == 20) {  // 4-row body: the image is the LDS layout
-            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) lds32[idx] = img[idx];
+            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) lds32[idx] = img[idx];
         } else {
-            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += kBlock) {
+            for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) {
                 const int c = idx / COLD;
                 lds32[idx] = img[c * 20 + (idx - c * COLD)];
             }
         }
         __syncthreads();
     };
-    if (!STAGE_LATE) stage();
+    stage();
     auto base = [&](uint32_t v) {
         return reinterpret_cast<g_u8*>(a.ptr[v]) + static_cast<int64_t>(s) * a.ss[a.sid[v] & 3];
     };
-    chunk_body<KB, KFIX, MC, false, 1, VAR, kAuxNt, kAuxNt, 0, LQ, kBlock>(
+    chunk_body<KB, KFIX, MC, false, 1, VAR, kAuxNt, kAuxNt, 0, LQ, BS>(
         a, lds_tab, cols, ncols_pad, static_cast<int>(P->nout), cb, a.body / (4 * LQ),
         [&](int c) { return const_cast<const g_u8*>(base(P->in_idx[c])); },
-        [&](int r) { return base(P->out_idx[r]); }, [&]() { if (STAGE_LATE) stage(); });
+        [&](int r) { return base(P->out_idx[r]); });
 }
 
-template <int KB, bool KFIX, int MC, bool STAGE_LATE = false, int LQ = 4, int VAR = kVarDefault>
-__global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
+template <int KB, bool KFIX, int MC, int BS, int LQ, int VAR = kVarDefault>
+__global__ __launch_bounds__(BS) void gf_matmul_multi(const MatmulArgs a, const PatternDesc* __restrict__ pats,
                                                           const int32_t* __restrict__ stripe_pat) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
     const uint32_t chunk = blockIdx.x;
@@ -509,12 +507,12 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_multi(const MatmulArgs a, co
     const PatternDesc* P = pats + pid;
     const uint32_t nout = P->nout;
     if constexpr (MC > 2) {
-        if (nout > 2) return multi_chunk<MC, KB, KFIX, STAGE_LATE, LQ, VAR>(a, P, s, cb, lds32);
+        if (nout > 2) return multi_chunk<MC, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
     }
     if constexpr (MC > 1) {
-        if (nout == 2) return multi_chunk<2, KB, KFIX, STAGE_LATE, LQ, VAR>(a, P, s, cb, lds32);
+        if (nout == 2) return multi_chunk<2, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
     }
-    multi_chunk<1, KB, KFIX, STAGE_LATE, LQ, VAR>(a, P, s, cb, lds32);
+    multi_chunk<1, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
 }
 
 // ---------------------------------------------------------------------------
@@ -739,41 +737,15 @@ static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body, bool l
 }
 
 // Lane width of the one-chunk kernels: 8-byte units (dwordx2, 512 B per wave
-// instruction) or 16-byte units (dwordx4, 1 KiB); rs_tune("lane_bytes", 8 |
-// 16) forces one.  Chosen per launch from same-process A/B on MI355X
-// (tools/ab.py AB_VEC=..., profiles/r01/ab_lane_width.log and ab_shift64.log):
-//   * accumulate (Update / Replace) or < 3 outputs (Reconst of 1-2): 8-byte
-//     units at every size (Reconst of 1 at 8 KiB 5.87 vs 5.54 TB/s, at 1 MiB
-//     6.41 vs 5.75; Update 5.95 vs 5.61 at 8 KiB);
-//   * 3-4 outputs with vectors <= 32 KiB: 16-byte units (Encode 8 KiB split
-//     6.35 vs 6.28, interleaved 5.77 vs 5.43; 32 KiB interleaved 6.48 vs 5.97,
-//     Reconst of 4 6.38 vs 6.20);
-//   * Encode-shaped launches (outputs after all inputs in the same stripe
-//     pitch: the interleaved [S][d+p][len] layout) up to 256 KiB: 16-byte
-//     units (64 KiB 6.34 vs 6.13, 128 KiB 5.88 vs 5.50, 256 KiB 6.02 vs 5.93);
-//   * everything else, i.e. larger vectors: 8-byte units (1 MiB split Encode
-//     6.54 vs 6.40, interleaved 6.51 vs 5.95; 256 KiB split 6.61 vs 6.37,
-//     Reconst of 4 6.45 vs 6.10).
-// XOR-only diagnostics of the 1 MiB split Encode: 8-byte 6.63, 16-byte 6.27.
-static bool lane16_for(const MatmulArgs& a) {
-    if (tuning().lane_bytes == 16) return true;
-    if (tuning().lane_bytes == 8) return false;
-    if (a.accumulate || a.rows < 3) return false;
-    if (a.len <= (32u << 10)) return true;
-    if (a.len > (256u << 10) || a.nstripes < 2) return false;
-    const int64_t pitch = a.ss[a.sid[0] & 3];
-    uint64_t max_in = 0, min_out = ~uint64_t{0};
-    for (int c = 0; c < a.cols; ++c) {
-        if (a.ss[a.sid[c] & 3] != pitch) return false;
-        max_in = a.ptr[c] > max_in ? a.ptr[c] : max_in;
-    }
-    for (int r = 0; r < a.rows; ++r) {
-        const uint64_t o = a.ptr[a.cols + r];
-        if (a.ss[a.sid[a.cols + r] & 3] != pitch) return false;
-        min_out = o < min_out ? o : min_out;
-    }
-    return min_out > max_in && static_cast<int64_t>(min_out - max_in) < pitch;
-}
+// instruction) on 128-lane workgroups, unless rs_tune("lane_bytes", 16)
+// forces 16-byte units (dwordx4, 1 KiB) on 256-lane workgroups.  Same-process
+// A/B on MI355X (tools/ab.py AB_VEC=..., profiles/r01/ab_lane_size_sweep.log):
+// with 256-lane workgroups the 16-byte build won 3-4-output launches on
+// vectors <= 32 KiB and interleaved Encode up to 256 KiB; with the 8-byte
+// build on 128-lane workgroups, 8-byte units win every size and shape tried
+// (8 KiB split Encode 6.65 vs 6.30 TB/s, interleaved 6.42 vs 5.78, Reconst
+// of 4 6.46 vs 6.05; 32 KiB-1 MiB: +0-8 %).
+static bool lane16_for(const MatmulArgs&) { return tuning().lane_bytes == 16; }
 
 const char* vector_kernel_name(int rows, int cols, int accumulate) {
     return pick(rows, cols, accumulate != 0, tuning().vpt, 0, tuning().lane_bytes == 16).name;
@@ -785,11 +757,14 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     if (a.len == 0 || a.nstripes <= 0) return hipSuccess;
     a.body = a.len;  // caller guarantees len % 16 == 0, aligned vectors, len < 2 GiB
     a.tail_start = a.len;
-    a.units_per_chunk = kBlock;
     a.nt_store = 1;
+    // the one-chunk kernels' shapes: 8-byte lanes on block8-lane workgroups
+    // (128 by default) or 16-byte lanes on 256
     const int lq = tuning().lane_bytes == 16 ? 4 : 2;
+    const int bs = lq == 4 ? kBlock : tuning().block8;
+    a.units_per_chunk = bs;
     const uint64_t nunits = a.body / (4 * lq);
-    a.chunks_per_stripe = static_cast<int64_t>((nunits + kBlock - 1) / kBlock);
+    a.chunks_per_stripe = static_cast<int64_t>((nunits + bs - 1) / bs);
     a.total_chunks = a.chunks_per_stripe * a.nstripes;
     a.cps_shift = -1;
     for (int sh = 0; sh < 31; ++sh)
@@ -800,19 +775,17 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
     const size_t lds = static_cast<size_t>(ncols_pad) * (((mc * 5 + 3) / 4) * 4) * 4;
     const dim3 grid(static_cast<unsigned>(a.total_chunks));
-#define RSAMD_MULTI_L(KB, KFIX, MC, LATE, VAR)                                                                    \
-    do {                                                                                                  \
-        if (lq == 4)                                                                                      \
-            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 4, VAR>), grid, dim3(kBlock), lds, stream, a, pats, \
-                               stripe_pat);                                                               \
-        else                                                                                              \
-            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, LATE, 2, VAR>), grid, dim3(kBlock), lds, stream, a, pats, \
-                               stripe_pat);                                                               \
-    } while (0)
 #define RSAMD_MULTI(KB, KFIX, MC)                                                                          \
     do {                                                                                                  \
-        if (tuning().stage_late) RSAMD_MULTI_L(KB, KFIX, MC, true, kVarDefault);                          \
-        else RSAMD_MULTI_L(KB, KFIX, MC, false, kVarDefault);                                             \
+        if (lq == 4)                                                                                      \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, kBlock, 4>), grid, dim3(kBlock), lds, stream, a, \
+                               pats, stripe_pat);                                                         \
+        else if (bs == 128)                                                                               \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, 128, 2>), grid, dim3(128), lds, stream, a, pats, \
+                               stripe_pat);                                                               \
+        else                                                                                              \
+            hipLaunchKernelGGL((gf_matmul_multi<KB, KFIX, MC, kBlock, 2>), grid, dim3(kBlock), lds, stream, a, \
+                               pats, stripe_pat);                                                         \
     } while (0)
     if (k10) {
         if (mc == 1) RSAMD_MULTI(10, true, 1);
@@ -824,7 +797,6 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
         else RSAMD_MULTI(4, false, 4);
     }
 #undef RSAMD_MULTI
-#undef RSAMD_MULTI_L
     return hipGetLastError();
 }
 

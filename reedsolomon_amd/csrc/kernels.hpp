@@ -60,8 +60,7 @@ struct LaunchTuning {
     int nt_store;     // non-temporal parity stores
     int var;          // experimental 10+4 code shape (RSAMD_VAR), -1 = default
     int lds_pad;      // minimum dynamic LDS per workgroup (caps occupancy; experiments)
-    int stage_late;   // multi-pattern kernel: stage LDS tables after issuing the data loads
-    int lane_bytes;   // one-chunk kernels: bytes per lane unit (8 | 16; 0 = per launch); multi-pattern: 16 or 8
+    int lane_bytes;   // one-chunk and multi-pattern kernels: bytes per lane unit (8 default | 16)
     int block8;       // one-chunk kernels with 8-byte units: lanes per workgroup (256 or 128)
 };
 LaunchTuning& tuning();

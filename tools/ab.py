@@ -4,7 +4,7 @@ rule 24): variants are switched with rs_tune() and timed in interleaved
 rounds on the same device and buffers; reports median / min kernel time.
 
     python tools/ab.py "var=12" "var=14" "var=14,layout=inter" ...
-    python tools/ab.py "op=rec1" "op=rec1,stage_late=1" "op=multi16" ...
+    python tools/ab.py "op=rec1" "op=rec1,block8=256" "op=multi16" ...
 
 op: enc (Encode, default) | rec1 / rec2 / rec4 (Reconst of 1 / 2 / 4 lost data
 vectors, split layout) | multi16 (rs_reconst_batch_multi, 16 patterns) |
@@ -27,7 +27,7 @@ VEC = int(os.environ.get("AB_VEC", str(1 << 20)))  # bytes per vector; stripes k
 S = 256 * (1 << 20) // VEC
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
-DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "stage_late": 0, "lane_bytes": 0, "block8": 128}
+DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "lane_bytes": 8, "block8": 128}
 LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9]}
 
 
