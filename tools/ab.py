@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 import reedsolomon_amd as rs  # noqa: E402
 
-K, M = int(os.environ.get("AB_K", "10")), 4
+K, M = int(os.environ.get("AB_K", "10")), int(os.environ.get("AB_M", "4"))
 VEC = int(os.environ.get("AB_VEC", str(1 << 20)))  # bytes per vector; stripes keep ~3.5 GiB per launch
 S = 256 * (1 << 20) // VEC
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
