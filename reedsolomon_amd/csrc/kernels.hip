@@ -643,6 +643,8 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
         case 155: *out = RSAMD_BSV(true, 4, 128, "vec1<10,16B,bs128,late>"); return true;
         case 156: *out = RSAMD_BSV(true, 2, 128, "vec1<10,8B,bs128,late>"); return true;
         case 157: *out = RSAMD_BSV(false, 2, 512, "vec1<10,8B,bs512>"); return true;
+        case 159: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 2, 1, kVarDefault | kVarXorOnly, 128>, 10,
+                                 4, 1, true, "vec1<10,8B,bs128,xor>", true, 2, 128}; return true;
         case 158: *out = RSAMD_BSV(false, 2, 1024, "vec1<10,8B,bs1024>"); return true;
 #undef RSAMD_BSV
         default: break;
