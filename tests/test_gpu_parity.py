@@ -27,6 +27,15 @@ def _rand(rng, *shape):
     return rng.integers(0, 256, shape, dtype=np.uint8)
 
 
+def _first_diff(got, exp):
+    """(index, got, expected) of the first differing byte, and the count."""
+    bad = np.argwhere(got != exp)
+    if not len(bad):
+        return None
+    i = tuple(int(x) for x in bad[0])
+    return i, int(got[i]), int(exp[i]), len(bad)
+
+
 def _oracle_encode(orc, d, p, data_list):
     size = data_list[0].size
     v = [x.copy() for x in data_list] + [np.zeros(size, np.uint8) for _ in range(p)]
@@ -612,18 +621,20 @@ def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
         host = _rand(rng, S, d + p, n)
         exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
         a = host.copy()
-        r.encode_host_batch(a, spc, st)
-        assert np.array_equal(a[:, d:], exp)
-        assert np.array_equal(a[:, :d], host[:, :d])
+        r.encode_host_batch(a, spc, st)  # pageable: DMA pipeline
+        assert np.array_equal(a[:, d:], exp), ("pageable parity", S, n, _first_diff(a[:, d:], exp))
+        assert np.array_equal(a[:, :d], host[:, :d]), ("pageable data", S, n)
         pinned = torch.from_numpy(host.copy()).pin_memory()
         r.encode_host_batch(pinned, spc, st)  # zero-copy: kernels straight over pinned memory
-        assert np.array_equal(pinned.numpy()[:, d:], exp)
+        got = pinned.numpy()[:, d:]
+        assert np.array_equal(got, exp), ("zero-copy parity", S, n, _first_diff(got, exp))
         L = rslib.lib()
         assert L.rs_tune(b"host_batch_zc", 0) == 0
         try:
             pinned = torch.from_numpy(host.copy()).pin_memory()
             r.encode_host_batch(pinned, spc, st)  # DMA pipeline over pinned memory
-            assert np.array_equal(pinned.numpy()[:, d:], exp)
+            got = pinned.numpy()[:, d:]
+            assert np.array_equal(got, exp), ("pinned DMA parity", S, n, _first_diff(got, exp))
         finally:
             L.rs_tune(b"host_batch_zc", 1)
 
