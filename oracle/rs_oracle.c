@@ -455,6 +455,20 @@ __attribute__((target("avx2"))) static void mul_vect_avx2(const uint8_t* tbl, co
     __m256i hi = _mm256_broadcastsi128_si256(hi128);
     __m256i mask = _mm256_set1_epi8(0x0f);
     size_t i = 0;
+    /* 256 B per iteration, as the reference's unrolled loop (gmu_amd64.s:64-144) */
+    for (; i + 256 <= n; i += 256) {
+        __m256i r[8];
+        for (int u = 0; u < 8; u++) {
+            __m256i x = _mm256_loadu_si256((const __m256i*)(in + i + 32 * u));
+            __m256i xl = _mm256_and_si256(x, mask);
+            __m256i xh = _mm256_and_si256(_mm256_srli_epi64(x, 4), mask);
+            r[u] = _mm256_xor_si256(_mm256_shuffle_epi8(lo, xl), _mm256_shuffle_epi8(hi, xh));
+        }
+        if (xor_out)
+            for (int u = 0; u < 8; u++)
+                r[u] = _mm256_xor_si256(r[u], _mm256_loadu_si256((const __m256i*)(out + i + 32 * u)));
+        for (int u = 0; u < 8; u++) _mm256_storeu_si256((__m256i*)(out + i + 32 * u), r[u]);
+    }
     for (; i + 32 <= n; i += 32) {
         __m256i x = _mm256_loadu_si256((const __m256i*)(in + i));
         __m256i xl = _mm256_and_si256(x, mask);
