@@ -43,7 +43,7 @@ CONFIGS = {
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="10+4@1MiB", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=0, help="stripes per GPU (default: per config)")
