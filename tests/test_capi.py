@@ -256,3 +256,30 @@ def test_group_handles(rslib):
         rslib.NewGroup(200, 57, [0])
     L = rslib.lib()
     assert L.rs_group_codec(g._g, 3) is None and L.rs_group_codec(g._g, -1) is None
+
+
+def test_tune_accepts_every_documented_knob(rslib):
+    """Every knob name the header documents for rs_tune is accepted, and an
+    unknown name is RS_ERR_INVAL (run in a child process: rs_tune changes
+    process-wide state)."""
+    import subprocess
+    import sys
+
+    text = open(os.path.join(ROOT, "include", "rs_amd.h")).read()
+    doc = text[text.index("Expert launch knobs"):text.index("RS_API int rs_tune")]
+    names = sorted(set(re.findall(r'"(\w+)"', doc)))
+    assert {"lane_bytes", "block8", "host_coalesce_max", "table_registry_max"} <= set(names)
+    code = (
+        "import sys, ctypes\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import reedsolomon_amd as rs\n"
+        "L = rs.lib()\n"
+        f"names = {names!r}\n"
+        "bad = [n for n in names if L.rs_tune(n.encode(), 1) != 0]\n"
+        "assert not bad, bad\n"
+        "assert L.rs_tune(b'no_such_knob', 1) == 13\n"
+        "print('ok', len(names))\n"
+    )
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.startswith("ok")
