@@ -296,6 +296,12 @@ def main(argv=None):
             dist.init_process_group(backend)
         pg = dist
 
+    if world > 1:
+        # one rank per GPU: keep this process (and the threads it starts) on
+        # the GPU's NUMA node, so the host-resident leg's pinned buffers are
+        # local to its PCIe link (best effort; no-op where sysfs is absent)
+        rs.lib().rs_bind_thread_to_device(dev_idx)
+
     k, m, vec, S = CONFIGS[args.config]
     if args.stripes:
         S = args.stripes

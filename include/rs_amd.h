@@ -230,6 +230,12 @@ RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stri
  * no staging): 72 GiB/s for 10+4 encode on one MI355X vs 57 GiB/s through
  * the DMA pipeline used for pageable memory. */
 RS_API int rs_host_register(void* ptr, size_t bytes);
+/* Bind the calling thread to the CPUs local to `device` (its PCI function's
+ * NUMA node, from sysfs), within the process's affinity, so page-locked
+ * buffers and staging copies stay near the GPU.  Device-group workers do
+ * this themselves (rs_tune "bind_numa", default 1).  RS_ERR_INVAL when the
+ * topology cannot be read. */
+RS_API int rs_bind_thread_to_device(int device);
 RS_API int rs_host_unregister(void* ptr);
 /* Device address of host range [host_ptr, host_ptr+bytes) if all of it is
  * pinned / registered and device-mapped; RS_ERR_INVAL for pageable memory.
@@ -311,7 +317,8 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * concurrent host calls of one shape share a launch; 0 = off),
  * "host_coalesce_linger_us" (a ready shared batch waits this long for more
  * callers before it launches; default 0),
- * "host_batch_zc" (0/1), "table_registry_max" (distinct coefficient matrices
+ * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "bind_numa" (0/1),
+ * "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name. */
 RS_API int rs_tune(const char* name, int value);

@@ -312,7 +312,8 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
               size_t size, bool accumulate);
 
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
-extern int g_host_batch_zc, g_host_dma_1d;
+extern int g_host_batch_zc, g_host_dma_1d, g_bind_numa;
+int bind_thread_to_device(int device);
 int host_device_range(const void* p, size_t bytes, uint8_t** dev);
 // Device address of [p, p+bytes) inside a range registered with
 // rs_host_register, or nullptr.

@@ -1,7 +1,12 @@
 // host_batches.cpp — host-resident batches of stripes: zero-copy kernels
 // over pinned / registered memory, the H2D / kernel / D2H pipeline for
 // pageable memory, and device groups (one process, several GPUs).
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
 #include <thread>
 
 #include "codec_internal.hpp"
@@ -62,6 +67,34 @@ uint8_t* registered_device_ptr(const void* p, size_t bytes) {
     return it->second.dev + (a - it->first);
 }
 
+// Bind the calling thread to the CPUs local to `device` (its PCI function's
+// sysfs local_cpulist), within the process's current affinity.  Host-side
+// staging copies and page-locked buffers then stay on the GPU's NUMA node.
+// Best effort: returns RS_ERR_INVAL when the topology cannot be read.
+int bind_thread_to_device(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return RS_ERR_INVAL;
+    for (char* c = bus; *c; ++c) *c = static_cast<char>(std::tolower(static_cast<unsigned char>(*c)));
+    std::FILE* f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist").c_str(), "r");
+    if (!f) return RS_ERR_INVAL;
+    char list[4096] = {0};
+    const bool got = std::fgets(list, sizeof list, f) != nullptr;
+    std::fclose(f);
+    if (!got) return RS_ERR_INVAL;
+    cpu_set_t allowed, want;
+    CPU_ZERO(&want);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return RS_ERR_INVAL;
+    for (char* tok = std::strtok(list, ",\n"); tok; tok = std::strtok(nullptr, ",\n")) {
+        int a = -1, b = -1;
+        if (std::sscanf(tok, "%d-%d", &a, &b) < 1) continue;
+        if (b < a) b = a;
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (c >= 0 && CPU_ISSET(c, &allowed)) CPU_SET(c, &want);
+    }
+    if (CPU_COUNT(&want) == 0) return RS_ERR_INVAL;
+    return pthread_setaffinity_np(pthread_self(), sizeof want, &want) == 0 ? RS_OK : RS_ERR_INVAL;
+}
+
 // Bytes spanned by a [S][nvec][len] batch with non-negative strides.
 size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len) {
     return static_cast<size_t>(nstripes - 1) * static_cast<size_t>(ss) +
@@ -76,6 +109,8 @@ int g_host_batch_zc = 1;
 // 70.4-70.7 GiB/s for 10+4 @ 1 MiB x 128 vs 66.8-67.1 with 1-D copies,
 // tools/dma_ab.py), 1 = one 1-D hipMemcpyAsync per stripe.
 int g_host_dma_1d = 0;
+// Group worker threads bind to their GPU's local CPUs (bind_thread_to_device).
+int g_bind_numa = 1;
 
 }  // namespace detail
 }  // namespace rsamd
@@ -107,6 +142,10 @@ int rs_host_device_pointer(const void* host_ptr, size_t bytes, void** dev_ptr) {
         *dev_ptr = d;
         return RS_OK;
     });
+}
+
+int rs_bind_thread_to_device(int device) {
+    return abi_guard([&]() -> int { return bind_thread_to_device(device); });
 }
 
 int rs_host_unregister(void* ptr) {
@@ -308,7 +347,11 @@ int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stri
                                              stripe_stride, vect_stride, hi - lo, len, stripes_per_chunk, streams);
             };
             try {
-                th.emplace_back(job);
+                const int dev = g->members[i]->device;
+                th.emplace_back([job, dev] {  // a worker of its own: bind it to the GPU's NUMA node
+                    if (g_bind_numa) (void)bind_thread_to_device(dev);
+                    job();
+                });
             } catch (...) {
                 job();  // no thread available: run this slice here
             }
@@ -360,9 +403,13 @@ int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stri
                                                     stripe_stride, vect_stride, hi - lo, len, need_masks + lo);
             };
             try {
-                th.emplace_back(job);
+                const int dev = g->members[i]->device;
+                th.emplace_back([job, dev] {  // a worker of its own: bind it to the GPU's NUMA node
+                    if (g_bind_numa) (void)bind_thread_to_device(dev);
+                    job();
+                });
             } catch (...) {
-                job();
+                job();  // no thread available: run this slice here
             }
         }
         for (std::thread& t : th) t.join();
