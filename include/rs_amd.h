@@ -323,6 +323,10 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * RS_OK, or RS_ERR_INVAL for an unknown name. */
 RS_API int rs_tune(const char* name, int value);
 
+/* The calling thread's last RS_ERR_DEVICE cause ("where: hipErrorName (code)"),
+ * or "" if none; diagnostic text only. */
+RS_API const char* rs_last_device_error(void);
+
 /* GF(2^8) multiply (gmu.go:26-28) — for tests. */
 RS_API uint8_t rs_gf_mul(uint8_t a, uint8_t b);
 

@@ -79,6 +79,7 @@ SIGNATURES = {
     "rs_host_register": (c_int, [c_void, c_sz]),
     "rs_host_unregister": (c_int, [c_void]),
     "rs_bind_thread_to_device": (c_int, [c_int]),
+    "rs_last_device_error": (ctypes.c_char_p, []),
     "rs_xor_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_void, c_i64, c_int, c_sz, c_void]),
     "rs_gf_matmul_batch": (c_int, [c_void, c_u8p, c_int, c_int, c_void, c_i64, c_i64, c_intp, c_void, c_i64,
                                    c_i64, c_intp, c_int, c_sz, c_int, c_void]),

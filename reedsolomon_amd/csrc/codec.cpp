@@ -11,6 +11,7 @@
 //   * conversion of a small coefficient matrix into per-coefficient device
 //     perm tables, uploaded once per distinct matrix (registry below).
 // What runs on the GPU: every byte of every vector (kernels.hip).
+#include <cstdio>
 #include <algorithm>
 #include <cstdlib>
 
@@ -104,6 +105,14 @@ int ensure_device(rs_t* rs) {
 
 size_t g_registry_max = size_t{1} << 14;
 
+thread_local char g_last_dev_err[192] = {0};
+
+int dev_fail(hipError_t e, const char* where) {
+    std::snprintf(g_last_dev_err, sizeof g_last_dev_err, "%s: %s (%d)", where, hipGetErrorName(e),
+                  static_cast<int>(e));
+    return RS_ERR_DEVICE;
+}
+
 // Perm tables for a rows x cols coefficient matrix, laid out
 // [col][rows_pad][5] dwords (rows padded to a multiple of 8 so that every
 // kernel row group reads inside the allocation), followed - for rows <= 4 -
@@ -179,7 +188,8 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         a.ptr[cols + r] = reinterpret_cast<uint64_t>(out_ptrs[r]);
         a.sid[cols + r] = out_sid ? out_sid[r] : 1;
     }
-    return launch_gf_matmul(a, stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+    const hipError_t e = launch_gf_matmul(a, stream);
+    return e == hipSuccess ? RS_OK : dev_fail(e, "kernel launch");
 }
 
 int matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs, int64_t in_ss,
@@ -507,6 +517,8 @@ int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out) {
 }
 
 uint64_t rs_inverse_cache_key(const int* survived, int ns) { return cache_key(survived, ns); }
+
+const char* rs_last_device_error(void) { return g_last_dev_err; }
 
 int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls) {
     return abi_guard([&]() -> int {

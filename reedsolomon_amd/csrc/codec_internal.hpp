@@ -323,6 +323,10 @@ size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Record which HIP call failed (thread-local, read by rs_last_device_error)
+// and return RS_ERR_DEVICE.
+int dev_fail(hipError_t e, const char* where);
+
 // Every int-returning C ABI entry point runs its body through this guard, so
 // no C++ exception (an allocation failure in a std:: container, a thread
 // that cannot start) ever unwinds into a C or cgo caller.

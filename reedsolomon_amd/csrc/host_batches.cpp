@@ -232,7 +232,7 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
         hipEvent_t* ev_enc = rs->dma_ev[1];
         hipEvent_t* ev_free = rs->dma_ev[2];
         auto ok = [&](hipError_t e) {
-            if (e != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
+            if (e != hipSuccess && rc == RS_OK) rc = dev_fail(e, "host-batch DMA pipeline");
             return rc == RS_OK;
         };
         const uint8_t* in[kMaxVects];
@@ -285,8 +285,10 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             }
             if (!ok(hipEventRecord(ev_free[slot], sd))) break;
         }
-        for (hipStream_t s : {sh, sc, sd})
-            if (hipStreamSynchronize(s) != hipSuccess) rc = RS_ERR_DEVICE;
+        for (hipStream_t s : {sh, sc, sd}) {
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = dev_fail(e, "host-batch DMA pipeline sync");
+        }
         return rc;
     });
 }

@@ -76,7 +76,10 @@ int h2d(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
 int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
     return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
 }
-int sync(rs_t* rs) { return hipStreamSynchronize(rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE; }
+int sync(rs_t* rs) {
+    const hipError_t e = hipStreamSynchronize(rs->stream);
+    return e == hipSuccess ? RS_OK : dev_fail(e, "host-call stream sync");
+}
 
 int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots) {
     if (n <= 0) return RS_OK;
@@ -306,8 +309,8 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     for (int r = 0; r < b.rows; ++r) out[r] = b.dev + static_cast<size_t>(b.cols + r) * b.pitch;
     const int rc = matmul(rs, b.mat.data(), b.rows, b.cols, in, static_cast<int64_t>(b.stride), out,
                           static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
-    const bool ok = hipStreamSynchronize(rs->co_stream) == hipSuccess;  // never leave a kernel on the buffer
-    return rc ? rc : (ok ? RS_OK : RS_ERR_DEVICE);
+    const hipError_t e = hipStreamSynchronize(rs->co_stream);  // never leave a kernel on the buffer
+    return rc ? rc : (e == hipSuccess ? RS_OK : dev_fail(e, "coalesced batch sync"));
 }
 
 // The synchronous host calls' entry (rs_encode / rs_reconst / rs_update /

@@ -777,6 +777,10 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
     const size_t lds = static_cast<size_t>(ncols_pad) * (((mc * 5 + 3) / 4) * 4) * 4;
     const dim3 grid(static_cast<unsigned>(a.total_chunks));
+    // HIP keeps the last failing call's status until read: clear anything an
+    // unrelated earlier call (ours, the caller's, a framework's) left there,
+    // so the hipGetLastError below reports this launch only
+    (void)hipGetLastError();
 #define RSAMD_MULTI(KB, KFIX, MC)                                                                          \
     do {                                                                                                  \
         if (lq == 4)                                                                                      \
@@ -840,6 +844,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         size_t lds = static_cast<size_t>(ncols_pad) * cold * 4;
         if (tu.lds_pad > 0 && static_cast<size_t>(tu.lds_pad) > lds) lds = tu.lds_pad;  // occupancy experiments
 
+        (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
         hipLaunchKernelGGL(var.fn, dim3(static_cast<unsigned>(grid)), dim3(var.bs), lds, stream, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -848,6 +853,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         const uint64_t groups = (a.len - a.tail_start + 3) / 4;
         const uint64_t total = groups * static_cast<uint64_t>(a.nstripes);
         const uint64_t grid = (total + kBlock - 1) / kBlock;
+        (void)hipGetLastError();
         hipLaunchKernelGGL(gf_matmul_bytes, dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, stream, a,
                            a.tail_start, groups);
         hipError_t e = hipGetLastError();

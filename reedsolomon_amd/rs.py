@@ -103,7 +103,10 @@ _ERRORS = {cls.code: cls for cls in (
 
 def _check(rc: int) -> None:
     if rc:
-        raise _ERRORS.get(rc, RSError)()
+        cls = _ERRORS.get(rc, RSError)
+        if cls is ErrDevice:  # say which HIP call failed
+            raise cls(f"HIP device error: {lib().rs_last_device_error().decode(errors='replace')}")
+        raise cls()
 
 
 # ---------------------------------------------------------------- marshalling
