@@ -219,10 +219,9 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
                 a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
                 a.sid[v] = A.sid(v);
             }
-            return launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
-                                   reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st) == hipSuccess
-                       ? RS_OK
-                       : RS_ERR_DEVICE;
+            return hip_ok(launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
+                                          reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st),
+                          "multi-pattern kernel launch");
         }
 
         UploadLease lease(rs);

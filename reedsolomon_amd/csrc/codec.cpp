@@ -92,13 +92,14 @@ int ensure_device(rs_t* rs) {
     std::lock_guard<std::mutex> lk(rs->dev_mu);
     if (rs->device_ready) return RS_OK;
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RS_ERR_DEVICE;
+    RS_TRY(hip_ok(hipGetDeviceCount(&count), "hipGetDeviceCount"));
+    if (count <= 0) return dev_fail(hipErrorNoDevice, "hipGetDeviceCount");
     if (rs->device < 0) {
         int cur = 0;
-        if (hipGetDevice(&cur) != hipSuccess) return RS_ERR_DEVICE;
+        RS_TRY(hip_ok(hipGetDevice(&cur), "hipGetDevice"));
         rs->device = cur;
     }
-    if (rs->device >= count) return RS_ERR_DEVICE;
+    if (rs->device >= count) return dev_fail(hipErrorInvalidDevice, "device ordinal");
     rs->device_ready = true;
     return RS_OK;
 }
@@ -135,7 +136,7 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
     }
     if (rs->tables.size() >= g_registry_max) {
         // Bounded registry: drain the device before recycling table memory.
-        if (hipDeviceSynchronize() != hipSuccess) return RS_ERR_DEVICE;
+        RS_TRY(hip_ok(hipDeviceSynchronize(), "table registry drain"));
         for (auto& kv : rs->tables) (void)hipFree(kv.second);
         rs->tables.clear();
     }
@@ -148,10 +149,11 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
             if (img_dw) perm_table(mat[static_cast<size_t>(r) * cols + c], &host[main_dw + static_cast<size_t>(c) * 20 + r * 5]);
         }
     uint32_t* dptr = nullptr;
-    if (hipMalloc(&dptr, host.size() * 4) != hipSuccess) return RS_ERR_DEVICE;
-    if (hipMemcpy(dptr, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&dptr, host.size() * 4) != hipSuccess) return RS_ERR_NOMEM;
+    const hipError_t e = hipMemcpy(dptr, host.data(), host.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
         (void)hipFree(dptr);
-        return RS_ERR_DEVICE;
+        return dev_fail(e, "table upload");
     }
     rs->tables.emplace(std::move(key), dptr);
     *out = dptr;

@@ -12,6 +12,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <new>
@@ -35,6 +36,12 @@ namespace detail {
 constexpr int kMaxVects = 256;                              // rs.go:47
 constexpr uint64_t kMaxInverseCacheBytes = 16ull << 20;     // rs.go:50
 extern size_t g_registry_max;  // coefficient-table registry cap (distinct matrices per handle)
+
+// Record which HIP call failed (thread-local, read by rs_last_device_error)
+// and return RS_ERR_DEVICE.
+int dev_fail(hipError_t e, const char* where);
+// RS_OK, or dev_fail(e, where) when the HIP call failed.
+inline int hip_ok(hipError_t e, const char* where) { return e == hipSuccess ? RS_OK : dev_fail(e, where); }
 
 // ---------------------------------------------------------------- device helpers
 
@@ -210,17 +217,22 @@ public:
     int acquire(size_t bytes, uint8_t** host) {
         rs_codec::UploadSlot& u = rs_->up[rs_->up_next];
         rs_->up_next = (rs_->up_next + 1) % rs_codec::kUploadSlots;
-        if (!rs_->up_stream && hipStreamCreateWithFlags(&rs_->up_stream, hipStreamNonBlocking) != hipSuccess) {
-            rs_->up_stream = nullptr;
-            return RS_ERR_DEVICE;
+        if (!rs_->up_stream) {
+            const hipError_t e = hipStreamCreateWithFlags(&rs_->up_stream, hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                rs_->up_stream = nullptr;
+                return dev_fail(e, "upload stream create");
+            }
         }
         if (u.in_flight) {  // the kernel that read this slot's device copy has finished
-            if (hipEventSynchronize(u.done) != hipSuccess) return RS_ERR_DEVICE;
+            RS_TRY(hip_ok(hipEventSynchronize(u.done), "upload slot event sync"));
             u.in_flight = false;
         }
-        if (!u.copied && (hipEventCreateWithFlags(&u.copied, hipEventDisableTiming) != hipSuccess ||
-                          hipEventCreateWithFlags(&u.done, hipEventDisableTiming) != hipSuccess))
-            return RS_ERR_DEVICE;
+        for (hipEvent_t* ev : {&u.copied, &u.done})
+            if (!*ev && hip_ok(hipEventCreateWithFlags(ev, hipEventDisableTiming), "upload event create")) {
+                *ev = nullptr;
+                return RS_ERR_DEVICE;
+            }
         if (u.cap < bytes) {
             if (u.host) (void)hipHostFree(u.host);
             if (u.dev) (void)hipFree(u.dev);
@@ -248,10 +260,10 @@ public:
     // Copy the filled host buffer to the device and make `st` wait for it.
     int upload(hipStream_t st, uint8_t** dev) {
         st_ = st;
-        if (hipMemcpyAsync(slot_->dev, slot_->host, bytes_, hipMemcpyHostToDevice, rs_->up_stream) != hipSuccess ||
-            hipEventRecord(slot_->copied, rs_->up_stream) != hipSuccess ||
-            hipStreamWaitEvent(st, slot_->copied, 0) != hipSuccess)
-            return RS_ERR_DEVICE;
+        RS_TRY(hip_ok(hipMemcpyAsync(slot_->dev, slot_->host, bytes_, hipMemcpyHostToDevice, rs_->up_stream),
+                      "upload copy"));
+        RS_TRY(hip_ok(hipEventRecord(slot_->copied, rs_->up_stream), "upload event record"));
+        RS_TRY(hip_ok(hipStreamWaitEvent(st, slot_->copied, 0), "upload stream wait"));
         *dev = slot_->dev;
         return RS_OK;
     }
@@ -323,10 +335,6 @@ size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Record which HIP call failed (thread-local, read by rs_last_device_error)
-// and return RS_ERR_DEVICE.
-int dev_fail(hipError_t e, const char* where);
-
 // Every int-returning C ABI entry point runs its body through this guard, so
 // no C++ exception (an allocation failure in a std:: container, a thread
 // that cannot start) ever unwinds into a C or cgo caller.
@@ -337,7 +345,7 @@ int abi_guard(F&& body) noexcept {
     } catch (const std::bad_alloc&) {
         return RS_ERR_NOMEM;
     } catch (...) {
-        return RS_ERR_DEVICE;
+        return dev_fail(hipErrorUnknown, "unexpected C++ exception");
     }
 }
 

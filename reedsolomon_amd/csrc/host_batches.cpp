@@ -121,8 +121,7 @@ int rs_host_register(void* ptr, size_t bytes) {
     return abi_guard([&]() -> int {
         if (!ptr || !bytes) return RS_ERR_INVAL;
         // mapped: kernels may address it directly (zero-copy host batches and calls)
-        if (hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess)
-            return RS_ERR_DEVICE;
+        RS_TRY(hip_ok(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister"));
         void* dev = nullptr;
         if (hipHostGetDevicePointer(&dev, ptr, 0) == hipSuccess && dev) {
             std::lock_guard<std::mutex> lk(g_reg_mu);
@@ -156,7 +155,7 @@ int rs_host_unregister(void* ptr) {
             g_reg.erase(reinterpret_cast<uintptr_t>(ptr));
             g_reg_count.store(static_cast<int>(g_reg.size()));
         }
-        return hipHostUnregister(ptr) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+        return hip_ok(hipHostUnregister(ptr), "hipHostUnregister");
     });
 }
 
@@ -183,16 +182,16 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) == RS_OK) {
             // pinned / registered caller memory: one launch straight over it
             std::lock_guard<std::mutex> lk(rs->stage_mu);
-            if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-                return RS_ERR_DEVICE;
+            if (!rs->stream)
+                RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
             const uint8_t* in[kMaxVects];
             uint8_t* out[kMaxVects];
             for (int i = 0; i < d; ++i) in[i] = zc + i * vect_stride;
             for (int j = 0; j < p; ++j) out[j] = zc + (d + j) * vect_stride;
             int rc = matmul(rs, rs->gen(), p, d, in, stripe_stride, out, stripe_stride, nstripes, len, false,
                             rs->stream);
-            if (hipStreamSynchronize(rs->stream) != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
-            return rc;
+            const int sync_rc = hip_ok(hipStreamSynchronize(rs->stream), "host-batch sync");
+            return rc ? rc : sync_rc;
         }
         // [S][d+p][len] with 256-B-multiple len: data and parity of a stripe are contiguous rows
         const bool dense = vect_stride == static_cast<int64_t>(len) && len % 256 == 0;
@@ -211,19 +210,19 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             rs->dma_ring_bytes = 0;
             if (hipMalloc(&rs->dma_ring, slot_bytes * slots) != hipSuccess) {
                 rs->dma_ring = nullptr;
-                return RS_ERR_DEVICE;
+                return RS_ERR_NOMEM;
             }
             rs->dma_ring_bytes = slot_bytes * slots;
         }
         uint8_t* ring = rs->dma_ring;
         for (hipStream_t& s : rs->dma_stream)
-            if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            if (!s && hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream create")) {
                 s = nullptr;
                 return RS_ERR_DEVICE;
             }
         for (auto& row : rs->dma_ev)
             for (int i = 0; i < slots; ++i)
-                if (!row[i] && hipEventCreateWithFlags(&row[i], hipEventDisableTiming) != hipSuccess) {
+                if (!row[i] && hip_ok(hipEventCreateWithFlags(&row[i], hipEventDisableTiming), "event create")) {
                     row[i] = nullptr;
                     return RS_ERR_DEVICE;
                 }
@@ -380,11 +379,10 @@ int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, 
         rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
                       vect_stride};
         std::lock_guard<std::mutex> lk(rs->stage_mu);
-        if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-            return RS_ERR_DEVICE;
+        if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
         int rc = rs_reconst_batch_multi(rs, &L, nstripes, len, need_masks, rs->stream);
-        if (hipStreamSynchronize(rs->stream) != hipSuccess && rc == RS_OK) rc = RS_ERR_DEVICE;
-        return rc;
+        const int sync_rc = hip_ok(hipStreamSynchronize(rs->stream), "host-batch sync");
+        return rc ? rc : sync_rc;
     });
 }
 

@@ -49,8 +49,7 @@ bool use_pinned(rs_t* rs, int slots, size_t pitch) {
 int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
     *pitch = rup(size, 256);
     const size_t need = *pitch * static_cast<size_t>(slots);
-    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-        return RS_ERR_DEVICE;
+    if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
     if (need > rs->stage_bytes) {
         if (rs->stage) {
             (void)hipStreamSynchronize(rs->stream);
@@ -58,7 +57,10 @@ int ensure_stage(rs_t* rs, int slots, size_t size, size_t* pitch) {
             rs->stage = nullptr;
             rs->stage_bytes = 0;
         }
-        if (hipMalloc(&rs->stage, need) != hipSuccess) return RS_ERR_DEVICE;
+        if (hipMalloc(&rs->stage, need) != hipSuccess) {
+            rs->stage = nullptr;
+            return RS_ERR_NOMEM;
+        }
         rs->stage_bytes = need;
     }
     rs->slots = rs->stage;
@@ -71,14 +73,13 @@ int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pit
 int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, int first, int total_slots);
 
 int h2d(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
-    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+    return hip_ok(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, rs->stream), "host-call H2D copy");
 }
 int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
-    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, rs->stream) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+    return hip_ok(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, rs->stream), "host-call D2H copy");
 }
 int sync(rs_t* rs) {
-    const hipError_t e = hipStreamSynchronize(rs->stream);
-    return e == hipSuccess ? RS_OK : dev_fail(e, "host-call stream sync");
+    return hip_ok(hipStreamSynchronize(rs->stream), "host-call stream sync");
 }
 
 int stage_in(rs_t* rs, const uint8_t* const* src, int n, size_t size, size_t pitch, int first, int total_slots) {
@@ -142,8 +143,7 @@ void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t
 int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
                 size_t size, bool accumulate) {
     const int nvec = rows + cols;
-    if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-        return RS_ERR_DEVICE;
+    if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
     // chunk: <= g_chunk per vector and <= 8 MiB per slot, 4 KiB multiple
     size_t C = rup(size, 256);
     const size_t cap = std::max<size_t>(4096, std::min(g_chunk, (size_t{8} << 20) / nvec) & ~size_t{4095});
@@ -165,9 +165,10 @@ int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
         rs->hstage_bytes = slot * ns;
     }
     void* dbase = nullptr;
-    if (hipHostGetDevicePointer(&dbase, rs->hstage, 0) != hipSuccess || !dbase) return RS_ERR_DEVICE;
+    RS_TRY(hip_ok(hipHostGetDevicePointer(&dbase, rs->hstage, 0), "mirror device pointer"));
+    if (!dbase) return dev_fail(hipErrorInvalidValue, "mirror device pointer");
     for (int i = 0; i < ns; ++i)
-        if (!rs->chunk_ev[i] && hipEventCreateWithFlags(&rs->chunk_ev[i], hipEventDisableTiming) != hipSuccess) {
+        if (!rs->chunk_ev[i] && hip_ok(hipEventCreateWithFlags(&rs->chunk_ev[i], hipEventDisableTiming), "event create")) {
             rs->chunk_ev[i] = nullptr;
             return RS_ERR_DEVICE;
         }
@@ -177,7 +178,7 @@ int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
     };
     auto clen = [&](size_t c) { return std::min(C, size - c * C); };
     auto finish = [&](size_t c) -> int {  // wait for chunk c, copy its outputs back
-        if (hipEventSynchronize(rs->chunk_ev[c % ns]) != hipSuccess) return RS_ERR_DEVICE;
+        RS_TRY(hip_ok(hipEventSynchronize(rs->chunk_ev[c % ns]), "host-call chunk sync"));
         uint8_t* d[kMaxVects];
         const uint8_t* h[kMaxVects];
         for (int r = 0; r < rows; ++r) {
@@ -214,7 +215,7 @@ int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
         for (int r = 0; r < rows; ++r) out[r] = dslot(c, cols + r);
         rs->zc_pending = true;
         rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, len, accumulate, rs->stream);
-        if (rc == RS_OK && hipEventRecord(rs->chunk_ev[c % ns], rs->stream) != hipSuccess) rc = RS_ERR_DEVICE;
+        if (rc == RS_OK) rc = hip_ok(hipEventRecord(rs->chunk_ev[c % ns], rs->stream), "host-call chunk record");
     }
     while (rc == RS_OK && done < nch) rc = finish(done++);
     if (rc) (void)hipStreamSynchronize(rs->stream);  // never leave a kernel on the mirror
@@ -285,10 +286,11 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
             return RS_ERR_NOMEM;
         }
         void* dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, b.host, 0) != hipSuccess || !dp) {
+        const hipError_t e = hipHostGetDevicePointer(&dp, b.host, 0);
+        if (e != hipSuccess || !dp) {
             (void)hipHostFree(b.host);
             b.host = nullptr;
-            return RS_ERR_DEVICE;
+            return dev_fail(e != hipSuccess ? e : hipErrorInvalidValue, "coalescing buffer device pointer");
         }
         b.dev = static_cast<uint8_t*>(dp);
         b.host_bytes = need;
@@ -336,8 +338,8 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
             direct = (out[r] = registered_device_ptr(dst[r], size)) && (reinterpret_cast<uintptr_t>(dst[r]) & 15) == 0;
         if (direct) {
             std::lock_guard<std::mutex> lk(rs->stage_mu);
-            if (!rs->stream && hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking) != hipSuccess)
-                return RS_ERR_DEVICE;
+            if (!rs->stream)
+                RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
             if (rs->zc_pending) RS_TRY(sync(rs));
             const int rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, size, accumulate, rs->stream);
             const int src_rc = sync(rs);
@@ -349,7 +351,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         return host_product(rs, mat, rows, cols, src, dst, size, accumulate);
     }
     std::unique_lock<std::mutex> lk(rs->co_mu);
-    if (!rs->co_stream && hipStreamCreateWithFlags(&rs->co_stream, hipStreamNonBlocking) != hipSuccess) {
+    if (!rs->co_stream && hip_ok(hipStreamCreateWithFlags(&rs->co_stream, hipStreamNonBlocking), "stream create")) {
         rs->co_stream = nullptr;
         return RS_ERR_DEVICE;
     }
