@@ -198,8 +198,9 @@ RS_API int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_str
  * `base` is a HOST pointer.  The call pipelines H2D copies of the data
  * vectors, the device encode and D2H copies of the parity vectors over
  * `streams` HIP streams with `stripes_per_chunk` stripes per step, and
- * returns when every parity byte is back in host memory.  Host memory should
- * be pinned (rs_host_register) for full PCIe rate.
+ * returns when every parity byte is back in host memory.  Strides are
+ * non-negative (RS_ERR_INVAL otherwise).  Host memory should be pinned
+ * (rs_host_register) for full PCIe rate.
  * ------------------------------------------------------------------------ */
 RS_API int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                 int nstripes, size_t len, int stripes_per_chunk, int streams);

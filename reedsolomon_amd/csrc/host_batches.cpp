@@ -170,6 +170,7 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
                          size_t len, int stripes_per_chunk, int streams) {
     return abi_guard([&]() -> int {
         if (!rs || nstripes < 0 || (nstripes > 0 && !base)) return RS_ERR_INVAL;
+        if (stripe_stride < 0 || vect_stride < 0) return RS_ERR_INVAL;  // host extents are [base, base+extent)
         if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
         if (nstripes == 0) return RS_OK;
         if (stripes_per_chunk <= 0) stripes_per_chunk = 8;
@@ -178,7 +179,7 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
         DeviceGuard g(rs->device);
         const int d = rs->d, p = rs->p;
         uint8_t* zc = nullptr;
-        if (g_host_batch_zc && stripe_stride >= 0 && vect_stride >= 0 &&
+        if (g_host_batch_zc &&
             host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) == RS_OK) {
             // pinned / registered caller memory: one launch straight over it
             std::lock_guard<std::mutex> lk(rs->stage_mu);

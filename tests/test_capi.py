@@ -201,6 +201,21 @@ def test_host_checks_before_device(rslib, orc):
     r.Reconst([_z(8)] * 14, [0, 1], [])
 
 
+def test_host_batch_argument_checks(rslib):
+    """rs_encode_host_batch validates its layout before touching a device."""
+    import ctypes
+    L = rslib.lib()
+    r = rslib.New(10, 4)
+    buf = (ctypes.c_uint8 * (14 * 256))()
+    base = ctypes.cast(buf, ctypes.POINTER(ctypes.c_uint8))
+    assert L.rs_encode_host_batch(r._h, base, -14 * 256, 256, 1, 256, 0, 0) == 13  # RS_ERR_INVAL
+    assert L.rs_encode_host_batch(r._h, base, 14 * 256, -256, 1, 256, 0, 0) == 13
+    assert L.rs_encode_host_batch(r._h, None, 14 * 256, 256, 1, 256, 0, 0) == 13
+    assert L.rs_encode_host_batch(r._h, base, 14 * 256, 256, -1, 256, 0, 0) == 13
+    assert L.rs_encode_host_batch(r._h, base, 14 * 256, 256, 1, 0, 0, 0) == 3  # ErrZeroVectSize
+    assert L.rs_encode_host_batch(r._h, base, 14 * 256, 256, 0, 256, 0, 0) == 0
+
+
 def test_reconst_matrix_from_cache(rslib):  # TestRS_getReconstMatrixFromCache rs_test.go:355-404
     """The reference force-enables the cache on 64+64 (white-box); here the
     widest shape the cache serves by policy (d+p = 64, rs.go:70) with d = 60,
