@@ -25,7 +25,7 @@ GiB = 2 ** 30
 out = {}
 
 
-def dev_time(fn, iters=50, warm=20):
+def dev_time(fn, iters=50, warm=50):
     st = torch.cuda.current_stream()
     for _ in range(warm):
         fn()
@@ -73,7 +73,10 @@ def main():
         pats.append(sum(1 << int(v) for v in lost))
     masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
     nrec = sum(bin(int(x)).count("1") for x in masks)
-    t = dev_time(lambda: r.reconst_batch_multi(buf[:, :k], buf[:, k:], masks), iters=20, warm=5)
+    # full warm-up: the single-stripe calls above leave the GPU idle enough to
+    # drop its clocks, and 5 warm-up calls did not bring them back (4,934 GiB/s
+    # with warm=5 vs ~5,700 in tools/multi_mix.py on the same box)
+    t = dev_time(lambda: r.reconst_batch_multi(buf[:, :k], buf[:, k:], masks))
     rec(f"reconst_multi 10+4 8KiB 16 patterns x{S}", (S * k + nrec) * vec, t)
     # ---- update / replace 10+4 @ 8 KiB (config 5)
     old = buf[:, 3].clone()
