@@ -167,6 +167,19 @@ def replace(d, p, data, rows, parity) -> int:
     return lib().orc_replace(d, p, darr, dlens, len(data), r, nr, parr, plens, len(parity))
 
 
+def update_quirk_range(size: int, l1d: int = 32 * 1024):
+    """Byte range [lo, hi) where the reference's Update / Replace keep the old
+    parity (rs_oracle.c encode_part: the tail pass of rs.go:190-200 covers the
+    whole last chunk, XORing its 16-byte body twice), or None.  getSplitSize
+    rs.go:158-173 with the given L1D size."""
+    if size < l1d // 2:
+        return None  # chunks: 16-byte multiples, then a < 16-byte tail alone
+    last = size % (l1d // 2)
+    if last >= 16 and last % 16:
+        return size - last, size - last + (last & ~15)
+    return None
+
+
 def naive_mul(gen, d, p, vects):
     gen = np.ascontiguousarray(gen, dtype=np.uint8)
     arr, _ = _vec_table(vects)

@@ -191,8 +191,8 @@ uint64_t orc_inverse_cache_key(const int* survived, int ns) {
 }
 
 /* getSplitSize rs.go:158-173 with the default L1D of 32 KiB (cpu.X86.Cache.L1D
- * unknown, rs.go:160-162). Chunking changes no output byte; it is restated
- * so the oracle walks the same loop structure as the reference. */
+ * unknown, rs.go:160-162). For Encode the chunking changes no output byte;
+ * for Update / Replace (updateOnly) it does, see encode_part. */
 static size_t split_size(size_t n) {
     const size_t l1d = 32 * 1024;
     if (n < 16) return 16;
@@ -201,7 +201,20 @@ static size_t split_size(size_t n) {
 }
 
 /* encodePart rs.go:175-203 on the no-SIMD feature (gmu_generic.go:6-9): the
- * first data row overwrites unless updateOnly, every other term XORs. */
+ * first data row overwrites unless updateOnly, every other term XORs.
+ *
+ * Restated as written, including a reference defect: the sub-16-byte tail
+ * pass (rs.go:190-200) runs over the WHOLE chunk [start, end), not just
+ * [start + done, end).  For Encode that is harmless (its i == 0 term
+ * overwrites the chunk again).  For updateOnly (Update rs.go:447, Replace
+ * rs.go:527) the chunk's 16-byte-multiple body is XORed twice, so it keeps
+ * its old parity: whenever the last chunk has >= 16 bytes and a length that
+ * is not a multiple of 16 (vectors >= L1D/2 whose size mod L1D/2 is such a
+ * length), the reference's Update / Replace differ from re-encoding there.
+ * The region depends on the host's L1D size (cpu.X86.Cache.L1D).  The
+ * reference's own tests define Update / Replace as equal to re-encoding
+ * (rs_test.go:225-331, at 1 KiB, outside this case); librsamd computes that
+ * definition for every size (DESIGN.md §4 "Reference defect"). */
 static void encode_part(size_t start, size_t end, int d, int p, const uint8_t* g,
                         uint8_t* const* dv, uint8_t* const* pv, int update_only) {
     size_t undone = end - start;

@@ -1,0 +1,202 @@
+"""Seeded random sweep: shapes, sizes and operations the targeted tests do
+not pin one by one, each through the C ABI and compared byte-for-byte with
+the CPU oracle (rs_oracle.c restating rs.go / matrix.go / gmu.go).
+
+Host API: Encode / Reconst / Update / Replace on d in 1..40, p in 1..12,
+(Update / Replace against re-encoding, and against the restated reference
+outside its tail defect: DESIGN.md §4 "Reference defect"),
+sizes from 1 B to ~300 KiB (odd sizes take the byte-tail kernel, small
+ones the coalesced path, large ones the chunked pipeline).  Device batches:
+split-layout Encode and per-stripe-pattern Reconst on random shapes and
+stripe counts, every stripe checked against the oracle.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    torch.cuda.init()
+    return torch
+
+
+def _size(rng):
+    kind = int(rng.integers(4))
+    if kind == 0:
+        return int(rng.integers(1, 300))
+    if kind == 1:
+        return 4096 + int(rng.integers(-17, 18))
+    if kind == 2:
+        return int(rng.integers(8192, 70000))
+    return int(rng.integers(130000, 300000))
+
+
+def _shape(rng):
+    d = int(rng.integers(1, 41))
+    p = int(rng.integers(1, 13))
+    return d, p
+
+
+def _rand(rng, n):
+    return rng.integers(0, 256, n, dtype=np.uint8)
+
+
+def _check_update_like(orc, act, ora, exp, d, p, size, tag):
+    """Update / Replace: every parity byte equals re-encoding (the reference's
+    own definition, rs_test.go:225-331), and equals the restated reference
+    byte-for-byte outside its tail defect (rs_oracle.c encode_part)."""
+    q = orc.update_quirk_range(size)
+    for j in range(d, d + p):
+        assert np.array_equal(act[j], exp[j]), tag + (j,)
+        if q is None:
+            assert np.array_equal(act[j], ora[j]), tag + (j,)
+        else:
+            lo, hi = q
+            assert np.array_equal(act[j][:lo], ora[j][:lo]) and np.array_equal(act[j][hi:], ora[j][hi:]), tag
+
+
+def test_host_api_random_sweep(rslib, orc, torch_dev):
+    rng = np.random.default_rng(2024)
+    counts = {"encode": 0, "reconst": 0, "update": 0, "replace": 0}
+    for case in range(80):
+        d, p = _shape(rng)
+        size = _size(rng)
+        r = rslib.New(d, p)
+        data = [_rand(rng, size) for _ in range(d)]
+        enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+        assert orc.encode(d, p, enc) == 0
+        op = ("encode", "reconst", "update", "replace")[case % 4]
+        counts[op] += 1
+        tag = (case, op, d, p, size)
+        if op == "encode":
+            act = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
+            r.Encode(act)
+            for j in range(p):
+                assert np.array_equal(act[d + j], enc[d + j]), tag + (j,)
+        elif op == "reconst":
+            nlost = int(rng.integers(1, p + 1))
+            lost = sorted(int(v) for v in rng.choice(d + p, nlost, replace=False))
+            surv = [v for v in range(d + p) if v not in lost]
+            act = [x.copy() for x in enc]
+            for v in lost:
+                act[v][:] = _rand(rng, size)  # garbage where the lost vectors were
+            ora = [x.copy() for x in act]
+            r.Reconst(act, surv, lost)
+            assert orc.reconst(d, p, ora, surv, lost) == 0
+            for v in range(d + p):
+                assert np.array_equal(act[v], ora[v]), tag + (v,)
+            for v in lost:
+                assert np.array_equal(act[v], enc[v]), tag + (v,)
+        elif op == "update":
+            row = int(rng.integers(d))
+            new = _rand(rng, size)
+            act = [x.copy() for x in enc]
+            ora = [x.copy() for x in enc]
+            r.Update(act[row], new, row, act[d:])
+            assert orc.update(d, p, ora[row], new, row, ora[d:]) == 0
+            exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            exp[row] = new.copy()
+            assert orc.encode(d, p, exp) == 0
+            _check_update_like(orc, act, ora, exp, d, p, size, tag)
+        else:
+            rn = int(rng.integers(1, d + 1))
+            rows = [int(v) for v in rng.choice(d, rn, replace=False)]
+            delta = [_rand(rng, size) for _ in range(rn)]
+            act = [x.copy() for x in enc]
+            ora = [x.copy() for x in enc]
+            r.Replace(delta, rows, act[d:])
+            assert orc.replace(d, p, [x.copy() for x in delta], rows, ora[d:]) == 0
+            exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            for k_, rr in enumerate(rows):
+                exp[rr] = np.bitwise_xor(exp[rr], delta[k_])
+            assert orc.encode(d, p, exp) == 0
+            _check_update_like(orc, act, ora, exp, d, p, size, tag)
+    assert all(v == 20 for v in counts.values())
+
+
+def test_device_batch_random_sweep(rslib, orc, torch_dev):
+    torch = torch_dev
+    rng = np.random.default_rng(77)
+    for case in range(24):
+        d = int(rng.integers(1, 25))
+        p = int(rng.integers(1, 9))
+        S = int(rng.integers(1, 40))
+        n = int(rng.choice([16, 48, 1003, 1024, 4096 + 16 * int(rng.integers(1, 9)), 8192, 20000 * 16]))
+        if n > 8192:
+            S = min(S, 4)
+        r = rslib.New(d, p)
+        host = rng.integers(0, 256, (S, d, n), dtype=np.uint8)
+        data = torch.from_numpy(host).cuda()
+        parity = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
+        r.encode_batch_split(data, parity)
+        torch.cuda.synchronize()
+        par = parity.cpu().numpy()
+        exp = []
+        for s in range(S):
+            v = [host[s, i].copy() for i in range(d)] + [np.zeros(n, np.uint8) for _ in range(p)]
+            assert orc.encode(d, p, v) == 0
+            exp.append(v)
+            for j in range(p):
+                assert np.array_equal(par[s, j], v[d + j]), (case, d, p, S, n, s, j)
+        if d + p > 64:
+            continue
+        # a different 1..min(p,4)-erasure pattern per stripe (some stripes intact)
+        masks = np.zeros(S, np.uint64)
+        for s in range(S):
+            if rng.integers(5) == 0:
+                continue
+            k = int(rng.integers(1, min(p, 4) + 1))
+            masks[s] = sum(1 << int(v) for v in rng.choice(d + p, k, replace=False))
+        for s in range(S):
+            for v in range(d + p):
+                if int(masks[s]) >> v & 1:
+                    (data[s, v] if v < d else parity[s, v - d]).fill_(int(rng.integers(256)))
+        r.reconst_batch_multi(data, parity, masks)
+        torch.cuda.synchronize()
+        got_d, got_p = data.cpu().numpy(), parity.cpu().numpy()
+        for s in range(S):
+            for v in range(d + p):
+                got = got_d[s, v] if v < d else got_p[s, v - d]
+                assert np.array_equal(got, exp[s][v]), (case, d, p, S, n, s, v, int(masks[s]))
+
+
+@pytest.mark.parametrize("size", [16384 + 16 * 40 + 7, 49263, 236667])
+def test_update_replace_at_reference_defect_sizes(rslib, orc, torch_dev, size):
+    """Sizes where the reference's Update / Replace keep stale parity in the
+    last chunk's body (rs_oracle.c encode_part): the host API and
+    the device call equal re-encoding there, and the restated reference
+    everywhere else."""
+    torch = torch_dev
+    d, p, row = 10, 4, 7
+    rng = np.random.default_rng(size)
+    data = [_rand(rng, size) for _ in range(d)]
+    enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+    assert orc.encode(d, p, enc) == 0
+    new = _rand(rng, size)
+    exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+    exp[row] = new.copy()
+    assert orc.encode(d, p, exp) == 0
+    r = rslib.New(d, p)
+    # Update, host API and device call
+    act = [x.copy() for x in enc]
+    ora = [x.copy() for x in enc]
+    r.Update(act[row], new, row, act[d:])
+    assert orc.update(d, p, ora[row], new, row, ora[d:]) == 0
+    _check_update_like(orc, act, ora, exp, d, p, size, ("update", size))
+    dv = [torch.from_numpy(x.copy()).cuda() for x in enc]
+    r.update_dev(dv[row], torch.from_numpy(new.copy()).cuda(), row, dv[d:])
+    torch.cuda.synchronize()
+    for j in range(d, d + p):
+        assert np.array_equal(dv[j].cpu().numpy(), exp[j]), ("update_dev", size, j)
+    # Replace of the same row (delta = old ^ new)
+    act = [x.copy() for x in enc]
+    ora = [x.copy() for x in enc]
+    delta = np.bitwise_xor(data[row], new)
+    r.Replace([delta], [row], act[d:])
+    assert orc.replace(d, p, [delta.copy()], [row], ora[d:]) == 0
+    _check_update_like(orc, act, ora, exp, d, p, size, ("replace", size))

@@ -233,6 +233,36 @@ def test_update_equals_reencode(orc):  # TestRS_Update rs_test.go:219-266
             assert np.array_equal(act[j], exp[j])
 
 
+@pytest.mark.parametrize("size", [16384 + 16 * 40 + 7, 49263, 236667, 16384 * 5 + 17])
+def test_reference_update_replace_tail_defect(orc, size):
+    """The reference's Update / Replace (restated faithfully) equal re-encoding
+    everywhere except the body of a last chunk with a >= 16-byte, non-16-multiple
+    length, where they keep the old parity (rs.go:190-200 XORs that body twice).
+    Pins the analysis behind DESIGN.md §4 "Reference defect"; librsamd computes
+    the re-encode result there."""
+    d, p, row = 10, 4, 3
+    rng = np.random.default_rng(size)
+    base = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(d)] + \
+           [np.zeros(size, np.uint8) for _ in range(p)]
+    orc.encode(d, p, base)
+    new = rng.integers(0, 256, size, dtype=np.uint8)
+    upd = [x.copy() for x in base]
+    assert orc.update(d, p, upd[row], new, row, upd[d:]) == 0
+    rep = [x.copy() for x in base]
+    delta = np.bitwise_xor(base[row], new)
+    assert orc.replace(d, p, [delta], [row], rep[d:]) == 0
+    exp = [x.copy() for x in base]
+    exp[row] = new.copy()
+    orc.encode(d, p, exp)
+    lo, hi = orc.update_quirk_range(size)
+    for got in (upd, rep):
+        for j in range(d, d + p):
+            assert np.array_equal(got[j][:lo], exp[j][:lo]) and np.array_equal(got[j][hi:], exp[j][hi:])
+            assert np.array_equal(got[j][lo:hi], base[j][lo:hi])  # untouched: the old parity
+    for ok_size in (1024, 16384, 16384 * 3 + 5, 16384 * 2 + 32, 40000 - 40000 % 16):
+        assert orc.update_quirk_range(ok_size) is None
+
+
 @pytest.mark.parametrize("to_zero", [True, False])
 def test_replace_equals_reencode(orc, to_zero):  # TestRS_Replace rs_test.go:268-331
     d, p, size = 10, 4, 1024
