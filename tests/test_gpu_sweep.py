@@ -200,3 +200,94 @@ def test_update_replace_at_reference_defect_sizes(rslib, orc, torch_dev, size):
     r.Replace([delta], [row], act[d:])
     assert orc.replace(d, p, [delta.copy()], [row], ora[d:]) == 0
     _check_update_like(orc, act, ora, exp, d, p, size, ("replace", size))
+
+
+def _padded(torch, rng, S, nvec, n, device):
+    """[S, nvec, n] view of a larger random buffer (padding between vectors and
+    stripes, sometimes an odd vector stride: the unaligned / byte-kernel paths)."""
+    vpad = int(rng.choice([0, 16, 5, 256]))
+    spad = int(rng.choice([0, 1, 3]))
+    full = torch.randint(0, 256, (S, nvec + spad, n + vpad), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(int(rng.integers(1 << 30))))
+    if device == "cuda":
+        full = full.cuda()
+    elif device == "pinned":
+        full = full.pin_memory()
+    return full[:, :nvec, :n]
+
+
+def _encode_expect(orc, host, d, p):
+    """Parity of every stripe of host[S, >= d, n] (numpy), per the oracle."""
+    S, _, n = host.shape
+    out = np.zeros((S, p, n), np.uint8)
+    for s in range(S):
+        v = [host[s, i].copy() for i in range(d)] + [np.zeros(n, np.uint8) for _ in range(p)]
+        assert orc.encode(d, p, v) == 0
+        out[s] = np.stack(v[d:])
+    return out
+
+
+def test_batch_update_replace_random_sweep(rslib, orc, torch_dev):
+    """rs_update_batch / rs_replace_batch on padded, sometimes unaligned
+    layouts: parity equals re-encoding the changed stripes."""
+    torch = torch_dev
+    rng = np.random.default_rng(91)
+    for case in range(16):
+        d = int(rng.integers(1, 21))
+        p = int(rng.integers(1, 9))
+        S = int(rng.integers(1, 17))
+        n = int(rng.choice([1, 15, 16, 100, 1024, 4099, 8192, 40000]))
+        r = rslib.New(d, p)
+        buf = _padded(torch, rng, S, d + p, n, "cuda")
+        r.encode_batch(buf)
+        host = buf.cpu().numpy()
+        assert np.array_equal(host[:, d:], _encode_expect(orc, host, d, p)), (case, "encode")
+        if case % 2 == 0:
+            row = int(rng.integers(d))
+            new = torch.randint(0, 256, (S, n), dtype=torch.uint8, device="cuda")
+            old = buf[:, row].clone()
+            r.update_batch(old, new, row, buf)
+            host2 = host.copy()
+            host2[:, row] = new.cpu().numpy()
+        else:
+            rn = int(rng.integers(1, d + 1))
+            rows = [int(v) for v in rng.choice(d, rn, replace=False)]
+            delta = torch.randint(0, 256, (S, rn, n), dtype=torch.uint8, device="cuda")
+            r.replace_batch(delta, rows, buf)
+            host2 = host.copy()
+            dh = delta.cpu().numpy()
+            for k_, rr in enumerate(rows):
+                host2[:, rr] ^= dh[:, k_]
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()[:, d:]
+        assert np.array_equal(got, _encode_expect(orc, host2, d, p)), (case, d, p, S, n)
+
+
+def test_host_batch_random_sweep(rslib, orc, torch_dev):
+    """rs_encode_host_batch on pageable (DMA pipeline) and pinned (zero-copy)
+    padded layouts, and rs_reconst_host_batch_multi on pinned memory."""
+    torch = torch_dev
+    rng = np.random.default_rng(92)
+    for case in range(12):
+        d = int(rng.integers(1, 17))
+        p = int(rng.integers(1, 7))
+        S = int(rng.integers(1, 25))
+        n = int(rng.choice([16, 256, 1000, 4096, 65536 + 256]))
+        where = "pinned" if case % 2 else "pageable"
+        r = rslib.New(d, p)
+        buf = _padded(torch, rng, S, d + p, n, where)
+        arr = buf if where == "pinned" else buf.numpy()
+        r.encode_host_batch(arr, stripes_per_chunk=int(rng.integers(1, 6)), streams=int(rng.integers(1, 4)))
+        host = buf.numpy().copy()
+        assert np.array_equal(host[:, d:], _encode_expect(orc, host, d, p)), (case, where, d, p, S, n)
+        if where != "pinned" or d + p > 64 or n % 16:
+            continue
+        masks = np.zeros(S, np.uint64)
+        for s in range(S):
+            k = int(rng.integers(0, min(p, 4) + 1))
+            lost = rng.choice(d + p, k, replace=False)
+            masks[s] = sum(1 << int(v) for v in lost)
+            for v in lost:
+                buf[s, int(v)].fill_(0x3C)
+        r.reconst_host_batch_multi(buf, masks)
+        assert np.array_equal(buf.numpy(), host), (case, "reconst", d, p, S, n)
