@@ -693,6 +693,12 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
      : tuning().block8 == 128 ? RSAMD_V1(KB, KFIX, MC, ACC, WIN, 2, 128, "8B,128 lanes")             \
                                  : RSAMD_V1(KB, KFIX, MC, ACC, WIN, 2, 256, "8B"))
 
+// 5-8 output rows: VALU-bound, and 16-byte lane units amortise each column's
+// 40-dword LDS table over twice the data of 8-byte units (10+8 Encode @ 1 MiB:
+// 5.29 TB/s vs 4.60 with 8-byte units and 4.43 with the looped kernel,
+// profiles/r01/ab_rows8.log).  rs_tune("lane_bytes", 8) does not apply here.
+#define RSAMD_VARIANT1_WIDE(KB, KFIX, MC, ACC, WIN) RSAMD_V1(KB, KFIX, MC, ACC, WIN, 4, 256, "16B")
+
 // Loop-free one-chunk-per-workgroup kernels (the default launch: grid = all
 // chunks, rows <= MC).  A/B on MI355X, 10+4 @ 1 MiB x 256 (tools/ab.py, 2 x 30
 // interleaved rounds): vec1 all-loads-up-front 0.589 ms, vec1 5-column window
@@ -704,15 +710,31 @@ static bool pick_one_chunk(int rows, int cols, bool acc, bool lane16, Variant* o
         if (cols == 12 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(12, true, 4, false, 0); return true; }
         if (cols == 10 && rows == 1) { *out = RSAMD_VARIANT1(10, true, 1, false, 0); return true; }
         if (cols == 10 && rows == 2) { *out = RSAMD_VARIANT1(10, true, 2, false, 0); return true; }
+        // 5-8 columns: one 8-column batch instead of two of 4 (all loads in
+        // flight at once; 8+4 Encode +6.6 %, 6+3 +7 %, 8+6 +11 %, Reconst
+        // +1.5-9.5 %, profiles/r01/ab_cols8.log).  var=200: also above 8.
+        if (cols > 4 && (cols <= 8 || tuning().var == 200)) {
+            if (rows == 1) { *out = RSAMD_VARIANT1(8, false, 1, false, 0); return true; }
+            if (rows == 2) { *out = RSAMD_VARIANT1(8, false, 2, false, 0); return true; }
+            if (rows <= 4) { *out = RSAMD_VARIANT1(8, false, 4, false, 0); return true; }
+        }
         if (rows == 1) { *out = RSAMD_VARIANT1(4, false, 1, false, 0); return true; }
         if (rows == 2) { *out = RSAMD_VARIANT1(4, false, 2, false, 0); return true; }
         if (rows <= 4) { *out = RSAMD_VARIANT1(4, false, 4, false, 0); return true; }
+        if (cols == 10 && rows <= 8) { *out = RSAMD_VARIANT1_WIDE(10, true, 8, false, 0); return true; }
+        if (cols == 12 && rows <= 8) { *out = RSAMD_VARIANT1_WIDE(12, true, 8, false, 0); return true; }
+        if (rows <= 8 && cols > 4 && (cols <= 8 || tuning().var == 200)) {
+            *out = RSAMD_VARIANT1_WIDE(8, false, 8, false, 0);
+            return true;
+        }
+        if (rows <= 8) { *out = RSAMD_VARIANT1_WIDE(4, false, 8, false, 0); return true; }
         return false;
     }
     if (cols == 2 && rows > 2 && rows <= 4) { *out = RSAMD_VARIANT1(2, true, 4, true, 0); return true; }
     if (rows == 1) { *out = RSAMD_VARIANT1(4, false, 1, true, 0); return true; }
     if (rows == 2) { *out = RSAMD_VARIANT1(4, false, 2, true, 0); return true; }
     if (rows <= 4) { *out = RSAMD_VARIANT1(4, false, 4, true, 0); return true; }
+    if (rows <= 8) { *out = RSAMD_VARIANT1_WIDE(4, false, 8, true, 0); return true; }
     return false;
 }
 
