@@ -318,7 +318,8 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * concurrent host calls of one shape share a launch; 0 = off),
  * "host_coalesce_linger_us" (a ready shared batch waits this long for more
  * callers before it launches; default 0),
- * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "bind_numa" (0/1),
+ * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
+ * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
  * "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name. */

@@ -324,7 +324,9 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
               size_t size, bool accumulate);
 
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
-extern int g_host_batch_zc, g_host_dma_1d, g_bind_numa;
+extern int g_host_batch_zc, g_host_dma_1d, g_bind_numa, g_host_pageable_stage;
+// dst[i] <- src[i] (n vectors, len bytes each) on the host copy pool (host_calls.cpp).
+void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t len);
 int bind_thread_to_device(int device);
 int host_device_range(const void* p, size_t bytes, uint8_t** dev);
 // Device address of [p, p+bytes) inside a range registered with

@@ -111,9 +111,100 @@ int g_host_batch_zc = 1;
 int g_host_dma_1d = 0;
 // Group worker threads bind to their GPU's local CPUs (bind_thread_to_device).
 int g_bind_numa = 1;
+// Pageable host batches with stripes up to 4 MiB are staged through the
+// pinned mirror (encode_pageable_batch); 0 = the DMA pipeline's 1-D copies.
+int g_host_pageable_stage = 1;
 
 }  // namespace detail
 }  // namespace rsamd
+
+// Pageable caller memory, stripes up to kPageableStripeMax bytes: staged
+// through the handle's pinned mirror (rs->hstage).  Chunks of stripes are
+// copied in by the host copy pool, encoded by one zero-copy kernel straight
+// out of the mirror, and their parity copied back, with 3 chunks in flight
+// (the copy-in of chunk c+1 overlaps chunk c's kernel).  The runtime's
+// pageable hipMemcpyAsync costs a staging round trip per copy (10+4 @ 8 KiB:
+// 4.2 GiB/s with one 1-D copy per stripe).  Caller holds stage_mu.
+constexpr size_t kPageableStripeMax = size_t{16} << 20;
+constexpr size_t kPageableSlot = size_t{8} << 20;
+
+static int encode_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len) {
+    const int d = rs->d, p = rs->p, nvec = d + p;
+    if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
+    if (rs->zc_pending) RS_TRY(hip_ok(hipStreamSynchronize(rs->stream), "host-call stream sync"));
+    const size_t pitch = rup(len, 256);
+    const size_t sbytes = pitch * static_cast<size_t>(nvec);
+    const int cs = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, kPageableSlot / sbytes)));
+    const int nch = (nstripes + cs - 1) / cs;
+    const int ns = nch > 1 ? 3 : 1;
+    const size_t slot = sbytes * static_cast<size_t>(cs);
+    if (slot * ns > rs->hstage_bytes) {
+        if (rs->hstage) (void)hipHostFree(rs->hstage);
+        rs->hstage = nullptr;
+        rs->hstage_bytes = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&rs->hstage), slot * ns, hipHostMallocDefault) != hipSuccess) {
+            rs->hstage = nullptr;
+            return RS_ERR_NOMEM;
+        }
+        rs->hstage_bytes = slot * ns;
+    }
+    void* dbase = nullptr;
+    RS_TRY(hip_ok(hipHostGetDevicePointer(&dbase, rs->hstage, 0), "mirror device pointer"));
+    if (!dbase) return dev_fail(hipErrorInvalidValue, "mirror device pointer");
+    for (int i = 0; i < ns; ++i)
+        if (!rs->chunk_ev[i] && hip_ok(hipEventCreateWithFlags(&rs->chunk_ev[i], hipEventDisableTiming), "event create")) {
+            rs->chunk_ev[i] = nullptr;
+            return RS_ERR_DEVICE;
+        }
+    std::vector<uint8_t*> cd(static_cast<size_t>(cs) * nvec);
+    std::vector<const uint8_t*> csrc(cd.size());
+    auto first = [&](int c) { return c * cs; };
+    auto count = [&](int c) { return std::min(cs, nstripes - c * cs); };
+    auto hslot = [&](int c) { return rs->hstage + static_cast<size_t>(c % ns) * slot; };
+    auto finish = [&](int c) -> int {  // wait for chunk c, copy its parity back
+        RS_TRY(hip_ok(hipEventSynchronize(rs->chunk_ev[c % ns]), "pageable batch chunk sync"));
+        int n = 0;
+        for (int t = 0; t < count(c); ++t) {
+            uint8_t* st = base + static_cast<int64_t>(first(c) + t) * ss;
+            for (int j = 0; j < p; ++j, ++n) {
+                cd[n] = st + (d + j) * vs;
+                csrc[n] = hslot(c) + static_cast<size_t>(t) * sbytes + static_cast<size_t>(d + j) * pitch;
+            }
+        }
+        parallel_copy(cd.data(), csrc.data(), n, len);
+        return RS_OK;
+    };
+    int rc = RS_OK;
+    int done = 0;
+    rs->zc_pending = true;
+    for (int c = 0; c < nch && rc == RS_OK; ++c) {
+        if (c >= ns) {
+            rc = finish(done++);
+            if (rc) break;
+        }
+        int n = 0;
+        for (int t = 0; t < count(c); ++t) {
+            const uint8_t* st = base + static_cast<int64_t>(first(c) + t) * ss;
+            for (int i = 0; i < d; ++i, ++n) {
+                cd[n] = hslot(c) + static_cast<size_t>(t) * sbytes + static_cast<size_t>(i) * pitch;
+                csrc[n] = st + i * vs;
+            }
+        }
+        parallel_copy(cd.data(), csrc.data(), n, len);
+        uint8_t* dslot = static_cast<uint8_t*>(dbase) + static_cast<size_t>(c % ns) * slot;
+        const uint8_t* in[kMaxVects];
+        uint8_t* out[kMaxVects];
+        for (int i = 0; i < d; ++i) in[i] = dslot + static_cast<size_t>(i) * pitch;
+        for (int j = 0; j < p; ++j) out[j] = dslot + static_cast<size_t>(d + j) * pitch;
+        rc = matmul(rs, rs->gen(), p, d, in, static_cast<int64_t>(sbytes), out, static_cast<int64_t>(sbytes), count(c),
+                    len, false, rs->stream);
+        if (rc == RS_OK) rc = hip_ok(hipEventRecord(rs->chunk_ev[c % ns], rs->stream), "pageable batch chunk record");
+    }
+    while (rc == RS_OK && done < nch) rc = finish(done++);
+    if (rc) (void)hipStreamSynchronize(rs->stream);  // never leave a kernel on the mirror
+    rs->zc_pending = false;
+    return rc;
+}
 
 extern "C" {
 
@@ -179,8 +270,9 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
         DeviceGuard g(rs->device);
         const int d = rs->d, p = rs->p;
         uint8_t* zc = nullptr;
-        if (g_host_batch_zc &&
-            host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) == RS_OK) {
+        const bool pinned =
+            host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) == RS_OK;
+        if (g_host_batch_zc && pinned) {
             // pinned / registered caller memory: one launch straight over it
             std::lock_guard<std::mutex> lk(rs->stage_mu);
             if (!rs->stream)
@@ -194,8 +286,19 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             const int sync_rc = hip_ok(hipStreamSynchronize(rs->stream), "host-batch sync");
             return rc ? rc : sync_rc;
         }
+        if (!pinned && g_host_pageable_stage && rup(len, 256) * static_cast<size_t>(d + p) <= kPageableStripeMax) {
+            std::lock_guard<std::mutex> lk(rs->stage_mu);
+            return encode_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len);
+        }
         // [S][d+p][len] with 256-B-multiple len: data and parity of a stripe are contiguous rows
         const bool dense = vect_stride == static_cast<int64_t>(len) && len % 256 == 0;
+        // Pageable memory takes 1-D copies only: a 2-D (rectangle) copy from
+        // pageable memory with unaligned widths / pitches (8,195-byte vectors)
+        // faulted inside the runtime's copy (hipErrorIllegalAddress at the
+        // stream sync, intermittently, tests/test_gpu_parity.py
+        // test_encode_host_batch_pipeline); pinned memory keeps the 2-D
+        // copies (70.4-70.7 vs 66.8-67.1 GiB/s, tools/dma_ab.py).
+        const bool rect = pinned && !g_host_dma_1d;
         const size_t pitch = dense ? len : rup(len, 256);
         const int64_t dstripe = static_cast<int64_t>(pitch) * (d + p);
         const size_t slot_bytes = static_cast<size_t>(dstripe) * stripes_per_chunk;
@@ -244,7 +347,7 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             uint8_t* dev = ring + static_cast<size_t>(slot) * slot_bytes;
             uint8_t* hb = base + static_cast<int64_t>(c0) * stripe_stride;
             if (chunk >= slots && !ok(hipStreamWaitEvent(sh, ev_free[slot], 0))) break;
-            if (dense && g_host_dma_1d) {  // cn 1-D copies of d*len bytes
+            if (dense && !rect) {  // cn 1-D copies of d*len bytes
                 bool good = true;
                 for (int s = 0; s < cn && good; ++s)
                     good = ok(hipMemcpyAsync(dev + static_cast<int64_t>(s) * dstripe, hb + s * stripe_stride,
@@ -254,11 +357,20 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
                 if (!ok(hipMemcpy2DAsync(dev, dstripe, hb, stripe_stride, static_cast<size_t>(d) * len, cn,
                                          hipMemcpyHostToDevice, sh)))
                     break;
+            } else if (!rect) {  // cn * d 1-D copies of len bytes
+                bool good = true;
+                for (int s = 0; s < cn && good; ++s)
+                    for (int i = 0; i < d && good; ++i)
+                        good = ok(hipMemcpyAsync(dev + static_cast<int64_t>(s) * dstripe + i * pitch,
+                                                 hb + s * stripe_stride + i * vect_stride, len, hipMemcpyHostToDevice,
+                                                 sh));
+                if (!good) break;
             } else {
-                for (int i = 0; i < d; ++i)
-                    if (!ok(hipMemcpy2DAsync(dev + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len, cn,
-                                             hipMemcpyHostToDevice, sh)))
-                        break;
+                bool good = true;
+                for (int i = 0; i < d && good; ++i)
+                    good = ok(hipMemcpy2DAsync(dev + i * pitch, dstripe, hb + i * vect_stride, stripe_stride, len,
+                                               cn, hipMemcpyHostToDevice, sh));
+                if (!good) break;
             }
             if (!ok(hipEventRecord(ev_in[slot], sh)) || !ok(hipStreamWaitEvent(sc, ev_in[slot], 0))) break;
             for (int i = 0; i < d; ++i) in[i] = dev + i * pitch;
@@ -266,7 +378,7 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             rc = matmul(rs, rs->gen(), p, d, in, dstripe, out, dstripe, cn, len, false, sc);
             if (rc) break;
             if (!ok(hipEventRecord(ev_enc[slot], sc)) || !ok(hipStreamWaitEvent(sd, ev_enc[slot], 0))) break;
-            if (dense && g_host_dma_1d) {
+            if (dense && !rect) {
                 bool good = true;
                 for (int s = 0; s < cn && good; ++s)
                     good = ok(hipMemcpyAsync(hb + s * stripe_stride + d * vect_stride,
@@ -277,11 +389,20 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
                 if (!ok(hipMemcpy2DAsync(hb + d * vect_stride, stripe_stride, dev + d * pitch, dstripe,
                                          static_cast<size_t>(p) * len, cn, hipMemcpyDeviceToHost, sd)))
                     break;
+            } else if (!rect) {
+                bool good = true;
+                for (int s = 0; s < cn && good; ++s)
+                    for (int j = 0; j < p && good; ++j)
+                        good = ok(hipMemcpyAsync(hb + s * stripe_stride + (d + j) * vect_stride,
+                                                 dev + static_cast<int64_t>(s) * dstripe + (d + j) * pitch, len,
+                                                 hipMemcpyDeviceToHost, sd));
+                if (!good) break;
             } else {
-                for (int j = 0; j < p; ++j)
-                    if (!ok(hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, dev + (d + j) * pitch, dstripe,
-                                             len, cn, hipMemcpyDeviceToHost, sd)))
-                        break;
+                bool good = true;
+                for (int j = 0; j < p && good; ++j)
+                    good = ok(hipMemcpy2DAsync(hb + (d + j) * vect_stride, stripe_stride, dev + (d + j) * pitch,
+                                               dstripe, len, cn, hipMemcpyDeviceToHost, sd));
+                if (!good) break;
             }
             if (!ok(hipEventRecord(ev_free[slot], sd))) break;
         }

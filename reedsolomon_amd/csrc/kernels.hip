@@ -713,13 +713,21 @@ static bool pick_one_chunk(int rows, int cols, bool acc, bool lane16, Variant* o
         // 5-8 columns: one 8-column batch instead of two of 4 (all loads in
         // flight at once; 8+4 Encode +6.6 %, 6+3 +7 %, 8+6 +11 %, Reconst
         // +1.5-9.5 %, profiles/r01/ab_cols8.log).  var=200: also above 8.
+        // 3-4 rows over more than 4 runtime columns: 16-byte units (8+3
+        // Encode +6 %, 6+3 +7 %, 16+3 +7.7 %, 16+4 +8 %, 20+4 +5.6 %, 8+4 +3 %;
+        // the fixed-column 10 / 12 kernels, 1-2 rows and accumulate launches
+        // stay on 8-byte units, profiles/r01/ab_lane_generic*.log).  var=201
+        // keeps 8-byte units (A/B).
+        const bool wide34 = rows > 2 && rows <= 4 && cols > 4 && tuning().var != 201;
         if (cols > 4 && (cols <= 8 || tuning().var == 200)) {
             if (rows == 1) { *out = RSAMD_VARIANT1(8, false, 1, false, 0); return true; }
             if (rows == 2) { *out = RSAMD_VARIANT1(8, false, 2, false, 0); return true; }
+            if (wide34) { *out = RSAMD_VARIANT1_WIDE(8, false, 4, false, 0); return true; }
             if (rows <= 4) { *out = RSAMD_VARIANT1(8, false, 4, false, 0); return true; }
         }
         if (rows == 1) { *out = RSAMD_VARIANT1(4, false, 1, false, 0); return true; }
         if (rows == 2) { *out = RSAMD_VARIANT1(4, false, 2, false, 0); return true; }
+        if (wide34) { *out = RSAMD_VARIANT1_WIDE(4, false, 4, false, 0); return true; }
         if (rows <= 4) { *out = RSAMD_VARIANT1(4, false, 4, false, 0); return true; }
         if (cols == 10 && rows <= 8) { *out = RSAMD_VARIANT1_WIDE(10, true, 8, false, 0); return true; }
         if (cols == 12 && rows <= 8) { *out = RSAMD_VARIANT1_WIDE(12, true, 8, false, 0); return true; }

@@ -621,14 +621,22 @@ def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
         host = _rand(rng, S, d + p, n)
         exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
         a = host.copy()
-        r.encode_host_batch(a, spc, st)  # pageable: DMA pipeline
+        r.encode_host_batch(a, spc, st)  # pageable: staged through the pinned mirror
         assert np.array_equal(a[:, d:], exp), ("pageable parity", S, n, _first_diff(a[:, d:], exp))
         assert np.array_equal(a[:, :d], host[:, :d]), ("pageable data", S, n)
+        L = rslib.lib()
+        assert L.rs_tune(b"host_pageable_stage", 0) == 0
+        try:
+            a = host.copy()
+            r.encode_host_batch(a, spc, st)  # pageable: DMA pipeline, 1-D copies
+            assert np.array_equal(a[:, d:], exp), ("pageable DMA parity", S, n, _first_diff(a[:, d:], exp))
+            assert np.array_equal(a[:, :d], host[:, :d]), ("pageable DMA data", S, n)
+        finally:
+            L.rs_tune(b"host_pageable_stage", 1)
         pinned = torch.from_numpy(host.copy()).pin_memory()
         r.encode_host_batch(pinned, spc, st)  # zero-copy: kernels straight over pinned memory
         got = pinned.numpy()[:, d:]
         assert np.array_equal(got, exp), ("zero-copy parity", S, n, _first_diff(got, exp))
-        L = rslib.lib()
         assert L.rs_tune(b"host_batch_zc", 0) == 0
         try:
             pinned = torch.from_numpy(host.copy()).pin_memory()

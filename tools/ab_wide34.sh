@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+# A/B: generic 3-4-row Encode on 16-byte units (default) vs 8-byte units (var=201).
+set -e
+for km in "8 4" "6 3" "16 4" "8 3" "20 4" "5 4" "9 3"; do
+  set -- $km
+  echo "== $1+$2 encode"
+  AB_K=$1 AB_M=$2 AB_ROUNDS=8 timeout -k 10 200 python -u tools/ab.py "" "var=201"
+done
