@@ -774,9 +774,10 @@ static Variant pick(int rows, int cols, bool acc, int vpt, uint64_t body, bool l
 // A/B on MI355X (tools/ab.py AB_VEC=..., profiles/r01/ab_lane_size_sweep.log):
 // with 256-lane workgroups the 16-byte build won 3-4-output launches on
 // vectors <= 32 KiB and interleaved Encode up to 256 KiB; with the 8-byte
-// build on 128-lane workgroups, 8-byte units win every size and shape tried
-// (8 KiB split Encode 6.65 vs 6.30 TB/s, interleaved 6.42 vs 5.78, Reconst
-// of 4 6.46 vs 6.05; 32 KiB-1 MiB: +0-8 %).
+// build on 128-lane workgroups, 8-byte units win every size and shape of the
+// 10-column kernels (8 KiB split Encode 6.65 vs 6.30 TB/s, interleaved 6.42
+// vs 5.78, Reconst of 4 6.46 vs 6.05; 32 KiB-1 MiB: +0-8 %).  Runtime-column
+// launches with 3-8 rows pick 16-byte units themselves (pick_one_chunk).
 static bool lane16_for(const MatmulArgs&) { return tuning().lane_bytes == 16; }
 
 const char* vector_kernel_name(int rows, int cols, int accumulate) {
