@@ -10,6 +10,8 @@ ones the coalesced path, large ones the chunked pipeline).  Device batches:
 split-layout Encode and per-stripe-pattern Reconst on random shapes and
 stripe counts, every stripe checked against the oracle.
 """
+import threading
+
 import numpy as np
 import pytest
 
@@ -291,3 +293,63 @@ def test_host_batch_random_sweep(rslib, orc, torch_dev):
                 buf[s, int(v)].fill_(0x3C)
         r.reconst_host_batch_multi(buf, masks)
         assert np.array_equal(buf.numpy(), host), (case, "reconst", d, p, S, n)
+
+
+def test_concurrent_random_host_calls(rslib, orc, torch_dev):
+    """8 threads of random host calls (Encode / Reconst / Update / Replace,
+    sizes on both sides of the coalescing and chunking thresholds) on ONE
+    handle: every result equals the oracle's (re-encoding for Update /
+    Replace) for that call made alone."""
+    d, p = 10, 4
+    r = rslib.New(d, p)
+    errors = []
+    barrier = threading.Barrier(8)
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(5000 + t)
+            barrier.wait()
+            for it in range(15):
+                size = int(rng.choice([100, 4096, 8197, 70000, 200000]))
+                data = [_rand(rng, size) for _ in range(d)]
+                enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, enc) == 0
+                op = int(rng.integers(4))
+                if op == 0:
+                    v = [x.copy() for x in data] + [np.full(size, 0x5A, np.uint8) for _ in range(p)]
+                    r.Encode(v)
+                    ok = all(np.array_equal(v[d + j], enc[d + j]) for j in range(p))
+                elif op == 1:
+                    lost = sorted(int(x) for x in rng.choice(d + p, int(rng.integers(1, p + 1)), replace=False))
+                    v = [x.copy() for x in enc]
+                    for i in lost:
+                        v[i][:] = 0
+                    r.Reconst(v, [], lost)
+                    ok = all(np.array_equal(v[i], enc[i]) for i in lost)
+                else:
+                    exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                    par = [x.copy() for x in enc[d:]]
+                    if op == 2:
+                        row = int(rng.integers(d))
+                        new = _rand(rng, size)
+                        r.Update(data[row], new, row, par)
+                        exp[row] = new
+                    else:
+                        rows = [int(x) for x in rng.choice(d, int(rng.integers(1, 4)), replace=False)]
+                        delta = [_rand(rng, size) for _ in rows]
+                        r.Replace(delta, rows, par)
+                        for k_, rr in enumerate(rows):
+                            exp[rr] = np.bitwise_xor(exp[rr], delta[k_])
+                    assert orc.encode(d, p, exp) == 0
+                    ok = all(np.array_equal(par[j], exp[d + j]) for j in range(p))
+                if not ok:
+                    errors.append((t, it, op, size))
+        except Exception as e:  # pragma: no cover
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:10]
