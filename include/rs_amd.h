@@ -245,9 +245,12 @@ RS_API int rs_host_device_pointer(const void* host_ptr, size_t bytes, void** dev
 
 /* Reconst of a host-resident batch, a different erasure set per stripe
  * (need_masks as in rs_reconst_batch_multi): stripe s, vector v at
- * base + s*stripe_stride + v*vect_stride (data 0..d-1, then parity).  The
- * memory must be pinned / registered (zero-copy; RS_ERR_INVAL otherwise).
- * Synchronous. */
+ * base + s*stripe_stride + v*vect_stride (data 0..d-1, then parity).
+ * Pinned / registered memory is processed in place (zero-copy); pageable
+ * memory with stripes up to 16 MiB is staged through a pinned mirror (the
+ * first d survivors in, the rebuilt vectors out); larger pageable stripes,
+ * or rs_tune("host_pageable_stage", 0), give RS_ERR_INVAL.  Every mask is
+ * validated before anything is copied or launched.  Synchronous. */
 RS_API int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                        int nstripes, size_t len, const uint64_t* need_masks);
 RS_API int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stripe_stride,

@@ -120,16 +120,21 @@ int g_host_pageable_stage = 1;
 
 // Pageable caller memory, stripes up to kPageableStripeMax bytes: staged
 // through the handle's pinned mirror (rs->hstage).  Chunks of stripes are
-// copied in by the host copy pool, encoded by one zero-copy kernel straight
-// out of the mirror, and their parity copied back, with 3 chunks in flight
+// copied in by the host copy pool, processed by one zero-copy launch straight
+// out of the mirror, and their outputs copied back, with 3 chunks in flight
 // (the copy-in of chunk c+1 overlaps chunk c's kernel).  The runtime's
 // pageable hipMemcpyAsync costs a staging round trip per copy (10+4 @ 8 KiB:
-// 4.2 GiB/s with one 1-D copy per stripe).  Caller holds stage_mu.
+// 4.2 GiB/s with one 1-D copy per stripe).  A mirror stripe is [d+p][pitch].
+// rows_in(s, add) / rows_out(s, add) name the vectors of stripe s to copy in
+// / out (add(v) per vector index); launch(first, count, dev_slot, stripe
+// bytes, pitch) enqueues the kernel on rs->stream.  Caller holds stage_mu.
 constexpr size_t kPageableStripeMax = size_t{16} << 20;
 constexpr size_t kPageableSlot = size_t{8} << 20;
 
-static int encode_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len) {
-    const int d = rs->d, p = rs->p, nvec = d + p;
+template <class RowsIn, class RowsOut, class Launch>
+static int pageable_pipeline(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len,
+                             RowsIn rows_in, RowsOut rows_out, Launch launch) {
+    const int nvec = rs->d + rs->p;
     if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
     if (rs->zc_pending) RS_TRY(hip_ok(hipStreamSynchronize(rs->stream), "host-call stream sync"));
     const size_t pitch = rup(len, 256);
@@ -158,18 +163,18 @@ static int encode_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs
         }
     std::vector<uint8_t*> cd(static_cast<size_t>(cs) * nvec);
     std::vector<const uint8_t*> csrc(cd.size());
-    auto first = [&](int c) { return c * cs; };
     auto count = [&](int c) { return std::min(cs, nstripes - c * cs); };
     auto hslot = [&](int c) { return rs->hstage + static_cast<size_t>(c % ns) * slot; };
-    auto finish = [&](int c) -> int {  // wait for chunk c, copy its parity back
+    auto finish = [&](int c) -> int {  // wait for chunk c, copy its outputs back
         RS_TRY(hip_ok(hipEventSynchronize(rs->chunk_ev[c % ns]), "pageable batch chunk sync"));
         int n = 0;
         for (int t = 0; t < count(c); ++t) {
-            uint8_t* st = base + static_cast<int64_t>(first(c) + t) * ss;
-            for (int j = 0; j < p; ++j, ++n) {
-                cd[n] = st + (d + j) * vs;
-                csrc[n] = hslot(c) + static_cast<size_t>(t) * sbytes + static_cast<size_t>(d + j) * pitch;
-            }
+            uint8_t* st = base + static_cast<int64_t>(c * cs + t) * ss;
+            const uint8_t* h = hslot(c) + static_cast<size_t>(t) * sbytes;
+            rows_out(c * cs + t, [&](int v) {
+                cd[n] = st + v * vs;
+                csrc[n++] = h + static_cast<size_t>(v) * pitch;
+            });
         }
         parallel_copy(cd.data(), csrc.data(), n, len);
         return RS_OK;
@@ -184,26 +189,81 @@ static int encode_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs
         }
         int n = 0;
         for (int t = 0; t < count(c); ++t) {
-            const uint8_t* st = base + static_cast<int64_t>(first(c) + t) * ss;
-            for (int i = 0; i < d; ++i, ++n) {
-                cd[n] = hslot(c) + static_cast<size_t>(t) * sbytes + static_cast<size_t>(i) * pitch;
-                csrc[n] = st + i * vs;
-            }
+            const uint8_t* st = base + static_cast<int64_t>(c * cs + t) * ss;
+            uint8_t* h = hslot(c) + static_cast<size_t>(t) * sbytes;
+            rows_in(c * cs + t, [&](int v) {
+                cd[n] = h + static_cast<size_t>(v) * pitch;
+                csrc[n++] = st + v * vs;
+            });
         }
         parallel_copy(cd.data(), csrc.data(), n, len);
-        uint8_t* dslot = static_cast<uint8_t*>(dbase) + static_cast<size_t>(c % ns) * slot;
-        const uint8_t* in[kMaxVects];
-        uint8_t* out[kMaxVects];
-        for (int i = 0; i < d; ++i) in[i] = dslot + static_cast<size_t>(i) * pitch;
-        for (int j = 0; j < p; ++j) out[j] = dslot + static_cast<size_t>(d + j) * pitch;
-        rc = matmul(rs, rs->gen(), p, d, in, static_cast<int64_t>(sbytes), out, static_cast<int64_t>(sbytes), count(c),
-                    len, false, rs->stream);
+        rc = launch(c * cs, count(c), static_cast<uint8_t*>(dbase) + static_cast<size_t>(c % ns) * slot, sbytes,
+                    pitch);
         if (rc == RS_OK) rc = hip_ok(hipEventRecord(rs->chunk_ev[c % ns], rs->stream), "pageable batch chunk record");
     }
     while (rc == RS_OK && done < nch) rc = finish(done++);
     if (rc) (void)hipStreamSynchronize(rs->stream);  // never leave a kernel on the mirror
     rs->zc_pending = false;
     return rc;
+}
+
+// Encode of a pageable batch: data vectors in, parity out.
+static int encode_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len) {
+    const int d = rs->d, p = rs->p;
+    return pageable_pipeline(
+        rs, base, ss, vs, nstripes, len,
+        [&](int, auto add) { for (int i = 0; i < d; ++i) add(i); },
+        [&](int, auto add) { for (int j = 0; j < p; ++j) add(d + j); },
+        [&](int, int n, uint8_t* dslot, size_t sbytes, size_t pitch) {
+            const uint8_t* in[kMaxVects];
+            uint8_t* out[kMaxVects];
+            for (int i = 0; i < d; ++i) in[i] = dslot + static_cast<size_t>(i) * pitch;
+            for (int j = 0; j < p; ++j) out[j] = dslot + static_cast<size_t>(d + j) * pitch;
+            return matmul(rs, rs->gen(), p, d, in, static_cast<int64_t>(sbytes), out, static_cast<int64_t>(sbytes), n,
+                          len, false, rs->stream);
+        });
+}
+
+// The errors rs_reconst_batch_multi would return for these masks, before
+// anything is copied or launched.
+static int check_masks(int d, int p, const uint64_t* masks, int nstripes) {
+    const int nvec = d + p;
+    if (nvec > 64) return RS_ERR_INVAL;
+    const uint64_t valid = nvec == 64 ? ~uint64_t{0} : ((uint64_t{1} << nvec) - 1);
+    for (int s = 0; s < nstripes; ++s) {
+        if (masks[s] & ~valid) return RS_ERR_ILLEGAL_VECTS;
+        if (__builtin_popcountll(masks[s]) > p) return RS_ERR_TOO_MANY_LOST;
+    }
+    return RS_OK;
+}
+
+// Multi-pattern Reconst of a pageable batch: the first d survivors of every
+// stripe with work in, the lost vectors (rebuilt in the mirror) out.  Masks
+// are validated before any copy or launch.
+static int reconst_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len,
+                                  const uint64_t* masks) {
+    const int d = rs->d, p = rs->p, nvec = d + p;
+    RS_TRY(check_masks(d, p, masks, nstripes));
+    return pageable_pipeline(
+        rs, base, ss, vs, nstripes, len,
+        [&](int s, auto add) {  // the first d survivors: all the kernel reads (rs.go's choice)
+            if (!masks[s]) return;
+            for (int v = 0, n = 0; v < nvec && n < d; ++v)
+                if (!(masks[s] >> v & 1)) {
+                    add(v);
+                    ++n;
+                }
+        },
+        [&](int s, auto add) {
+            for (int v = 0; v < nvec; ++v)
+                if (masks[s] >> v & 1) add(v);
+        },
+        [&](int first, int n, uint8_t* dslot, size_t sbytes, size_t pitch) {
+            const rs_layout_t L{dslot, static_cast<int64_t>(sbytes), static_cast<int64_t>(pitch),
+                                dslot + static_cast<size_t>(d) * pitch, static_cast<int64_t>(sbytes),
+                                static_cast<int64_t>(pitch)};
+            return rs_reconst_batch_multi(rs, &L, n, len, masks + first, rs->stream);
+        });
 }
 
 extern "C" {
@@ -497,7 +557,13 @@ int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, 
         DeviceGuard g(rs->device);
         const int d = rs->d, p = rs->p;
         uint8_t* zc = nullptr;
-        RS_TRY(host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc));
+        if (host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) != RS_OK) {
+            // pageable memory: staged through the pinned mirror
+            if (!g_host_pageable_stage || rup(len, 256) * static_cast<size_t>(d + p) > kPageableStripeMax)
+                return RS_ERR_INVAL;
+            std::lock_guard<std::mutex> lk(rs->stage_mu);
+            return reconst_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len, need_masks);
+        }
         rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
                       vect_stride};
         std::lock_guard<std::mutex> lk(rs->stage_mu);
@@ -513,6 +579,8 @@ int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stri
     return abi_guard([&]() -> int {
         if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
         if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+        // every slice's masks checked before any member starts (no partial batch)
+        RS_TRY(check_masks(g->members[0]->d, g->members[0]->p, need_masks, nstripes));
         const int n = static_cast<int>(g->members.size());
         std::vector<int> rc(n, RS_OK);
         std::vector<std::thread> th;

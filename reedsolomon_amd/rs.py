@@ -337,8 +337,9 @@ class RS:
                                           int(streams)))
 
     def reconst_host_batch_multi(self, buf, need_masks) -> None:
-        """Reconst a pinned host batch [S, d+p, len] in place, need_masks[s] =
-        bitmap of the vectors of stripe s to rebuild (zero-copy kernels)."""
+        """Reconst a host batch [S, d+p, len] in place, need_masks[s] = bitmap of
+        the vectors of stripe s to rebuild (zero-copy kernels over pinned
+        memory; pageable memory is staged through a pinned mirror)."""
         ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
         masks = _masks(need_masks, S)
         _check(lib().rs_reconst_host_batch_multi(self._h, ctypes.c_void_p(ptr), ss, vs, S, n,

@@ -649,8 +649,9 @@ def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
 
 def test_host_batch_zero_copy(rslib, orc, torch_dev):
     """Zero-copy host batches: registered numpy memory (rs_host_register),
-    multi-pattern Reconst in place on pinned memory (single and group), and
-    a clean RS_ERR_INVAL (no kernel) for pageable memory."""
+    multi-pattern Reconst in place on pinned and on pageable memory (single
+    and group), mask validation before any copy, and a clean RS_ERR_INVAL (no
+    kernel) for pageable memory with staging off."""
     torch = torch_dev
     d, p, S, n = 10, 4, 33, 8192 + 16
     r = rslib.New(d, p)
@@ -684,9 +685,28 @@ def test_host_batch_zero_copy(rslib, orc, torch_dev):
     pinned = torch.from_numpy(broken.copy()).pin_memory()
     rslib.NewGroup(d, p, [0, 0]).reconst_host_batch_multi(pinned, masks)
     assert np.array_equal(pinned.numpy(), full)
+    # pageable memory: staged through the pinned mirror (single and group)
     pageable = broken.copy()
-    with pytest.raises(rslib.ErrInvalidArgument):
-        r.reconst_host_batch_multi(pageable, masks)
+    r.reconst_host_batch_multi(pageable, masks)
+    assert np.array_equal(pageable, full)
+    pageable = broken.copy()
+    rslib.NewGroup(d, p, [0, 0]).reconst_host_batch_multi(pageable, masks)
+    assert np.array_equal(pageable, full)
+    # a 5-erasure stripe is rejected before anything is copied or launched
+    bad = masks.copy()
+    bad[S - 1] = np.uint64(0b11111)
+    pageable = broken.copy()
+    with pytest.raises(rslib.ErrTooManyLost):
+        r.reconst_host_batch_multi(pageable, bad)
+    assert np.array_equal(pageable, broken)
+    # staging off: a clean RS_ERR_INVAL (no kernel) for pageable memory
+    L = rslib.lib()
+    assert L.rs_tune(b"host_pageable_stage", 0) == 0
+    try:
+        with pytest.raises(rslib.ErrInvalidArgument):
+            r.reconst_host_batch_multi(pageable, masks)
+    finally:
+        L.rs_tune(b"host_pageable_stage", 1)
     with pytest.raises(rslib.ErrInvalidArgument):
         rslib.host_device_pointer(pageable.ctypes.data, pageable.nbytes)
     assert np.array_equal(pageable, broken)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""rs_encode_host_batch on PAGEABLE numpy memory (the DMA pipeline's 1-D copy
-path): GiB/s of (k+m)*vec, 10+4, dense and padded layouts."""
+"""rs_encode_host_batch / rs_reconst_host_batch_multi on PAGEABLE numpy
+memory (staged through the pinned mirror up to 16 MiB stripes, the DMA
+pipeline's 1-D copies above): GiB/s, 10+4, dense and padded layouts."""
 import os
 import sys
 import time
@@ -27,6 +28,17 @@ def main():
             r.encode_host_batch(buf, 8, 3)
         dt = (time.perf_counter() - t0) / reps
         print(f"pageable {vec} B x {S} pad {pad}: {S * 14 * vec / dt / 2**30:.1f} GiB/s", flush=True)
+        # multi-pattern Reconst, 16 patterns of 1-4 erasures, (k + lost) * vec per stripe
+        rng = np.random.default_rng(5)
+        pats = [sum(1 << int(v) for v in rng.choice(14, int(rng.integers(1, 5)), replace=False)) for _ in range(16)]
+        masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
+        nrec = sum(bin(int(x)).count("1") for x in masks)
+        r.reconst_host_batch_multi(buf, masks)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r.reconst_host_batch_multi(buf, masks)
+        dt = (time.perf_counter() - t0) / reps
+        print(f"  reconst 16 patterns: {(S * 10 + nrec) * vec / dt / 2**30:.1f} GiB/s", flush=True)
 
 
 if __name__ == "__main__":
