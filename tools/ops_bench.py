@@ -53,6 +53,14 @@ def main():
         t = dev_time(lambda: r.encode_batch(buf))
         rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
         del buf
+    # ---- other shapes (runtime-column kernels; 5-8 rows are VALU-bound)
+    for k, m in ((8, 4), (6, 3), (16, 4), (10, 6), (10, 8), (12, 8)):
+        vec, S = 1 << 20, 256 * 14 // (k + m)
+        r = rs.New(k, m)
+        buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+        t = dev_time(lambda: r.encode_batch(buf))
+        rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
+        del buf
     # ---- reconst 10+4 @ 8 KiB, 1-4 lost data shards (config 3)
     k, m, vec, S = 10, 4, 8 << 10, 32768
     r = rs.New(k, m)
@@ -110,6 +118,16 @@ def main():
         t = (time.perf_counter() - t0) / reps
         rec(f"encode 10+4 1MiB x{S} host->host pinned, DMA pipeline spc={spc} streams={nst}", S * (k + m) * vec, t)
     L.rs_tune(b"host_batch_zc", 1)
+    # pageable (ordinary) host memory: staged through the pinned mirror
+    for pv, pS in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64)):
+        pg = np.random.default_rng(3).integers(0, 256, (pS, k + m, pv), dtype=np.uint8)
+        r.encode_host_batch(pg)  # warm
+        t0 = time.perf_counter()
+        for _ in range(3):
+            r.encode_host_batch(pg)
+        rec(f"encode 10+4 {pv >> 10}KiB x{pS} host->host pageable (staged)", pS * (k + m) * pv,
+            (time.perf_counter() - t0) / 3)
+        del pg
     # PCIe reference rates (one direction at a time, then both at once)
     dbuf = torch.empty((S * k * vec,), dtype=torch.uint8, device="cuda")
     hflat = host.view(-1)[: S * k * vec]
