@@ -353,3 +353,58 @@ def test_concurrent_random_host_calls(rslib, orc, torch_dev):
     for t in ts:
         t.join()
     assert not errors, errors[:10]
+
+
+def test_device_single_stripe_random_sweep(rslib, orc, torch_dev):
+    """rs_*_dev on vectors at random byte offsets inside one device buffer
+    (Go slices start anywhere): Encode / Reconst / Update / Replace against
+    the oracle (re-encoding for Update / Replace)."""
+    torch = torch_dev
+    rng = np.random.default_rng(93)
+    for case in range(40):
+        d = int(rng.integers(1, 21))
+        p = int(rng.integers(1, 9))
+        size = int(rng.choice([1, 5, 16, 33, 1000, 4096, 4099, 65536 + 48, 200003]))
+        r = rslib.New(d, p)
+        gap = int(rng.integers(0, 40))
+        start = int(rng.integers(0, 16))
+        big = torch.from_numpy(_rand(rng, start + (d + p) * (size + gap))).cuda()
+        vecs = [big[start + i * (size + gap): start + i * (size + gap) + size] for i in range(d + p)]
+        data = [v.cpu().numpy().copy() for v in vecs[:d]]
+        enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+        assert orc.encode(d, p, enc) == 0
+        r.encode_dev(vecs)
+        torch.cuda.synchronize()
+        tag = (case, d, p, size, gap, start)
+        for j in range(p):
+            assert np.array_equal(vecs[d + j].cpu().numpy(), enc[d + j]), tag + ("encode", j)
+        op = case % 3
+        if op == 0:
+            lost = sorted(int(v) for v in rng.choice(d + p, int(rng.integers(1, p + 1)), replace=False))
+            for v in lost:
+                vecs[v].fill_(0x77)
+            r.reconst_dev(vecs, [], lost)
+            torch.cuda.synchronize()
+            for v in lost:
+                assert np.array_equal(vecs[v].cpu().numpy(), enc[v]), tag + ("reconst", v)
+        elif op == 1:
+            row = int(rng.integers(d))
+            new = torch.from_numpy(_rand(rng, size)).cuda()
+            r.update_dev(vecs[row], new, row, vecs[d:])
+            torch.cuda.synchronize()
+            exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            exp[row] = new.cpu().numpy()
+            assert orc.encode(d, p, exp) == 0
+            for j in range(p):
+                assert np.array_equal(vecs[d + j].cpu().numpy(), exp[d + j]), tag + ("update", j)
+        else:
+            rows = [int(v) for v in rng.choice(d, int(rng.integers(1, d + 1)), replace=False)]
+            delta = [torch.from_numpy(_rand(rng, size)).cuda() for _ in rows]
+            r.replace_dev(delta, rows, vecs[d:])
+            torch.cuda.synchronize()
+            exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            for k_, rr in enumerate(rows):
+                exp[rr] = np.bitwise_xor(exp[rr], delta[k_].cpu().numpy())
+            assert orc.encode(d, p, exp) == 0
+            for j in range(p):
+                assert np.array_equal(vecs[d + j].cpu().numpy(), exp[d + j]), tag + ("replace", j)
