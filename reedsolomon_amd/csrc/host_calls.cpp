@@ -117,7 +117,8 @@ size_t g_chunk = 128 * 1024;
 constexpr size_t kParallelCopyMin = 512 * 1024;
 
 // dst[i] <- src[i] (n vectors, len bytes each) on the copy pool, in
-// 64 KiB pieces so every thread gets work.
+// 64 KiB pieces so every thread gets work; on the calling thread alone when
+// the pool is busy with another caller's copies.
 void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t len) {
     const size_t piece = 64 * 1024;
     const size_t per = (len + piece - 1) / piece;
@@ -126,7 +127,7 @@ void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t
         for (int i = 0; i < n; ++i) std::memcpy(dst[i], src[i], len);
         return;
     }
-    CopyPool::get().run(total, [&](size_t k) {
+    CopyPool::get().run_or_inline(total, [&](size_t k) {
         const size_t v = k / per, off = (k % per) * piece;
         const size_t b = std::min(piece, len - off);
         std::memcpy(dst[v] + off, src[v] + off, b);

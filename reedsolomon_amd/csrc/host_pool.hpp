@@ -33,6 +33,32 @@ public:
             return;
         }
         std::lock_guard<std::mutex> one(run_mu_);
+        run_locked(n, fn);
+    }
+
+    // run() if the pool is idle; otherwise fn(i) for every i on the calling
+    // thread alone (concurrent callers - device-group workers, several host
+    // calls - copy in parallel on their own threads instead of queueing).
+    void run_or_inline(size_t n, const std::function<void(size_t)>& fn) {
+        std::unique_lock<std::mutex> one(run_mu_, std::try_to_lock);
+        if (workers_.empty() || n <= 1 || !one.owns_lock()) {
+            for (size_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        run_locked(n, fn);
+    }
+
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : workers_) t.join();
+    }
+
+private:
+    void run_locked(size_t n, const std::function<void(size_t)>& fn) {
         {
             std::lock_guard<std::mutex> lk(mu_);
             job_ = &fn;
@@ -48,16 +74,6 @@ public:
         job_ = nullptr;
     }
 
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (std::thread& t : workers_) t.join();
-    }
-
-private:
     explicit CopyPool(int threads) {
         for (int i = 1; i < threads; ++i) workers_.emplace_back([this] { loop(); });
     }
