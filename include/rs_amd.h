@@ -228,8 +228,8 @@ RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stri
 /* Page-lock / unlock caller memory (hipHostRegister, mapped + portable).
  * Registered (or hipHostMalloc'd) memory is device-addressable: the host
  * batch entry points then run their kernels straight over it (zero-copy,
- * no staging): 72 GiB/s for 10+4 encode on one MI355X vs 57 GiB/s through
- * the DMA pipeline used for pageable memory. */
+ * no staging): 72 GiB/s for 10+4 encode on one MI355X vs 20-57 GiB/s for
+ * pageable memory (staged through a pinned mirror by host threads). */
 RS_API int rs_host_register(void* ptr, size_t bytes);
 /* Bind the calling thread to the CPUs local to `device` (its PCI function's
  * NUMA node, from sysfs), within the process's affinity, so page-locked
