@@ -195,12 +195,15 @@ RS_API int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_str
 /* ------------------------------------------------------------------------
  * Host-resident batches (the path storage callers see: stripes arrive in
  * host memory from disk or the network).  Layout as for rs_encode_batch but
- * `base` is a HOST pointer.  The call pipelines H2D copies of the data
- * vectors, the device encode and D2H copies of the parity vectors over
- * `streams` HIP streams with `stripes_per_chunk` stripes per step, and
- * returns when every parity byte is back in host memory.  Strides are
- * non-negative (RS_ERR_INVAL otherwise).  Host memory should be pinned
- * (rs_host_register) for full PCIe rate.
+ * `base` is a HOST pointer.  Pinned / registered memory: one zero-copy launch
+ * straight over it.  Pageable memory with stripes up to 16 MiB: staged
+ * through a pinned mirror by host copy threads, zero-copy kernels on the
+ * mirror.  Otherwise (or with rs_tune("host_batch_zc" / "host_pageable_stage",
+ * 0)): H2D copies of the data vectors, the device encode and D2H copies of the
+ * parity vectors pipelined over `streams` HIP streams with
+ * `stripes_per_chunk` stripes per step.  Returns when every parity byte is
+ * back in host memory.  Strides are non-negative (RS_ERR_INVAL otherwise).
+ * Pin the memory (rs_host_register) for the full PCIe rate.
  * ------------------------------------------------------------------------ */
 RS_API int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                 int nstripes, size_t len, int stripes_per_chunk, int streams);
