@@ -310,10 +310,12 @@ int rs_host_unregister(void* ptr) {
     });
 }
 
-// Host-resident encode: a three-stage pipeline over a ring of `streams`
-// device slots.  H2D copies run on one stream, kernels on a second, D2H on a
-// third, linked by events, so the copy engines of both PCIe directions and
-// the CUs work on different chunks at the same time:
+// Host-resident encode, three paths: pinned / registered memory -> one
+// zero-copy launch over it; pageable memory with stripes <= 16 MiB ->
+// encode_pageable_batch (pinned mirror); otherwise a three-stage DMA pipeline
+// over a ring of `streams` device slots.  H2D copies run on one stream,
+// kernels on a second, D2H on a third, linked by events, so the copy engines
+// of both PCIe directions and the CUs work on different chunks at once:
 //     h2d:  [wait slot free] copy data(c)  -> ev_in[slot]
 //     comp: [wait ev_in]     encode(c)     -> ev_enc[slot]
 //     d2h:  [wait ev_enc]    copy parity(c)-> ev_free[slot]
