@@ -175,6 +175,7 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     int rc = get_tables(rs, mat, rows, cols, &a.tables, &a.rows_pad);
     if (rc) return rc;
     a.img4 = rows <= 4 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
+    a.host_mat = mat;
     a.rows = rows;
     a.cols = cols;
     a.nstripes = nstripes;
@@ -497,6 +498,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "lds_pad") t.lds_pad = value;
             else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
         else if (n == "block8") t.block8 = value == 128 ? 128 : 256;
+        else if (n == "bitslice") t.bitslice = value ? 1 : 0;
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;

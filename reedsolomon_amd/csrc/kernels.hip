@@ -58,6 +58,8 @@ LaunchTuning& tuning() {
         x.lane_bytes = (lb && std::atoi(lb) == 16) ? 16 : 8;
         const char* b8 = std::getenv("RSAMD_BLOCK8");
         x.block8 = (b8 && std::atoi(b8) == 256) ? 256 : 128;
+        const char* bsl = std::getenv("RSAMD_BITSLICE");
+        x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
 
 
         return x;
@@ -550,6 +552,107 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_bytes(const MatmulArgs a, ui
 }
 
 // ---------------------------------------------------------------------------
+// Bit-sliced Encode for fixed generator matrices with 5-8 parity rows
+// (networks generated by tools/gen_bitslice.py into bitslice_gen.inc).  A lane
+// owns 32 bytes of every vector; an 8x8 SWAR bit transpose turns each
+// column's 8 dwords into 8 bit-planes (plane b = bit b of the 32 bytes), a
+// fixed XOR network over the planes gives every parity plane (multiplying by
+// a constant is GF(2)-linear), and the same transpose (an involution) turns
+// the parity planes back into bytes.  The networks are column-major: each
+// column's planes are combined into the XORs of each 4-plane half's subsets,
+// and every parity plane takes one subset of each half per column
+// (xor3(acc, lo, hi)).  10+8: ~22 VALU per (column, dword) against ~40 on the
+// perm-table path, which is VALU-bound above 4 rows; measured 5.90 vs 5.32
+// TB/s (10+8), 6.00 vs 5.05 (10+6), 6.22 vs 4.91 (8+5) (ab_bitslice*.log).
+// 4-row shapes stay on the perm-table kernels (6.58 vs 6.01 TB/s at 10+4).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void bs_swap(uint32_t& a, uint32_t& b, int s, uint32_t m) {
+    const uint32_t t = ((a >> s) ^ b) & m;
+    b ^= t;
+    a ^= t << s;
+}
+
+__device__ __forceinline__ void bs_transpose8(uint32_t (&w)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs_swap(w[i], w[i + 4], 4, 0x0F0F0F0Fu);
+    bs_swap(w[0], w[2], 2, 0x33333333u);
+    bs_swap(w[1], w[3], 2, 0x33333333u);
+    bs_swap(w[4], w[6], 2, 0x33333333u);
+    bs_swap(w[5], w[7], 2, 0x33333333u);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) bs_swap(w[i], w[i + 1], 1, 0x55555555u);
+}
+
+__device__ __forceinline__ uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+template <int D, int P>
+struct BsNet;
+#include "bitslice_gen.inc"
+
+template <int D, int P, int BS, int Q = 8>
+__global__ __launch_bounds__(BS) void gf_bitslice(const MatmulArgs a) {
+    // A workgroup covers 32*BS bytes of every vector.  Lane t's 32-byte unit
+    // is 32/Q pieces of Q bytes, piece k at Q*t + k*Q*BS of the chunk, so each
+    // wave instruction reads / writes 64*Q bytes contiguously (Q = 8: the
+    // dwordx2 pattern of the perm-table kernels).  Pieces past `body` read 0
+    // and are not written (buffer range checks), so no lane masks.
+    static_assert(Q == 8 || Q == 16, "piece size");
+    constexpr int NP = 32 / Q;   // pieces per lane unit
+    constexpr int DW = Q / 4;    // dwords per piece
+    typedef typename LaneWord<DW>::type W;
+    const uint32_t chunk = blockIdx.x;
+    const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
+    const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
+    const int s = static_cast<int>(su);
+    const uint32_t cb = chunk - su * cps;
+    const uint32_t off = cb * (32u * BS) + static_cast<uint32_t>(Q) * threadIdx.x;
+    const uint32_t nbytes = static_cast<uint32_t>(a.body);
+    auto fetch = [&](int c, uint32_t (&w)[8]) {  // issue the loads of column c's 32 bytes
+        const g_u8* p = in_ptr(a, c, s);
+        // the offset passes through a volatile asm, which stays after the
+        // previous column's pins: the loads are issued here, a few columns
+        // ahead, not all hoisted to the top (VGPRs, occupancy)
+        uint32_t o32 = off;
+        asm volatile("" : "+v"(o32));
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const W v = load16<kAuxNt, DW>(p, o32 + static_cast<uint32_t>(k * Q * BS), nbytes, true);
+#pragma unroll
+            for (int q = 0; q < DW; ++q) w[k * DW + q] = v[q];
+        }
+    };
+    BsNet<D, P>::run(fetch, [&](int r, uint32_t (&o)[8]) {
+        bs_transpose8(o);
+        g_u8* q = out_ptr(a, D, r, s);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            W v;
+#pragma unroll
+            for (int e = 0; e < DW; ++e) v[e] = o[k * DW + e];
+            store16<kAuxNt, DW>(q, off + static_cast<uint32_t>(k * Q * BS), nbytes, v, true);
+        }
+    });
+}
+
+// The bit-sliced kernel for this launch, or null: Encode (overwrite) of a
+// generated shape whose matrix equals the generated one byte for byte.
+typedef void (*BsKernel)(const MatmulArgs);
+static BsKernel bs_kernel_for(const MatmulArgs& a) {
+    if (!tuning().bitslice || a.accumulate || !a.host_mat) return nullptr;
+    for (const BsShape& sh : kBsShapes)
+        if (sh.d == a.cols && sh.p == a.rows &&
+            std::memcmp(sh.gen, a.host_mat, static_cast<size_t>(sh.d) * sh.p) == 0) {
+#define RSAMD_BS_CASE(D, P) \
+    if (sh.d == D && sh.p == P) return gf_bitslice<D, P, 128, 8>;
+            RSAMD_BS_SHAPES(RSAMD_BS_CASE)
+#undef RSAMD_BS_CASE
+        }
+    return nullptr;
+}
+
+// ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
 using VecKernel = void (*)(const MatmulArgs);
@@ -848,6 +951,28 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         aligned = aligned16(a.ptr[v]) && (a.nstripes == 1 || aligned16(static_cast<uint64_t>(a.ss[a.sid[v] & 3])));
     a.body = aligned ? (a.len & ~static_cast<uint64_t>(15)) : 0;
     a.tail_start = a.body;
+
+    if (BsKernel bk = a.body ? bs_kernel_for(a) : nullptr) {
+        // bit-sliced Encode: 32-byte lane units (two 16-byte halves) on
+        // 128-lane workgroups, 4 KiB of every vector per workgroup
+        constexpr int bs = 128;
+        a.units_per_chunk = bs;
+        a.nt_store = 1;
+        a.chunks_per_stripe = static_cast<int64_t>((a.body + 32 * bs - 1) / (32 * bs));
+        a.total_chunks = a.chunks_per_stripe * a.nstripes;
+        a.cps_shift = -1;
+        for (int sh = 0; sh < 31; ++sh)
+            if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
+        if (a.total_chunks <= 0x7fffffff && a.body < (uint64_t{1} << 31)) {
+            (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
+            hipLaunchKernelGGL(bk, dim3(static_cast<unsigned>(a.total_chunks)), dim3(bs), 0, stream, a);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        } else {  // too large for one grid / 31-bit buffer offsets: the perm-table kernels
+            bk = nullptr;
+        }
+        if (bk) a.body = 0;  // the vector path below is done; only the tail remains
+    }
 
     if (a.body) {
         const LaunchTuning& tu = tuning();

@@ -22,6 +22,7 @@ constexpr int kMaxPtrs = 260;  // inputs + outputs of one launch (d+p <= 256, Up
 struct MatmulArgs {
     const uint32_t* tables;   // device perm tables, [cols][rows_pad][5] dwords
     const uint32_t* img4;     // the same as a 4-row LDS image [rup(cols, 4)][20] (rows <= 4), or null
+    const uint8_t* host_mat;  // HOST copy of the rows x cols matrix (launch dispatch only; never read on device)
     int rows, cols, rows_pad;
     int nstripes;
     int accumulate;           // 0: overwrite (Encode), 1: XOR into out (updateOnly)
@@ -62,6 +63,7 @@ struct LaunchTuning {
     int lds_pad;      // minimum dynamic LDS per workgroup (caps occupancy; experiments)
     int lane_bytes;   // one-chunk and multi-pattern kernels: bytes per lane unit (8 default | 16)
     int block8;       // one-chunk kernels with 8-byte units: lanes per workgroup (256 or 128)
+    int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
 };
 LaunchTuning& tuning();
 

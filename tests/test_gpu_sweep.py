@@ -408,3 +408,33 @@ def test_device_single_stripe_random_sweep(rslib, orc, torch_dev):
             assert orc.encode(d, p, exp) == 0
             for j in range(p):
                 assert np.array_equal(vecs[d + j].cpu().numpy(), exp[d + j]), tag + ("replace", j)
+
+
+@pytest.mark.parametrize("bitslice", [1, 0])
+def test_bitsliced_encode_shapes(rslib, orc, torch_dev, bitslice):
+    """Every generated bit-sliced shape (tools/gen_bitslice.py) at sizes that
+    exercise whole 32-byte units, ragged workgroups and the byte tail, against
+    the oracle, with the bit-sliced kernels on and off."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "gen_bitslice", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "gen_bitslice.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    L = rslib.lib()
+    assert L.rs_tune(b"bitslice", bitslice) == 0
+    try:
+        rng = np.random.default_rng(94 + bitslice)
+        for d, p in gen.SHAPES:
+            r = rslib.New(d, p)
+            for size in (16, 23, 32, 33, 2048 + 16, 4096 + 5, 65536 + 96, 1 << 20):
+                data = [_rand(rng, size) for _ in range(d)]
+                v = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
+                r.Encode(v)
+                exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, exp) == 0
+                for j in range(p):
+                    assert np.array_equal(v[d + j], exp[d + j]), (d, p, size, j, bitslice)
+    finally:
+        L.rs_tune(b"bitslice", 1)

@@ -312,3 +312,31 @@ def test_check_errors(orc):
     assert orc.replace(10, 4, [z(8)] * 2, [0, 1], [z(8)] * 3) == 7
     assert orc.replace(10, 4, [], [], [z(8)] * 4) == 13                      # reference panics
     assert orc.replace(10, 4, [z(8)] * 2, [0, 10], [z(8)] * 4) == 8
+
+
+def test_bitslice_generator_matches_oracle(orc):
+    """tools/gen_bitslice.py (build tooling for the bit-sliced Encode kernels):
+    its generator matrices are the oracle's, its GF(2) bit matrices reproduce
+    every product, and the committed bitslice_gen.inc is what it emits."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gen_bitslice", os.path.join(root, "tools", "gen_bitslice.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    mul = orc.tables()["mul"]
+    for d, p in gen.SHAPES:
+        G = gen.gen_matrix(d, p)
+        assert np.array_equal(np.array(G, np.uint8).ravel(), orc.gen_matrix(d, p)), (d, p)
+    for c in range(256):
+        for x in (1, 2, 3, 0x55, 0x80, 0xFF, 0x9C):
+            prod = 0
+            for i in range(8):  # bit i of c*x = XOR of bits j of x with bit i of c*(1<<j)
+                b = 0
+                for j in range(8):
+                    if (x >> j) & 1 and (gen.gmul(c, 1 << j) >> i) & 1:
+                        b ^= 1
+                prod |= b << i
+            assert prod == mul[c, x], (c, x)
+    with open(gen.OUT) as f:
+        assert f.read() == gen.emit(), "bitslice_gen.inc is stale: run python tools/gen_bitslice.py"
