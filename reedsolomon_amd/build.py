@@ -20,7 +20,7 @@ LIB = os.path.join(LIB_DIR, "librsamd.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("codec.cpp", "host_calls.cpp", "batches.cpp", "host_batches.cpp",
                                            "kernels.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("gf256.hpp", "kernels.hpp", "codec_internal.hpp",
-                                                  "host_pool.hpp")] + [
+                                                  "host_pool.hpp", "bitslice_gen.inc")] + [
     os.path.join(ROOT, "include", "rs_amd.h")
 ]
 ARCH = os.environ.get("RSAMD_OFFLOAD_ARCH", "gfx950")
