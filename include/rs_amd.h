@@ -320,6 +320,8 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * "lane_bytes" (8 default | 16), "block8" (lanes
  * per workgroup of the 8-byte-lane kernels: 128 default | 256), "bitslice"
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
+ * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
+ * 0 default = 64, or 256 for interleaved stripes of d+p >= 18),
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
  * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),

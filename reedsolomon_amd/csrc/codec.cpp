@@ -496,18 +496,19 @@ int rs_tune(const char* name, int value) {
         else if (n == "nt_store") t.nt_store = value;
         else if (n == "var") t.var = value;
         else if (n == "lds_pad") t.lds_pad = value;
-            else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
+        else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
         else if (n == "block8") t.block8 = value == 128 ? 128 : 256;
         else if (n == "bitslice") t.bitslice = value ? 1 : 0;
+        else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;
         else if (n == "host_dma_1d") g_host_dma_1d = value;
         else if (n == "host_pageable_stage") g_host_pageable_stage = value;
-    else if (n == "bind_numa") g_bind_numa = value;
+        else if (n == "bind_numa") g_bind_numa = value;
         else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
-    else if (n == "host_coalesce_linger_us") g_coalesce_linger_us = value < 0 ? 0 : value;
-    else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
+        else if (n == "host_coalesce_linger_us") g_coalesce_linger_us = value < 0 ? 0 : value;
+        else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
         else return RS_ERR_INVAL;
         return RS_OK;

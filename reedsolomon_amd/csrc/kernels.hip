@@ -60,8 +60,7 @@ LaunchTuning& tuning() {
         x.block8 = (b8 && std::atoi(b8) == 256) ? 256 : 128;
         const char* bsl = std::getenv("RSAMD_BITSLICE");
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
-
-
+        x.bs_block = 0;
         return x;
     }();
     return t;
@@ -562,8 +561,9 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_bytes(const MatmulArgs a, ui
 // column's planes are combined into the XORs of each 4-plane half's subsets,
 // and every parity plane takes one subset of each half per column
 // (xor3(acc, lo, hi)).  10+8: ~22 VALU per (column, dword) against ~40 on the
-// perm-table path, which is VALU-bound above 4 rows; measured 5.90 vs 5.32
-// TB/s (10+8), 6.00 vs 5.05 (10+6), 6.22 vs 4.91 (8+5) (ab_bitslice*.log).
+// perm-table path, which is VALU-bound above 4 rows; measured 6.12 vs 5.32
+// TB/s (10+8), 6.15 vs 5.05 (10+6), 6.34 vs 4.91 (8+5) on the split layout
+// (ab_bitslice*.log, ab_bs_block.log; workgroup size per bs_block_for).
 // 4-row shapes stay on the perm-table kernels (6.58 vs 6.01 TB/s at 10+4).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void bs_swap(uint32_t& a, uint32_t& b, int s, uint32_t m) {
@@ -638,14 +638,36 @@ __global__ __launch_bounds__(BS) void gf_bitslice(const MatmulArgs a) {
 
 // The bit-sliced kernel for this launch, or null: Encode (overwrite) of a
 // generated shape whose matrix equals the generated one byte for byte.
+// `bs` receives the workgroup size: rs_tune("bs_block", 64 | 128 | 256), or
+// 0 (default) for the per-layout rule of bs_block_for().
 typedef void (*BsKernel)(const MatmulArgs);
-static BsKernel bs_kernel_for(const MatmulArgs& a) {
-    if (!tuning().bitslice || a.accumulate || !a.host_mat) return nullptr;
+static int bs_block_for(const MatmulArgs& a) {
+    const int b = tuning().bs_block;
+    if (b) return b;
+    // Same-process A/B on two boxes (tools/ab_bs_block.sh,
+    // profiles/r01/ab_bs_block.log, Encode @ 1 MiB): with parity in a
+    // separate region 64 lanes win or tie every shape (10+8 6.12-6.20 vs
+    // 5.86-6.14 TB/s at 128, 10+6 6.16-6.28 vs 5.95-6.09, 8+8 6.18-6.29 vs
+    // 5.48-5.97 at 256).  With parity inside the data's stripes (interleaved
+    // [S][d+p][len]) the best size follows the stripe pitch: 10+8 runs 5.78 at
+    // 256 vs 5.28 at 128 and 5.04 at 64, 12+8 5.75 / 5.79 / 5.50, while 10+6,
+    // 8+5 and 8+8 are best at 64 (5.90, 6.10, 6.00).
+    const int64_t stride = a.ss[a.sid[0] & 3];
+    const int64_t gap = static_cast<int64_t>(a.ptr[a.cols] - a.ptr[0]);
+    const bool interleaved = a.nstripes > 1 && a.ss[a.sid[a.cols] & 3] == stride && gap > 0 && gap < stride;
+    return interleaved && a.cols + a.rows >= 18 ? 256 : 64;
+}
+static BsKernel bs_kernel_for(const MatmulArgs& a, int* bs) {
+    const LaunchTuning& tu = tuning();
+    if (!tu.bitslice || a.accumulate || !a.host_mat) return nullptr;
+    *bs = bs_block_for(a);
     for (const BsShape& sh : kBsShapes)
         if (sh.d == a.cols && sh.p == a.rows &&
             std::memcmp(sh.gen, a.host_mat, static_cast<size_t>(sh.d) * sh.p) == 0) {
-#define RSAMD_BS_CASE(D, P) \
-    if (sh.d == D && sh.p == P) return gf_bitslice<D, P, 128, 8>;
+#define RSAMD_BS_CASE(D, P)                                                              \
+    if (sh.d == D && sh.p == P)                                                          \
+        return *bs == 64 ? gf_bitslice<D, P, 64, 8> : *bs == 256 ? gf_bitslice<D, P, 256, 8> \
+                                                                 : gf_bitslice<D, P, 128, 8>;
             RSAMD_BS_SHAPES(RSAMD_BS_CASE)
 #undef RSAMD_BS_CASE
         }
@@ -952,10 +974,10 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     a.body = aligned ? (a.len & ~static_cast<uint64_t>(15)) : 0;
     a.tail_start = a.body;
 
-    if (BsKernel bk = a.body ? bs_kernel_for(a) : nullptr) {
-        // bit-sliced Encode: 32-byte lane units (two 16-byte halves) on
-        // 128-lane workgroups, 4 KiB of every vector per workgroup
-        constexpr int bs = 128;
+    int bs = 128;
+    if (BsKernel bk = a.body ? bs_kernel_for(a, &bs) : nullptr) {
+        // bit-sliced Encode: 32-byte lane units (four 8-byte pieces) on
+        // bs-lane workgroups, 32 * bs bytes of every vector per workgroup
         a.units_per_chunk = bs;
         a.nt_store = 1;
         a.chunks_per_stripe = static_cast<int64_t>((a.body + 32 * bs - 1) / (32 * bs));

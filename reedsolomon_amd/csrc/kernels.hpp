@@ -64,6 +64,7 @@ struct LaunchTuning {
     int lane_bytes;   // one-chunk and multi-pattern kernels: bytes per lane unit (8 default | 16)
     int block8;       // one-chunk kernels with 8-byte units: lanes per workgroup (256 or 128)
     int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
+    int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
 };
 LaunchTuning& tuning();
 

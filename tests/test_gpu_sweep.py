@@ -438,3 +438,42 @@ def test_bitsliced_encode_shapes(rslib, orc, torch_dev, bitslice):
                     assert np.array_equal(v[d + j], exp[d + j]), (d, p, size, j, bitslice)
     finally:
         L.rs_tune(b"bitslice", 1)
+
+
+@pytest.mark.parametrize("bs_block", [64, 128, 256])
+def test_bitsliced_workgroup_sizes(rslib, orc, torch_dev, bs_block):
+    """Every bit-sliced shape at each workgroup size (rs_tune("bs_block")),
+    batched device Encode on both layouts (interleaved [S][d+p][n]; data and
+    parity in separate buffers), whole-unit, ragged and tail sizes, against
+    the oracle."""
+    import importlib.util
+    import os
+
+    torch = torch_dev
+    spec = importlib.util.spec_from_file_location(
+        "gen_bitslice", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "gen_bitslice.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    L = rslib.lib()
+    assert L.rs_tune(b"bs_block", bs_block) == 0
+    try:
+        rng = np.random.default_rng(1000 + bs_block)
+        for d, p in gen.SHAPES:
+            r = rslib.New(d, p)
+            G = orc.gen_matrix(d, p).reshape(p, d)
+            for S, n in [(3, 16), (5, 4096 + 5), (4, 65536 + 96)] + ([(3, 1 << 20)] if (d, p) == (10, 8) else []):
+                host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+                host[:, d:] = 0xA5
+                exp = orc.encode_numpy(G, host[:, :d])
+                buf = torch.from_numpy(host).cuda()
+                r.encode_batch(buf)
+                data = torch.from_numpy(np.ascontiguousarray(host[:, :d])).cuda()
+                par = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
+                r.encode_batch_split(data, par)
+                torch.cuda.synchronize()
+                got = buf.cpu().numpy()
+                assert np.array_equal(got[:, d:], exp), (d, p, S, n, bs_block, "interleaved")
+                assert np.array_equal(got[:, :d], host[:, :d])
+                assert np.array_equal(par.cpu().numpy(), exp), (d, p, S, n, bs_block, "split")
+    finally:
+        L.rs_tune(b"bs_block", 0)
