@@ -61,6 +61,7 @@ LaunchTuning& tuning() {
         const char* bsl = std::getenv("RSAMD_BITSLICE");
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
         x.bs_block = 0;
+        x.wide_block = 256;
         return x;
     }();
     return t;
@@ -822,7 +823,9 @@ static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 
 // 40-dword LDS table over twice the data of 8-byte units (10+8 Encode @ 1 MiB:
 // 5.29 TB/s vs 4.60 with 8-byte units and 4.43 with the looped kernel,
 // profiles/r01/ab_rows8.log).  rs_tune("lane_bytes", 8) does not apply here.
-#define RSAMD_VARIANT1_WIDE(KB, KFIX, MC, ACC, WIN) RSAMD_V1(KB, KFIX, MC, ACC, WIN, 4, 256, "16B")
+#define RSAMD_VARIANT1_WIDE(KB, KFIX, MC, ACC, WIN)                                                    \
+    (tuning().wide_block == 128 ? RSAMD_V1(KB, KFIX, MC, ACC, WIN, 4, 128, "16B,128 lanes")               \
+                                : RSAMD_V1(KB, KFIX, MC, ACC, WIN, 4, 256, "16B"))
 
 // Loop-free one-chunk-per-workgroup kernels (the default launch: grid = all
 // chunks, rows <= MC).  A/B on MI355X, 10+4 @ 1 MiB x 256 (tools/ab.py, 2 x 30

@@ -65,6 +65,7 @@ struct LaunchTuning {
     int block8;       // one-chunk kernels with 8-byte units: lanes per workgroup (256 or 128)
     int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
     int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
+    int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
 };
 LaunchTuning& tuning();
 
