@@ -14,6 +14,14 @@ independent, so N GPUs each encode their own S stripes with no collective on
 the data path (weak scaling); the only collectives are the timing barrier and
 the max-over-ranks of the elapsed time.
 
+`--gpus N` without a launcher starts N ranks itself (torch.distributed.run
+as a child process, before any GPU call); under a launcher WORLD_SIZE must
+equal N and every rank must join, or the run exits non-zero (`ranks_seen`).
+
+Order per rank: self-check (encode -> erase -> reconst), pre-warm until the
+launch time has settled (10 consecutive launches within 2 %, at least 60;
+`prewarm` in the line), W counted warm-up steps, K timed steps.
+
 Rank 0 prints ONE JSON line.  `value` = (k+m)*vec*S*N*K / max-rank time in
 GiB/s.  `roofline` prices the encode kernel itself: algorithmic bytes per
 launch / mean launch time from HIP events on the launch stream, against
@@ -55,6 +63,12 @@ def parse_args(argv=None):
     ap.add_argument("--e2e-stripes", type=int, default=128,
                     help="stripes per GPU for the host-resident end-to-end leg (0 = skip)")
     ap.add_argument("--e2e-reps", type=int, default=10)
+    ap.add_argument("--prewarm-min", type=int, default=60,
+                    help="pre-warm: at least this many launches before the counted warm-up")
+    ap.add_argument("--prewarm-max", type=int, default=2000, help="pre-warm: at most this many launches")
+    ap.add_argument("--rehearse-cpu", action="store_true",
+                    help="TEST ONLY: rehearse the launcher / rank / timing protocol on CPU (gloo, no GPU, "
+                         "no kernel); the line it prints is not a measurement")
     return ap.parse_args(argv)
 
 
@@ -257,23 +271,161 @@ def end_to_end(codec, data, parity, k, m, vec, S, reps, n_gpus, barrier, max_ove
 
 
 def load_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    """(HBM bytes per launch, source) from the committed rocprofv3 PMC summary
+    (profiles/traffic.json: FETCH_SIZE / WRITE_SIZE passes of this same
+    launch, corrected per MI355X_MICROARCH.md), or (None, None).  The counters
+    are not collected inside this run: `traffic_source` names the file."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
-        data = json.load(open(path))
-        return data.get(config, {}).get("hbm_bytes_per_launch")
+        ent = json.load(open(path)).get(config, {})
+        b = ent.get("hbm_bytes_per_launch")
+        return b, (f"profiles/traffic.json <- {ent.get('source')}" if b else None)
     except (OSError, ValueError):
-        return None
+        return None, None
+
+
+# ---------------------------------------------------------------- launcher
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`--gpus N` without a launcher: start N ranks (one process per GPU)
+    with torch.distributed.run as a CHILD process and return its exit code.
+    Runs before this process touches the GPU (no torch import yet), so no
+    GPU-initialised process is ever replaced (exec) by another."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    print("bench: --gpus %d without a launcher: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def check_world(args, world: int, launched: bool) -> None:
+    """A line claiming N GPUs must come from N ranks: refuse any mismatch."""
+    if launched and world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if not launched and args.gpus != 1:
+        raise SystemExit("bench: internal error: multi-GPU run without a launcher")
+
+
+# ---------------------------------------------------------------- pre-warm
+
+def prewarm(step, stream, min_launches: int, max_launches: int, window: int = 10, tol: float = 0.02,
+            max_seconds: float = 5.0):
+    """Run the step until the GPU has reached its steady state: after an idle
+    period the encode runs 0.57-0.88 ms per launch for ~50 launches before it
+    settles (power management; rocprof trace), and a short
+    warm-up would time that transient.  Each launch is bracketed by HIP events
+    on the launch stream; stop once `window` consecutive launches agree within
+    `tol` (max/min) and at least `min_launches` ran.  Returns (launches, wall
+    ms, last window's mean ms, converged)."""
+    import torch
+
+    t0 = time.perf_counter()
+    evs = []
+    n = 0
+    converged = False
+    last_mean = None
+    while n < max_launches:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step(0)
+        e1.record(stream)
+        evs.append((e0, e1))
+        n += 1
+        if n % window == 0:
+            e1.synchronize()
+            last = [a.elapsed_time(b) for a, b in evs[-window:]]
+            last_mean = sum(last) / len(last)
+            if n >= min_launches and max(last) <= min(last) * (1 + tol):
+                converged = True
+                break
+            if time.perf_counter() - t0 > max_seconds:
+                break
+    torch.cuda.synchronize()
+    return n, (time.perf_counter() - t0) * 1e3, last_mean, converged
+
+
+def metric_name(k: int, m: int, vec: int) -> str:
+    """BASELINE.json's metric, with the shape of the config actually run."""
+    size = f"{vec >> 20}MiB" if vec % (1 << 20) == 0 else f"{vec >> 10}KiB"
+    return f"Encode GiB/s device-resident ((k+m)*vec/cost), {k}+{m} @{size}, 1/2/4/8 GPU; %HBM peak"
+
+
+# ---------------------------------------------------------------- CPU rehearsal (tests only)
+
+def rehearse_cpu(args, world: int, rank: int) -> dict | None:
+    """The launcher / rank / timing protocol without a GPU (gloo): what
+    tests/test_dist.py drives as `bench.py --gpus 2 --rehearse-cpu`.  The step
+    is a numpy XOR over a small buffer; the printed line is marked as a
+    rehearsal and carries no measurement."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    pg = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        pg = dist
+    ranks_seen = count_ranks(pg, torch.device("cpu"))
+    if ranks_seen != args.gpus:
+        raise SystemExit(f"bench: {ranks_seen} ranks joined, --gpus {args.gpus}")
+    barrier, max_over = make_collectives(pg, torch.device("cpu"))
+    buf = np.random.default_rng(rank).integers(0, 256, (4, 14, 4096), dtype=np.uint8)
+
+    def step(_i):
+        np.bitwise_xor.reduce(buf[:, :10], axis=1)
+
+    for _ in range(args.warmup):
+        step(0)
+    el = timed_region(step, args.steps, barrier, lambda: None, max_over)
+    out = None
+    if rank == 0:
+        out = {"metric": "REHEARSAL (no GPU, no kernel)", "value": None, "n_gpus": world, "ranks_seen": ranks_seen,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+               "data": "rehearsal: numpy XOR stand-in, not a measurement"}
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.barrier()
+        pg.destroy_process_group()
+    return out
+
+
+def count_ranks(pg, device) -> int:
+    """Ranks that actually joined the process group (1 without one)."""
+    import torch
+
+    if pg is None:
+        return 1
+    if pg.get_backend() == "gloo":
+        device = torch.device("cpu")
+    t = torch.ones(1, dtype=torch.float64, device=device)
+    pg.all_reduce(t)
+    return int(t.item())
 
 
 # ---------------------------------------------------------------- main
 
 def main(argv=None):
-    args = parse_args(argv)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(raw)
     world, rank, local = dist_env()
-    if world != args.gpus and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        raise SystemExit(spawn_ranks(args.gpus, raw))
+    check_world(args, world, launched)
     n_gpus = world
+    if args.rehearse_cpu:
+        return rehearse_cpu(args, world, rank)
 
     import torch
 
@@ -284,6 +436,8 @@ def main(argv=None):
     # rehearse the multi-rank path on a 1-GPU box (gloo, ranks sharing cuda:0).
     dev_idx = int(os.environ.get("RSAMD_BENCH_DEVICE", local))
     backend = os.environ.get("RSAMD_BENCH_BACKEND", "nccl")
+    if "RSAMD_BENCH_DEVICE" not in os.environ and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench: {world} ranks but only {torch.cuda.device_count()} visible GPUs")
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
     pg = None
@@ -355,9 +509,16 @@ def main(argv=None):
     # Initialise the timing collectives now (the first NCCL call builds the
     # communicator) so nothing slow sits between the warm-up and the timed region.
     barrier, max_over = make_collectives(pg, dev)
+    ranks_seen = count_ranks(pg, dev)
+    if ranks_seen != args.gpus:
+        raise SystemExit(f"bench: {ranks_seen} ranks joined the process group, --gpus {args.gpus}")
     barrier()
     max_over(0.0)
 
+    # Pre-warm until launch times settle, then the counted warm-up and the
+    # timed region follow back to back (no idle gap, no per-launch events).
+    pw_n, pw_ms, pw_mean, pw_ok = prewarm(step, stream, args.prewarm_min, args.prewarm_max)
+    barrier()
     for _ in range(args.warmup):
         step(0)
     torch.cuda.synchronize(dev)
@@ -387,12 +548,13 @@ def main(argv=None):
 
     result = None
     if rank == 0:
-        traffic = load_traffic(args.config)
+        traffic, traffic_src = load_traffic(args.config)
         result = {
-            "metric": "Encode GiB/s device-resident ((k+m)*vec/cost), 10+4 @1MiB, 1/2/4/8 GPU; %HBM peak",
+            "metric": metric_name(k, m, vec),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": n_gpus,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -418,10 +580,15 @@ def main(argv=None):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": bytes_per_step_rank,
                 "kernel_ms_mean": round(kern_mean_s * 1e3, 4),
                 "kernel_timing": "HIP event pair on the launch stream around the K timed launches / K",
             },
+            "prewarm": {"launches": pw_n, "ms": round(pw_ms, 1), "converged": pw_ok,
+                        "last10_mean_ms": round(pw_mean, 4) if pw_mean else None,
+                        "rule": f"untimed launches until 10 consecutive agree within 2 % (>= {args.prewarm_min}), "
+                                "before the counted warm-up"},
         }
         result["end_to_end"] = e2e
         if n_gpus == 1 and args.cpu_seconds > 0:

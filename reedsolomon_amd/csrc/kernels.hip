@@ -606,7 +606,8 @@ __global__ __launch_bounds__(BS) void gf_bitslice(const MatmulArgs a) {
     const uint32_t chunk = blockIdx.x;
     const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
     const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
-    const int s = static_cast<int>(su);
+    // grouped launches (multi-pattern Reconst fallback) name their stripes
+    const int s = a.stripe_ids ? a.stripe_ids[su] : static_cast<int>(su);
     const uint32_t cb = chunk - su * cps;
     const uint32_t off = cb * (32u * BS) + static_cast<uint32_t>(Q) * threadIdx.x;
     const uint32_t nbytes = static_cast<uint32_t>(a.body);

@@ -157,14 +157,6 @@ def _ints(xs):
     return (ctypes.c_int * max(len(xs), 1))(*xs), len(xs)
 
 
-def _stream(stream) -> ctypes.c_void_p:
-    if stream is None:
-        import torch
-
-        stream = torch.cuda.current_stream()
-    if hasattr(stream, "cuda_stream"):
-        stream = stream.cuda_stream
-    return ctypes.c_void_p(int(stream))
 
 
 # ---------------------------------------------------------------- codec
@@ -195,6 +187,27 @@ class RS:
             except Exception:
                 pass
             self._h = None
+
+    def _stream(self, stream, *tensors) -> ctypes.c_void_p:
+        """The HIP stream to launch on, on the codec's device.  Every tensor
+        must live on that device (the C side switches to the handle's device
+        and would otherwise get another device's pointers); stream=None means
+        torch's current stream OF THAT DEVICE, not of the current device."""
+        import torch
+
+        dev = self.device
+        if dev is None or dev < 0:  # New(..., device=-1): the current device (rs_new)
+            dev = torch.cuda.current_device()
+        for t in tensors:
+            if t.device.index != dev:
+                raise TypeError(f"tensor on {t.device} but the codec runs on cuda:{dev}")
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        elif isinstance(stream, torch.cuda.Stream) and stream.device.index != dev:
+            raise TypeError(f"stream on {stream.device} but the codec runs on cuda:{dev}")
+        if hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        return ctypes.c_void_p(int(stream))
 
     # ------------------------------------------------ host memory (Go API)
 
@@ -229,13 +242,13 @@ class RS:
 
     def encode_dev(self, vects: Sequence, stream=None) -> None:
         ptrs, lens, n = _dev_vecs(vects)
-        _check(lib().rs_encode_dev(self._h, ptrs, lens, n, _stream(stream)))
+        _check(lib().rs_encode_dev(self._h, ptrs, lens, n, self._stream(stream, *vects)))
 
     def reconst_dev(self, vects: Sequence, survived, needReconst, stream=None) -> None:
         ptrs, lens, n = _dev_vecs(vects)
         s, ns = _ints(survived)
         q, nq = _ints(needReconst)
-        _check(lib().rs_reconst_dev(self._h, ptrs, lens, n, s, ns, q, nq, _stream(stream)))
+        _check(lib().rs_reconst_dev(self._h, ptrs, lens, n, s, ns, q, nq, self._stream(stream, *vects)))
 
     def update_dev(self, oldData, newData, row: int, parity: Sequence, stream=None) -> None:
         _check_tensor(oldData)
@@ -244,13 +257,14 @@ class RS:
         _check(lib().rs_update_dev(
             self._h, ctypes.cast(ctypes.c_void_p(oldData.data_ptr()), c_u8p), oldData.numel(),
             ctypes.cast(ctypes.c_void_p(newData.data_ptr()), c_u8p), newData.numel(), int(row), ptrs, lens, n,
-            _stream(stream)))
+            self._stream(stream, oldData, newData, *parity)))
 
     def replace_dev(self, data: Sequence, replaceRows, parity: Sequence, stream=None) -> None:
         dptrs, dlens, nd = _dev_vecs(data)
         r, nr = _ints(replaceRows)
         pptrs, plens, np_ = _dev_vecs(parity)
-        _check(lib().rs_replace_dev(self._h, dptrs, dlens, nd, r, nr, pptrs, plens, np_, _stream(stream)))
+        _check(lib().rs_replace_dev(self._h, dptrs, dlens, nd, r, nr, pptrs, plens, np_,
+                                    self._stream(stream, *data, *parity)))
 
     # ------------------------------------------------ device memory, batched stripes
 
@@ -265,7 +279,7 @@ class RS:
     def encode_batch(self, buf, stream=None) -> None:
         """Encode every stripe of buf[S, d+p, len] (the north-star hot path)."""
         base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
-        _check(lib().rs_encode_batch(self._h, base, ss, vs, S, n, _stream(stream)))
+        _check(lib().rs_encode_batch(self._h, base, ss, vs, S, n, self._stream(stream, buf)))
 
     def _split_layout(self, data, parity):
         _check_tensor_any(data)
@@ -282,13 +296,14 @@ class RS:
     def encode_batch_split(self, data, parity, stream=None) -> None:
         """Encode S stripes whose data [S, d, len] and parity [S, p, len] live in separate buffers."""
         L, S, n = self._split_layout(data, parity)
-        _check(lib().rs_encode_batch_layout(self._h, ctypes.byref(L), S, n, _stream(stream)))
+        _check(lib().rs_encode_batch_layout(self._h, ctypes.byref(L), S, n, self._stream(stream, data, parity)))
 
     def reconst_batch_split(self, data, parity, survived, needReconst, stream=None) -> None:
         L, S, n = self._split_layout(data, parity)
         s, ns = _ints(survived)
         q, nq = _ints(needReconst)
-        _check(lib().rs_reconst_batch_layout(self._h, ctypes.byref(L), S, n, s, ns, q, nq, _stream(stream)))
+        _check(lib().rs_reconst_batch_layout(self._h, ctypes.byref(L), S, n, s, ns, q, nq,
+                                             self._stream(stream, data, parity)))
 
     def reconst_batch_multi(self, data, parity, need_masks, stream=None) -> None:
         """Per-stripe erasure patterns: need_masks[s] = bitmap of vectors of stripe s to rebuild
@@ -297,13 +312,14 @@ class RS:
         L, S, n = self._split_layout(data, parity)
         masks = _masks(need_masks, S)
         _check(lib().rs_reconst_batch_multi(self._h, ctypes.byref(L), S, n,
-                                            masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _stream(stream)))
+                                            masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                            self._stream(stream, data, parity)))
 
     def reconst_batch(self, buf, survived, needReconst, stream=None) -> None:
         base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
         s, ns = _ints(survived)
         q, nq = _ints(needReconst)
-        _check(lib().rs_reconst_batch(self._h, base, ss, vs, S, n, s, ns, q, nq, _stream(stream)))
+        _check(lib().rs_reconst_batch(self._h, base, ss, vs, S, n, s, ns, q, nq, self._stream(stream, buf)))
 
     def update_batch(self, old, new, row: int, buf, stream=None) -> None:
         """old/new: [S, len] GPU tensors; parity rows of buf[S, d+p, len] are updated."""
@@ -314,7 +330,7 @@ class RS:
                 raise TypeError("old/new must be [stripes, len] uint8 GPU tensors")
         _check(lib().rs_update_batch(self._h, ctypes.c_void_p(old.data_ptr()), old.stride(0),
                                      ctypes.c_void_p(new.data_ptr()), new.stride(0), int(row), base, ss, vs, S, n,
-                                     _stream(stream)))
+                                     self._stream(stream, old, new, buf)))
 
     def replace_batch(self, data, replaceRows, buf, stream=None) -> None:
         """data: [S, rn, len] GPU tensor of replacement vectors."""
@@ -326,7 +342,7 @@ class RS:
         if data.shape[1] != nr:
             raise ErrMismatchReplace()
         _check(lib().rs_replace_batch(self._h, ctypes.c_void_p(data.data_ptr()), data.stride(0), data.stride(1),
-                                      r, nr, base, ss, vs, S, n, _stream(stream)))
+                                      r, nr, base, ss, vs, S, n, self._stream(stream, data, buf)))
 
     def encode_host_batch(self, buf, stripes_per_chunk: int = 8, streams: int = 3) -> None:
         """Encode stripes held in HOST memory: buf is a [S, d+p, len] uint8
@@ -354,7 +370,7 @@ class RS:
             raise TypeError("expected src [S, n, len] and dst [S, len] uint8 GPU tensors")
         _check(lib().rs_xor_batch(self._h, ctypes.c_void_p(src.data_ptr()), src.stride(0), src.stride(1),
                                   src.shape[1], ctypes.c_void_p(dst.data_ptr()), dst.stride(0), src.shape[0],
-                                  src.shape[2], _stream(stream)))
+                                  src.shape[2], self._stream(stream, src, dst)))
 
     def gf_matmul_batch(self, mat: np.ndarray, src, in_map, dst, out_map, accumulate=False, stream=None) -> None:
         """dst[:, out_map[r]] (=|^=) sum_c mat[r, c] x src[:, in_map[c]] for every stripe."""
@@ -369,7 +385,7 @@ class RS:
         _check(lib().rs_gf_matmul_batch(
             self._h, mat.ctypes.data_as(c_u8p), rows, cols, ctypes.c_void_p(src.data_ptr()), src.stride(0),
             src.stride(1), im, ctypes.c_void_p(dst.data_ptr()), dst.stride(0), dst.stride(1), om,
-            src.shape[0], src.shape[2], int(bool(accumulate)), _stream(stream)))
+            src.shape[0], src.shape[2], int(bool(accumulate)), self._stream(stream, src, dst)))
 
     # ------------------------------------------------ host-side planning
 

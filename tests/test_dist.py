@@ -74,3 +74,61 @@ def test_two_rank_gloo_timing_protocol():
     assert el0 >= 5 * 0.02, "the slowest rank (rank 1) bounds the timed region"
     assert (lo0, hi0, lo1, hi1) == (0, 4, 4, 8), "ranks own disjoint, adjacent stripe ranges"
     assert abs(v0 - 4 * 14 * 256 * 2 * 5 / el0 / 2 ** 30) < 1e-9
+
+
+def _bench_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    env["HIP_VISIBLE_DEVICES"] = ""  # CPU only: the rehearsal never touches a GPU
+    return env
+
+
+def _last_json(out: str) -> dict:
+    import json
+
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(240)
+def test_bench_spawns_ranks_without_launcher():
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself (the driver's
+    SCALE runs must never silently measure one GPU): the line reports
+    n_gpus 2 and 2 ranks that joined the process group."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--rehearse-cpu"], capture_output=True, text=True, env=_bench_env(),
+                       timeout=220, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2, line
+
+
+@pytest.mark.timeout(240)
+def test_bench_under_torchrun_like_the_driver():
+    """The driver's own command shape: torch.distributed.run --nproc-per-node 2
+    ... bench.py --gpus 2."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--rehearse-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=_bench_env(), timeout=220, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2, line
+
+
+@pytest.mark.timeout(120)
+def test_bench_refuses_world_mismatch():
+    """WORLD_SIZE != --gpus exits non-zero before any work."""
+    import subprocess
+
+    env = _bench_env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--rehearse-cpu"],
+                       capture_output=True, text=True, env=env, timeout=100, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)

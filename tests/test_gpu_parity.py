@@ -824,6 +824,50 @@ def test_reconst_batch_multi_single_launch(rslib, torch_dev, d, p, n):
     assert torch.equal(data, ref_d) and torch.equal(parity, ref_p)
 
 
+@pytest.mark.parametrize("d,p", [(10, 8), (8, 8), (10, 6)])
+def test_reconst_batch_multi_parity_rows_bitsliced(rslib, orc, torch_dev, d, p):
+    """Stripes that lose only parity rows p' in 5..p: the grouped fallback's
+    combined matrix is then the first p' rows of the generator, which the
+    bit-sliced Encode kernels match byte for byte (10+8 losing rows 10..14 =
+    BsShape(10, 5)).  Those launches name their stripes through a device id
+    list: every listed stripe must be rebuilt and no other stripe touched."""
+    torch = torch_dev
+    S, n = 48, 65536
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(d * 31 + p)
+    data = torch.randint(0, 256, (S, d, n), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    torch.cuda.synchronize()
+    # the encode itself against the oracle on two stripes
+    for s in (0, S - 1):
+        host = data[s].cpu().numpy()
+        exp = _oracle_encode(orc, d, p, [host[i].copy() for i in range(d)])
+        assert np.array_equal(parity[s].cpu().numpy(), np.stack(exp)), s
+    ref_d, ref_p = data.clone(), parity.clone()
+    rng = np.random.default_rng(d * 7 + p)
+    masks = np.zeros(S, np.uint64)
+    for s in range(S):
+        kind = s % 6
+        if kind in (1, 4):  # untouched, interleaved with the damaged ones
+            continue
+        if kind == 0:
+            lost = list(range(d, d + 5))                 # exactly the first 5 parity rows
+        elif kind == 2:
+            lost = list(range(d, d + p))                 # every parity row
+        elif kind == 3:
+            lost = list(range(d, d + int(rng.integers(5, p + 1))))  # a prefix of 5..p rows
+        else:
+            lost = sorted(int(v) for v in rng.choice(d + p, int(rng.integers(1, p + 1)), replace=False))
+        for v in lost:
+            masks[s] |= np.uint64(1) << np.uint64(v)
+            (data[s, v] if v < d else parity[s, v - d]).fill_(0x3C)
+    r.reconst_batch_multi(data, parity, masks)
+    torch.cuda.synchronize()
+    for s in range(S):
+        assert torch.equal(data[s], ref_d[s]) and torch.equal(parity[s], ref_p[s]), (s, int(masks[s]))
+
+
 # ---------------------------------------------------------------- host-call staging paths
 
 @pytest.mark.parametrize("mode", ["chunked", "small_chunks", "staged_pinned", "staged_pageable"])
