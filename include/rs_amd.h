@@ -321,7 +321,10 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * per workgroup of the 8-byte-lane kernels: 128 default | 256), "bitslice"
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
- * 0 default = 64, or 256 for interleaved stripes of d+p >= 18),
+ * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "rg4" (more
+ * than 4 output rows on runtime matrices: 1 default = groups of 4 rows on
+ * XCD-paired workgroups, nt loads | 2 = the same with default-policy loads |
+ * 0 = one workgroup holds every row), "wide_block" (128 | 256),
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
  * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),

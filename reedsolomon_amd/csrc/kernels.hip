@@ -62,6 +62,8 @@ LaunchTuning& tuning() {
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
         x.bs_block = 0;
         x.wide_block = 256;
+        const char* rg = std::getenv("RSAMD_RG4");
+        x.rg4 = rg ? std::atoi(rg) : 1;
         return x;
     }();
     return t;
@@ -456,6 +458,64 @@ __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
     chunk_body<KB, KFIX, MC, ACC, VPT, VAR, kAuxNt, kAuxNt, WIN, LQ, BS>(
         a, lds_tab, cols, ncols_pad, a.rows, cb, a.body / (4 * LQ), [&](int c) { return in_ptr(a, c, s); },
         [&](int r) { return out_ptr(a, cols, r, s); }, [&]() { if (STAGE_LATE) stage(); });
+}
+
+// More than 4 output rows on runtime matrices: groups of 4 rows, one
+// workgroup per (chunk, row group).  Every group's workgroup reads the same
+// input columns; the groups of one chunk get block ids b, b+8, b+16, ...
+// (dispatched together and, with round-robin placement, on one XCD), so the
+// repeated column reads are served by that XCD's L2 and HBM still sees each
+// input byte about once.  Each workgroup is the 4-row kernel (64 VGPRs, 8
+// waves/SIMD) instead of one 8-row body (~150 VGPRs, 3 waves/SIMD) whose
+// VALU work could not hide under the stream.  Block b -> (chunk, group):
+// b = (q / 8) * 8G + g * 8 + q % 8.
+template <int KB, bool KFIX, bool ACC, int LQ, int BS, int LAUX>
+__global__ __launch_bounds__(BS) void gf_matmul_rg4(const MatmulArgs a) {
+    constexpr int MC = 4, COLD = 20;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+    const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32);
+    const int cols = KFIX ? KB : a.cols;
+    const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
+    const uint32_t G = static_cast<uint32_t>(a.row_groups);
+    const uint32_t b = blockIdx.x;
+    const uint32_t hi = b / (8u * G);
+    const uint32_t rem = b - hi * 8u * G;
+    const int g = static_cast<int>(rem >> 3);
+    const uint32_t chunk = hi * 8u + (rem & 7u);
+    if (chunk >= static_cast<uint64_t>(a.total_chunks)) return;  // ragged last octet (uniform)
+    const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
+    const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
+    const int64_t cb = static_cast<int64_t>(chunk - su * cps);
+    const int s = a.stripe_ids ? a.stripe_ids[su] : static_cast<int>(su);
+    const int row0 = 4 * g;
+    const int nrows = (a.rows - row0) < MC ? (a.rows - row0) : MC;
+    for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) {
+        const int i = idx / COLD;
+        const int w = idx - i * COLD;
+        const int rr = w / 5;
+        uint32_t v = 0;
+        if (i < cols && rr < nrows)
+            v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + row0 + rr) * 5 + (w - rr * 5)];
+        lds32[idx] = v;
+    }
+    __syncthreads();
+    chunk_body<KB, KFIX, MC, ACC, 1, kVarDefault, LAUX, kAuxNt, 0, LQ, BS>(
+        a, lds_tab, cols, ncols_pad, nrows, cb, a.body / (4 * LQ), [&](int c) { return in_ptr(a, c, s); },
+        [&](int r) { return out_ptr(a, cols, row0 + r, s); });
+}
+
+typedef void (*Rg4Kernel)(const MatmulArgs);
+template <bool ACC, int LAUX>
+static Rg4Kernel rg4_for_cols(int cols, int* kb, bool* kfix) {
+    if (cols == 10) { *kb = 10; *kfix = true; return gf_matmul_rg4<10, true, ACC, 2, 128, LAUX>; }
+    if (cols == 12) { *kb = 12; *kfix = true; return gf_matmul_rg4<12, true, ACC, 2, 128, LAUX>; }
+    if (cols > 4 && cols <= 8) { *kb = 8; *kfix = false; return gf_matmul_rg4<8, false, ACC, 2, 128, LAUX>; }
+    *kb = 4; *kfix = false;
+    return gf_matmul_rg4<4, false, ACC, 2, 128, LAUX>;
+}
+static Rg4Kernel rg4_kernel(const MatmulArgs& a, int mode, int* kb, bool* kfix) {
+    if (a.accumulate) return mode == 2 ? rg4_for_cols<true, 0>(a.cols, kb, kfix) : rg4_for_cols<true, kAuxNt>(a.cols, kb, kfix);
+    return mode == 2 ? rg4_for_cols<false, 0>(a.cols, kb, kfix) : rg4_for_cols<false, kAuxNt>(a.cols, kb, kfix);
 }
 
 // Multi-pattern mode (rs_reconst_batch_multi): every stripe names a pattern;
@@ -998,6 +1058,34 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
             bk = nullptr;
         }
         if (bk) a.body = 0;  // the vector path below is done; only the tail remains
+    }
+
+    if (a.body && a.rows > 4 && tuning().rg4 && tuning().var < 0 && tuning().vpt == 1 && tuning().max_grid <= 0 &&
+        a.body < (uint64_t{1} << 31)) {
+        // > 4 output rows: 4-row groups on XCD-paired workgroups (gf_matmul_rg4)
+        int kb = 4;
+        bool kfix = false;
+        Rg4Kernel rk = rg4_kernel(a, tuning().rg4, &kb, &kfix);
+        const int bs = 128, lq = 2;
+        a.units_per_chunk = bs;
+        a.nt_store = 1;
+        a.row_groups = (a.rows + 3) / 4;
+        const uint64_t nunits = a.body / (4 * lq);
+        a.chunks_per_stripe = static_cast<int64_t>((nunits + bs - 1) / bs);
+        a.total_chunks = a.chunks_per_stripe * a.nstripes;
+        a.cps_shift = -1;
+        for (int sh = 0; sh < 31; ++sh)
+            if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
+        const uint64_t grid = static_cast<uint64_t>((a.total_chunks + 7) / 8) * 8u * a.row_groups;
+        if (grid <= 0x7fffffffull) {
+            const int ncols_pad = kfix ? kb : ((a.cols + kb - 1) / kb) * kb;
+            const size_t lds = static_cast<size_t>(ncols_pad) * 20 * 4;
+            (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
+            hipLaunchKernelGGL(rk, dim3(static_cast<unsigned>(grid)), dim3(bs), lds, stream, a);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            a.body = 0;  // the vector body is done; only the tail remains
+        }
     }
 
     if (a.body) {
