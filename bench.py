@@ -19,9 +19,9 @@ as a child process, before any GPU call); under a launcher WORLD_SIZE must
 equal N and every rank must join, or the run exits non-zero (`ranks_seen`).
 
 Order per rank: self-check (encode -> erase -> reconst), pre-warm until the
-launch time has settled (at least 60 launches; 10 consecutive within 3 %
-and within 1 % of the 10 before; `prewarm` in the line), W counted warm-up
-steps queued right behind it, K timed steps.
+launch time has settled (at least 250 launches; 20 consecutive within 3 %
+and within 0.5 % of the 20 before; `prewarm` in the line), W counted
+warm-up steps queued right behind it, K timed steps.
 
 Rank 0 prints ONE JSON line.  `value` = (k+m)*vec*S*N*K / max-rank time in
 GiB/s.  `roofline` prices the encode kernel itself: algorithmic bytes per
@@ -67,7 +67,7 @@ def parse_args(argv=None):
     ap.add_argument("--e2e-stripes", type=int, default=128,
                     help="stripes per GPU for the host-resident end-to-end leg (0 = skip)")
     ap.add_argument("--e2e-reps", type=int, default=10)
-    ap.add_argument("--prewarm-min", type=int, default=60,
+    ap.add_argument("--prewarm-min", type=int, default=250,
                     help="pre-warm: at least this many launches before the counted warm-up")
     ap.add_argument("--prewarm-max", type=int, default=2000, help="pre-warm: at most this many launches")
     ap.add_argument("--rehearse-cpu", action="store_true",
@@ -323,8 +323,8 @@ def check_world(args, world: int, launched: bool) -> None:
 
 # ---------------------------------------------------------------- pre-warm
 
-def prewarm(step, stream, min_launches: int, max_launches: int, window: int = 10, tol: float = 0.03,
-            drift: float = 0.01, depth: int = 4, max_seconds: float = 5.0):
+def prewarm(step, stream, min_launches: int, max_launches: int, window: int = 20, tol: float = 0.03,
+            drift: float = 0.005, depth: int = 4, max_seconds: float = 5.0):
     """Run the step until the GPU has reached its steady state.  After an idle
     period of a few ms the encode runs 0.57 -> 0.87 -> 0.57 ms per launch over
     ~30-50 launches (power management; rocprof trace), so a short
@@ -596,9 +596,9 @@ def main(argv=None):
                 "kernel_timing": "HIP event pair on the launch stream around the K timed launches / K",
             },
             "prewarm": {"launches": pw_n, "ms": round(pw_ms, 1), "converged": pw_ok,
-                        "last10_mean_ms": round(pw_mean, 4) if pw_mean else None,
-                        "rule": f"untimed launches (>= {args.prewarm_min}) until 10 consecutive agree within 3 % "
-                                "and their mean within 1 % of the 10 before; the counted warm-up is queued "
+                        "last20_mean_ms": round(pw_mean, 4) if pw_mean else None,
+                        "rule": f"untimed launches (>= {args.prewarm_min}) until 20 consecutive agree within 3 % "
+                                "and their mean within 0.5 % of the 20 before; the counted warm-up is queued "
                                 "behind them with no idle gap"},
         }
         result["end_to_end"] = e2e

@@ -167,6 +167,11 @@ def replace(d, p, data, rows, parity) -> int:
     return lib().orc_replace(d, p, darr, dlens, len(data), r, nr, parr, plens, len(parity))
 
 
+def set_l1d(l1d: int) -> None:
+    """The L1D size the restated getSplitSize (rs.go:158-173) uses; 0 = 32 KiB."""
+    lib().orc_set_l1d(ctypes.c_size_t(int(l1d)))
+
+
 def update_quirk_range(size: int, l1d: int = 32 * 1024):
     """Byte range [lo, hi) where the reference's Update / Replace keep the old
     parity (rs_oracle.c encode_part: the tail pass of rs.go:190-200 covers the

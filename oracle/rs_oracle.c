@@ -191,10 +191,15 @@ uint64_t orc_inverse_cache_key(const int* survived, int ns) {
 }
 
 /* getSplitSize rs.go:158-173 with the default L1D of 32 KiB (cpu.X86.Cache.L1D
- * unknown, rs.go:160-162). For Encode the chunking changes no output byte;
+ * unknown, rs.go:160-162; orc_set_l1d sets another). For Encode the chunking changes no output byte;
  * for Update / Replace (updateOnly) it does, see encode_part. */
+static size_t g_l1d = 32 * 1024;
+/* cpu.X86.Cache.L1D as the reference would read it on another host (tests of
+ * librsamd's rs_tune("ref_update_tail") compat mode); 0 restores 32 KiB. */
+void orc_set_l1d(size_t l1d) { g_l1d = l1d ? l1d : 32 * 1024; }
+
 static size_t split_size(size_t n) {
-    const size_t l1d = 32 * 1024;
+    const size_t l1d = g_l1d;
     if (n < 16) return 16;
     if (n < l1d / 2) return (n >> 4) << 4;
     return l1d / 2;

@@ -76,4 +76,7 @@ void orc_naive_mul(const uint8_t* gen, int input, int output, uint8_t* const* ve
 int  orc_has_avx2(void);
 int  orc_encode_avx2(int d, int p, uint8_t* const* vects, size_t size);
 
+/* L1D size the restated getSplitSize uses (rs.go:158-173; default 32 KiB). */
+void orc_set_l1d(size_t l1d);
+
 #endif

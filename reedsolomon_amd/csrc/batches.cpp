@@ -266,9 +266,13 @@ int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8
         if (!old_data || !new_data) return RS_ERR_INVAL;
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
-        const uint8_t* in[2] = {old_data, new_data};
         std::vector<uint8_t> gm = update_matrix(rs, row);
-        return matmul(rs, gm.data(), rs->p, 2, in, 0, parity, 0, 1, new_len, true, as_stream(stream));
+        return update_ranges(new_len, [&](uint64_t off, uint64_t n) {
+            const uint8_t* in[2] = {old_data + off, new_data + off};
+            uint8_t* out[kMaxVects];
+            for (int j = 0; j < rs->p; ++j) out[j] = parity[j] + off;
+            return matmul(rs, gm.data(), rs->p, 2, in, 0, out, 0, 1, n, true, as_stream(stream));
+        });
     });
 }
 
@@ -283,17 +287,17 @@ int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride, const
         if (!old_base || !new_base || !base) return RS_ERR_INVAL;
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
-        const uint8_t* in[2] = {old_base, new_base};
         const uint8_t isid[2] = {0, 1};
-        uint8_t* out[kMaxVects];
         uint8_t osid[kMaxVects];
-        for (int j = 0; j < rs->p; ++j) {
-            out[j] = base + (rs->d + j) * vect_stride;
-            osid[j] = 2;
-        }
+        for (int j = 0; j < rs->p; ++j) osid[j] = 2;
         const int64_t ss[4] = {old_stride, new_stride, stripe_stride, 0};
         std::vector<uint8_t> gm = update_matrix(rs, row);
-        return matmul_ex(rs, gm.data(), rs->p, 2, in, isid, out, osid, ss, nstripes, len, true, as_stream(stream));
+        return update_ranges(len, [&](uint64_t off, uint64_t n) {
+            const uint8_t* in[2] = {old_base + off, new_base + off};
+            uint8_t* out[kMaxVects];
+            for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride + off;
+            return matmul_ex(rs, gm.data(), rs->p, 2, in, isid, out, osid, ss, nstripes, n, true, as_stream(stream));
+        });
     });
 }
 
@@ -307,7 +311,13 @@ int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-        return matmul(rs, gm.data(), rs->p, nr, data, 0, parity, 0, 1, data_lens[0], true, as_stream(stream));
+        return update_ranges(data_lens[0], [&](uint64_t off, uint64_t n) {
+            const uint8_t* in[kMaxVects];
+            uint8_t* out[kMaxVects];
+            for (int i = 0; i < nr; ++i) in[i] = data[i] + off;
+            for (int j = 0; j < rs->p; ++j) out[j] = parity[j] + off;
+            return matmul(rs, gm.data(), rs->p, nr, in, 0, out, 0, 1, n, true, as_stream(stream));
+        });
     });
 }
 
@@ -325,13 +335,15 @@ int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_stripe_str
         if (!data_base || !base) return RS_ERR_INVAL;
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
-        const uint8_t* in[kMaxVects];
-        uint8_t* out[kMaxVects];
-        for (int i = 0; i < nr; ++i) in[i] = data_base + i * data_vect_stride;
-        for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride;
         std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-        return matmul(rs, gm.data(), rs->p, nr, in, data_stripe_stride, out, stripe_stride, nstripes, len, true,
-                      as_stream(stream));
+        return update_ranges(len, [&](uint64_t off, uint64_t n) {
+            const uint8_t* in[kMaxVects];
+            uint8_t* out[kMaxVects];
+            for (int i = 0; i < nr; ++i) in[i] = data_base + i * data_vect_stride + off;
+            for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride + off;
+            return matmul(rs, gm.data(), rs->p, nr, in, data_stripe_stride, out, stripe_stride, nstripes, n, true,
+                          as_stream(stream));
+        });
     });
 }
 

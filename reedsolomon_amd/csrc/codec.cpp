@@ -366,6 +366,19 @@ int check_replace(const rs_t* rs, const size_t* dlens, int nd, const int* rows, 
 
 // Update's matrix: p x 2, both columns G[j][row] (g*old ^ g*new == g*(old^new),
 // so xorsimd's step rs.go:432-433 folds into the product).
+int g_ref_update_tail = 0;
+
+bool ref_update_skip(uint64_t size, uint64_t* lo, uint64_t* hi) {
+    if (g_ref_update_tail <= 0) return false;
+    const uint64_t split = static_cast<uint64_t>(g_ref_update_tail) / 2;  // getSplitSize rs.go:158-173
+    if (size < split) return false;  // chunks of (n>>4)<<4 bytes, then a < 16-byte tail on its own
+    const uint64_t last = size % split;
+    if (last < 16 || (last & 15) == 0) return false;
+    *lo = size - last;
+    *hi = *lo + (last & ~uint64_t{15});
+    return true;
+}
+
 std::vector<uint8_t> update_matrix(const rs_t* rs, int row) {
     std::vector<uint8_t> m(static_cast<size_t>(rs->p) * 2);
     for (int j = 0; j < rs->p; ++j) m[2 * j] = m[2 * j + 1] = rs->gen()[static_cast<size_t>(j) * rs->d + row];
@@ -501,6 +514,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "bitslice") t.bitslice = value ? 1 : 0;
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
+        else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
         else if (n == "rg4") t.rg4 = (value == 1 || value == 2) ? value : 0;
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);

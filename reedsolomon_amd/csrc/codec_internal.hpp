@@ -301,6 +301,27 @@ int check_replace(const rs_t* rs, const size_t* dlens, int nd, const int* rows, 
 std::vector<uint8_t> update_matrix(const rs_t* rs, int row);
 std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr);
 
+// Reference-compat mode for Update / Replace (rs_tune("ref_update_tail",
+// l1d_bytes); 0 = off, the default).  The reference's encodePart
+// (rs.go:175-203) runs its sub-16-byte tail pass over the WHOLE last chunk
+// [start, end) of getSplitSize (rs.go:158-173: L1D/2 bytes), so under
+// updateOnly (Update rs.go:447, Replace rs.go:527) that chunk's 16-byte body
+// is XORed twice and keeps its old parity.  With the mode on, the product
+// skips exactly that byte range [lo, hi) for the given L1D size, so the
+// parity bytes equal the reference's on a host with that L1D.  Returns false
+// when the size has no such range (or the mode is off).
+extern int g_ref_update_tail;
+bool ref_update_skip(uint64_t size, uint64_t* lo, uint64_t* hi);
+// Run op(offset, length) over [0, size) minus the skipped range.
+template <class Op>
+int update_ranges(uint64_t size, Op op) {
+    uint64_t lo = 0, hi = 0;
+    if (!ref_update_skip(size, &lo, &hi)) return op(uint64_t{0}, size);
+    if (lo > 0) RS_TRY(op(uint64_t{0}, lo));
+    if (hi < size) RS_TRY(op(hi, size - hi));
+    return RS_OK;
+}
+
 // Reconst on one stripe whose vectors are addressed by `ptr` (host staging
 // slots or caller device pointers).  Shared by rs_reconst / rs_reconst_dev /
 // rs_reconst_batch.  `before_parity` lets the host path copy the rebuilt data

@@ -509,9 +509,13 @@ int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* 
         if (!old_data || !new_data) return RS_ERR_INVAL;
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
-        const uint8_t* src[2] = {old_data, new_data};
         std::vector<uint8_t> gm = update_matrix(rs, row);
-        return host_call(rs, gm.data(), rs->p, 2, src, parity, new_len, true);
+        return update_ranges(new_len, [&](uint64_t off, uint64_t n) {
+            const uint8_t* src[2] = {old_data + off, new_data + off};
+            uint8_t* dst[kMaxVects];
+            for (int j = 0; j < rs->p; ++j) dst[j] = parity[j] + off;
+            return host_call(rs, gm.data(), rs->p, 2, src, dst, n, true);
+        });
     });
 }
 
@@ -525,7 +529,13 @@ int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, in
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-        return host_call(rs, gm.data(), rs->p, nr, data, parity, data_lens[0], true);
+        return update_ranges(data_lens[0], [&](uint64_t off, uint64_t n) {
+            const uint8_t* src[kMaxVects];
+            uint8_t* dst[kMaxVects];
+            for (int i = 0; i < nr; ++i) src[i] = data[i] + off;
+            for (int j = 0; j < rs->p; ++j) dst[j] = parity[j] + off;
+            return host_call(rs, gm.data(), rs->p, nr, src, dst, n, true);
+        });
     });
 }
 

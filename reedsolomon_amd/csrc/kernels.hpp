@@ -36,7 +36,6 @@ struct MatmulArgs {
     int64_t chunks_per_stripe;
     int64_t total_chunks;
     int cps_shift;            // log2(chunks_per_stripe) when a power of two, else -1
-    int row_groups;           // gf_matmul_rg4: groups of <= 4 output rows, one workgroup each per chunk
     uint64_t ptr[kMaxPtrs];   // inputs [0, cols), outputs [cols, cols+rows)
     uint32_t sid[kMaxPtrs];   // stride selector of each vector (0..3); dwords so the
                               // kernel reads them with scalar loads
@@ -67,8 +66,8 @@ struct LaunchTuning {
     int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
     int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
-    int rg4;          // > 4 output rows: 4-row groups on XCD-paired workgroups (1: nt loads, 2: default
-                      // policy loads, 0: one workgroup holds every row)
+    int rg4;          // 5-16 output rows: 4-row lane groups sharing a chunk (1: default-policy loads,
+                      // 2: nt loads, 0: one lane holds every row)
 };
 LaunchTuning& tuning();
 

@@ -101,8 +101,25 @@ def test_encode_batch_vs_oracle(rslib, orc, torch_dev):
         assert np.array_equal(got[:, :d], host[:, :d])
 
 
+def _check_every_stripe(orc, d, p, buf, batch=16):
+    """Every stripe of a device batch [S, d+p, n] against the oracle's AVX2
+    restatement of the reference's encode (orc.encode_avx2, pinned to the
+    table path by tests/test_oracle.py), copied back `batch` stripes at a time."""
+    S, n = buf.shape[0], buf.shape[2]
+    for s0 in range(0, S, batch):
+        host = buf[s0:s0 + batch].cpu().numpy()
+        for k in range(host.shape[0]):
+            v = [np.ascontiguousarray(host[k, i]) for i in range(d)] + [np.zeros(n, np.uint8) for _ in range(p)]
+            orc.encode_avx2(d, p, v)
+            for j in range(p):
+                if not np.array_equal(host[k, d + j], v[d + j]):
+                    raise AssertionError(("stripe", s0 + k, "parity", j, _first_diff(host[k, d + j], v[d + j])))
+
+
 def test_encode_batch_full_size_round_trip(rslib, orc, torch_dev):
-    """BASELINE config 2 at full size: 256 stripes x (10+4) x 1 MiB (3.5 GiB)."""
+    """BASELINE config 2 at full size: 256 stripes x (10+4) x 1 MiB (3.5 GiB),
+    every stripe against the oracle, then an erase / rebuild round trip and
+    linearity."""
     torch = torch_dev
     d, p, S, n = 10, 4, 256, 1 << 20
     r = rslib.New(d, p)
@@ -111,12 +128,7 @@ def test_encode_batch_full_size_round_trip(rslib, orc, torch_dev):
     buf[:, d:] = 0xA5
     r.encode_batch(buf)
     torch.cuda.synchronize()
-    # spot-check stripes against the oracle
-    for s in (0, 137, S - 1):
-        host = buf[s].cpu().numpy()
-        exp = _oracle_encode(orc, d, p, [host[i].copy() for i in range(d)])
-        for j in range(p):
-            assert np.array_equal(host[d + j], exp[j]), (s, j)
+    _check_every_stripe(orc, d, p, buf)
     # erase 4 vectors of every stripe (two data, two parity), rebuild, compare
     ref = buf.clone()
     lost = [0, 7, 11, 13]
@@ -132,6 +144,20 @@ def test_encode_batch_full_size_round_trip(rslib, orc, torch_dev):
     r.encode_batch(c)
     torch.cuda.synchronize()
     assert torch.equal(c[:, d:], a[:, d:] ^ b[:, d:])
+
+
+def test_encode_12_4_full_size_every_stripe(rslib, orc, torch_dev):
+    """BASELINE config 4 per GPU at full size: 256 stripes x (12+4) x 1 MiB
+    (4 GiB), split layout as bench.py runs it, every stripe against the oracle."""
+    torch = torch_dev
+    d, p, S, n = 12, 4, 256, 1 << 20
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(0x5EED + 12)
+    data = torch.randint(0, 256, (S, d, n), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    torch.cuda.synchronize()
+    _check_every_stripe(orc, d, p, torch.cat([data, parity], dim=1))
 
 
 def test_encode_dev_single_stripe(rslib, orc, torch_dev):

@@ -204,6 +204,72 @@ def test_update_replace_at_reference_defect_sizes(rslib, orc, torch_dev, size):
     _check_update_like(orc, act, ora, exp, d, p, size, ("replace", size))
 
 
+@pytest.mark.parametrize("l1d,size", [(32768, 17031), (32768, 49263), (32768, 236667), (49152, 24576 + 33),
+                                      (49152, 3 * 24576 + 1000 + 5), (32768, 16384 * 3)])
+def test_update_replace_reference_compat_mode(rslib, orc, torch_dev, l1d, size):
+    """rs_tune("ref_update_tail", l1d) reproduces the reference's Update /
+    Replace bytes (rs.go:190-200 tail pass, rs_oracle.c encode_part) on a host
+    whose L1D is `l1d`: host API, single-stripe device call and device batch,
+    byte for byte against the restated reference with the same L1D.  The last
+    size has no defect range (a whole number of chunks): compat = re-encode."""
+    torch = torch_dev
+    L = rslib.lib()
+    d, p, row, rows = 10, 4, 3, [1, 6, 9]
+    rng = np.random.default_rng(size + l1d)
+    data = [_rand(rng, size) for _ in range(d)]
+    enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+    assert orc.encode(d, p, enc) == 0
+    new = _rand(rng, size)
+    r = rslib.New(d, p)
+    assert L.rs_tune(b"ref_update_tail", l1d) == 0
+    orc.set_l1d(l1d)
+    try:
+        # Update: restated reference, then each librsamd entry point
+        ora = [x.copy() for x in enc]
+        assert orc.update(d, p, ora[row], new, row, ora[d:]) == 0
+        q = orc.update_quirk_range(size, l1d)
+        if q is not None:  # the defect is real at this size: some parity byte differs from re-encoding
+            reenc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            reenc[row] = new.copy()
+            assert orc.encode(d, p, reenc) == 0
+            assert any(not np.array_equal(ora[j], reenc[j]) for j in range(d, d + p))
+        act = [x.copy() for x in enc]
+        r.Update(act[row], new, row, act[d:])
+        dv = [torch.from_numpy(x.copy()).cuda() for x in enc]
+        r.update_dev(dv[row], torch.from_numpy(new.copy()).cuda(), row, dv[d:])
+        S = 3
+        buf = torch.from_numpy(np.stack([np.stack(enc)] * S)).cuda()
+        old_b = buf[:, row].clone()
+        new_b = torch.from_numpy(np.stack([new] * S)).cuda()
+        r.update_batch(old_b, new_b, row, buf)
+        torch.cuda.synchronize()
+        for j in range(d, d + p):
+            assert np.array_equal(act[j], ora[j]), ("Update", l1d, size, j)
+            assert np.array_equal(dv[j].cpu().numpy(), ora[j]), ("update_dev", l1d, size, j)
+            for s_ in range(S):
+                assert np.array_equal(buf[s_, j].cpu().numpy(), ora[j]), ("update_batch", l1d, size, s_, j)
+        # Replace of three rows
+        delta = [_rand(rng, size) for _ in rows]
+        ora = [x.copy() for x in enc]
+        assert orc.replace(d, p, [x.copy() for x in delta], rows, ora[d:]) == 0
+        act = [x.copy() for x in enc]
+        r.Replace([x.copy() for x in delta], rows, act[d:])
+        dv = [torch.from_numpy(x.copy()).cuda() for x in enc]
+        r.replace_dev([torch.from_numpy(x.copy()).cuda() for x in delta], rows, dv[d:])
+        buf = torch.from_numpy(np.stack([np.stack(enc)] * S)).cuda()
+        dl = torch.from_numpy(np.stack([np.stack(delta)] * S)).cuda()
+        r.replace_batch(dl, rows, buf)
+        torch.cuda.synchronize()
+        for j in range(d, d + p):
+            assert np.array_equal(act[j], ora[j]), ("Replace", l1d, size, j)
+            assert np.array_equal(dv[j].cpu().numpy(), ora[j]), ("replace_dev", l1d, size, j)
+            for s_ in range(S):
+                assert np.array_equal(buf[s_, j].cpu().numpy(), ora[j]), ("replace_batch", l1d, size, s_, j)
+    finally:
+        L.rs_tune(b"ref_update_tail", 0)
+        orc.set_l1d(0)
+
+
 def _padded(torch, rng, S, nvec, n, device):
     """[S, nvec, n] view of a larger random buffer (padding between vectors and
     stripes, sometimes an odd vector stride: the unaligned / byte-kernel paths)."""

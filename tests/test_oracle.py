@@ -340,3 +340,32 @@ def test_bitslice_generator_matches_oracle(orc):
             assert prod == mul[c, x], (c, x)
     with open(gen.OUT) as f:
         assert f.read() == gen.emit(), "bitslice_gen.inc is stale: run python tools/gen_bitslice.py"
+
+
+def test_oracle_l1d_setting_moves_the_defect(orc):
+    """orc_set_l1d (getSplitSize's L1D, rs.go:158-173) moves the Update tail
+    defect exactly to update_quirk_range(size, l1d)."""
+    d, p, row = 4, 2, 1
+    rng = np.random.default_rng(5)
+    for l1d, size in [(49152, 24576 + 33), (32768, 24576 + 33), (65536, 3 * 32768 + 47)]:
+        data = [rng.integers(0, 256, size, dtype=np.uint8) for _ in range(d)]
+        enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+        assert orc.encode(d, p, enc) == 0
+        new = rng.integers(0, 256, size, dtype=np.uint8)
+        reenc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+        reenc[row] = new.copy()
+        assert orc.encode(d, p, reenc) == 0
+        orc.set_l1d(l1d)
+        try:
+            ora = [x.copy() for x in enc]
+            assert orc.update(d, p, ora[row], new, row, ora[d:]) == 0
+        finally:
+            orc.set_l1d(0)
+        q = orc.update_quirk_range(size, l1d)
+        for j in range(d, d + p):
+            diff = np.flatnonzero(ora[j] != reenc[j])
+            if q is None:
+                assert diff.size == 0, (l1d, size)
+            else:
+                assert diff.size and diff.min() >= q[0] and diff.max() < q[1], (l1d, size)
+                assert np.array_equal(ora[j][q[0]:q[1]], enc[j][q[0]:q[1]])  # stale parity kept
