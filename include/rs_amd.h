@@ -321,10 +321,7 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * per workgroup of the 8-byte-lane kernels: 128 default | 256), "bitslice"
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
- * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "rg4" (5-16
- * output rows on runtime matrices: 1 = 4-row lane groups of one workgroup
- * sharing a chunk, default-policy loads | 2 = the same with nt loads | 0 =
- * one lane holds every row), "wide_block" (128 | 256),
+ * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "wide_block" (128 | 256),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;

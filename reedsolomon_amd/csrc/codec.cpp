@@ -515,7 +515,6 @@ int rs_tune(const char* name, int value) {
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
         else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
-        else if (n == "rg4") t.rg4 = (value == 1 || value == 2) ? value : 0;
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;

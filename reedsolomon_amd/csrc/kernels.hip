@@ -62,8 +62,6 @@ LaunchTuning& tuning() {
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
         x.bs_block = 0;
         x.wide_block = 256;
-        const char* rg = std::getenv("RSAMD_RG4");
-        x.rg4 = rg ? std::atoi(rg) : 1;
         return x;
     }();
     return t;
@@ -200,7 +198,7 @@ __device__ __forceinline__ void chunk_body(const MatmulArgs& a, const lds_u32x4*
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;  // dwords per column in LDS (16-B multiple)
     constexpr int COLW = COLD / 4;                // 16-byte LDS words per column
     typedef typename LaneWord<LQ>::type W;  // the lane's unit: 4*LQ bytes of one vector
-    const int tid = static_cast<int>(threadIdx.x) % BS;  // lane within its group (gf_matmul_rgw: G groups)
+    const int tid = threadIdx.x;
     uint64_t off[VPT];
     bool ok[VPT];
 #pragma unroll
@@ -458,71 +456,6 @@ __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
     chunk_body<KB, KFIX, MC, ACC, VPT, VAR, kAuxNt, kAuxNt, WIN, LQ, BS>(
         a, lds_tab, cols, ncols_pad, a.rows, cb, a.body / (4 * LQ), [&](int c) { return in_ptr(a, c, s); },
         [&](int r) { return out_ptr(a, cols, r, s); }, [&]() { if (STAGE_LATE) stage(); });
-}
-
-// More than 4 output rows on runtime matrices: groups of 4 rows inside one
-// workgroup.  A workgroup of G x 128 lanes covers one 1 KiB chunk of every
-// vector; lane group h (threads [128h, 128h+128)) computes rows 4h..4h+3
-// with the 4-row body (64 VGPRs) and its own LDS table image.  Every group
-// loads the same column bytes at the same addresses: with default-policy
-// loads the CU's L1 (or its XCD's L2) serves the repeats, so HBM sees each
-// input byte once while each wave keeps the register budget of the 4-row
-// kernel.
-template <int KB, bool KFIX, bool ACC, int G, int LAUX>
-__global__ __launch_bounds__(128 * G) void gf_matmul_rgw(const MatmulArgs a) {
-    constexpr int MC = 4, COLD = 20, BS = 128, LQ = 2;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
-    const int cols = KFIX ? KB : a.cols;
-    const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
-    const int h = static_cast<int>(threadIdx.x) / BS;  // lane group (wave-uniform)
-    const uint32_t chunk = blockIdx.x;
-    const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
-    const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
-    const int64_t cb = static_cast<int64_t>(chunk - su * cps);
-    const int s = a.stripe_ids ? a.stripe_ids[su] : static_cast<int>(su);
-    // every group's table image: group hh, column i, row rr -> lds32[(hh*ncols_pad + i)*20 + rr*5 + e]
-    for (int idx = threadIdx.x; idx < G * ncols_pad * COLD; idx += G * BS) {
-        const int hc = idx / COLD;
-        const int hh = hc / ncols_pad;
-        const int i = hc - hh * ncols_pad;
-        const int w = idx - hc * COLD;
-        const int rr = w / 5;
-        const int row = 4 * hh + rr;
-        uint32_t v = 0;
-        if (i < cols && rr < MC && row < a.rows)
-            v = a.tables[(static_cast<int64_t>(i) * a.rows_pad + row) * 5 + (w - rr * 5)];
-        lds32[idx] = v;
-    }
-    __syncthreads();
-    const int row0 = 4 * h;
-    if (row0 >= a.rows) return;  // idle group of the last (partial) row group: uniform per group
-    const int nrows = (a.rows - row0) < MC ? (a.rows - row0) : MC;
-    const lds_u32x4* lds_tab = (const lds_u32x4*)(lds32 + h * ncols_pad * COLD);
-    chunk_body<KB, KFIX, MC, ACC, 1, kVarDefault, LAUX, kAuxNt, 0, LQ, BS>(
-        a, lds_tab, cols, ncols_pad, nrows, cb, a.body / (4 * LQ), [&](int c) { return in_ptr(a, c, s); },
-        [&](int r) { return out_ptr(a, cols, row0 + r, s); });
-}
-
-typedef void (*RgKernel)(const MatmulArgs);
-template <bool ACC, int G, int LAUX>
-static RgKernel rgw_for_cols(int cols, int* kb, bool* kfix) {
-    if (cols == 10) { *kb = 10; *kfix = true; return gf_matmul_rgw<10, true, ACC, G, LAUX>; }
-    if (cols == 12) { *kb = 12; *kfix = true; return gf_matmul_rgw<12, true, ACC, G, LAUX>; }
-    if (cols > 4 && cols <= 8) { *kb = 8; *kfix = false; return gf_matmul_rgw<8, false, ACC, G, LAUX>; }
-    *kb = 4; *kfix = false;
-    return gf_matmul_rgw<4, false, ACC, G, LAUX>;
-}
-template <bool ACC, int LAUX>
-static RgKernel rgw_for(int groups, int cols, int* kb, bool* kfix) {
-    if (groups == 2) return rgw_for_cols<ACC, 2, LAUX>(cols, kb, kfix);
-    if (groups == 3) return rgw_for_cols<ACC, 3, LAUX>(cols, kb, kfix);
-    return rgw_for_cols<ACC, 4, LAUX>(cols, kb, kfix);
-}
-// mode 1: default-policy loads (L1 shares the repeats), 2: nt loads
-static RgKernel rg_kernel(const MatmulArgs& a, int mode, int groups, int* kb, bool* kfix) {
-    if (a.accumulate)
-        return mode == 2 ? rgw_for<true, kAuxNt>(groups, a.cols, kb, kfix) : rgw_for<true, 0>(groups, a.cols, kb, kfix);
-    return mode == 2 ? rgw_for<false, kAuxNt>(groups, a.cols, kb, kfix) : rgw_for<false, 0>(groups, a.cols, kb, kfix);
 }
 
 // Multi-pattern mode (rs_reconst_batch_multi): every stripe names a pattern;
@@ -1065,33 +998,6 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
             bk = nullptr;
         }
         if (bk) a.body = 0;  // the vector path below is done; only the tail remains
-    }
-
-    if (a.body && a.rows > 4 && a.rows <= 16 && tuning().rg4 && tuning().var < 0 && tuning().vpt == 1 &&
-        tuning().max_grid <= 0 && a.body < (uint64_t{1} << 31)) {
-        // 5-16 output rows: 4-row lane groups sharing one chunk (gf_matmul_rgw)
-        const int groups = (a.rows + 3) / 4;
-        int kb = 4;
-        bool kfix = false;
-        RgKernel rk = rg_kernel(a, tuning().rg4, groups, &kb, &kfix);
-        const int lanes = 128, lq = 2;
-        a.units_per_chunk = lanes;
-        a.nt_store = 1;
-        const uint64_t nunits = a.body / (4 * lq);
-        a.chunks_per_stripe = static_cast<int64_t>((nunits + lanes - 1) / lanes);
-        a.total_chunks = a.chunks_per_stripe * a.nstripes;
-        a.cps_shift = -1;
-        for (int sh = 0; sh < 31; ++sh)
-            if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
-        if (a.total_chunks <= 0x7fffffff) {
-            const int ncols_pad = kfix ? kb : ((a.cols + kb - 1) / kb) * kb;
-            const size_t lds = static_cast<size_t>(groups) * ncols_pad * 20 * 4;
-            (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
-            hipLaunchKernelGGL(rk, dim3(static_cast<unsigned>(a.total_chunks)), dim3(lanes * groups), lds, stream, a);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-            a.body = 0;  // the vector body is done; only the tail remains
-        }
     }
 
     if (a.body) {

@@ -66,8 +66,6 @@ struct LaunchTuning {
     int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
     int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
-    int rg4;          // 5-16 output rows: 4-row lane groups sharing a chunk (1: default-policy loads,
-                      // 2: nt loads, 0: one lane holds every row)
 };
 LaunchTuning& tuning();
 

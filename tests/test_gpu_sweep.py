@@ -545,88 +545,82 @@ def test_bitsliced_workgroup_sizes(rslib, orc, torch_dev, bs_block):
         L.rs_tune(b"bs_block", 0)
 
 
-@pytest.mark.parametrize("rg4", [1, 2, 0])
-def test_row_group_kernels(rslib, orc, torch_dev, rg4):
-    """More than 4 output rows on runtime matrices (rs_tune("rg4")): groups of
-    4 rows on XCD-paired workgroups (1: nt loads, 2: default-policy loads) and
-    the one-workgroup-per-chunk kernels (0), against the oracle: the generic
-    product (overwrite and accumulate, 5..20 rows, ragged and tail sizes, a
-    device stripe-id list through multi-pattern Reconst), Encode of shapes with
-    no generated network, Reconst of 5..8 lost vectors, Update and Replace
-    with 8 parity rows."""
+def test_many_row_runtime_matrices(rslib, orc, torch_dev):
+    """More than 4 output rows on runtime matrices (the 8-row one-chunk
+    kernels and, above 8 rows, the row-group loop), against the oracle: the
+    generic product (overwrite and accumulate, 5..20 rows, ragged and tail
+    sizes), Encode of shapes with no generated network, Reconst of 5..8 lost
+    vectors, Update and Replace with 8 parity rows, and multi-pattern Reconst
+    whose > 4-output patterns run over a device stripe-id list."""
     torch = torch_dev
-    L = rslib.lib()
-    assert L.rs_tune(b"rg4", rg4) == 0
-    try:
-        rng = np.random.default_rng(700 + rg4)
-        r = rslib.New(10, 8)
-        for rows, cols, S, n, acc in [(5, 10, 6, 8192, False), (8, 10, 5, 65536 + 16, True), (6, 12, 4, 4096 + 7, False),
-                                      (7, 7, 3, 2048, True), (8, 16, 4, 40960, False), (13, 3, 3, 1 << 16, True),
-                                      (20, 20, 2, 8192 + 48, False), (9, 1, 7, 16, True)]:
-            mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
-            src = torch.from_numpy(rng.integers(0, 256, (S, cols, n), dtype=np.uint8)).cuda()
-            init = rng.integers(0, 256, (S, rows, n), dtype=np.uint8)
-            dst = torch.from_numpy(init.copy()).cuda()
-            r.gf_matmul_batch(mat, src, None, dst, None, accumulate=acc)
-            torch.cuda.synchronize()
-            exp = orc.encode_numpy(mat, src.cpu().numpy())
-            if acc:
-                exp ^= init
-            assert np.array_equal(dst.cpu().numpy(), exp), (rows, cols, S, n, acc, rg4)
-        for d, p in [(16, 8), (7, 6), (20, 5)]:  # no generated network: runtime-matrix Encode
-            rs_ = rslib.New(d, p)
-            S, n = 5, 65536 + 32
-            data = torch.from_numpy(rng.integers(0, 256, (S, d, n), dtype=np.uint8)).cuda()
-            par = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
-            rs_.encode_batch_split(data, par)
-            torch.cuda.synchronize()
-            exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), data.cpu().numpy())
-            assert np.array_equal(par.cpu().numpy(), exp), (d, p, rg4)
-        for d, p in [(10, 8), (12, 8)]:  # Reconst of 5..8 lost (data and parity)
-            rs_ = rslib.New(d, p)
-            S, n = 6, 32768 + 48
-            buf = torch.from_numpy(rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)).cuda()
-            rs_.encode_batch(buf)
-            ref = buf.clone()
-            for k in range(5, p + 1):
-                lost = sorted(int(v) for v in rng.choice(d + p, k, replace=False))
-                buf[:, lost] = 0x77
-                rs_.reconst_batch(buf, [], lost)
-                torch.cuda.synchronize()
-                assert torch.equal(buf, ref), (d, p, lost, rg4)
-            # Update of one row, Replace of 3 rows, against re-encoding
-            new = torch.from_numpy(rng.integers(0, 256, (S, n), dtype=np.uint8)).cuda()
-            rs_.update_batch(buf[:, 2].clone(), new, 2, buf)
-            buf[:, 2] = new
-            exp = buf.clone()
-            rs_.encode_batch(exp)
-            torch.cuda.synchronize()
-            assert torch.equal(buf, exp), (d, p, "update", rg4)
-            rows = [1, 4, 7]
-            delta = torch.from_numpy(rng.integers(0, 256, (S, 3, n), dtype=np.uint8)).cuda()
-            rs_.replace_batch(delta, rows, buf)
-            for k_, rr in enumerate(rows):
-                buf[:, rr] ^= delta[:, k_]
-            exp = buf.clone()
-            rs_.encode_batch(exp)
-            torch.cuda.synchronize()
-            assert torch.equal(buf, exp), (d, p, "replace", rg4)
-        # multi-pattern Reconst: stripes losing > 4 vectors run per-pattern
-        # launches over a device stripe-id list
-        d, p, S, n = 10, 8, 40, 16384
-        rs_ = rslib.New(d, p)
-        data = torch.from_numpy(rng.integers(0, 256, (S, d, n), dtype=np.uint8)).cuda()
-        par = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
-        rs_.encode_batch_split(data, par)
-        ref_d, ref_p = data.clone(), par.clone()
-        masks = np.zeros(S, np.uint64)
-        for s in range(1, S, 3):
-            for v in rng.choice(d + p, int(rng.integers(5, p + 1)), replace=False):
-                v = int(v)
-                masks[s] |= np.uint64(1) << np.uint64(v)
-                (data[s, v] if v < d else par[s, v - d]).fill_(0x99)
-        rs_.reconst_batch_multi(data, par, masks)
+    rng = np.random.default_rng(700)
+    r = rslib.New(10, 8)
+    for rows, cols, S, n, acc in [(5, 10, 6, 8192, False), (8, 10, 5, 65536 + 16, True), (6, 12, 4, 4096 + 7, False),
+                                  (7, 7, 3, 2048, True), (8, 16, 4, 40960, False), (13, 3, 3, 1 << 16, True),
+                                  (20, 20, 2, 8192 + 48, False), (9, 1, 7, 16, True)]:
+        mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
+        src = torch.from_numpy(rng.integers(0, 256, (S, cols, n), dtype=np.uint8)).cuda()
+        init = rng.integers(0, 256, (S, rows, n), dtype=np.uint8)
+        dst = torch.from_numpy(init.copy()).cuda()
+        r.gf_matmul_batch(mat, src, None, dst, None, accumulate=acc)
         torch.cuda.synchronize()
-        assert torch.equal(data, ref_d) and torch.equal(par, ref_p), rg4
-    finally:
-        L.rs_tune(b"rg4", 1)
+        exp = orc.encode_numpy(mat, src.cpu().numpy())
+        if acc:
+            exp ^= init
+        assert np.array_equal(dst.cpu().numpy(), exp), (rows, cols, S, n, acc)
+    for d, p in [(16, 8), (7, 6), (20, 5)]:  # no generated network: runtime-matrix Encode
+        rs_ = rslib.New(d, p)
+        S, n = 5, 65536 + 32
+        data = torch.from_numpy(rng.integers(0, 256, (S, d, n), dtype=np.uint8)).cuda()
+        par = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
+        rs_.encode_batch_split(data, par)
+        torch.cuda.synchronize()
+        exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), data.cpu().numpy())
+        assert np.array_equal(par.cpu().numpy(), exp), (d, p)
+    for d, p in [(10, 8), (12, 8)]:  # Reconst of 5..8 lost (data and parity)
+        rs_ = rslib.New(d, p)
+        S, n = 6, 32768 + 48
+        buf = torch.from_numpy(rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)).cuda()
+        rs_.encode_batch(buf)
+        ref = buf.clone()
+        for k in range(5, p + 1):
+            lost = sorted(int(v) for v in rng.choice(d + p, k, replace=False))
+            buf[:, lost] = 0x77
+            rs_.reconst_batch(buf, [], lost)
+            torch.cuda.synchronize()
+            assert torch.equal(buf, ref), (d, p, lost)
+        # Update of one row, Replace of 3 rows, against re-encoding
+        new = torch.from_numpy(rng.integers(0, 256, (S, n), dtype=np.uint8)).cuda()
+        rs_.update_batch(buf[:, 2].clone(), new, 2, buf)
+        buf[:, 2] = new
+        exp = buf.clone()
+        rs_.encode_batch(exp)
+        torch.cuda.synchronize()
+        assert torch.equal(buf, exp), (d, p, "update")
+        rows = [1, 4, 7]
+        delta = torch.from_numpy(rng.integers(0, 256, (S, 3, n), dtype=np.uint8)).cuda()
+        rs_.replace_batch(delta, rows, buf)
+        for k_, rr in enumerate(rows):
+            buf[:, rr] ^= delta[:, k_]
+        exp = buf.clone()
+        rs_.encode_batch(exp)
+        torch.cuda.synchronize()
+        assert torch.equal(buf, exp), (d, p, "replace")
+    # multi-pattern Reconst: stripes losing > 4 vectors run per-pattern
+    # launches over a device stripe-id list
+    d, p, S, n = 10, 8, 40, 16384
+    rs_ = rslib.New(d, p)
+    data = torch.from_numpy(rng.integers(0, 256, (S, d, n), dtype=np.uint8)).cuda()
+    par = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
+    rs_.encode_batch_split(data, par)
+    ref_d, ref_p = data.clone(), par.clone()
+    masks = np.zeros(S, np.uint64)
+    for s in range(1, S, 3):
+        for v in rng.choice(d + p, int(rng.integers(5, p + 1)), replace=False):
+            v = int(v)
+            masks[s] |= np.uint64(1) << np.uint64(v)
+            (data[s, v] if v < d else par[s, v - d]).fill_(0x99)
+    rs_.reconst_batch_multi(data, par, masks)
+    torch.cuda.synchronize()
+    assert torch.equal(data, ref_d) and torch.equal(par, ref_p)
+

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Reconcile a bench.py line with the rocprofv3 kernel trace of the same run.
+
+    python tools/trace_window.py <kt_kernel_trace.csv> <bench log with the JSON line> [out.json]
+
+Takes the device-resident encode launches (the kernel and grid of the bench's
+step: the largest grid of gf_* kernels; the self-check and end-to-end legs use
+other grids), splits them into pre-warm, counted warm-up and the K timed
+launches (the last K of that grid), and reports the timed window's mean launch
+duration from the trace next to the line's kernel_ms_mean / ms_per_step and the
+roofline fraction each implies."""
+import csv
+import json
+import statistics
+import sys
+
+
+def main():
+    trace, log = sys.argv[1], sys.argv[2]
+    line = next(json.loads(ln) for ln in open(log) if ln.startswith("{"))
+    rows = [r for r in csv.DictReader(open(trace)) if "rsamd::gf_" in r["Kernel_Name"]]
+    big = max(int(r["Grid_Size_X"]) for r in rows)
+    main_rows = [r for r in rows if int(r["Grid_Size_X"]) == big]
+    main_rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in main_rows]
+    K, W = line["steps"], line["warmup"]
+    timed = dur[-K:]
+    pre = dur[:-(K + W)]
+    alg = line["roofline"]["algorithmic_bytes_per_launch"]
+    mean_t = statistics.mean(timed)
+    out = {
+        "kernel": main_rows[0]["Kernel_Name"],
+        "grid_size_x": big,
+        "launches_of_this_grid": len(dur),
+        "timed_window": {"launches": K, "mean_ms": round(mean_t, 4), "min_ms": round(min(timed), 4),
+                         "max_ms": round(max(timed), 4),
+                         "frac_of_8TBps": round(alg / (mean_t * 1e-3) / 8e12, 4)},
+        "warmup_mean_ms": round(statistics.mean(dur[-(K + W):-K]), 4) if W else None,
+        "prewarm": {"launches": len(pre), "first_10_ms": [round(x, 3) for x in pre[:10]],
+                    "max_ms": round(max(pre), 4) if pre else None,
+                    "last_20_mean_ms": round(statistics.mean(pre[-20:]), 4) if len(pre) >= 20 else None},
+        "bench_line": {"ms_per_step": line["ms_per_step"], "kernel_ms_mean": line["roofline"]["kernel_ms_mean"],
+                       "frac": line["roofline"]["frac"], "value_GiBps": line["value"],
+                       "prewarm": line.get("prewarm")},
+        "agreement": {"ms_per_step_vs_trace_mean": round(line["ms_per_step"] / mean_t - 1, 4),
+                      "kernel_ms_mean_vs_trace_mean": round(line["roofline"]["kernel_ms_mean"] / mean_t - 1, 4)},
+    }
+    s = json.dumps(out, indent=1)
+    print(s)
+    if len(sys.argv) > 3:
+        open(sys.argv[3], "w").write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
