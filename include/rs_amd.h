@@ -171,6 +171,14 @@ RS_API int rs_reconst_batch_layout(rs_t* rs, const rs_layout_t* layout, int nstr
 RS_API int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* layout, int nstripes, size_t len,
                                   const uint64_t* need_masks, void* stream);
 
+/* The same for any d+p <= 256 (rs.go:61; the reference's Reconst has no
+ * 64-vector limit, only its inverse cache does, rs.go:70-74): stripe s's
+ * mask is the 256-bit set need_masks[4*s .. 4*s+3], vector v at bit v % 64
+ * of word v / 64.  The *_multi256 host-batch and group variants below take
+ * masks the same way. */
+RS_API int rs_reconst_batch_multi256(rs_t* rs, const rs_layout_t* layout, int nstripes, size_t len,
+                                     const uint64_t* need_masks, void* stream);
+
 /* Reconst every stripe with the same survived/need pattern
  * (one host plan + one cached matrix, then at most two device passes). */
 RS_API int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
@@ -259,6 +267,11 @@ RS_API int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_s
 RS_API int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stripe_stride,
                                              int64_t vect_stride, int nstripes, size_t len,
                                              const uint64_t* need_masks);
+RS_API int rs_reconst_host_batch_multi256(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                                          int nstripes, size_t len, const uint64_t* need_masks);
+RS_API int rs_group_reconst_host_batch_multi256(rs_group_t* g, uint8_t* base, int64_t stripe_stride,
+                                                int64_t vect_stride, int nstripes, size_t len,
+                                                const uint64_t* need_masks);
 
 /* ------------------------------------------------------------------------
  * Generic GF(2^8) matrix product over device vectors — the primitive all of

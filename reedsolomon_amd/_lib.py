@@ -59,6 +59,7 @@ SIGNATURES = {
     "rs_encode_batch_layout": (c_int, [c_void, c_layoutp, c_int, c_sz, c_void]),
     "rs_reconst_batch_layout": (c_int, [c_void, c_layoutp, c_int, c_sz, c_intp, c_int, c_intp, c_int, c_void]),
     "rs_reconst_batch_multi": (c_int, [c_void, c_layoutp, c_int, c_sz, ctypes.POINTER(ctypes.c_uint64), c_void]),
+    "rs_reconst_batch_multi256": (c_int, [c_void, c_layoutp, c_int, c_sz, ctypes.POINTER(ctypes.c_uint64), c_void]),
     "rs_reconst_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_intp, c_int, c_intp, c_int,
                                  c_void]),
     "rs_update_batch": (c_int, [c_void, c_void, c_i64, c_void, c_i64, c_int, c_void, c_i64, c_i64, c_int, c_sz,
@@ -75,6 +76,10 @@ SIGNATURES = {
                                                   ctypes.POINTER(ctypes.c_uint64)]),
     "rs_reconst_host_batch_multi": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
                                             ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_reconst_host_batch_multi256": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
+                                               ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_group_reconst_host_batch_multi256": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
+                                                     ctypes.POINTER(ctypes.c_uint64)]),
     "rs_host_device_pointer": (c_int, [c_void, c_sz, ctypes.POINTER(c_void)]),
     "rs_host_register": (c_int, [c_void, c_sz]),
     "rs_host_unregister": (c_int, [c_void]),

@@ -3,6 +3,7 @@
 // erasure pattern per stripe (rs_reconst_batch_multi), the XOR primitive and
 // the generic product.  All asynchronous on the caller's stream.
 #include <algorithm>
+#include <array>
 #include <unordered_map>
 
 #include "codec_internal.hpp"
@@ -121,25 +122,40 @@ int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vec
     });
 }
 
-int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const uint64_t* need_masks,
-                           void* stream) {
-    return abi_guard([&]() -> int {
-        if (!rs || !L || nstripes < 0 || (nstripes > 0 && !need_masks)) return RS_ERR_INVAL;
+}  // extern "C"
+
+namespace {
+typedef std::array<uint64_t, 4> Mask256;
+struct Mask256Hash {
+    size_t operator()(const Mask256& m) const {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (uint64_t w : m) h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+        return static_cast<size_t>(h ^ (h >> 31));
+    }
+};
+}  // namespace
+
+namespace rsamd {
+namespace detail {
+
+// rs_reconst_batch_multi / rs_reconst_batch_multi256 (masks of 1 or 4 words).
+int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, MaskView masks, void* stream) {
+    {
+        if (!rs || !L || nstripes < 0 || (nstripes > 0 && !masks.m)) return RS_ERR_INVAL;
         const int d = rs->d, p = rs->p;
-        if (d + p > 64) return RS_ERR_INVAL;  // masks are 64-bit survivor bitmaps, like the cache key
+        if (d + p > 64 * masks.words) return RS_ERR_INVAL;  // the mask cannot name every vector
         if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-        const uint64_t valid = (d + p == 64) ? ~uint64_t{0} : ((uint64_t{1} << (d + p)) - 1);
         // Group stripes by erasure pattern (host, O(S)); validate every pattern before any launch.
-        std::unordered_map<uint64_t, std::vector<int32_t>> groups;
+        std::unordered_map<Mask256, std::vector<int32_t>, Mask256Hash> groups;
         for (int s = 0; s < nstripes; ++s) {
-            const uint64_t m = need_masks[s];
-            if (!m) continue;
-            if (m & ~valid) return RS_ERR_ILLEGAL_VECTS;
-            groups[m].push_back(s);
+            if (!masks.any(s)) continue;
+            if (masks.beyond(s, d + p)) return RS_ERR_ILLEGAL_VECTS;
+            Mask256 key{};
+            for (int w = 0; w < masks.words; ++w) key[w] = masks.row(s)[w];
+            groups[key].push_back(s);
         }
         if (groups.empty()) return RS_OK;
         struct Group {
-            uint64_t mask;
             ReconstPlan pl;
             size_t off, n;
         };
@@ -148,10 +164,9 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
         ids.reserve(nstripes);
         for (auto& kv : groups) {
             Group gr;
-            gr.mask = kv.first;
-            int need[64], nn = 0;
+            int need[kMaxVects], nn = 0;
             for (int v = 0; v < d + p; ++v)
-                if (kv.first >> v & 1) need[nn++] = v;
+                if (kv.first[v >> 6] >> (v & 63) & 1) need[nn++] = v;
             int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
             if (rc) return rc;  // RS_ERR_TOO_MANY_LOST for a pattern beyond p erasures
             gr.off = ids.size();
@@ -199,7 +214,7 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
                 PatternDesc& pd = descs[gi];
                 pd.tab_off = static_cast<uint32_t>(gi * tdw);
                 pd.nout = static_cast<uint32_t>(gr.pl.nnr);
-                for (int i = 0; i < d; ++i) pd.in_idx[i] = static_cast<uint32_t>(gr.pl.vs[i]);
+                for (int i = 0; i < d; ++i) pd.in_idx[i] = static_cast<uint16_t>(gr.pl.vs[i]);
                 for (int r = 0; r < gr.pl.nnr; ++r) pd.out_idx[r] = static_cast<uint32_t>(gr.pl.nr[r]);
                 for (size_t t = 0; t < gr.n; ++t) spat[ids[gr.off + t]] = gi;
             }
@@ -255,7 +270,22 @@ int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t 
                            dids + gr.off);
         }
         return rc;
-    });
+    }
+}
+
+}  // namespace detail
+}  // namespace rsamd
+
+extern "C" {
+
+int rs_reconst_batch_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const uint64_t* need_masks,
+                           void* stream) {
+    return abi_guard([&]() -> int { return reconst_multi(rs, L, nstripes, len, MaskView{need_masks, 1}, stream); });
+}
+
+int rs_reconst_batch_multi256(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, const uint64_t* need_masks,
+                              void* stream) {
+    return abi_guard([&]() -> int { return reconst_multi(rs, L, nstripes, len, MaskView{need_masks, 4}, stream); });
 }
 
 int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* new_data, size_t new_len, int row,

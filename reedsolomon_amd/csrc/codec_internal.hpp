@@ -310,6 +310,38 @@ std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr);
 // skips exactly that byte range [lo, hi) for the given L1D size, so the
 // parity bytes equal the reference's on a host with that L1D.  Returns false
 // when the size has no such range (or the mode is off).
+// Per-stripe erasure masks of the multi-pattern Reconst entry points:
+// `words` uint64 words per stripe (1: the d+p <= 64 API, 4: the *_multi256
+// API), vector v at bit v % 64 of word v / 64.
+struct MaskView {
+    const uint64_t* m;
+    int words;
+    const uint64_t* row(int s) const { return m + static_cast<size_t>(s) * words; }
+    bool bit(int s, int v) const { return (v >> 6) < words && (row(s)[v >> 6] >> (v & 63) & 1); }
+    bool any(int s) const {
+        for (int w = 0; w < words; ++w)
+            if (row(s)[w]) return true;
+        return false;
+    }
+    int count(int s) const {
+        int c = 0;
+        for (int w = 0; w < words; ++w) c += __builtin_popcountll(row(s)[w]);
+        return c;
+    }
+    // any bit at or above nvec (a vector the stripe does not have)
+    bool beyond(int s, int nvec) const {
+        for (int w = 0; w < words; ++w) {
+            const int lo = w * 64;
+            const uint64_t valid = nvec >= lo + 64 ? ~uint64_t{0} : nvec <= lo ? 0 : ((uint64_t{1} << (nvec - lo)) - 1);
+            if (row(s)[w] & ~valid) return true;
+        }
+        return false;
+    }
+    MaskView from(int first) const { return MaskView{row(first), words}; }
+};
+int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, MaskView masks, void* stream);
+int check_masks(int d, int p, MaskView masks, int nstripes);
+
 extern int g_ref_update_tail;
 bool ref_update_skip(uint64_t size, uint64_t* lo, uint64_t* hi);
 // Run op(offset, length) over [0, size) minus the skipped range.

@@ -226,13 +226,12 @@ static int encode_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs
 
 // The errors rs_reconst_batch_multi would return for these masks, before
 // anything is copied or launched.
-static int check_masks(int d, int p, const uint64_t* masks, int nstripes) {
+int rsamd::detail::check_masks(int d, int p, MaskView masks, int nstripes) {
     const int nvec = d + p;
-    if (nvec > 64) return RS_ERR_INVAL;
-    const uint64_t valid = nvec == 64 ? ~uint64_t{0} : ((uint64_t{1} << nvec) - 1);
+    if (nvec > 64 * masks.words) return RS_ERR_INVAL;
     for (int s = 0; s < nstripes; ++s) {
-        if (masks[s] & ~valid) return RS_ERR_ILLEGAL_VECTS;
-        if (__builtin_popcountll(masks[s]) > p) return RS_ERR_TOO_MANY_LOST;
+        if (masks.beyond(s, nvec)) return RS_ERR_ILLEGAL_VECTS;
+        if (masks.count(s) > p) return RS_ERR_TOO_MANY_LOST;
     }
     return RS_OK;
 }
@@ -241,28 +240,28 @@ static int check_masks(int d, int p, const uint64_t* masks, int nstripes) {
 // stripe with work in, the lost vectors (rebuilt in the mirror) out.  Masks
 // are validated before any copy or launch.
 static int reconst_pageable_batch(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len,
-                                  const uint64_t* masks) {
+                                  MaskView masks) {
     const int d = rs->d, p = rs->p, nvec = d + p;
     RS_TRY(check_masks(d, p, masks, nstripes));
     return pageable_pipeline(
         rs, base, ss, vs, nstripes, len,
         [&](int s, auto add) {  // the first d survivors: all the kernel reads (rs.go's choice)
-            if (!masks[s]) return;
+            if (!masks.any(s)) return;
             for (int v = 0, n = 0; v < nvec && n < d; ++v)
-                if (!(masks[s] >> v & 1)) {
+                if (!masks.bit(s, v)) {
                     add(v);
                     ++n;
                 }
         },
         [&](int s, auto add) {
             for (int v = 0; v < nvec; ++v)
-                if (masks[s] >> v & 1) add(v);
+                if (masks.bit(s, v)) add(v);
         },
         [&](int first, int n, uint8_t* dslot, size_t sbytes, size_t pitch) {
             const rs_layout_t L{dslot, static_cast<int64_t>(sbytes), static_cast<int64_t>(pitch),
                                 dslot + static_cast<size_t>(d) * pitch, static_cast<int64_t>(sbytes),
                                 static_cast<int64_t>(pitch)};
-            return rs_reconst_batch_multi(rs, &L, n, len, masks + first, rs->stream);
+            return reconst_multi(rs, &L, n, len, masks.from(first), rs->stream);
         });
 }
 
@@ -548,66 +547,91 @@ int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stri
     });
 }
 
+static int reconst_host_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
+                              size_t len, MaskView masks) {
+    if (!rs || nstripes < 0 || (nstripes > 0 && (!base || !masks.m))) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    if (nstripes == 0) return RS_OK;
+    if (stripe_stride < 0 || vect_stride < 0) return RS_ERR_INVAL;
+    const int d = rs->d, p = rs->p;
+    RS_TRY(check_masks(d, p, masks, nstripes));  // before any device work, copy or launch
+    RS_TRY(ensure_device(rs));
+    DeviceGuard g(rs->device);
+    uint8_t* zc = nullptr;
+    if (host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) != RS_OK) {
+        // pageable memory: staged through the pinned mirror
+        if (!g_host_pageable_stage || rup(len, 256) * static_cast<size_t>(d + p) > kPageableStripeMax)
+            return RS_ERR_INVAL;
+        std::lock_guard<std::mutex> lk(rs->stage_mu);
+        return reconst_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len, masks);
+    }
+    rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
+                  vect_stride};
+    std::lock_guard<std::mutex> lk(rs->stage_mu);
+    if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
+    int rc = reconst_multi(rs, &L, nstripes, len, masks, rs->stream);
+    const int sync_rc = hip_ok(hipStreamSynchronize(rs->stream), "host-batch sync");
+    return rc ? rc : sync_rc;
+}
+
+static int group_reconst_host_multi(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                                    int nstripes, size_t len, MaskView masks) {
+    if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && (!base || !masks.m))) return RS_ERR_INVAL;
+    if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
+    // every slice's masks checked before any member starts (no partial batch)
+    RS_TRY(check_masks(g->members[0]->d, g->members[0]->p, masks, nstripes));
+    const int n = static_cast<int>(g->members.size());
+    std::vector<int> rc(n, RS_OK);
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; ++i) {
+        const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
+        const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+        if (hi <= lo) continue;
+        auto job = [&, i, lo, hi] {
+            rc[i] = reconst_host_multi(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride, stripe_stride,
+                                       vect_stride, hi - lo, len, masks.from(lo));
+        };
+        try {
+            const int dev = g->members[i]->device;
+            th.emplace_back([job, dev] {  // a worker of its own: bind it to the GPU's NUMA node
+                if (g_bind_numa) (void)bind_thread_to_device(dev);
+                job();
+            });
+        } catch (...) {
+            job();  // no thread available: run this slice here
+        }
+    }
+    for (std::thread& t : th) t.join();
+    for (int r : rc)
+        if (r) return r;
+    return RS_OK;
+}
+
 int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
                                 size_t len, const uint64_t* need_masks) {
     return abi_guard([&]() -> int {
-        if (!rs || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
-        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-        if (nstripes == 0) return RS_OK;
-        if (stripe_stride < 0 || vect_stride < 0) return RS_ERR_INVAL;
-        RS_TRY(ensure_device(rs));
-        DeviceGuard g(rs->device);
-        const int d = rs->d, p = rs->p;
-        uint8_t* zc = nullptr;
-        if (host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) != RS_OK) {
-            // pageable memory: staged through the pinned mirror
-            if (!g_host_pageable_stage || rup(len, 256) * static_cast<size_t>(d + p) > kPageableStripeMax)
-                return RS_ERR_INVAL;
-            std::lock_guard<std::mutex> lk(rs->stage_mu);
-            return reconst_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len, need_masks);
-        }
-        rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
-                      vect_stride};
-        std::lock_guard<std::mutex> lk(rs->stage_mu);
-        if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
-        int rc = rs_reconst_batch_multi(rs, &L, nstripes, len, need_masks, rs->stream);
-        const int sync_rc = hip_ok(hipStreamSynchronize(rs->stream), "host-batch sync");
-        return rc ? rc : sync_rc;
+        return reconst_host_multi(rs, base, stripe_stride, vect_stride, nstripes, len, MaskView{need_masks, 1});
+    });
+}
+
+int rs_reconst_host_batch_multi256(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride, int nstripes,
+                                   size_t len, const uint64_t* need_masks) {
+    return abi_guard([&]() -> int {
+        return reconst_host_multi(rs, base, stripe_stride, vect_stride, nstripes, len, MaskView{need_masks, 4});
     });
 }
 
 int rs_group_reconst_host_batch_multi(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                       int nstripes, size_t len, const uint64_t* need_masks) {
     return abi_guard([&]() -> int {
-        if (!g || g->members.empty() || nstripes < 0 || (nstripes > 0 && (!base || !need_masks))) return RS_ERR_INVAL;
-        if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-        // every slice's masks checked before any member starts (no partial batch)
-        RS_TRY(check_masks(g->members[0]->d, g->members[0]->p, need_masks, nstripes));
-        const int n = static_cast<int>(g->members.size());
-        std::vector<int> rc(n, RS_OK);
-        std::vector<std::thread> th;
-        for (int i = 0; i < n; ++i) {
-            const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
-            const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
-            if (hi <= lo) continue;
-            auto job = [&, i, lo, hi] {
-                rc[i] = rs_reconst_host_batch_multi(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
-                                                    stripe_stride, vect_stride, hi - lo, len, need_masks + lo);
-            };
-            try {
-                const int dev = g->members[i]->device;
-                th.emplace_back([job, dev] {  // a worker of its own: bind it to the GPU's NUMA node
-                    if (g_bind_numa) (void)bind_thread_to_device(dev);
-                    job();
-                });
-            } catch (...) {
-                job();  // no thread available: run this slice here
-            }
-        }
-        for (std::thread& t : th) t.join();
-        for (int r : rc)
-            if (r) return r;
-        return RS_OK;
+        return group_reconst_host_multi(g, base, stripe_stride, vect_stride, nstripes, len, MaskView{need_masks, 1});
+    });
+}
+
+int rs_group_reconst_host_batch_multi256(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
+                                         int nstripes, size_t len, const uint64_t* need_masks) {
+    return abi_guard([&]() -> int {
+        return group_reconst_host_multi(g, base, stripe_stride, vect_stride, nstripes, len, MaskView{need_masks, 4});
     });
 }
 

@@ -48,7 +48,7 @@ struct MatmulArgs {
 struct PatternDesc {
     uint32_t tab_off;
     uint32_t nout;        // <= 4 outputs
-    uint32_t in_idx[64];  // the d input vectors (indexes into MatmulArgs::ptr)
+    uint16_t in_idx[256];  // the d input vectors (indexes into MatmulArgs::ptr; d+p <= 256)
     uint32_t out_idx[4];  // the output vectors
 };
 int multi_table_dwords(int cols);

@@ -310,10 +310,9 @@ class RS:
         (data in [S, d, len], parity in [S, p, len]; the interleaved buffer can be passed as
         data=buf[:, :d], parity=buf[:, d:])."""
         L, S, n = self._split_layout(data, parity)
-        masks = _masks(need_masks, S)
-        _check(lib().rs_reconst_batch_multi(self._h, ctypes.byref(L), S, n,
-                                            masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
-                                            self._stream(stream, data, parity)))
+        masks, fn = _masks_for(need_masks, S, self.DataNum + self.ParityNum, "rs_reconst_batch_multi")
+        _check(getattr(lib(), fn)(self._h, ctypes.byref(L), S, n, masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                  self._stream(stream, data, parity)))
 
     def reconst_batch(self, buf, survived, needReconst, stream=None) -> None:
         base, ss, vs, S, n = self._stripes(buf, self.DataNum + self.ParityNum)
@@ -357,9 +356,9 @@ class RS:
         the vectors of stripe s to rebuild (zero-copy kernels over pinned
         memory; pageable memory is staged through a pinned mirror)."""
         ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
-        masks = _masks(need_masks, S)
-        _check(lib().rs_reconst_host_batch_multi(self._h, ctypes.c_void_p(ptr), ss, vs, S, n,
-                                                 masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        masks, fn = _masks_for(need_masks, S, self.DataNum + self.ParityNum, "rs_reconst_host_batch_multi")
+        _check(getattr(lib(), fn)(self._h, ctypes.c_void_p(ptr), ss, vs, S, n,
+                                  masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
 
     def xor_batch(self, src, dst, stream=None) -> None:
         """dst[s] = src[s, 0] ^ src[s, 1] ^ ... (xorsimd xor.Encode) for [S, n, len] / [S, len] GPU tensors."""
@@ -448,6 +447,35 @@ def _masks(need_masks, S: int) -> np.ndarray:
     return masks
 
 
+def _masks_for(need_masks, S: int, nvec: int, fn64: str):
+    """(mask array, entry point): 64-bit masks through `fn64` when the codec
+    has <= 64 vectors and every mask fits in 64 bits, else [S, 4] words
+    through the *_multi256 variant (d+p <= 256).  need_masks: one int per
+    stripe (Python ints may exceed 64 bits), a uint64 [S] array, or a uint64
+    [S, 4] array of 256-bit masks (vector v at bit v % 64 of word v // 64)."""
+    if isinstance(need_masks, np.ndarray) and need_masks.ndim == 2:
+        m = np.ascontiguousarray(need_masks, dtype=np.uint64)
+        if m.shape != (S, 4):
+            raise TypeError("256-bit need_masks must be a [stripes, 4] uint64 array")
+        return m, fn64 + "256"
+    if isinstance(need_masks, np.ndarray):
+        if nvec <= 64:
+            return _masks(need_masks, S), fn64
+        need_masks = [int(x) for x in need_masks]
+    vals = [int(x) for x in need_masks]
+    if len(vals) != S:
+        raise TypeError("need_masks must hold one mask per stripe")
+    if nvec <= 64 and all(0 <= v < (1 << 64) for v in vals):
+        return np.asarray(vals, dtype=np.uint64), fn64
+    m = np.zeros((S, 4), np.uint64)
+    for s, v in enumerate(vals):
+        if v < 0 or v >> 256:
+            raise ErrIllegalVects()
+        for w in range(4):
+            m[s, w] = (v >> (64 * w)) & 0xFFFFFFFFFFFFFFFF
+    return m, fn64 + "256"
+
+
 def host_device_pointer(ptr: int, nbytes: int) -> int:
     """Device address of a pinned / registered host range (rs_host_device_pointer)."""
     d = ctypes.c_void_p()
@@ -479,9 +507,9 @@ class Group:
     def reconst_host_batch_multi(self, buf, need_masks) -> None:
         """RS.reconst_host_batch_multi with the stripes split across the group's devices."""
         ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
-        masks = _masks(need_masks, S)
-        _check(lib().rs_group_reconst_host_batch_multi(self._g, ctypes.c_void_p(ptr), ss, vs, S, n,
-                                                       masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        masks, fn = _masks_for(need_masks, S, self.DataNum + self.ParityNum, "rs_group_reconst_host_batch_multi")
+        _check(getattr(lib(), fn)(self._g, ctypes.c_void_p(ptr), ss, vs, S, n,
+                                  masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
 
     def __del__(self):
         g = getattr(self, "_g", None)

@@ -298,3 +298,42 @@ def test_tune_accepts_every_documented_knob(rslib):
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.startswith("ok")
+
+
+def test_multi_pattern_mask_validation_wide(rslib):
+    """Multi-pattern Reconst masks are validated on the host before any device
+    work (no GPU needed here): the 64-bit API refuses codecs of more than 64
+    vectors (RS_ERR_INVAL), the 256-bit API (rs_reconst_batch_multi256, any
+    d+p <= 256 as rs.go:61) rejects bits past d+p (ErrIllegalVects) and more
+    than p erasures (ErrTooManyLost); the Python mirror picks the API from
+    the codec's size and the masks."""
+    import ctypes
+
+    from reedsolomon_amd._lib import RSLayout
+
+    L = rslib.lib()
+    d, p, S = 100, 28, 3
+    h = ctypes.c_void_p()
+    assert L.rs_new(d, p, -1, ctypes.byref(h)) == 0
+    try:
+        lay = RSLayout(0x1000, 1 << 20, 4096, 0x2000, 1 << 20, 4096)  # never dereferenced: validation fails first
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        m64 = np.ones(S, np.uint64)
+        assert L.rs_reconst_batch_multi(h, ctypes.byref(lay), S, 4096, m64.ctypes.data_as(u64p), None) == 13
+        wide = np.zeros((S, 4), np.uint64)
+        wide[1, 2] = np.uint64(1) << np.uint64(128 - 128 + 0)  # vector 128: past d+p = 128
+        assert L.rs_reconst_batch_multi256(h, ctypes.byref(lay), S, 4096, wide.ctypes.data_as(u64p), None) == 1
+        too_many = [sum(1 << v for v in range(0, 29)), 0, 0]  # 29 > p erasures
+        m, fn = rslib.rs._masks_for(too_many, S, d + p, "rs_reconst_batch_multi")
+        assert fn == "rs_reconst_batch_multi256" and m.shape == (S, 4)
+        assert L.rs_reconst_batch_multi256(h, ctypes.byref(lay), S, 4096, m.ctypes.data_as(u64p), None) == 6
+        # host batch variant: same validation before any copy
+        assert L.rs_reconst_host_batch_multi256(h, ctypes.c_void_p(0x1000), 1 << 20, 4096, S, 4096,
+                                                m.ctypes.data_as(u64p)) == 6
+    finally:
+        L.rs_free(h)
+    # small codecs keep the 64-bit API
+    m, fn = rslib.rs._masks_for([1, 2, 3], 3, 14, "rs_reconst_batch_multi")
+    assert fn == "rs_reconst_batch_multi" and m.dtype == np.uint64 and m.shape == (3,)
+    m, fn = rslib.rs._masks_for([1 << 127, 0], 2, 128, "rs_reconst_batch_multi")
+    assert fn == "rs_reconst_batch_multi256" and int(m[0, 1]) == 1 << 63

@@ -961,3 +961,50 @@ def test_group_encode_host_batch(rslib, torch_dev):
         grp = rslib.NewGroup(d, p, devs)
         grp.encode_host_batch(h, 4, 3)
         assert torch.equal(h, ref.cpu()), devs
+
+
+@pytest.mark.parametrize("d,p,n", [(100, 28, 4096), (200, 56, 1024 + 16), (40, 30, 8192 + 5)])
+def test_reconst_batch_multi_wide_masks(rslib, orc, torch_dev, d, p, n):
+    """Multi-pattern Reconst beyond 64 vectors (256-bit masks,
+    rs_reconst_batch_multi256; rs.go:61 allows d+p <= 256): mixed patterns of
+    0..p erasures per stripe (data and parity), encode checked against the
+    oracle, every stripe rebuilt bit-exact, untouched stripes unchanged; then
+    the host-batch variant on pinned and on pageable memory."""
+    torch = torch_dev
+    S = 24
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(d * 7 + p)
+    host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+    exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:2, :d])
+    data = torch.from_numpy(np.ascontiguousarray(host[:, :d])).cuda()
+    parity = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    torch.cuda.synchronize()
+    assert np.array_equal(parity[:2].cpu().numpy(), exp)
+    ref_d, ref_p = data.clone(), parity.clone()
+    masks = []
+    for s in range(S):
+        k = 0 if s % 5 == 1 else int(rng.choice([1, 2, 3, 4, p // 2, p]))
+        lost = [int(v) for v in rng.choice(d + p, k, replace=False)]
+        if s % 7 == 3:
+            lost = sorted(set(lost) | {d + p - 1})[:p]  # the last vector (bit >= 64)
+        m = 0
+        for v in lost:
+            m |= 1 << v
+            (data[s, v] if v < d else parity[s, v - d]).fill_(0xC3)
+        masks.append(m)
+    assert any(m >> 64 for m in masks)
+    r.reconst_batch_multi(data, parity, masks)
+    torch.cuda.synchronize()
+    for s in range(S):
+        assert torch.equal(data[s], ref_d[s]) and torch.equal(parity[s], ref_p[s]), (s, bin(masks[s]))
+    # host batches: pinned (zero-copy) and pageable (staged)
+    full = torch.cat([ref_d, ref_p], dim=1).cpu()
+    for pinned in (True, False):
+        hb = full.clone().pin_memory() if pinned else full.clone()
+        for s, m in enumerate(masks):
+            for v in range(d + p):
+                if m >> v & 1:
+                    hb[s, v] = 0x3C
+        r.reconst_host_batch_multi(hb, masks)
+        assert torch.equal(hb, full), pinned
