@@ -328,6 +328,12 @@ RS_API int64_t rs_inverse_cache_size(const rs_t* rs);
  * when concurrent calls shared a launch).  Either pointer may be NULL. */
 RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls);
 
+/* Host-call engine counters since rs_new: calls served by the resident
+ * engine kernel (doorbell in host memory instead of a launch + stream sync
+ * per call) and the engine instances launched for them (a new one after each
+ * idle period).  Either pointer may be NULL. */
+RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launches);
+
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad",
  * "lane_bytes" (8 default | 16), "block8" (lanes
@@ -335,6 +341,12 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
  * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "wide_block" (128 | 256),
+ * "host_engine" (1 default: small synchronous host calls, coalesced or
+ * alone, are served by a resident kernel through a doorbell in host memory |
+ * 0: one launch + stream sync per call), "host_engine_waves" (1..16
+ * workgroups, default 8), "host_engine_idle_us" (the engine leaves after this
+ * long without a call, default 200), "host_engine_max_bytes" (larger batches
+ * launch; default 1 MiB),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;

@@ -94,6 +94,7 @@ SIGNATURES = {
     "rs_inverse_cache_key": (ctypes.c_uint64, [c_intp, c_int]),
     "rs_inverse_cache_size": (c_i64, [c_void]),
     "rs_host_call_stats": (c_int, [c_void, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "rs_host_engine_stats": (c_int, [c_void, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "rs_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
     "rs_tune": (c_int, [ctypes.c_char_p, c_int]),
 }

@@ -135,7 +135,10 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
         return RS_OK;
     }
     if (rs->tables.size() >= g_registry_max) {
-        // Bounded registry: drain the device before recycling table memory.
+        // Bounded registry: drain the device before recycling table memory
+        // (the resident host-call engine first: a device sync waits for it)
+        std::lock_guard<std::mutex> elk(rs->eng_mu);
+        engine_stop(rs);
         RS_TRY(hip_ok(hipDeviceSynchronize(), "table registry drain"));
         for (auto& kv : rs->tables) (void)hipFree(kv.second);
         rs->tables.clear();
@@ -515,6 +518,10 @@ int rs_tune(const char* name, int value) {
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
         else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
+        else if (n == "host_engine") g_engine = value ? 1 : 0;
+        else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxWaves ? kEngineMaxWaves : value;
+        else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
+        else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;
@@ -540,6 +547,15 @@ int rs_matrix_invert(const uint8_t* m, size_t m_len, int n, uint8_t* out) {
 uint64_t rs_inverse_cache_key(const int* survived, int ns) { return cache_key(survived, ns); }
 
 const char* rs_last_device_error(void) { return g_last_dev_err; }
+
+int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launches) {
+    return abi_guard([&]() -> int {
+        if (!rs) return RS_ERR_INVAL;
+        if (calls) *calls = rs->eng_calls.load(std::memory_order_relaxed);
+        if (launches) *launches = rs->eng_launches.load(std::memory_order_relaxed);
+        return RS_OK;
+    });
+}
 
 int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* calls) {
     return abi_guard([&]() -> int {

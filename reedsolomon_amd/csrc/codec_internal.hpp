@@ -149,10 +149,46 @@ struct rs_codec {
     int up_next = 0;
     hipStream_t up_stream = nullptr;
 
+    // Host-call engine (engine.cpp): resident kernel + doorbell ring serving
+    // the coalesced small host calls.  Guarded by eng_mu.
+    std::mutex eng_mu;
+    rsamd::EngineRing* eng_ring = nullptr;   // host address (fine-grained pinned)
+    rsamd::EngineRing* eng_dring = nullptr;  // its device address
+    hipStream_t eng_stream = nullptr;
+    bool eng_running = false;
+    int eng_waves = 0;
+    int eng_idle_us = 0;     // the running instance's idle window
+    uint64_t eng_seq = 0;
+    uint32_t eng_tab_id = 0;
+    std::vector<uint8_t> eng_tab_key;
+    std::chrono::steady_clock::time_point eng_last;
+    std::atomic<uint64_t> eng_calls{0}, eng_launches{0};
+
     const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
 
-    ~rs_codec() {
+    ~rs_codec();
+    void release_device();
+};
+
+inline rs_codec::~rs_codec() { release_device(); }
+
+namespace rsamd {
+namespace detail {
+// Host-call engine (engine.cpp).  engine_call: RS_ERR_INVAL when the call
+// does not fit the engine (the caller launches instead).
+int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
+                size_t stride, int nstripes, bool accumulate);
+void engine_stop(rs_t* rs);  // caller holds eng_mu
+void engine_shutdown(rs_t* rs);
+extern int g_engine, g_engine_waves, g_engine_idle_us;
+extern size_t g_engine_max_bytes;
+}  // namespace detail
+}  // namespace rsamd
+
+inline void rs_codec::release_device() {
+    {
         if (!device_ready) return;
+        rsamd::detail::engine_shutdown(this);
         rsamd::detail::DeviceGuard g(device);
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipDeviceSynchronize();
@@ -181,7 +217,7 @@ struct rs_codec {
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
-};
+}
 
 namespace rsamd {
 namespace detail {

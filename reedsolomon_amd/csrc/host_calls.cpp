@@ -282,7 +282,10 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
         b.host = nullptr;
         b.dev = nullptr;
         b.host_bytes = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&b.host), need, hipHostMallocDefault) != hipSuccess) {
+        // coherent (fine-grained): the resident engine reads and writes it
+        // while it runs, with no kernel boundary to flush or invalidate caches
+        if (hipHostMalloc(reinterpret_cast<void**>(&b.host), need, hipHostMallocCoherent | hipHostMallocMapped) !=
+            hipSuccess) {
             b.host = nullptr;
             return RS_ERR_NOMEM;
         }
@@ -306,6 +309,9 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
 // One launch over the batch's n stripes, straight out of the pinned buffer
 // (zero-copy), then wait for it.
 static int run_batch(rs_t* rs, const CoBatch& b, int n) {
+    // small batches: the resident engine (engine.cpp), no launch and no stream sync
+    const int erc = engine_call(rs, b.mat.data(), b.rows, b.cols, b.dev, b.pitch, b.stride, n, b.accumulate);
+    if (erc != RS_ERR_INVAL) return erc;
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
     for (int i = 0; i < b.cols; ++i) in[i] = b.dev + static_cast<size_t>(i) * b.pitch;

@@ -677,6 +677,150 @@ static BsKernel bs_kernel_for(const MatmulArgs& a, int* bs) {
 }
 
 // ---------------------------------------------------------------------------
+// Host-call engine (engine.cpp): one resident kernel serves the small
+// synchronous host calls.  Each workgroup (one wave) polls the doorbell line
+// of the ring in host memory; a new value in both seq words (written last by
+// the host) means the line's fields are the new call's.  The workgroup then
+// computes its share of the units straight out of / into the caller's pinned
+// staging buffer over PCIe, and reports the doorbell value in its done word.
+// Exit conditions every wave reaches: the stop word, or `idle_ticks` of the
+// 100 MHz realtime counter without a doorbell.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t sys_load64(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int lane) {
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), lane);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), lane);
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {  // every lane holds the same value
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+constexpr int kEngineColBatch = 16;  // column loads in flight per lane (one PCIe round trip per batch)
+
+struct EngineCall {
+    uint64_t base, stride;
+    uint32_t pitch, units, total;
+    int cols;
+    bool accumulate;
+};
+
+// This workgroup's units of one call: 16 bytes of every vector of one stripe
+// per lane and unit, all column loads of a batch in flight together (host
+// memory: one PCIe round trip per batch), ROWS output rows.
+template <int ROWS>
+__device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t* tab) {
+    typedef __attribute__((address_space(1))) u32x4 gq;
+    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < e.total; u += gridDim.x * 64u) {
+        const uint32_t si = u / e.units, k = u - si * e.units;
+        const uint64_t sb = e.base + static_cast<uint64_t>(si) * e.stride + static_cast<uint64_t>(k) * 16;
+        u32x4 acc[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r)
+            acc[r] = e.accumulate ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(
+                                        sb + static_cast<uint64_t>(e.cols + r) * e.pitch))
+                                  : u32x4{0, 0, 0, 0};
+        for (int c0 = 0; c0 < e.cols; c0 += kEngineColBatch) {
+            const int nb = (e.cols - c0) < kEngineColBatch ? (e.cols - c0) : kEngineColBatch;
+            u32x4 x[kEngineColBatch];
+#pragma unroll
+            for (int b = 0; b < kEngineColBatch; ++b)
+                if (b < nb)
+                    x[b] = __builtin_nontemporal_load(reinterpret_cast<const gq*>(sb + static_cast<uint64_t>(c0 + b) * e.pitch));
+#pragma unroll
+            for (int b = 0; b < kEngineColBatch; ++b) {
+                if (b < nb) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    uint32_t t[ROWS * 5];
+#pragma unroll
+                    for (int i = 0; i < ROWS * 5; ++i) t[i] = tab[((c0 + b) * kEngineMaxRows) * 5 + i];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t g0, g1, g2;
+                        split_groups(x[b][q], g0, g1, g2);
+#pragma unroll
+                        for (int r = 0; r < ROWS; ++r) acc[r][q] ^= gf_mul_packed(g0, g1, g2, &t[r * 5]);
+                    }
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r) asm volatile("" : "+v"(acc[r]));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r)
+            __builtin_nontemporal_store(acc[r], reinterpret_cast<gq*>(sb + static_cast<uint64_t>(e.cols + r) * e.pitch));
+    }
+}
+
+__global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start, uint64_t idle_ticks) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[kEngineMaxCols * kEngineMaxRows * 5];
+    const int lane = threadIdx.x;
+    const uint64_t* hdr = reinterpret_cast<const uint64_t*>(&ring->hdr);
+    // a relaunch resumes after the last call this workgroup completed
+    uint64_t last = uniform_u64(sys_load64(&ring->done[blockIdx.x]));
+    last = last > start ? last : start;
+    uint32_t tab_have = 0xffffffffu;
+    for (;;) {
+        uint64_t w = 0, seq = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t n = 1;; ++n) {
+            w = sys_load64(&hdr[lane & 7]);
+            const uint64_t s0 = lane_u64(w, 0), s1 = lane_u64(w, 7);
+            if (s0 == s1 && s0 != last) {
+                seq = s0;
+                break;
+            }
+            if ((n & 31) == 0 &&
+                (uniform_u64(sys_load64(&ring->stop)) || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks))
+                return;  // every lane of the wave leaves together (uniform values)
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's bytes of this call
+        const uint64_t base = lane_u64(w, 1), stride = lane_u64(w, 2);
+        const uint64_t w3 = lane_u64(w, 3), w4 = lane_u64(w, 4), w5 = lane_u64(w, 5);
+        const uint32_t pitch = static_cast<uint32_t>(w3), units = static_cast<uint32_t>(w3 >> 32);
+        const uint32_t nstripes = static_cast<uint32_t>(w4);
+        const int rows = static_cast<int>((w4 >> 32) & 0xffff), cols = static_cast<int>(w4 >> 48);
+        const bool accumulate = static_cast<uint32_t>(w5) != 0;
+        const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
+        if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords
+            for (int i = lane; i < cols * kEngineMaxRows * 5; i += 64)
+                tab[i] = __hip_atomic_load(&ring->tables[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            tab_have = tab_id;
+        }
+        __syncthreads();
+        const EngineCall call{base, stride, pitch, units, nstripes * units, cols, accumulate};
+        switch (rows) {
+            case 1: engine_units<1>(call, tab); break;
+            case 2: engine_units<2>(call, tab); break;
+            case 3: engine_units<3>(call, tab); break;
+            case 4: engine_units<4>(call, tab); break;
+            case 5: engine_units<5>(call, tab); break;
+            case 6: engine_units<6>(call, tab); break;
+            case 7: engine_units<7>(call, tab); break;
+            default: engine_units<8>(call, tab); break;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&ring->done[blockIdx.x], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = seq;
+    }
+}
+
+hipError_t launch_engine(EngineRing* ring_dev, int waves, uint64_t start, uint64_t idle_ticks, hipStream_t stream) {
+    if (waves < 1 || waves > kEngineMaxWaves) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(gf_engine, dim3(waves), dim3(64), 0, stream, ring_dev, start, idle_ticks);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
 using VecKernel = void (*)(const MatmulArgs);

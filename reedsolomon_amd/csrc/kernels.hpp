@@ -54,6 +54,38 @@ struct PatternDesc {
 int multi_table_dwords(int cols);
 hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream);
 
+// Host-call engine (engine.cpp): a resident kernel that serves small
+// synchronous host calls through a doorbell in host memory instead of one
+// launch + stream sync per call (DESIGN.md §5 "Host-call engine").
+// Everything below lives in fine-grained (coherent) pinned host memory that
+// the kernel reads and writes over PCIe.
+constexpr int kEngineMaxRows = 8, kEngineMaxCols = 32, kEngineMaxWaves = 16;
+struct EngineHeader {      // one 64-byte line; the host writes seq0 and seq1 LAST
+    uint64_t seq0;         // doorbell value (first word of the line)
+    uint64_t base;         // device address of stripe 0, vector 0
+    uint64_t stride;       // bytes between stripes
+    uint32_t pitch;        // bytes between the vectors of a stripe (16-byte multiple)
+    uint32_t units;        // 16-byte units per vector (pitch / 16: whole slots, padding included)
+    uint32_t nstripes;
+    uint16_t rows, cols;   // <= kEngineMaxRows / kEngineMaxCols
+    uint32_t accumulate;   // XOR into the output rows (Update / Replace)
+    uint32_t tab_id;       // identity of EngineRing::tables (reloaded into LDS when it changes)
+    uint64_t reserved;
+    uint64_t seq1;         // doorbell value again (last word of the line)
+};
+static_assert(sizeof(EngineHeader) == 64, "one cache line, seq1 in its last word");
+struct EngineRing {
+    EngineHeader hdr;
+    uint64_t stop;                      // host -> kernel: leave now
+    uint64_t pad[7];
+    uint64_t done[kEngineMaxWaves];     // workgroup w -> host: last doorbell value it completed
+    uint32_t tables[kEngineMaxCols * kEngineMaxRows * 5];  // perm tables, [col][row][5] dwords
+};
+// Launch the resident engine: `waves` workgroups of 64 lanes on `stream`,
+// serving doorbells after `start`; each workgroup leaves on `stop` or after
+// `idle_ticks` of the 100 MHz realtime counter without a doorbell.
+hipError_t launch_engine(EngineRing* ring_dev, int waves, uint64_t start, uint64_t idle_ticks, hipStream_t stream);
+
 // Launch tuning knobs (read from the environment once).
 struct LaunchTuning {
     int max_grid;     // cap on workgroups of the vector kernel (0 = one per chunk)

@@ -410,6 +410,12 @@ class RS:
     def inverse_cache_size(self) -> int:
         return int(lib().rs_inverse_cache_size(self._h))
 
+    def host_engine_stats(self) -> tuple:
+        """(calls, launches) of the resident host-call engine since New (rs_host_engine_stats)."""
+        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(lib().rs_host_engine_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return int(a.value), int(b.value)
+
     def host_call_stats(self) -> tuple:
         """(launches, calls) of coalesced host calls since New (see rs_host_call_stats)."""
         a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)

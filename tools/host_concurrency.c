@@ -87,6 +87,7 @@ int main(int argc, char** argv) {
     if (g_calls > MAXCALLS) g_calls = MAXCALLS;
     rs_tune("host_coalesce_max", atoi(argv[3]));
     g_mixed = atoi(argv[4]);
+    if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &g_rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;

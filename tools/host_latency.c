@@ -8,6 +8,8 @@
  *   (host_zc_max -1 = default chunked zero-copy for every size, 0 = staged paths)
  *   HL_REGISTER=1: page-aligned vectors registered with rs_host_register (the
  *   calls then run zero-copy over the caller's memory)
+ *   HL_ENGINE=0/1: the resident host-call engine off / on (default on);
+ *   HL_ENGINE_WAVES=n: its workgroups
  *
  * Prints one JSON object per (op, size).
  */
@@ -54,6 +56,8 @@ int main(int argc, char** argv) {
         rs_tune("host_pinned_max", atoi(argv[2]));
     }
     if (argc >= 4) rs_tune("host_chunk", atoi(argv[3]));
+    if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));  /* resident host-call engine on / off */
+    if (getenv("HL_ENGINE_WAVES")) rs_tune("host_engine_waves", atoi(getenv("HL_ENGINE_WAVES")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
@@ -118,6 +122,12 @@ int main(int argc, char** argv) {
             if (reg && atoi(reg)) rs_host_unregister(v[i]);
             free(v[i]);
         }
+    }
+    {
+        uint64_t calls = 0, launches = 0;
+        rs_host_engine_stats(rs, &calls, &launches);
+        printf("{\"engine_calls\": %llu, \"engine_launches\": %llu}\n", (unsigned long long)calls,
+               (unsigned long long)launches);
     }
     rs_free(rs);
     return 0;
