@@ -27,12 +27,17 @@
 // into their outputs).
 #include <immintrin.h>
 
+#include <cstdlib>
+
 #include "codec_internal.hpp"
 
 namespace rsamd {
 namespace detail {
 
-int g_engine = 1;                       // rs_tune("host_engine", 0 | 1)
+int g_engine = [] {                     // rs_tune("host_engine", 0 | 1); env RSAMD_HOST_ENGINE
+    const char* e = std::getenv("RSAMD_HOST_ENGINE");
+    return e ? (std::atoi(e) ? 1 : 0) : 1;
+}();
 int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..16): workgroups of one wave
 int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
 size_t g_engine_max_bytes = 1u << 20;   // rs_tune("host_engine_max_bytes"): larger batches launch
