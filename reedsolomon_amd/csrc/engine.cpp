@@ -42,6 +42,36 @@ int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..16): 
 int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
 size_t g_engine_max_bytes = 1u << 20;   // rs_tune("host_engine_max_bytes"): larger batches launch
 
+// Doorbell rings are fine-grained (coherent) pinned memory: allocated once
+// per process and device and recycled across handles, never freed (no
+// allocate / free churn of coherent mappings while other work runs).
+namespace {
+std::mutex g_ring_mu;
+std::vector<std::pair<int, EngineRing*>> g_ring_pool;  // (device, host address) of idle rings
+}  // namespace
+
+static EngineRing* ring_get(int device) {
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        for (size_t i = 0; i < g_ring_pool.size(); ++i)
+            if (g_ring_pool[i].first == device) {
+                EngineRing* r = g_ring_pool[i].second;
+                g_ring_pool.erase(g_ring_pool.begin() + static_cast<long>(i));
+                return r;
+            }
+    }
+    void* h = nullptr;
+    if (hipHostMalloc(&h, sizeof(EngineRing), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) !=
+        hipSuccess)
+        return nullptr;
+    return static_cast<EngineRing*>(h);
+}
+
+static void ring_put(int device, EngineRing* r) {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    g_ring_pool.emplace_back(device, r);
+}
+
 void engine_stop(rs_t* rs) {
     if (!rs->eng_running) return;
     __atomic_store_n(&rs->eng_ring->stop, 1, __ATOMIC_RELEASE);
@@ -56,7 +86,7 @@ void engine_shutdown(rs_t* rs) {
     DeviceGuard g(rs->device);
     engine_stop(rs);
     if (rs->eng_stream) (void)hipStreamDestroy(rs->eng_stream);
-    (void)hipHostFree(rs->eng_ring);
+    if (!rs->eng_running) ring_put(rs->device, rs->eng_ring);  // (a ring an instance may still read is dropped)
     rs->eng_stream = nullptr;
     rs->eng_ring = rs->eng_dring = nullptr;
 }
@@ -82,22 +112,21 @@ int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
         return RS_ERR_INVAL;
     std::lock_guard<std::mutex> lk(rs->eng_mu);
     if (!rs->eng_ring) {
-        void* h = nullptr;
-        RS_TRY(hip_ok(hipHostMalloc(&h, sizeof(EngineRing), hipHostMallocCoherent | hipHostMallocMapped),
-                      "engine ring"));
+        EngineRing* h = ring_get(rs->device);
+        if (!h) return RS_ERR_NOMEM;
         std::memset(h, 0, sizeof(EngineRing));
         void* d = nullptr;
         const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
         if (e != hipSuccess || !d) {
-            (void)hipHostFree(h);
+            ring_put(rs->device, h);
             return dev_fail(e != hipSuccess ? e : hipErrorInvalidValue, "engine ring device pointer");
         }
         hipStream_t st = nullptr;
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-            (void)hipHostFree(h);
+            ring_put(rs->device, h);
             return dev_fail(hipErrorInvalidValue, "engine stream");
         }
-        rs->eng_ring = static_cast<EngineRing*>(h);
+        rs->eng_ring = h;
         rs->eng_dring = static_cast<EngineRing*>(d);
         rs->eng_stream = st;
         rs->eng_seq = 0;

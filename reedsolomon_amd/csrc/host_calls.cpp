@@ -282,10 +282,9 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
         b.host = nullptr;
         b.dev = nullptr;
         b.host_bytes = 0;
-        // coherent (fine-grained): the resident engine reads and writes it
-        // while it runs, with no kernel boundary to flush or invalidate caches
-        if (hipHostMalloc(reinterpret_cast<void**>(&b.host), need, hipHostMallocCoherent | hipHostMallocMapped) !=
-            hipSuccess) {
+        // (the resident engine reads and writes it too: its system-scope
+        // acquire / release fences stand in for the kernel boundary)
+        if (hipHostMalloc(reinterpret_cast<void**>(&b.host), need, hipHostMallocDefault) != hipSuccess) {
             b.host = nullptr;
             return RS_ERR_NOMEM;
         }
