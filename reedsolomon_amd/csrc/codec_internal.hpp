@@ -60,6 +60,18 @@ struct DeviceGuard {  // switch to the handle's device, restore the caller's on 
 
 inline uint64_t rup(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
+// Process-wide pool of coherent (fine-grained) pinned host blocks, mapped
+// for every device (host_calls.cpp).  Blocks are recycled across handles and
+// never freed, so coherent mappings are not created and torn down while
+// other work runs; sizes are rounded up to a power of two (>= 64 KiB).
+struct PinnedBlock {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;   // device address (same for every device with unified addressing)
+    size_t bytes = 0;
+};
+int pinned_get(size_t bytes, PinnedBlock* out);
+void pinned_put(PinnedBlock& b);
+
 
 }  // namespace detail
 }  // namespace rsamd
@@ -108,9 +120,10 @@ struct rs_codec {
         bool accumulate = false;
         size_t pitch = 0, stride = 0;
         int cap = 0;               // stripes this batch may take
-        uint8_t* host = nullptr;   // pinned [cap][cols + rows][pitch]
+        uint8_t* host = nullptr;   // pinned [cap][cols + rows][pitch] (a pool block: coherent)
         uint8_t* dev = nullptr;    // its device-mapped address
         size_t host_bytes = 0;
+        rsamd::detail::PinnedBlock blk;
         int joined = 0, ready = 0, released = 0;
         int rc = 0;
         bool launchable = false;   // linger window started (host_coalesce_linger_us)
@@ -121,6 +134,7 @@ struct rs_codec {
     CoBatch co[2];
     bool co_gpu_busy = false;
     int co_active = 0;             // callers inside host_call
+    std::atomic<uint64_t> co_gen{0};  // bumped at every batch state change (spinning waiters watch it)
     std::atomic<uint64_t> co_launches{0}, co_calls{0};
 
     // DMA pipeline of rs_encode_host_batch (host_batches.cpp): device ring,
@@ -177,7 +191,7 @@ namespace detail {
 // Host-call engine (engine.cpp).  engine_call: RS_ERR_INVAL when the call
 // does not fit the engine (the caller launches instead).
 int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
-                size_t stride, int nstripes, bool accumulate);
+                size_t stride, int nstripes, bool accumulate, bool coherent);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
 extern int g_engine, g_engine_waves, g_engine_idle_us;
@@ -203,7 +217,7 @@ inline void rs_codec::release_device() {
         if (stage) (void)hipFree(stage);
         if (hstage) (void)hipHostFree(hstage);
         for (CoBatch& b : co)
-            if (b.host) (void)hipHostFree(b.host);
+            if (b.blk.host) rsamd::detail::pinned_put(b.blk);
         for (hipStream_t s : dma_stream)
             if (s) (void)hipStreamSynchronize(s);
         if (dma_ring) (void)hipFree(dma_ring);

@@ -248,6 +248,47 @@ int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t
     return stage_out(rs, dst, rows, size, pitch, cols, cols + rows);
 }
 
+// ---------------------------------------------------------------- pinned pool
+
+namespace {
+std::mutex g_pinned_mu;
+std::multimap<size_t, PinnedBlock> g_pinned_free;
+}  // namespace
+
+int pinned_get(size_t bytes, PinnedBlock* out) {
+    size_t cls = size_t{64} << 10;
+    while (cls < bytes) cls <<= 1;
+    {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        auto it = g_pinned_free.find(cls);
+        if (it != g_pinned_free.end()) {
+            *out = it->second;
+            g_pinned_free.erase(it);
+            return RS_OK;
+        }
+    }
+    void* h = nullptr;
+    if (hipHostMalloc(&h, cls, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+        return RS_ERR_NOMEM;
+    void* d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess || !d) {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned_free.emplace(cls, PinnedBlock{static_cast<uint8_t*>(h), nullptr, cls});  // kept, never handed out
+        return dev_fail(e != hipSuccess ? e : hipErrorInvalidValue, "pinned block device pointer");
+    }
+    *out = PinnedBlock{static_cast<uint8_t*>(h), static_cast<uint8_t*>(d), cls};
+    return RS_OK;
+}
+
+void pinned_put(PinnedBlock& b) {
+    if (b.host && b.dev) {
+        std::lock_guard<std::mutex> lk(g_pinned_mu);
+        g_pinned_free.emplace(b.bytes, b);
+    }
+    b = PinnedBlock{};
+}
+
 // ---------------------------------------------------------------- coalescing
 
 // Vectors up to this size take part in host-call coalescing (0 = off).
@@ -255,6 +296,8 @@ size_t g_coalesce_max = 128 * 1024;
 // Group-commit window: a ready batch waits up to this long for more callers
 // before it launches (0 = launch as soon as the GPU is free; the default).
 int g_coalesce_linger_us = 0;
+// Waiters spin this long on a batch state change before blocking.
+int g_co_spin_us = 50;
 // Upper bound on one coalesced batch's pinned bytes and stripe count.
 constexpr size_t kCoalesceBytes = size_t{32} << 20;
 constexpr int kCoalesceStripes = 256;
@@ -278,25 +321,13 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
     b.cap = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kCoalesceStripes, kCoalesceBytes / b.stride)));
     const size_t need = b.stride * static_cast<size_t>(b.cap);
     if (need > b.host_bytes) {
-        if (b.host) (void)hipHostFree(b.host);
-        b.host = nullptr;
-        b.dev = nullptr;
+        pinned_put(b.blk);
+        b.host = b.dev = nullptr;
         b.host_bytes = 0;
-        // (the resident engine reads and writes it too: its system-scope
-        // acquire / release fences stand in for the kernel boundary)
-        if (hipHostMalloc(reinterpret_cast<void**>(&b.host), need, hipHostMallocDefault) != hipSuccess) {
-            b.host = nullptr;
-            return RS_ERR_NOMEM;
-        }
-        void* dp = nullptr;
-        const hipError_t e = hipHostGetDevicePointer(&dp, b.host, 0);
-        if (e != hipSuccess || !dp) {
-            (void)hipHostFree(b.host);
-            b.host = nullptr;
-            return dev_fail(e != hipSuccess ? e : hipErrorInvalidValue, "coalescing buffer device pointer");
-        }
-        b.dev = static_cast<uint8_t*>(dp);
-        b.host_bytes = need;
+        RS_TRY(pinned_get(need, &b.blk));
+        b.host = b.blk.host;
+        b.dev = b.blk.dev;
+        b.host_bytes = b.blk.bytes;
     }
     b.joined = b.ready = b.released = 0;
     b.launchable = false;
@@ -309,7 +340,8 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
 // (zero-copy), then wait for it.
 static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     // small batches: the resident engine (engine.cpp), no launch and no stream sync
-    const int erc = engine_call(rs, b.mat.data(), b.rows, b.cols, b.dev, b.pitch, b.stride, n, b.accumulate);
+    const int erc = engine_call(rs, b.mat.data(), b.rows, b.cols, b.dev, b.pitch, b.stride, n, b.accumulate,
+                                /*coherent: a pool block*/ true);
     if (erc != RS_ERR_INVAL) return erc;
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];
@@ -319,6 +351,26 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
                           static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
     const hipError_t e = hipStreamSynchronize(rs->co_stream);  // never leave a kernel on the buffer
     return rc ? rc : (e == hipSuccess ? RS_OK : dev_fail(e, "coalesced batch sync"));
+}
+
+// Wait for the next batch state change: spin briefly on co_gen (a futex
+// wake costs several us, as much as a whole engine call), then block.
+static void co_wait(rs_t* rs, std::unique_lock<std::mutex>& lk) {
+    const uint64_t g = rs->co_gen.load(std::memory_order_acquire);
+    lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
+    bool changed = false;
+    for (uint32_t i = 0; !changed; ++i) {
+        changed = rs->co_gen.load(std::memory_order_acquire) != g;
+        if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(g_co_spin_us)) break;
+    }
+    lk.lock();
+    if (!changed && rs->co_gen.load(std::memory_order_acquire) == g) rs->co_cv.wait(lk);
+}
+
+static void co_changed(rs_t* rs) {  // caller holds co_mu
+    rs->co_gen.fetch_add(1, std::memory_order_acq_rel);
+    rs->co_cv.notify_all();
 }
 
 // The synchronous host calls' entry (rs_encode / rs_reconst / rs_update /
@@ -381,7 +433,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
                     b = &c;
                     break;
                 }
-        if (!b) rs->co_cv.wait(lk);
+        if (!b) co_wait(rs, lk);
     }
     idx = b->joined++;
     const bool alone = rs->co_active == 1;
@@ -409,6 +461,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
 
     lk.lock();
     ++b->ready;
+    co_changed(rs);
     while (b->state != CoBatch::kDone) {
         if (b->state == CoBatch::kFilling && !rs->co_gpu_busy && b->ready == b->joined) {
             if (g_coalesce_linger_us > 0 && b->joined < b->cap) {
@@ -434,10 +487,10 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
             b->rc = rc;
             b->state = CoBatch::kDone;
             rs->co_gpu_busy = false;
-            rs->co_cv.notify_all();
+            co_changed(rs);
             break;
         }
-        rs->co_cv.wait(lk);
+        co_wait(rs, lk);
     }
     const int rc = b->rc;
     lk.unlock();
@@ -457,7 +510,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     lk.lock();
     if (++b->released == b->joined) {
         b->state = CoBatch::kIdle;
-        rs->co_cv.notify_all();
+        co_changed(rs);
     }
     --rs->co_active;
     return rc;

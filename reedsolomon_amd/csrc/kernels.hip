@@ -780,13 +780,14 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
                 return;  // every lane of the wave leaves together (uniform values)
             __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's bytes of this call
         const uint64_t base = lane_u64(w, 1), stride = lane_u64(w, 2);
         const uint64_t w3 = lane_u64(w, 3), w4 = lane_u64(w, 4), w5 = lane_u64(w, 5);
         const uint32_t pitch = static_cast<uint32_t>(w3), units = static_cast<uint32_t>(w3 >> 32);
         const uint32_t nstripes = static_cast<uint32_t>(w4);
         const int rows = static_cast<int>((w4 >> 32) & 0xffff), cols = static_cast<int>(w4 >> 48);
-        const bool accumulate = static_cast<uint32_t>(w5) != 0;
+        const bool accumulate = (w5 & 1) != 0;
+        const bool coherent = (w5 & 2) != 0;  // fine-grained buffer: no invalidate / write-back
+        if (!coherent) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's bytes
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
         if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords
             for (int i = lane; i < cols * kEngineMaxRows * 5; i += 64)
@@ -805,9 +806,11 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
             case 7: engine_units<7>(call, tab); break;
             default: engine_units<8>(call, tab); break;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this call acknowledged
+        if (!coherent) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (lane == 0) __hip_atomic_store(&ring->done[blockIdx.x], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         last = seq;
     }
