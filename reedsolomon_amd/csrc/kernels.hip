@@ -786,8 +786,10 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
         const uint32_t nstripes = static_cast<uint32_t>(w4);
         const int rows = static_cast<int>((w4 >> 32) & 0xffff), cols = static_cast<int>(w4 >> 48);
         const bool accumulate = (w5 & 1) != 0;
-        const bool coherent = (w5 & 2) != 0;  // fine-grained buffer: no invalidate / write-back
-        if (!coherent) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's bytes
+        const bool coherent = (w5 & 2) != 0;  // fine-grained buffer: stores need no L2 write-back
+        // system-scope acquire, always: without it the first call on a fresh
+        // coherent block read zeros (lines the runtime's clear left in L2)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
         if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords
             for (int i = lane; i < cols * kEngineMaxRows * 5; i += 64)
