@@ -60,10 +60,10 @@ struct DeviceGuard {  // switch to the handle's device, restore the caller's on 
 
 inline uint64_t rup(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
-// Process-wide pool of coherent (fine-grained) pinned host blocks, mapped
-// for every device (host_calls.cpp).  Blocks are recycled across handles and
-// never freed, so coherent mappings are not created and torn down while
-// other work runs; sizes are rounded up to a power of two (>= 64 KiB).
+// Process-wide pool of pinned host blocks, mapped for every device
+// (host_calls.cpp).  Blocks are recycled across handles and never freed, so
+// pinned mappings are not created and torn down while other work runs;
+// sizes are rounded up to a power of two (>= 64 KiB).
 struct PinnedBlock {
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;   // device address (same for every device with unified addressing)
@@ -120,7 +120,7 @@ struct rs_codec {
         bool accumulate = false;
         size_t pitch = 0, stride = 0;
         int cap = 0;               // stripes this batch may take
-        uint8_t* host = nullptr;   // pinned [cap][cols + rows][pitch] (a pool block: coherent)
+        uint8_t* host = nullptr;   // pinned [cap][cols + rows][pitch] (a pool block)
         uint8_t* dev = nullptr;    // its device-mapped address
         size_t host_bytes = 0;
         rsamd::detail::PinnedBlock blk;

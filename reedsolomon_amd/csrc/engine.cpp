@@ -40,7 +40,11 @@ int g_engine = [] {                     // rs_tune("host_engine", 0 | 1); env RS
 }();
 int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..16): workgroups of one wave
 int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
-size_t g_engine_max_bytes = 1u << 20;   // rs_tune("host_engine_max_bytes"): larger batches launch
+// Batches up to this many bytes go to the engine, larger ones launch: its
+// few workgroups lose to a full-GPU launch past about one 10+4 @ 8 KiB stripe
+// (8 threads of 8 KiB calls: 15.2 GiB/s at 128 KiB, 11.0 at 1 MiB,
+// profiles/r02/host_concurrency_engine.log).
+size_t g_engine_max_bytes = 128u << 10;  // rs_tune("host_engine_max_bytes")
 
 // Doorbell rings are fine-grained (coherent) pinned memory: allocated once
 // per process and device and recycled across handles, never freed (no

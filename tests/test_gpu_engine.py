@@ -29,7 +29,7 @@ def engine(rslib):
     L.rs_tune(b"host_engine", 1)
     L.rs_tune(b"host_engine_waves", 8)
     L.rs_tune(b"host_engine_idle_us", 200)
-    L.rs_tune(b"host_engine_max_bytes", 1 << 20)
+    L.rs_tune(b"host_engine_max_bytes", 128 << 10)
 
 
 def _rand(rng, n):
