@@ -29,6 +29,8 @@
 
 #include <cstdlib>
 
+#include <hip/hip_ext.h>
+
 #include "codec_internal.hpp"
 
 namespace rsamd {
@@ -95,6 +97,29 @@ void engine_shutdown(rs_t* rs) {
     rs->eng_ring = rs->eng_dring = nullptr;
 }
 
+// The engine's stream must own its hardware queue: HIP maps streams onto a
+// few hardware queues, and a resident kernel holds its queue, so kernels of
+// any stream sharing it would wait until the engine leaves
+// (tools/queue_probe.hip, profiles/r02/queue_probe.log: with the resident
+// kernel on a plain stream 2 of 8 other streams stalled for the whole 50 ms
+// window; on a CU-masked or a high-priority stream none did).  A CU-masked
+// stream (every CU enabled) gets a queue of its own.
+static hipStream_t engine_stream() {
+    hipStream_t st = nullptr;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && cus > 0) {
+        std::vector<uint32_t> mask(static_cast<size_t>((cus + 31) / 32), 0);
+        for (int c = 0; c < cus; ++c) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess) return st;
+    }
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+        hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi) == hipSuccess)
+        return st;
+    return nullptr;
+}
+
 static int engine_launch(rs_t* rs, int waves, uint64_t start) {
     const uint64_t idle_ticks = static_cast<uint64_t>(g_engine_idle_us) * 100;  // 100 MHz realtime counter
     RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, start, idle_ticks, rs->eng_stream), "engine launch"));
@@ -125,8 +150,8 @@ int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
             ring_put(rs->device, h);
             return dev_fail(e != hipSuccess ? e : hipErrorInvalidValue, "engine ring device pointer");
         }
-        hipStream_t st = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        hipStream_t st = engine_stream();
+        if (!st) {
             ring_put(rs->device, h);
             return dev_fail(hipErrorInvalidValue, "engine stream");
         }

@@ -468,8 +468,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     }
 
     lk.lock();
-    ++b->ready;
-    co_changed(rs);
+    ++b->ready;  // (no wake-up: the member that completes the batch launches it itself)
     while (b->state != CoBatch::kDone) {
         if (b->state == CoBatch::kFilling && !rs->co_gpu_busy && b->ready == b->joined) {
             if (g_coalesce_linger_us > 0 && b->joined < b->cap) {
