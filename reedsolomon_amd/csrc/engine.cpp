@@ -27,6 +27,7 @@
 // into their outputs).
 #include <immintrin.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 #include <hip/hip_ext.h>
@@ -47,6 +48,7 @@ int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
 // (8 threads of 8 KiB calls: 15.2 GiB/s at 128 KiB, 11.0 at 1 MiB,
 // profiles/r02/host_concurrency_engine.log).
 size_t g_engine_max_bytes = 128u << 10;  // rs_tune("host_engine_max_bytes")
+static const bool g_engine_trace = std::getenv("RSAMD_ENGINE_TRACE") != nullptr;
 
 // Doorbell rings are fine-grained (coherent) pinned memory: allocated once
 // per process and device and recycled across handles, never freed (no
@@ -139,6 +141,7 @@ int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
     const uint64_t units = pitch / 16;
     if (units * static_cast<uint64_t>(nstripes) >= (uint64_t{1} << 31) || pitch >= (size_t{1} << 32))
         return RS_ERR_INVAL;
+    const auto t_call = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(rs->eng_mu);
     if (!rs->eng_ring) {
         EngineRing* h = ring_get(rs->device);
@@ -228,6 +231,13 @@ int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
     }
     rs->eng_last = std::chrono::steady_clock::now();
     rs->eng_calls.fetch_add(1, std::memory_order_relaxed);
+    if (g_engine_trace) {  // diagnostics: calls slower than 100 us, with where the time went
+        const double us = std::chrono::duration<double, std::micro>(rs->eng_last - t_call).count();
+        if (us > 100)
+            std::fprintf(stderr, "engine slow call: %.1f us total, %.1f us before the doorbell, seq %llu, n %d\n", us,
+                         std::chrono::duration<double, std::micro>(t_ring - t_call).count(),
+                         static_cast<unsigned long long>(seq), nstripes);
+    }
     return RS_OK;
 }
 

@@ -3,6 +3,8 @@
 // in pageable host memory): column-chunked zero-copy staging through a
 // pinned mirror, or the staged DMA paths for large vectors.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 
 #include "host_pool.hpp"
@@ -302,6 +304,7 @@ int g_coalesce_linger_us = 0;
 // while at most this many callers are inside host_call.
 int g_co_spin_us = 30;
 int g_co_spin_callers = 8;
+static const bool g_host_trace = std::getenv("RSAMD_ENGINE_TRACE") != nullptr;
 // Upper bound on one coalesced batch's pinned bytes and stripe count.
 constexpr size_t kCoalesceBytes = size_t{32} << 20;
 constexpr int kCoalesceStripes = 256;
@@ -416,6 +419,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         std::lock_guard<std::mutex> lk(rs->stage_mu);
         return host_product(rs, mat, rows, cols, src, dst, size, accumulate);
     }
+    const auto t_enter = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(rs->co_mu);
     if (!rs->co_stream && hip_ok(hipStreamCreateWithFlags(&rs->co_stream, hipStreamNonBlocking), "stream create")) {
         rs->co_stream = nullptr;
@@ -502,6 +506,10 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     const int rc = b->rc;
     lk.unlock();
 
+    if (g_host_trace) {
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_enter).count();
+        if (us > 200) std::fprintf(stderr, "host_call slow: %.1f us to batch done (joined %d)\n", us, b->joined);
+    }
     if (rc == RS_OK) {  // copy out: own output rows
         uint8_t* cd[kMaxVects];
         const uint8_t* cs[kMaxVects];
