@@ -791,9 +791,16 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
         // coherent block read zeros (lines the runtime's clear left in L2)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
-        if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords
-            for (int i = lane; i < cols * kEngineMaxRows * 5; i += 64)
-                tab[i] = __hip_atomic_load(&ring->tables[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords, every load in flight at once (one PCIe trip)
+            constexpr int kTabPerLane = kEngineMaxCols * kEngineMaxRows * 5 / 64;
+            const int n = cols * kEngineMaxRows * 5;
+            uint32_t t[kTabPerLane];
+#pragma unroll
+            for (int k = 0; k < kTabPerLane; ++k)
+                if (lane + 64 * k < n) t[k] = __builtin_nontemporal_load(&ring->tables[lane + 64 * k]);
+#pragma unroll
+            for (int k = 0; k < kTabPerLane; ++k)
+                if (lane + 64 * k < n) tab[lane + 64 * k] = t[k];
             tab_have = tab_id;
         }
         __syncthreads();
