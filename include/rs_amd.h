@@ -343,7 +343,7 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
  * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "wide_block" (128 | 256),
  * "host_engine" (1 default: small synchronous host calls, coalesced or
  * alone, are served by a resident kernel through a doorbell in host memory |
- * 0: one launch + stream sync per call), "host_engine_waves" (1..16
+ * 0: one launch + stream sync per call), "host_engine_waves" (1..64
  * workgroups, default 8), "host_engine_idle_us" (the engine leaves after this
  * long without a call, default 200), "host_engine_max_bytes" (larger batches
  * launch; default 128 KiB),

@@ -59,7 +59,7 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
 // launch + stream sync per call (DESIGN.md §5 "Host-call engine").
 // Everything below lives in fine-grained (coherent) pinned host memory that
 // the kernel reads and writes over PCIe.
-constexpr int kEngineMaxRows = 8, kEngineMaxCols = 32, kEngineMaxWaves = 16;
+constexpr int kEngineMaxRows = 8, kEngineMaxCols = 32, kEngineMaxWaves = 64;
 struct EngineHeader {      // one 64-byte line; the host writes seq0 and seq1 LAST
     uint64_t seq0;         // doorbell value (first word of the line)
     uint64_t base;         // device address of stripe 0, vector 0
