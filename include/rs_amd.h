@@ -346,8 +346,7 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
  * 0: one launch + stream sync per call), "host_engine_waves" (1..64
  * workgroups, default 8), "host_engine_idle_us" (the engine leaves after this
  * long without a call, default 200), "host_engine_max_bytes" (larger batches
- * launch; default 128 KiB), "host_engine_policy" (the engine's memory
- * accesses: 0 default = nt + system-scope fences, 1 = sc0 sc1, 2 = sc1),
+ * launch; default 128 KiB),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;

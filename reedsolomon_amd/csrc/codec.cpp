@@ -521,7 +521,6 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_engine") g_engine = value ? 1 : 0;
         else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxWaves ? kEngineMaxWaves : value;
         else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
-        else if (n == "host_engine_policy") g_engine_policy = (value >= 0 && value <= 2) ? value : 0;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);

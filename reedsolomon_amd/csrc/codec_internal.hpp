@@ -191,10 +191,10 @@ namespace detail {
 // Host-call engine (engine.cpp).  engine_call: RS_ERR_INVAL when the call
 // does not fit the engine (the caller launches instead).
 int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
-                size_t stride, int nstripes, bool accumulate);
+                size_t stride, int nstripes, bool accumulate, bool coherent);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
-extern int g_engine, g_engine_waves, g_engine_idle_us, g_engine_policy;
+extern int g_engine, g_engine_waves, g_engine_idle_us;
 extern size_t g_engine_max_bytes;
 }  // namespace detail
 }  // namespace rsamd

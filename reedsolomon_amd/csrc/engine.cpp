@@ -49,8 +49,6 @@ int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
 // profiles/r02/host_concurrency_engine.log).
 size_t g_engine_max_bytes = 128u << 10;  // rs_tune("host_engine_max_bytes")
 static const bool g_engine_trace = std::getenv("RSAMD_ENGINE_TRACE") != nullptr;
-// Memory policy of the engine's data accesses (EngineHeader::flags).
-int g_engine_policy = 0;  // rs_tune("host_engine_policy", 0 | 1 | 2)
 
 // Doorbell rings are fine-grained (coherent) pinned memory: allocated once
 // per process and device and recycled across handles, never freed (no
@@ -135,7 +133,7 @@ static int engine_launch(rs_t* rs, int waves, uint64_t start) {
 }
 
 int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
-                size_t stride, int nstripes, bool accumulate) {
+                size_t stride, int nstripes, bool accumulate, bool coherent) {
     if (!g_engine || rows < 1 || rows > kEngineMaxRows || cols < 1 || cols > kEngineMaxCols || nstripes < 1 ||
         pitch % 16 || stride % 16 || (reinterpret_cast<uintptr_t>(dev_base) & 15))
         return RS_ERR_INVAL;
@@ -201,7 +199,7 @@ int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
     h->nstripes = static_cast<uint32_t>(nstripes);
     h->rows = static_cast<uint16_t>(rows);
     h->cols = static_cast<uint16_t>(cols);
-    h->flags = (accumulate ? 1u : 0u) | (static_cast<uint32_t>(g_engine_policy & 3) << 2);
+    h->flags = (accumulate ? 1u : 0u) | (coherent ? 2u : 0u);
     h->tab_id = rs->eng_tab_id;
     const uint64_t seq = ++rs->eng_seq;
     std::atomic_thread_fence(std::memory_order_release);

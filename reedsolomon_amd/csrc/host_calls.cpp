@@ -347,7 +347,8 @@ static int init_batch(CoBatch& b, const uint8_t* mat, int rows, int cols, size_t
 // (zero-copy), then wait for it.
 static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     // small batches: the resident engine (engine.cpp), no launch and no stream sync
-    const int erc = engine_call(rs, b.mat.data(), b.rows, b.cols, b.dev, b.pitch, b.stride, n, b.accumulate);
+    const int erc = engine_call(rs, b.mat.data(), b.rows, b.cols, b.dev, b.pitch, b.stride, n, b.accumulate,
+                                /*coherent*/ false);  // measured: outputs stale without the release write-back
     if (erc != RS_ERR_INVAL) return erc;
     const uint8_t* in[kMaxVects];
     uint8_t* out[kMaxVects];

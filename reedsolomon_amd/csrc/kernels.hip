@@ -704,33 +704,33 @@ constexpr int kEngineColBatch = 16;  // column loads in flight per lane (one PCI
 
 struct EngineCall {
     uint64_t base, stride;
-    uint32_t pitch, units, total, bytes;  // bytes: the batch's extent from base
+    uint32_t pitch, units, total;
     int cols;
     bool accumulate;
 };
 
 // This workgroup's units of one call: 16 bytes of every vector of one stripe
 // per lane and unit, all column loads of a batch in flight together (host
-// memory: one PCIe round trip per batch), ROWS output rows.  AUX: the memory
-// instructions' cache policy (-1: global nt; >= 0: buffer instructions with
-// that policy over [base, base + bytes), e.g. 17 = sc0 sc1, system scope).
-template <int ROWS, int AUX>
+// memory: one PCIe round trip per batch), ROWS output rows.
+template <int ROWS>
 __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t* tab) {
-    const g_u8* base = reinterpret_cast<const g_u8*>(e.base);
+    typedef __attribute__((address_space(1))) u32x4 gq;
     for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < e.total; u += gridDim.x * 64u) {
         const uint32_t si = u / e.units, k = u - si * e.units;
-        const uint32_t sb = si * static_cast<uint32_t>(e.stride) + k * 16;  // offset from base (< 2^31)
+        const uint64_t sb = e.base + static_cast<uint64_t>(si) * e.stride + static_cast<uint64_t>(k) * 16;
         u32x4 acc[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; ++r)
-            acc[r] = e.accumulate ? load16<AUX, 4>(base, sb + static_cast<uint32_t>(e.cols + r) * e.pitch, e.bytes, true)
+            acc[r] = e.accumulate ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(
+                                        sb + static_cast<uint64_t>(e.cols + r) * e.pitch))
                                   : u32x4{0, 0, 0, 0};
         for (int c0 = 0; c0 < e.cols; c0 += kEngineColBatch) {
             const int nb = (e.cols - c0) < kEngineColBatch ? (e.cols - c0) : kEngineColBatch;
             u32x4 x[kEngineColBatch];
 #pragma unroll
             for (int b = 0; b < kEngineColBatch; ++b)
-                if (b < nb) x[b] = load16<AUX, 4>(base, sb + static_cast<uint32_t>(c0 + b) * e.pitch, e.bytes, true);
+                if (b < nb)
+                    x[b] = __builtin_nontemporal_load(reinterpret_cast<const gq*>(sb + static_cast<uint64_t>(c0 + b) * e.pitch));
 #pragma unroll
             for (int b = 0; b < kEngineColBatch; ++b) {
                 if (b < nb) {
@@ -753,21 +753,7 @@ __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t
         }
 #pragma unroll
         for (int r = 0; r < ROWS; ++r)
-            store16<AUX, 4>(const_cast<g_u8*>(base), sb + static_cast<uint32_t>(e.cols + r) * e.pitch, e.bytes, acc[r], true);
-    }
-}
-
-template <int AUX>
-__device__ __forceinline__ void engine_call_rows(const EngineCall& e, int rows, const uint32_t* tab) {
-    switch (rows) {
-        case 1: engine_units<1, AUX>(e, tab); break;
-        case 2: engine_units<2, AUX>(e, tab); break;
-        case 3: engine_units<3, AUX>(e, tab); break;
-        case 4: engine_units<4, AUX>(e, tab); break;
-        case 5: engine_units<5, AUX>(e, tab); break;
-        case 6: engine_units<6, AUX>(e, tab); break;
-        case 7: engine_units<7, AUX>(e, tab); break;
-        default: engine_units<8, AUX>(e, tab); break;
+            __builtin_nontemporal_store(acc[r], reinterpret_cast<gq*>(sb + static_cast<uint64_t>(e.cols + r) * e.pitch));
     }
 }
 
@@ -800,12 +786,10 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
         const uint32_t nstripes = static_cast<uint32_t>(w4);
         const int rows = static_cast<int>((w4 >> 32) & 0xffff), cols = static_cast<int>(w4 >> 48);
         const bool accumulate = (w5 & 1) != 0;
-        // memory policy: 0 = global nt loads / stores inside system-scope
-        // acquire / release fences; 1 = buffer loads / stores with sc0 sc1
-        // (system scope: no stale L2 line is read, a store is acknowledged once
-        // visible to the host), no fences; 2 = sc1 only, no fences
-        const int policy = static_cast<int>((w5 >> 2) & 3);
-        if (policy == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const bool coherent = (w5 & 2) != 0;  // fine-grained buffer: stores need no L2 write-back
+        // system-scope acquire, always: without it the first call on a fresh
+        // coherent block read zeros (lines the runtime's clear left in L2)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
         if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords, every load in flight at once (one PCIe trip)
             constexpr int kTabPerLane = kEngineMaxCols * kEngineMaxRows * 5 / 64;
@@ -820,13 +804,19 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
             tab_have = tab_id;
         }
         __syncthreads();
-        const EngineCall call{base, stride, pitch, units, nstripes * units,
-                              static_cast<uint32_t>(stride) * nstripes, cols, accumulate};
-        if (policy == 1) engine_call_rows<17>(call, rows, tab);
-        else if (policy == 2) engine_call_rows<16>(call, rows, tab);
-        else engine_call_rows<-1>(call, rows, tab);
+        const EngineCall call{base, stride, pitch, units, nstripes * units, cols, accumulate};
+        switch (rows) {
+            case 1: engine_units<1>(call, tab); break;
+            case 2: engine_units<2>(call, tab); break;
+            case 3: engine_units<3>(call, tab); break;
+            case 4: engine_units<4>(call, tab); break;
+            case 5: engine_units<5>(call, tab); break;
+            case 6: engine_units<6>(call, tab); break;
+            case 7: engine_units<7>(call, tab); break;
+            default: engine_units<8>(call, tab); break;
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this call acknowledged
-        if (policy == 0) {
+        if (!coherent) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }

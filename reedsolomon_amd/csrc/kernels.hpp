@@ -68,8 +68,8 @@ struct EngineHeader {      // one 64-byte line; the host writes seq0 and seq1 LA
     uint32_t units;        // 16-byte units per vector (pitch / 16: whole slots, padding included)
     uint32_t nstripes;
     uint16_t rows, cols;   // <= kEngineMaxRows / kEngineMaxCols
-    uint32_t flags;        // bit 0: XOR into the output rows (Update / Replace); bits 2-3: memory policy
-                           // (0: nt + system-scope fences, 1: sc0 sc1 accesses, 2: sc1 accesses)
+    uint32_t flags;        // bit 0: XOR into the output rows (Update / Replace); bit 1: the buffer is
+                           // coherent (fine-grained) memory, no cache invalidate / write-back needed
     uint32_t tab_id;       // identity of EngineRing::tables (reloaded into LDS when it changes)
     uint64_t reserved;
     uint64_t seq1;         // doorbell value again (last word of the line)

@@ -30,21 +30,19 @@ def engine(rslib):
     L.rs_tune(b"host_engine_waves", 8)
     L.rs_tune(b"host_engine_idle_us", 200)
     L.rs_tune(b"host_engine_max_bytes", 128 << 10)
-    L.rs_tune(b"host_engine_policy", 0)
 
 
 def _rand(rng, n):
     return rng.integers(0, 256, n, dtype=np.uint8)
 
 
-@pytest.mark.parametrize("waves,policy", [(8, 0), (1, 0), (16, 0), (8, 1), (16, 1), (8, 2)])
-def test_engine_calls_vs_oracle(rslib, orc, torch_dev, engine, waves, policy):
+@pytest.mark.parametrize("waves", [8, 1, 16])
+def test_engine_calls_vs_oracle(rslib, orc, torch_dev, engine, waves):
     """Encode / Reconst / Update / Replace host calls of many shapes and sizes
     (tails, 8 KiB, 128 KiB; up to 8 output rows and 32 columns through the
     engine, larger shapes through the launch path) against the oracle."""
     assert engine.rs_tune(b"host_engine_waves", waves) == 0
-    assert engine.rs_tune(b"host_engine_policy", policy) == 0
-    rng = np.random.default_rng(50 + waves + 100 * policy)
+    rng = np.random.default_rng(50 + waves)
     for d, p in [(10, 4), (12, 4), (6, 3), (8, 8), (20, 4), (32, 8), (3, 1), (40, 10)]:
         r = rslib.New(d, p)
         for size in (1, 17, 255, 1024, 4097, 8192, 131072):

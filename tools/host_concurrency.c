@@ -90,7 +90,6 @@ int main(int argc, char** argv) {
     g_mixed = atoi(argv[4]);
     if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));
     if (getenv("HL_ENGINE_MAX")) rs_tune("host_engine_max_bytes", atoi(getenv("HL_ENGINE_MAX")));
-    if (getenv("HL_ENGINE_POLICY")) rs_tune("host_engine_policy", atoi(getenv("HL_ENGINE_POLICY")));
     if (getenv("HL_ENGINE_WAVES")) rs_tune("host_engine_waves", atoi(getenv("HL_ENGINE_WAVES")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &g_rs) != RS_OK) {
         fprintf(stderr, "no device\n");

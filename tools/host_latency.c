@@ -57,8 +57,7 @@ int main(int argc, char** argv) {
     }
     if (argc >= 4) rs_tune("host_chunk", atoi(argv[3]));
     if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));
-    if (getenv("HL_ENGINE_MAX")) rs_tune("host_engine_max_bytes", atoi(getenv("HL_ENGINE_MAX")));
-    if (getenv("HL_ENGINE_POLICY")) rs_tune("host_engine_policy", atoi(getenv("HL_ENGINE_POLICY")));  /* resident host-call engine on / off */
+    if (getenv("HL_ENGINE_MAX")) rs_tune("host_engine_max_bytes", atoi(getenv("HL_ENGINE_MAX")));  /* resident host-call engine on / off */
     if (getenv("HL_ENGINE_WAVES")) rs_tune("host_engine_waves", atoi(getenv("HL_ENGINE_WAVES")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
