@@ -344,9 +344,16 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
  * "host_engine" (1 default: small synchronous host calls, coalesced or
  * alone, are served by a resident kernel through a doorbell in host memory |
  * 0: one launch + stream sync per call), "host_engine_waves" (1..64
- * workgroups, default 8), "host_engine_idle_us" (the engine leaves after this
- * long without a call, default 200), "host_engine_max_bytes" (larger batches
- * launch; default 128 KiB),
+ * workgroups, each polling the doorbell with its first wave; default 8),
+ * "host_engine_group_waves" (1..8 waves per workgroup; default 8),
+ * "host_engine_direct" (1 default: small calls the engine takes stage their
+ * stripe in a pinned block of their own and ring the engine directly, several
+ * callers' calls in flight at once | 0: they join coalesced batches),
+ * "host_engine_wg_units" (16-byte units per workgroup a call is spread over;
+ * 0 default = one per lane of a workgroup, so calls in flight run on
+ * different workgroups),
+ * "host_engine_idle_us" (the engine leaves after this long without a call,
+ * default 200), "host_engine_max_bytes" (larger batches launch; default 1 MiB),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;
@@ -355,7 +362,8 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
  * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),
  * "host_coalesce_linger_us" (a ready shared batch waits this long for more
- * callers before it launches; default 0),
+ * callers before it launches; default 0), "host_coalesce_running" (shared
+ * batches in flight at once: 1 | 2 default),
  * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
  * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
  * "table_registry_max" (distinct coefficient matrices

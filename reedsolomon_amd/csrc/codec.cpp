@@ -519,7 +519,10 @@ int rs_tune(const char* name, int value) {
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
         else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
         else if (n == "host_engine") g_engine = value ? 1 : 0;
-        else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxWaves ? kEngineMaxWaves : value;
+        else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxGroups ? kEngineMaxGroups : value;
+        else if (n == "host_engine_group_waves")
+            g_engine_group_waves = value < 1 ? 1 : value > kEngineMaxGroupWaves ? kEngineMaxGroupWaves : value;
+        else if (n == "host_engine_wg_units") g_engine_wg_units = value < 0 ? 0 : value;
         else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
@@ -530,6 +533,8 @@ int rs_tune(const char* name, int value) {
         else if (n == "bind_numa") g_bind_numa = value;
         else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
         else if (n == "host_coalesce_linger_us") g_coalesce_linger_us = value < 0 ? 0 : value;
+        else if (n == "host_engine_direct") g_engine_direct = value ? 1 : 0;
+        else if (n == "host_coalesce_running") g_co_running = value < 1 ? 1 : value > 2 ? 2 : value;
         else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
         else return RS_ERR_INVAL;

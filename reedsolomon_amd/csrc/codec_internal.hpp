@@ -131,8 +131,10 @@ struct rs_codec {
     };
     std::mutex co_mu;
     std::condition_variable co_cv;
-    CoBatch co[2];
-    bool co_gpu_busy = false;
+    static constexpr int kCoBatches = 3;
+    CoBatch co[kCoBatches];
+    int co_running = 0;
+    std::mutex co_launch_mu;       // the launch fallback: one batch at a time on co_stream
     int co_active = 0;             // callers inside host_call
     std::atomic<uint64_t> co_gen{0};  // bumped at every batch state change (spinning waiters watch it)
     std::atomic<uint64_t> co_launches{0}, co_calls{0};
@@ -164,18 +166,22 @@ struct rs_codec {
     hipStream_t up_stream = nullptr;
 
     // Host-call engine (engine.cpp): resident kernel + doorbell ring serving
-    // the coalesced small host calls.  Guarded by eng_mu.
+    // the small host calls.  eng_mu guards submission and the instance; a
+    // caller waits for its call's completion without it.
     std::mutex eng_mu;
     rsamd::EngineRing* eng_ring = nullptr;   // host address (fine-grained pinned)
     rsamd::EngineRing* eng_dring = nullptr;  // its device address
     hipStream_t eng_stream = nullptr;
     bool eng_running = false;
-    int eng_waves = 0;
+    int eng_waves = 0;       // the running instance's workgroups
+    int eng_group_waves = 0; // ... and waves per workgroup
     int eng_idle_us = 0;     // the running instance's idle window
     uint64_t eng_seq = 0;
-    uint32_t eng_tab_id = 0;
+    int eng_next_wg = 0;     // first workgroup of the next call
+    uint64_t eng_epoch = 0;  // the latest instance launched (its gone words / stop word carry it)
+    uint32_t eng_tab_id = 0;                          // the latest matrix's table id
+    uint32_t eng_slot_tab[rsamd::kEngineSlots] = {};  // table id each slot holds
     std::vector<uint8_t> eng_tab_key;
-    std::chrono::steady_clock::time_point eng_last;
     std::atomic<uint64_t> eng_calls{0}, eng_launches{0};
 
     const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
@@ -192,10 +198,38 @@ namespace detail {
 // does not fit the engine (the caller launches instead).
 int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
                 size_t stride, int nstripes, bool accumulate, bool coherent);
+// Address mode: one stripe whose vectors (cols inputs, rows outputs; device
+// addresses, 16-byte aligned, size a multiple of 16) lie anywhere, e.g. in
+// memory the caller registered.
+int engine_call_addr(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in, uint8_t* const* out,
+                     size_t size, bool accumulate);
+// Would the engine take a call of this shape moving `bytes` in all?
+bool engine_accepts(int rows, int cols, size_t bytes);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
-extern int g_engine, g_engine_waves, g_engine_idle_us;
+extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_wg_units;
 extern size_t g_engine_max_bytes;
+
+// Diagnostics (env RSAMD_ENGINE_TRACE): where the time of the synchronous
+// host calls goes, as mean us per call and phase, printed at process exit.
+enum HostPhase {
+    kPhJoin,      // enter -> own stripe slot in a batch
+    kPhCopyIn,    // caller vectors -> pinned slot
+    kPhWaitRun,   // ready -> this batch starts running (or is done, for non-runners)
+    kPhPreBell,   // engine_call entry -> doorbell rung (lock, relaunch, tables, header)
+    kPhBell,      // doorbell rung -> every done word seen
+    kPhWake,      // batch done -> caller resumes
+    kPhCopyOut,   // pinned slot -> caller vectors
+    kPhGpuTab,    // engine workgroup 0: doorbell seen -> acquire done, tables in LDS
+    kPhGpuWork,   //   -> its stores acknowledged
+    kPhGpuRel,    //   -> release write-back done, done word written
+    kPhCount
+};
+extern const bool g_phase_trace;
+void phase_add_ns(HostPhase p, uint64_t ns);
+inline void phase_add(HostPhase p, std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    phase_add_ns(p, static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count()));
+}
 }  // namespace detail
 }  // namespace rsamd
 
@@ -418,7 +452,7 @@ int check_reconst_passes(const rs_t* rs, const ReconstPlan& pl, const size_t* le
 
 // ---------------------------------------------------------------- host calls (host_calls.cpp)
 extern size_t g_pinned_max, g_zc_max, g_chunk, g_coalesce_max;
-extern int g_coalesce_linger_us;
+extern int g_coalesce_linger_us, g_co_running, g_engine_direct;
 int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
                  size_t size, bool accumulate);
 // host_product for a synchronous host call, coalesced with concurrent calls

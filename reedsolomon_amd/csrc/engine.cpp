@@ -28,7 +28,9 @@
 #include <immintrin.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
+#include <thread>
 
 #include <hip/hip_ext.h>
 
@@ -41,14 +43,38 @@ int g_engine = [] {                     // rs_tune("host_engine", 0 | 1); env RS
     const char* e = std::getenv("RSAMD_HOST_ENGINE");
     return e ? (std::atoi(e) ? 1 : 0) : 1;
 }();
-int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..16): workgroups of one wave
+int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..64): workgroups (one polling wave each)
+int g_engine_group_waves = 8;           // rs_tune("host_engine_group_waves", 1..8): waves per workgroup
 int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
-// Batches up to this many bytes go to the engine, larger ones launch: its
-// few workgroups lose to a full-GPU launch past about one 10+4 @ 8 KiB stripe
-// (8 threads of 8 KiB calls: 15.2 GiB/s at 128 KiB, 11.0 at 1 MiB,
-// profiles/r02/host_concurrency_engine.log).
-size_t g_engine_max_bytes = 128u << 10;  // rs_tune("host_engine_max_bytes")
+// Batches up to this many bytes go to the engine, larger ones launch.
+size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
+// 16-byte units per workgroup a call is spread over (0: one per lane of a
+// workgroup); rs_tune("host_engine_wg_units")
+int g_engine_wg_units = 0;
 static const bool g_engine_trace = std::getenv("RSAMD_ENGINE_TRACE") != nullptr;
+const bool g_phase_trace = g_engine_trace;
+
+namespace {
+std::atomic<uint64_t> g_phase_ns[kPhCount];
+std::atomic<uint64_t> g_phase_n[kPhCount];
+const char* const kPhaseName[kPhCount] = {"join",     "copy_in", "wait_run", "pre_bell", "bell",
+                                          "wake",     "copy_out", "gpu_tab", "gpu_work", "gpu_release"};
+void phase_report() {
+    std::fprintf(stderr, "{\"host_call_phases_mean_us\": {");
+    for (int p = 0; p < kPhCount; ++p) {
+        const uint64_t n = g_phase_n[p].load();
+        std::fprintf(stderr, "%s\"%s\": %.3f", p ? ", " : "", kPhaseName[p], n ? g_phase_ns[p].load() / 1e3 / n : 0.0);
+    }
+    std::fprintf(stderr, "}, \"calls\": %llu}\n", static_cast<unsigned long long>(g_phase_n[kPhCopyIn].load()));
+}
+}  // namespace
+
+void phase_add_ns(HostPhase p, uint64_t ns) {
+    static const bool registered = [] { return std::atexit(phase_report) == 0; }();
+    (void)registered;
+    g_phase_ns[p].fetch_add(ns, std::memory_order_relaxed);
+    g_phase_n[p].fetch_add(1, std::memory_order_relaxed);
+}
 
 // Doorbell rings are fine-grained (coherent) pinned memory: allocated once
 // per process and device and recycled across handles, never freed (no
@@ -80,11 +106,37 @@ static void ring_put(int device, EngineRing* r) {
     g_ring_pool.emplace_back(device, r);
 }
 
+static void engine_dump(const rs_t* rs, const char* what) {  // diagnostics
+    const EngineRing* r = rs->eng_ring;
+    std::fprintf(stderr, "engine %s: epoch %llu seq %llu running %d waves %d | done/gone:", what,
+                 static_cast<unsigned long long>(rs->eng_epoch), static_cast<unsigned long long>(rs->eng_seq),
+                 rs->eng_running ? 1 : 0, rs->eng_waves);
+    for (int w = 0; w < rs->eng_waves; ++w)
+        std::fprintf(stderr, " %llu/%llu", static_cast<unsigned long long>(r->done[w]),
+                     static_cast<unsigned long long>(r->gone[w]));
+    std::fprintf(stderr, "\n");
+}
+
+static void engine_signal_stop(rs_t* rs) {  // every slot: a wave polls whichever holds its next call
+    for (int i = 0; i < kEngineSlots; ++i) __atomic_store_n(&rs->eng_ring->slot[i].hdr.stop, rs->eng_epoch, __ATOMIC_RELEASE);
+}
+
+// Caller holds eng_mu.  Calls already rung are served first (a wave checks
+// its slot's call number before the stop word).
 void engine_stop(rs_t* rs) {
     if (!rs->eng_running) return;
-    __atomic_store_n(&rs->eng_ring->stop, 1, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(rs->eng_stream);  // every wave checks the stop word while polling
-    __atomic_store_n(&rs->eng_ring->stop, 0, __ATOMIC_RELEASE);
+    engine_signal_stop(rs);
+    const auto t0 = std::chrono::steady_clock::now();
+    bool told = false;
+    for (;;) {
+        const hipError_t q = hipStreamQuery(rs->eng_stream);
+        if (q != hipErrorNotReady) break;
+        if (!told && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+            engine_dump(rs, "stop still waiting after 1 s");
+            told = true;
+        }
+        std::this_thread::yield();
+    }
     rs->eng_running = false;
 }
 
@@ -122,27 +174,96 @@ static hipStream_t engine_stream() {
     return nullptr;
 }
 
-static int engine_launch(rs_t* rs, int waves, uint64_t start) {
+static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     const uint64_t idle_ticks = static_cast<uint64_t>(g_engine_idle_us) * 100;  // 100 MHz realtime counter
-    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, start, idle_ticks, rs->eng_stream), "engine launch"));
+    const uint64_t epoch = rs->eng_epoch + 1;
+    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks, rs->eng_stream),
+                  "engine launch"));
+    if (g_engine_trace) std::fprintf(stderr, "engine launch: epoch %llu start %llu\n",
+                                     static_cast<unsigned long long>(epoch), static_cast<unsigned long long>(start));
+    __atomic_store_n(&rs->eng_epoch, epoch, __ATOMIC_RELEASE);  // (waiters read it without eng_mu)
     rs->eng_running = true;
     rs->eng_waves = waves;
+    rs->eng_group_waves = group_waves;
     rs->eng_idle_us = g_engine_idle_us;
     rs->eng_launches.fetch_add(1, std::memory_order_relaxed);
     return RS_OK;
 }
 
-int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
-                size_t stride, int nstripes, bool accumulate, bool coherent) {
-    if (!g_engine || rows < 1 || rows > kEngineMaxRows || cols < 1 || cols > kEngineMaxCols || nstripes < 1 ||
-        pitch % 16 || stride % 16 || (reinterpret_cast<uintptr_t>(dev_base) & 15))
-        return RS_ERR_INVAL;
-    if (stride * static_cast<size_t>(nstripes) > g_engine_max_bytes) return RS_ERR_INVAL;
-    const uint64_t units = pitch / 16;
-    if (units * static_cast<uint64_t>(nstripes) >= (uint64_t{1} << 31) || pitch >= (size_t{1} << 32))
-        return RS_ERR_INVAL;
+// Some workgroup of the running instance left (idle window): tell the rest
+// to leave too (they see the stop word at their next poll) and queue a new
+// instance behind it on the stream; each of its workgroups resumes after its
+// own done word.  Caller holds eng_mu.
+static int engine_relaunch_if_gone(rs_t* rs) {
+    if (!rs->eng_running) return RS_OK;
+    bool gone = false;
+    for (int w = 0; w < rs->eng_waves && !gone; ++w)
+        gone = __atomic_load_n(&rs->eng_ring->gone[w], __ATOMIC_ACQUIRE) == rs->eng_epoch;
+    if (!gone) return RS_OK;
+    if (g_engine_trace) engine_dump(rs, "gone");
+    engine_signal_stop(rs);
+    rs->eng_running = false;
+    uint64_t start = ~uint64_t{0};
+    for (int w = 0; w < rs->eng_waves; ++w) start = std::min<uint64_t>(start, rs->eng_ring->done[w]);
+    return engine_launch(rs, rs->eng_waves, rs->eng_group_waves, start);
+}
+
+namespace {
+struct EngineWork {
+    const uint8_t* mat;
+    int rows, cols;
+    const uint8_t* base;           // batch mode: vector i of stripe s at base + s * stride + i * pitch
+    size_t pitch, stride;
+    int nstripes;
+    const uint8_t* const* addr;    // address mode (one stripe): vector i at addr[i] (cols inputs, rows outputs)
+    size_t units;                  // 16-byte units per vector
+    bool accumulate, coherent;
+};
+}  // namespace
+
+// Workgroups [w0, w0 + n) (mod waves) all past call `seq`.
+static bool all_done(const EngineRing* r, int waves, int w0, int n, uint64_t seq) {
+    for (int i = 0; i < n; ++i)
+        if (__atomic_load_n(&r->done[(w0 + i) % waves], __ATOMIC_ACQUIRE) < seq) return false;
+    return true;
+}
+
+// Wait until workgroups [w0, w0 + n) completed call `seq`: spin (calls take
+// ~10 us), relaunching the engine if a workgroup left before the call reached
+// it.  `locked`: the caller holds eng_mu (slot reuse wait); otherwise it is
+// taken only for a relaunch.
+static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool locked) {
+    const EngineRing* r = rs->eng_ring;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 1; !all_done(r, waves, w0, n, seq); ++spins) {
+        _mm_pause();
+        if ((spins & 63) != 0) continue;
+        bool gone = false;
+        for (int w = 0; w < waves && !gone; ++w)
+            gone = __atomic_load_n(&r->done[w], __ATOMIC_ACQUIRE) < seq &&
+                   __atomic_load_n(&r->gone[w], __ATOMIC_ACQUIRE) == __atomic_load_n(&rs->eng_epoch, __ATOMIC_ACQUIRE);
+        if (gone) {
+            std::unique_lock<std::mutex> lk(rs->eng_mu, std::defer_lock);
+            if (!locked) lk.lock();
+            RS_TRY(engine_relaunch_if_gone(rs));  // (no-op when another waiter already relaunched)
+        }
+        if ((spins & 4095) != 0) continue;
+        const auto now = std::chrono::steady_clock::now();
+        if (now - t0 < std::chrono::milliseconds(2)) continue;
+        const hipError_t q = hipStreamQuery(rs->eng_stream);  // a failed instance reports here
+        if (q != hipSuccess && q != hipErrorNotReady) return dev_fail(q, "engine call");
+        if (now - t0 > std::chrono::seconds(10)) {
+            if (g_engine_trace) engine_dump(rs, "no completion in 10 s");
+            return dev_fail(hipErrorLaunchTimeOut, "engine call (no completion in 10 s)");
+        }
+    }
+    return RS_OK;
+}
+
+static int engine_run(rs_t* rs, const EngineWork& wk) {
+    const int rows = wk.rows, cols = wk.cols;
     const auto t_call = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> lk(rs->eng_mu);
+    std::unique_lock<std::mutex> lk(rs->eng_mu);
     if (!rs->eng_ring) {
         EngineRing* h = ring_get(rs->device);
         if (!h) return RS_ERR_NOMEM;
@@ -162,83 +283,140 @@ int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
         rs->eng_dring = static_cast<EngineRing*>(d);
         rs->eng_stream = st;
         rs->eng_seq = 0;
+        rs->eng_epoch = 0;
         rs->eng_tab_key.clear();
+        for (uint32_t& t : rs->eng_slot_tab) t = 0;
     }
     EngineRing* ring = rs->eng_ring;
-    const int waves = g_engine_waves < 1 ? 1 : g_engine_waves > kEngineMaxWaves ? kEngineMaxWaves : g_engine_waves;
-    auto now = std::chrono::steady_clock::now();
-    // ring a running instance only well inside ITS idle window (it may have
-    // been launched with another host_engine_idle_us)
-    if (rs->eng_running && (now - rs->eng_last > std::chrono::microseconds(rs->eng_idle_us) / 2 ||
-                            rs->eng_waves != waves || rs->eng_idle_us != g_engine_idle_us))
-        engine_stop(rs);
-    if (!rs->eng_running) RS_TRY(engine_launch(rs, waves, rs->eng_seq));
-    const auto idle = std::chrono::microseconds(rs->eng_idle_us);
+    const int waves = g_engine_waves < 1 ? 1 : g_engine_waves > kEngineMaxGroups ? kEngineMaxGroups : g_engine_waves;
+    const int gwaves = g_engine_group_waves < 1                      ? 1
+                       : g_engine_group_waves > kEngineMaxGroupWaves ? kEngineMaxGroupWaves
+                                                                     : g_engine_group_waves;
+    if (rs->eng_running &&
+        (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us))
+        engine_stop(rs);  // new shape: the old instance must be gone before the next one reads done words
+    RS_TRY(engine_relaunch_if_gone(rs));
+    if (!rs->eng_running) RS_TRY(engine_launch(rs, waves, gwaves, rs->eng_seq));
+    const int inst_waves = rs->eng_waves;
 
-    // coefficient tables, [col][kEngineMaxRows][5] (kernel reloads them when tab_id changes)
+    const uint64_t seq = rs->eng_seq + 1;
+    EngineSlot* slot = &ring->slot[seq % kEngineSlots];
+    if (seq > static_cast<uint64_t>(kEngineSlots))  // the slot's previous call must be past every workgroup
+        RS_TRY(engine_wait(rs, seq - kEngineSlots, inst_waves, 0, inst_waves, true));
+    rs->eng_seq = seq;
+    // the call's workgroups: enough for one unit per lane, rotating, so
+    // small calls in flight run on different workgroups
+    const uint64_t per_wg = g_engine_wg_units > 0 ? static_cast<uint64_t>(g_engine_wg_units)
+                                                  : static_cast<uint64_t>(64 * rs->eng_group_waves);
+    const uint64_t total = wk.units * static_cast<uint64_t>(wk.nstripes);
+    const int nwg = static_cast<int>(std::min<uint64_t>(inst_waves, (total + per_wg - 1) / per_wg));
+    const int wg0 = rs->eng_next_wg % inst_waves;
+    rs->eng_next_wg = (wg0 + nwg) % inst_waves;
+
+    // coefficient tables, [col][kEngineMaxRows][5]; tab_id names the matrix
     const size_t mbytes = static_cast<size_t>(rows) * cols;
     const bool same = rs->eng_tab_key.size() == mbytes + 2 && rs->eng_tab_key[0] == rows &&
-                      rs->eng_tab_key[1] == cols && std::memcmp(rs->eng_tab_key.data() + 2, mat, mbytes) == 0;
+                      rs->eng_tab_key[1] == cols && std::memcmp(rs->eng_tab_key.data() + 2, wk.mat, mbytes) == 0;
     if (!same) {
-        uint32_t tmp[kEngineMaxCols * kEngineMaxRows * 5] = {};
-        for (int c = 0; c < cols; ++c)
-            for (int r = 0; r < rows; ++r)
-                perm_table(mat[static_cast<size_t>(r) * cols + c], &tmp[(c * kEngineMaxRows + r) * 5]);
-        std::memcpy(ring->tables, tmp, static_cast<size_t>(cols) * kEngineMaxRows * 5 * 4);
         rs->eng_tab_key.assign(2, 0);
         rs->eng_tab_key[0] = static_cast<uint8_t>(rows);
         rs->eng_tab_key[1] = static_cast<uint8_t>(cols);
-        rs->eng_tab_key.insert(rs->eng_tab_key.end(), mat, mat + mbytes);
+        rs->eng_tab_key.insert(rs->eng_tab_key.end(), wk.mat, wk.mat + mbytes);
         ++rs->eng_tab_id;
     }
-    volatile EngineHeader* h = &ring->hdr;
-    h->base = reinterpret_cast<uint64_t>(dev_base);
-    h->stride = stride;
-    h->pitch = static_cast<uint32_t>(pitch);
-    h->units = static_cast<uint32_t>(units);
-    h->nstripes = static_cast<uint32_t>(nstripes);
-    h->rows = static_cast<uint16_t>(rows);
-    h->cols = static_cast<uint16_t>(cols);
-    h->flags = (accumulate ? 1u : 0u) | (coherent ? 2u : 0u);
-    h->tab_id = rs->eng_tab_id;
-    const uint64_t seq = ++rs->eng_seq;
-    std::atomic_thread_fence(std::memory_order_release);
-    __atomic_store_n(&ring->hdr.seq0, seq, __ATOMIC_RELEASE);
-    __atomic_store_n(&ring->hdr.seq1, seq, __ATOMIC_RELEASE);
-
-    auto t_ring = std::chrono::steady_clock::now();
-    for (int w = 0; w < rs->eng_waves; ++w) {
-        uint32_t spins = 0;
-        while (__atomic_load_n(&ring->done[w], __ATOMIC_ACQUIRE) != seq) {
-            _mm_pause();
-            if ((++spins & 4095) != 0) continue;
-            now = std::chrono::steady_clock::now();
-            if (now - t_ring < idle + std::chrono::milliseconds(1)) continue;
-            // the instance may have left before this doorbell (host thread
-            // descheduled past the idle window): resume the call in a new one
-            const hipError_t q = hipStreamQuery(rs->eng_stream);
-            if (q == hipSuccess) {
-                rs->eng_running = false;
-                RS_TRY(engine_launch(rs, rs->eng_waves, seq - 1));
-                t_ring = std::chrono::steady_clock::now();
-            } else if (q != hipErrorNotReady) {
-                rs->eng_running = false;
-                return dev_fail(q, "engine call");
-            } else if (now - t_ring > std::chrono::seconds(10)) {
-                return dev_fail(hipErrorLaunchTimeOut, "engine call (no completion in 10 s)");
-            }
+    uint32_t& slot_tab = rs->eng_slot_tab[seq % kEngineSlots];
+    if (slot_tab != rs->eng_tab_id) {
+        uint32_t tmp[kEngineMaxCols * kEngineMaxRows * 5] = {};
+        for (int c = 0; c < cols; ++c)
+            for (int r = 0; r < rows; ++r)
+                perm_table(wk.mat[static_cast<size_t>(r) * cols + c], &tmp[(c * kEngineMaxRows + r) * 5]);
+        std::memcpy(slot->tables, tmp, static_cast<size_t>(cols) * kEngineMaxRows * 5 * 4);
+        slot_tab = rs->eng_tab_id;
+    }
+    if (wk.addr) {  // address lines, each tagged with this call's number
+        const int nv = rows + cols;
+        for (int l = 0; l < (nv + 6) / 7; ++l) {
+            volatile uint64_t* line = slot->ptr[l];
+            for (int j = 0; j < 7 && 7 * l + j < nv; ++j) line[j] = reinterpret_cast<uint64_t>(wk.addr[7 * l + j]);
+            line[7] = seq;
         }
     }
-    rs->eng_last = std::chrono::steady_clock::now();
+    volatile EngineHeader* h = &slot->hdr;
+    h->base = reinterpret_cast<uint64_t>(wk.base);
+    h->stride = wk.stride;
+    h->pitch = static_cast<uint32_t>(wk.pitch);
+    h->units = static_cast<uint32_t>(wk.units);
+    h->nstripes = static_cast<uint32_t>(wk.nstripes);
+    h->rows = static_cast<uint16_t>(rows);
+    h->cols = static_cast<uint16_t>(cols);
+    h->flags = (wk.accumulate ? 1u : 0u) | (wk.coherent ? 2u : 0u) | (g_engine_trace ? 4u : 0u) | (wk.addr ? 8u : 0u) |
+               (static_cast<uint32_t>(wg0) << 8) | (static_cast<uint32_t>(nwg) << 16);
+    h->tab_id = rs->eng_tab_id;
+    std::atomic_thread_fence(std::memory_order_release);
+    __atomic_store_n(&slot->hdr.seq0, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&slot->hdr.seq1, seq, __ATOMIC_RELEASE);
+    lk.unlock();
+
+    const auto t_ring = std::chrono::steady_clock::now();
+    RS_TRY(engine_wait(rs, seq, inst_waves, wg0, nwg, false));
+    const auto t_done = std::chrono::steady_clock::now();
     rs->eng_calls.fetch_add(1, std::memory_order_relaxed);
     if (g_engine_trace) {  // diagnostics: calls slower than 100 us, with where the time went
-        const double us = std::chrono::duration<double, std::micro>(rs->eng_last - t_call).count();
+        phase_add(kPhPreBell, t_call, t_ring);
+        phase_add(kPhBell, t_ring, t_done);
+        // workgroup 0's stamps land just after its done word (bounded wait; other calls may overwrite them)
+        for (int i = 0; i < 100000 && __atomic_load_n(&ring->stamp[4], __ATOMIC_ACQUIRE) != seq; ++i) _mm_pause();
+        if (__atomic_load_n(&ring->stamp[4], __ATOMIC_ACQUIRE) == seq) {
+            uint64_t st[4];
+            for (int i = 0; i < 4; ++i) st[i] = __atomic_load_n(&ring->stamp[i], __ATOMIC_ACQUIRE);
+            if (__atomic_load_n(&ring->stamp[4], __ATOMIC_ACQUIRE) == seq) {
+                phase_add_ns(kPhGpuTab, (st[1] - st[0]) * 10);
+                phase_add_ns(kPhGpuWork, (st[2] - st[1]) * 10);
+                phase_add_ns(kPhGpuRel, (st[3] - st[2]) * 10);
+            }
+        }
+        const double us = std::chrono::duration<double, std::micro>(t_done - t_call).count();
         if (us > 100)
             std::fprintf(stderr, "engine slow call: %.1f us total, %.1f us before the doorbell, seq %llu, n %d\n", us,
                          std::chrono::duration<double, std::micro>(t_ring - t_call).count(),
-                         static_cast<unsigned long long>(seq), nstripes);
+                         static_cast<unsigned long long>(seq), wk.nstripes);
     }
     return RS_OK;
+}
+
+static bool engine_shape_ok(int rows, int cols) {
+    return g_engine && rows >= 1 && rows <= kEngineMaxRows && cols >= 1 && cols <= kEngineMaxCols;
+}
+
+bool engine_accepts(int rows, int cols, size_t bytes) {
+    return engine_shape_ok(rows, cols) && bytes <= g_engine_max_bytes;
+}
+
+int engine_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* dev_base, size_t pitch,
+                size_t stride, int nstripes, bool accumulate, bool coherent) {
+    if (!engine_shape_ok(rows, cols) || nstripes < 1 || pitch % 16 || stride % 16 ||
+        (reinterpret_cast<uintptr_t>(dev_base) & 15))
+        return RS_ERR_INVAL;
+    if (stride * static_cast<size_t>(nstripes) > g_engine_max_bytes) return RS_ERR_INVAL;
+    const uint64_t units = pitch / 16;
+    if (units * static_cast<uint64_t>(nstripes) >= (uint64_t{1} << 31) || pitch >= (size_t{1} << 32))
+        return RS_ERR_INVAL;
+    EngineWork wk{mat, rows, cols, dev_base, pitch, stride, nstripes, nullptr, units, accumulate, coherent};
+    return engine_run(rs, wk);
+}
+
+int engine_call_addr(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in, uint8_t* const* out,
+                     size_t size, bool accumulate) {
+    if (!engine_shape_ok(rows, cols) || size == 0 || size % 16 ||
+        size * static_cast<size_t>(rows + cols) > g_engine_max_bytes)
+        return RS_ERR_INVAL;
+    const uint8_t* addr[kEngineMaxCols + kEngineMaxRows];
+    for (int i = 0; i < cols + rows; ++i) {
+        addr[i] = i < cols ? in[i] : out[i - cols];
+        if (reinterpret_cast<uintptr_t>(addr[i]) & 15) return RS_ERR_INVAL;
+    }
+    EngineWork wk{mat, rows, cols, nullptr, 0, 0, 1, addr, size / 16, accumulate, false};
+    return engine_run(rs, wk);
 }
 
 }  // namespace detail

@@ -304,6 +304,12 @@ int g_coalesce_linger_us = 0;
 // while at most this many callers are inside host_call.
 int g_co_spin_us = 30;
 int g_co_spin_callers = 8;
+// Coalesced batches in flight at once (the engine overlaps their round trips).
+int g_co_running = 2;
+// Small calls the engine takes skip coalescing: each caller stages its own
+// stripe in a pinned pool block and rings the engine itself; calls of
+// several threads are in flight at once on different engine workgroups.
+int g_engine_direct = 1;
 static const bool g_host_trace = std::getenv("RSAMD_ENGINE_TRACE") != nullptr;
 // Upper bound on one coalesced batch's pinned bytes and stripe count.
 constexpr size_t kCoalesceBytes = size_t{32} << 20;
@@ -354,6 +360,7 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     uint8_t* out[kMaxVects];
     for (int i = 0; i < b.cols; ++i) in[i] = b.dev + static_cast<size_t>(i) * b.pitch;
     for (int r = 0; r < b.rows; ++r) out[r] = b.dev + static_cast<size_t>(b.cols + r) * b.pitch;
+    std::lock_guard<std::mutex> lk(rs->co_launch_mu);
     const int rc = matmul(rs, b.mat.data(), b.rows, b.cols, in, static_cast<int64_t>(b.stride), out,
                           static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
     const hipError_t e = hipStreamSynchronize(rs->co_stream);  // never leave a kernel on the buffer
@@ -406,6 +413,9 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         for (int r = 0; r < rows && direct; ++r)
             direct = (out[r] = registered_device_ptr(dst[r], size)) && (reinterpret_cast<uintptr_t>(dst[r]) & 15) == 0;
         if (direct) {
+            // small calls: the resident engine straight over the caller's memory
+            const int erc = engine_call_addr(rs, mat, rows, cols, in, out, size, accumulate);
+            if (erc != RS_ERR_INVAL) return erc;
             std::lock_guard<std::mutex> lk(rs->stage_mu);
             if (!rs->stream)
                 RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
@@ -418,6 +428,32 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     if (size > g_coalesce_max || size == 0) {
         std::lock_guard<std::mutex> lk(rs->stage_mu);
         return host_product(rs, mat, rows, cols, src, dst, size, accumulate);
+    }
+    if (g_engine_direct) {
+        const size_t pitch = rup(size, 64), stride = pitch * static_cast<size_t>(rows + cols);
+        if (engine_accepts(rows, cols, stride)) {
+            using clk = std::chrono::steady_clock;
+            clk::time_point t0, t1, t2;
+            if (g_phase_trace) t0 = clk::now();
+            PinnedBlock blk;
+            RS_TRY(pinned_get(stride, &blk));
+            for (int i = 0; i < cols; ++i) std::memcpy(blk.host + static_cast<size_t>(i) * pitch, src[i], size);
+            if (accumulate)
+                for (int r = 0; r < rows; ++r)
+                    std::memcpy(blk.host + static_cast<size_t>(cols + r) * pitch, dst[r], size);
+            if (g_phase_trace) t1 = clk::now();
+            const int rc = engine_call(rs, mat, rows, cols, blk.dev, pitch, stride, 1, accumulate, false);
+            if (g_phase_trace) t2 = clk::now();
+            if (rc == RS_OK)
+                for (int r = 0; r < rows; ++r)
+                    std::memcpy(dst[r], blk.host + static_cast<size_t>(cols + r) * pitch, size);
+            pinned_put(blk);
+            if (g_phase_trace && rc == RS_OK) {
+                phase_add(kPhCopyIn, t0, t1);
+                phase_add(kPhCopyOut, t2, clk::now());
+            }
+            if (rc != RS_ERR_INVAL) return rc;
+        }
     }
     const auto t_enter = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(rs->co_mu);
@@ -450,6 +486,9 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     idx = b->joined++;
     const bool alone = rs->co_active == 1;
     lk.unlock();
+    using clk = std::chrono::steady_clock;
+    clk::time_point t_joined, t_ready, t_ran, t_done;
+    if (g_phase_trace) t_joined = clk::now();
 
     // copy in: own stripe slot [cols inputs | rows outputs (accumulate)]
     uint8_t* slot = b->host + static_cast<size_t>(idx) * b->stride;
@@ -471,10 +510,12 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
             for (int i = 0; i < n; ++i) std::memcpy(cd[i], cs[i], size);
     }
 
+    if (g_phase_trace) t_ready = clk::now();
     lk.lock();
     ++b->ready;  // (no wake-up: the member that completes the batch launches it itself)
+    bool ran = false;
     while (b->state != CoBatch::kDone) {
-        if (b->state == CoBatch::kFilling && !rs->co_gpu_busy && b->ready == b->joined) {
+        if (b->state == CoBatch::kFilling && rs->co_running < g_co_running && b->ready == b->joined) {
             if (g_coalesce_linger_us > 0 && b->joined < b->cap) {
                 // group-commit window: give other callers until the deadline to join
                 const auto now = std::chrono::steady_clock::now();
@@ -488,16 +529,19 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
                 }
             }
             b->state = CoBatch::kRunning;
-            rs->co_gpu_busy = true;
+            ++rs->co_running;
             const int n = b->joined;
             lk.unlock();
             rs->co_launches.fetch_add(1, std::memory_order_relaxed);
             rs->co_calls.fetch_add(static_cast<uint64_t>(n), std::memory_order_relaxed);
+            if (g_phase_trace) t_ran = clk::now();
             const int rc = run_batch(rs, *b, n);
+            if (g_phase_trace) t_done = clk::now();
+            ran = true;
             lk.lock();
             b->rc = rc;
             b->state = CoBatch::kDone;
-            rs->co_gpu_busy = false;
+            --rs->co_running;
             co_changed(rs);
             break;
         }
@@ -505,6 +549,14 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     }
     const int rc = b->rc;
     lk.unlock();
+    clk::time_point t_out;
+    if (g_phase_trace) {
+        t_out = clk::now();
+        phase_add(kPhJoin, t_enter, t_joined);
+        phase_add(kPhCopyIn, t_joined, t_ready);
+        phase_add(kPhWaitRun, t_ready, ran ? t_ran : t_out);
+        if (ran) phase_add(kPhWake, t_done, t_out);
+    }
 
     if (g_host_trace) {
         const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_enter).count();
@@ -521,6 +573,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         else
             for (int r = 0; r < rows; ++r) std::memcpy(cd[r], cs[r], size);
     }
+    if (g_phase_trace) phase_add(kPhCopyOut, t_out, clk::now());
 
     lk.lock();
     if (++b->released == b->joined) {

@@ -703,10 +703,12 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {  // every lane hol
 constexpr int kEngineColBatch = 16;  // column loads in flight per lane (one PCIe round trip per batch)
 
 struct EngineCall {
-    uint64_t base, stride;
-    uint32_t pitch, units, total;
+    const uint64_t* vaddr;  // LDS: device address of vector i of stripe 0
+    uint64_t stride;
+    uint32_t units, total;
     int cols;
     bool accumulate;
+    uint32_t local, nwg;    // this workgroup's index among the call's nwg workgroups
 };
 
 // This workgroup's units of one call: 16 bytes of every vector of one stripe
@@ -715,22 +717,24 @@ struct EngineCall {
 template <int ROWS>
 __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t* tab) {
     typedef __attribute__((address_space(1))) u32x4 gq;
-    for (uint32_t u = blockIdx.x * 64u + threadIdx.x; u < e.total; u += gridDim.x * 64u) {
+    // lanes enumerated wave-major: a call of up to nwg * 64 units runs on
+    // the first wave of each of its workgroups, larger ones spread over them all
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t step = e.nwg * blockDim.x;
+    for (uint32_t u = (wave * e.nwg + e.local) * 64u + lane; u < e.total; u += step) {
         const uint32_t si = u / e.units, k = u - si * e.units;
-        const uint64_t sb = e.base + static_cast<uint64_t>(si) * e.stride + static_cast<uint64_t>(k) * 16;
+        const uint64_t sb = static_cast<uint64_t>(si) * e.stride + static_cast<uint64_t>(k) * 16;
         u32x4 acc[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; ++r)
-            acc[r] = e.accumulate ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(
-                                        sb + static_cast<uint64_t>(e.cols + r) * e.pitch))
+            acc[r] = e.accumulate ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(e.vaddr[e.cols + r] + sb))
                                   : u32x4{0, 0, 0, 0};
         for (int c0 = 0; c0 < e.cols; c0 += kEngineColBatch) {
             const int nb = (e.cols - c0) < kEngineColBatch ? (e.cols - c0) : kEngineColBatch;
             u32x4 x[kEngineColBatch];
 #pragma unroll
             for (int b = 0; b < kEngineColBatch; ++b)
-                if (b < nb)
-                    x[b] = __builtin_nontemporal_load(reinterpret_cast<const gq*>(sb + static_cast<uint64_t>(c0 + b) * e.pitch));
+                if (b < nb) x[b] = __builtin_nontemporal_load(reinterpret_cast<const gq*>(e.vaddr[c0 + b] + sb));
 #pragma unroll
             for (int b = 0; b < kEngineColBatch; ++b) {
                 if (b < nb) {
@@ -753,59 +757,96 @@ __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t
         }
 #pragma unroll
         for (int r = 0; r < ROWS; ++r)
-            __builtin_nontemporal_store(acc[r], reinterpret_cast<gq*>(sb + static_cast<uint64_t>(e.cols + r) * e.pitch));
+            __builtin_nontemporal_store(acc[r], reinterpret_cast<gq*>(e.vaddr[e.cols + r] + sb));
     }
 }
 
-__global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start, uint64_t idle_ticks) {
+__global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t start, uint64_t epoch,
+                                                 uint64_t idle_ticks) {
+    constexpr int kPollWords = 8 * (1 + kEnginePtrLines);  // a slot's header + address lines
     __shared__ __attribute__((aligned(16))) uint32_t tab[kEngineMaxCols * kEngineMaxRows * 5];
-    const int lane = threadIdx.x;
-    const uint64_t* hdr = reinterpret_cast<const uint64_t*>(&ring->hdr);
+    __shared__ uint64_t s_raw[kPollWords];  // the lines wave 0 saw (s_raw[0] = 0: leave)
+    __shared__ uint64_t s_vaddr[kEngineMaxCols + kEngineMaxRows];
+    const int lane = threadIdx.x & 63;
+    const bool poller = threadIdx.x < 64;  // wave 0 polls and signals; the others wait at the barrier
     // a relaunch resumes after the last call this workgroup completed
     uint64_t last = uniform_u64(sys_load64(&ring->done[blockIdx.x]));
     last = last > start ? last : start;
     uint32_t tab_have = 0xffffffffu;
     for (;;) {
-        uint64_t w = 0, seq = 0;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (uint32_t n = 1;; ++n) {
-            w = sys_load64(&hdr[lane & 7]);
-            const uint64_t s0 = lane_u64(w, 0), s1 = lane_u64(w, 7);
-            if (s0 == s1 && s0 != last) {
-                seq = s0;
-                break;
+        uint64_t t_seen = 0;
+        const EngineSlot* slot = &ring->slot[(last + 1) % kEngineSlots];
+        if (poller) {
+            const uint64_t* lines = reinterpret_cast<const uint64_t*>(slot);
+            uint64_t w = 0, seq = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t n = 1;; ++n) {
+                w = lane < kPollWords ? sys_load64(&lines[lane]) : 0;
+                const uint64_t s0 = lane_u64(w, 0), s1 = lane_u64(w, 7);
+                if (s0 == s1 && s0 == last + 1) {
+                    // address mode: the lines holding this call's addresses carry its tag
+                    const uint64_t w4 = lane_u64(w, 4), w5 = lane_u64(w, 5);
+                    const int nv = static_cast<int>((w4 >> 32) & 0xffff) + static_cast<int>(w4 >> 48);
+                    bool tagged = true;
+                    if (w5 & 8)
+                        for (int l = 1; l <= (nv + 6) / 7 && l <= kEnginePtrLines; ++l)
+                            tagged = tagged && lane_u64(w, 8 * l + 7) == s0;
+                    if (tagged) {
+                        seq = s0;
+                        break;
+                    }
+                }
+                if (lane_u64(w, 6) >= epoch || ((n & 31) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks))
+                    break;  // seq stays 0: every wave leaves
+                __builtin_amdgcn_s_sleep(2);
             }
-            if ((n & 31) == 0 &&
-                (uniform_u64(sys_load64(&ring->stop)) || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks))
-                return;  // every lane of the wave leaves together (uniform values)
-            __builtin_amdgcn_s_sleep(2);
+            t_seen = __builtin_amdgcn_s_memrealtime();
+            if (lane < kPollWords) s_raw[lane] = lane == 0 ? seq : w;
+            if (seq == 0 && lane == 0)  // (release: after this workgroup's last done word)
+                __hip_atomic_store(&ring->gone[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        const uint64_t base = lane_u64(w, 1), stride = lane_u64(w, 2);
-        const uint64_t w3 = lane_u64(w, 3), w4 = lane_u64(w, 4), w5 = lane_u64(w, 5);
+        __syncthreads();
+        const uint64_t seq = s_raw[0];
+        if (seq == 0) return;  // uniform over the workgroup (doorbell values start at 1)
+        const uint64_t base = s_raw[1], stride = s_raw[2];
+        const uint64_t w3 = s_raw[3], w4 = s_raw[4], w5 = s_raw[5];
         const uint32_t pitch = static_cast<uint32_t>(w3), units = static_cast<uint32_t>(w3 >> 32);
         const uint32_t nstripes = static_cast<uint32_t>(w4);
         const int rows = static_cast<int>((w4 >> 32) & 0xffff), cols = static_cast<int>(w4 >> 48);
         const bool accumulate = (w5 & 1) != 0;
         const bool coherent = (w5 & 2) != 0;  // fine-grained buffer: stores need no L2 write-back
+        const bool addressed = (w5 & 8) != 0;
+        // the call's workgroups: nwg of them from wg0 on (wrapping); the others only pass it
+        const uint32_t wg0 = static_cast<uint32_t>(w5 >> 8) & 0xff, nwg = static_cast<uint32_t>(w5 >> 16) & 0xff;
+        const uint32_t local = (blockIdx.x + gridDim.x - wg0) % gridDim.x;
+        const bool works = local < nwg;
+        const bool stamps = (w5 & 4) != 0 && local == 0;
+        if (works && static_cast<int>(threadIdx.x) < rows + cols) {
+            const int i = threadIdx.x;
+            s_vaddr[i] = addressed ? s_raw[8 * (1 + i / 7) + i % 7] : base + static_cast<uint64_t>(i) * pitch;
+        }
         // system-scope acquire, always: without it the first call on a fresh
         // coherent block read zeros (lines the runtime's clear left in L2)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (works) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
-        if (tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords, every load in flight at once (one PCIe trip)
-            constexpr int kTabPerLane = kEngineMaxCols * kEngineMaxRows * 5 / 64;
-            const int n = cols * kEngineMaxRows * 5;
-            uint32_t t[kTabPerLane];
+        if (works && tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords, every load in flight at once (one PCIe trip)
+            if (poller) {
+                constexpr int kTabPerLane = kEngineMaxCols * kEngineMaxRows * 5 / 64;
+                const int n = cols * kEngineMaxRows * 5;
+                uint32_t t[kTabPerLane];
 #pragma unroll
-            for (int k = 0; k < kTabPerLane; ++k)
-                if (lane + 64 * k < n) t[k] = __builtin_nontemporal_load(&ring->tables[lane + 64 * k]);
+                for (int k = 0; k < kTabPerLane; ++k)
+                    if (lane + 64 * k < n) t[k] = __builtin_nontemporal_load(&slot->tables[lane + 64 * k]);
 #pragma unroll
-            for (int k = 0; k < kTabPerLane; ++k)
-                if (lane + 64 * k < n) tab[lane + 64 * k] = t[k];
+                for (int k = 0; k < kTabPerLane; ++k)
+                    if (lane + 64 * k < n) tab[lane + 64 * k] = t[k];
+            }
             tab_have = tab_id;
         }
-        __syncthreads();
-        const EngineCall call{base, stride, pitch, units, nstripes * units, cols, accumulate};
-        switch (rows) {
+        __syncthreads();  // tables and addresses ready; s_raw read by every wave
+        const uint64_t t_tab = __builtin_amdgcn_s_memrealtime();
+        const EngineCall call{s_vaddr, stride, units, works ? nstripes * units : 0u, cols, accumulate, local, nwg};
+        if (works) switch (rows) {
             case 1: engine_units<1>(call, tab); break;
             case 2: engine_units<2>(call, tab); break;
             case 3: engine_units<3>(call, tab); break;
@@ -815,20 +856,33 @@ __global__ __launch_bounds__(64) void gf_engine(EngineRing* ring, uint64_t start
             case 7: engine_units<7>(call, tab); break;
             default: engine_units<8>(call, tab); break;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this call acknowledged
-        if (!coherent) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave acknowledged
+        __syncthreads();                                   // ... and of every wave
+        if (poller) {
+            const uint64_t t_stored = __builtin_amdgcn_s_memrealtime();
+            if (works && !coherent) {  // write back the L2 (every wave's stores are in it)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (lane == 0) __hip_atomic_store(&ring->done[blockIdx.x], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (stamps && lane < 5) {  // after the done word: diagnostics never delay the call
+                const uint64_t t_rel = __builtin_amdgcn_s_memrealtime();
+                const uint64_t v =
+                    lane == 0 ? t_seen : lane == 1 ? t_tab : lane == 2 ? t_stored : lane == 3 ? t_rel : seq;
+                __hip_atomic_store(&ring->stamp[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
-        if (lane == 0) __hip_atomic_store(&ring->done[blockIdx.x], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         last = seq;
     }
 }
 
-hipError_t launch_engine(EngineRing* ring_dev, int waves, uint64_t start, uint64_t idle_ticks, hipStream_t stream) {
-    if (waves < 1 || waves > kEngineMaxWaves) return hipErrorInvalidValue;
+hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
+                         uint64_t idle_ticks, hipStream_t stream) {
+    if (groups < 1 || groups > kEngineMaxGroups || waves_per_group < 1 || waves_per_group > kEngineMaxGroupWaves)
+        return hipErrorInvalidValue;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(gf_engine, dim3(waves), dim3(64), 0, stream, ring_dev, start, idle_ticks);
+    hipLaunchKernelGGL(gf_engine, dim3(groups), dim3(64 * waves_per_group), 0, stream, ring_dev, start, epoch,
+                       idle_ticks);
     return hipGetLastError();
 }
 

@@ -55,37 +55,59 @@ int multi_table_dwords(int cols);
 hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream);
 
 // Host-call engine (engine.cpp): a resident kernel that serves small
-// synchronous host calls through a doorbell in host memory instead of one
+// synchronous host calls through doorbells in host memory instead of one
 // launch + stream sync per call (DESIGN.md §5 "Host-call engine").
 // Everything below lives in fine-grained (coherent) pinned host memory that
-// the kernel reads and writes over PCIe.
-constexpr int kEngineMaxRows = 8, kEngineMaxCols = 32, kEngineMaxWaves = 64;
+// the kernel reads and writes over PCIe.  Calls are numbered 1, 2, ...; call
+// q is described in slot q % kEngineSlots, so up to kEngineSlots calls can be
+// in flight (the host reuses a slot only once every workgroup is past it).
+constexpr int kEngineMaxRows = 8, kEngineMaxCols = 32;
+constexpr int kEngineMaxGroups = 64, kEngineMaxGroupWaves = 8;  // workgroups; waves (of 64 lanes) per workgroup
+constexpr int kEnginePtrLines = 6;  // vector-address lines: 7 addresses + a tag each, >= 40 addresses
+constexpr int kEngineSlots = 8;
 struct EngineHeader {      // one 64-byte line; the host writes seq0 and seq1 LAST
-    uint64_t seq0;         // doorbell value (first word of the line)
-    uint64_t base;         // device address of stripe 0, vector 0
+    uint64_t seq0;         // call number (first word of the line)
+    uint64_t base;         // device address of stripe 0, vector 0 (batch mode)
     uint64_t stride;       // bytes between stripes
-    uint32_t pitch;        // bytes between the vectors of a stripe (16-byte multiple)
-    uint32_t units;        // 16-byte units per vector (pitch / 16: whole slots, padding included)
+    uint32_t pitch;        // bytes between the vectors of a stripe (16-byte multiple; batch mode)
+    uint32_t units;        // 16-byte units per vector (whole slots, padding included)
     uint32_t nstripes;
     uint16_t rows, cols;   // <= kEngineMaxRows / kEngineMaxCols
     uint32_t flags;        // bit 0: XOR into the output rows (Update / Replace); bit 1: the buffer is
-                           // coherent (fine-grained) memory, no cache invalidate / write-back needed
-    uint32_t tab_id;       // identity of EngineRing::tables (reloaded into LDS when it changes)
-    uint64_t reserved;
-    uint64_t seq1;         // doorbell value again (last word of the line)
+                           // coherent (fine-grained) memory, no cache invalidate / write-back needed;
+                           // bit 2: workgroup 0 writes EngineRing::stamp (diagnostics);
+                           // bit 3: address mode: vector i of the (single) stripe is at
+                           // EngineSlot::ptr[i / 7][i % 7] instead of base + i * pitch;
+                           // bits 8-15: first workgroup of the call, 16-23: its workgroups
+                           // (wrapping; the others pass the call without work)
+    uint32_t tab_id;       // identity of the slot's tables (reloaded into LDS when it changes)
+    uint64_t stop;         // host -> kernel: instances with an epoch up to this leave (polled with the doorbell)
+    uint64_t seq1;         // call number again (last word of the line)
 };
 static_assert(sizeof(EngineHeader) == 64, "one cache line, seq1 in its last word");
-struct EngineRing {
+// Everything the kernel polls is in a slot's first 7 lines: the header and
+// the address lines, each address line tagged with its call's number in its
+// last word (a line read before the host rewrote it shows an old tag).
+struct EngineSlot {
     EngineHeader hdr;
-    uint64_t stop;                      // host -> kernel: leave now
-    uint64_t pad[7];
-    uint64_t done[kEngineMaxWaves];     // workgroup w -> host: last doorbell value it completed
+    uint64_t ptr[kEnginePtrLines][8];   // address mode: [line][0..6] device addresses, [line][7] tag
     uint32_t tables[kEngineMaxCols * kEngineMaxRows * 5];  // perm tables, [col][row][5] dwords
 };
-// Launch the resident engine: `waves` workgroups of 64 lanes on `stream`,
-// serving doorbells after `start`; each workgroup leaves on `stop` or after
-// `idle_ticks` of the 100 MHz realtime counter without a doorbell.
-hipError_t launch_engine(EngineRing* ring_dev, int waves, uint64_t start, uint64_t idle_ticks, hipStream_t stream);
+struct EngineRing {
+    EngineSlot slot[kEngineSlots];
+    uint64_t done[kEngineMaxGroups];    // workgroup w -> host: last call it completed
+    uint64_t gone[kEngineMaxGroups];    // workgroup w -> host: epoch of the instance it left
+    uint64_t stamp[8];                  // diagnostics (flags bit 2), workgroup 0, 100 MHz realtime:
+                                        // call seen, tables ready, stores done, released, call number
+};
+// Launch the resident engine instance `epoch`: `groups` workgroups of
+// `waves_per_group` waves on `stream`; workgroup w serves the calls after
+// max(start, done[w]), in order.  Wave 0 of each workgroup polls the slot of
+// its next call.  Each workgroup leaves when that slot's stop word reaches
+// its epoch or after `idle_ticks` of the 100 MHz realtime counter without a
+// call, and records `epoch` in its `gone` word.
+hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
+                         uint64_t idle_ticks, hipStream_t stream);
 
 // Launch tuning knobs (read from the environment once).
 struct LaunchTuning {

@@ -28,21 +28,30 @@ def engine(rslib):
     yield L
     L.rs_tune(b"host_engine", 1)
     L.rs_tune(b"host_engine_waves", 8)
+    L.rs_tune(b"host_engine_group_waves", 8)
     L.rs_tune(b"host_engine_idle_us", 200)
-    L.rs_tune(b"host_engine_max_bytes", 128 << 10)
+    L.rs_tune(b"host_engine_max_bytes", 1 << 20)
+    L.rs_tune(b"host_engine_wg_units", 0)
+    L.rs_tune(b"host_engine_direct", 1)
 
 
 def _rand(rng, n):
     return rng.integers(0, 256, n, dtype=np.uint8)
 
 
-@pytest.mark.parametrize("waves", [8, 1, 16])
-def test_engine_calls_vs_oracle(rslib, orc, torch_dev, engine, waves):
+@pytest.mark.parametrize("waves,group_waves,max_bytes,wg_units", [(8, 8, 1 << 20, 0), (1, 1, 1 << 20, 0),
+                                                                 (16, 2, 128 << 10, 0), (3, 8, 8 << 20, 0),
+                                                                 (8, 8, 1 << 20, 64), (5, 4, 1 << 20, 1000)])
+def test_engine_calls_vs_oracle(rslib, orc, torch_dev, engine, waves, group_waves, max_bytes, wg_units):
     """Encode / Reconst / Update / Replace host calls of many shapes and sizes
     (tails, 8 KiB, 128 KiB; up to 8 output rows and 32 columns through the
-    engine, larger shapes through the launch path) against the oracle."""
+    engine, larger shapes through the launch path) against the oracle, with
+    the engine's workgroups, waves per workgroup and batch limit varied."""
     assert engine.rs_tune(b"host_engine_waves", waves) == 0
-    rng = np.random.default_rng(50 + waves)
+    assert engine.rs_tune(b"host_engine_group_waves", group_waves) == 0
+    assert engine.rs_tune(b"host_engine_max_bytes", max_bytes) == 0
+    assert engine.rs_tune(b"host_engine_wg_units", wg_units) == 0
+    rng = np.random.default_rng(50 + waves + group_waves + wg_units)
     for d, p in [(10, 4), (12, 4), (6, 3), (8, 8), (20, 4), (32, 8), (3, 1), (40, 10)]:
         r = rslib.New(d, p)
         for size in (1, 17, 255, 1024, 4097, 8192, 131072):
@@ -112,10 +121,13 @@ def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
     assert engine.rs_tune(b"host_engine_idle_us", 200) == 0
 
 
-def test_engine_concurrent_threads_and_torch_sync(rslib, orc, torch_dev, engine):
-    """16 threads of mixed host calls on one handle (coalesced batches through
-    the engine), every result checked; then a device-wide torch sync right
-    after a call returns promptly (the engine leaves within its idle window)."""
+@pytest.mark.parametrize("direct", [1, 0])
+def test_engine_concurrent_threads_and_torch_sync(rslib, orc, torch_dev, engine, direct):
+    """16 threads of mixed host calls on one handle (each ringing the engine,
+    or coalesced batches through it), every result checked; then a
+    device-wide torch sync right after a call returns promptly (the engine
+    leaves within its idle window)."""
+    assert engine.rs_tune(b"host_engine_direct", direct) == 0
     torch = torch_dev
     d, p = 10, 4
     r = rslib.New(d, p)
@@ -176,3 +188,155 @@ def test_engine_on_off_identical(rslib, torch_dev, engine):
             outs.append((v[d:], par))
         for a, b in zip(outs[0][0] + outs[0][1], outs[1][0] + outs[1][1]):
             assert np.array_equal(a, b), (d, p, size)
+
+
+def _registered_arena(rslib, nvec, size):
+    """nvec vectors of `size` bytes, 4 KiB apart, in one page-aligned range
+    registered with rs_host_register (unregister the returned base)."""
+    pitch = (size + 4095) // 4096 * 4096
+    arena = np.zeros(nvec * pitch + 4096, np.uint8)
+    off = (-arena.ctypes.data) % 4096
+    base = arena[off: off + nvec * pitch]
+    rslib.host_register(base.ctypes.data, base.nbytes)
+    return base, [base[i * pitch: i * pitch + size] for i in range(nvec)]
+
+
+def test_engine_address_mode_registered_memory(rslib, orc, torch_dev, engine):
+    """Calls whose vectors all lie in registered memory run through the
+    engine straight over the caller's bytes (address mode: one address per
+    vector, up to 32 inputs + 8 outputs), Encode / Reconst / Update / Replace
+    against the oracle; a size that is not a multiple of 16 takes the launch
+    path with the same bytes."""
+    rng = np.random.default_rng(91)
+    for d, p, size in [(10, 4, 8192), (32, 8, 4096), (3, 1, 16), (12, 4, 65536), (10, 4, 8192 + 8)]:
+        r = rslib.New(d, p)
+        base, v = _registered_arena(rslib, d + p, size)
+        try:
+            c0, _ = r.host_engine_stats()
+            data = [_rand(rng, size) for _ in range(d)]
+            for i in range(d):
+                v[i][:] = data[i]
+            for j in range(d, d + p):
+                v[j][:] = 0x5A
+            r.Encode(v)
+            c1, _ = r.host_engine_stats()
+            assert c1 - c0 == (1 if size % 16 == 0 else 0), (d, p, size, c0, c1)
+            exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            assert orc.encode(d, p, exp) == 0
+            for j in range(d, d + p):
+                assert np.array_equal(v[j], exp[j]), ("encode", d, p, size, j)
+            lost = sorted(int(x) for x in rng.choice(d + p, min(p, 3), replace=False))
+            for i in lost:
+                v[i][:] = 0
+            r.Reconst(v, [], lost)
+            for i in range(d + p):
+                assert np.array_equal(v[i], exp[i]), ("reconst", d, p, size, lost, i)
+            row = int(rng.integers(0, d))
+            new = _rand(rng, size)
+            old = v[row].copy()
+            v[row][:] = new
+            r.Update(old, v[row], row, v[d:])
+            ref = [x.copy() for x in exp]
+            ref[row] = new.copy()
+            assert orc.encode(d, p, ref) == 0
+            for j in range(d, d + p):
+                assert np.array_equal(v[j], ref[j]), ("update", d, p, size, j)
+            rows = sorted(int(x) for x in rng.choice(d, min(d, 2), replace=False))
+            deltas = [_rand(rng, size) for _ in rows]
+            r.Replace(deltas, rows, v[d:])
+            for k, rr in enumerate(rows):
+                ref[rr] = np.bitwise_xor(ref[rr], deltas[k])
+            assert orc.encode(d, p, ref) == 0
+            for j in range(d, d + p):
+                assert np.array_equal(v[j], ref[j]), ("replace", d, p, size, rows, j)
+        finally:
+            rslib.host_unregister(base.ctypes.data)
+
+
+def test_engine_address_mode_concurrent(rslib, orc, torch_dev, engine):
+    """8 threads, each with its own registered stripe, Encode through the
+    engine's address mode concurrently on one handle (calls serialise on the
+    engine); every result checked."""
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    errors = []
+
+    def worker(tid):
+        rng = np.random.default_rng(300 + tid)
+        base, v = _registered_arena(rslib, d + p, size)
+        try:
+            for it in range(30):
+                data = [_rand(rng, size) for _ in range(d)]
+                for i in range(d):
+                    v[i][:] = data[i]
+                r.Encode(v)
+                exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, exp) == 0
+                for j in range(d, d + p):
+                    if not np.array_equal(v[j], exp[j]):
+                        errors.append((tid, it, j))
+                        return
+        except Exception as e:  # noqa: BLE001
+            errors.append((tid, repr(e)))
+        finally:
+            rslib.host_unregister(base.ctypes.data)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors[:5]
+    calls, _ = r.host_engine_stats()
+    assert calls >= 8 * 30
+
+
+def test_engine_relaunch_under_concurrent_calls(rslib, orc, torch_dev, engine):
+    """A 20 us idle window with 8 threads making calls at random intervals:
+    workgroups leave while other threads' calls are in flight or about to be
+    rung, and new instances resume them.  Every result is checked; no call
+    is lost or computed twice (Update XORs into its parity)."""
+    assert engine.rs_tune(b"host_engine_idle_us", 20) == 0
+    d, p, size = 10, 4, 4096
+    r = rslib.New(d, p)
+    errors = []
+
+    def worker(tid):
+        rng = np.random.default_rng(700 + tid)
+        base, v = _registered_arena(rslib, d + p, size)
+        try:
+            data = [_rand(rng, size) for _ in range(d)]
+            for i in range(d):
+                v[i][:] = data[i]
+            r.Encode(v)
+            for it in range(40):
+                row = int(rng.integers(0, d))
+                new = _rand(rng, size)
+                old = v[row].copy()
+                v[row][:] = new
+                data[row] = new
+                if tid % 2:
+                    r.Update(old, v[row], row, v[d:])  # pageable old: coalesced batch path
+                else:
+                    r.Encode(v)  # registered: address mode
+                exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, exp) == 0
+                for j in range(d, d + p):
+                    if not np.array_equal(v[j], exp[j]):
+                        errors.append((tid, it, j))
+                        return
+                if rng.random() < 0.3:
+                    time.sleep(float(rng.random()) * 0.0005)
+        except Exception as e:  # noqa: BLE001
+            errors.append((tid, repr(e)))
+        finally:
+            rslib.host_unregister(base.ctypes.data)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors[:5]
+    calls, launches = r.host_engine_stats()
+    assert calls > 0 and launches > 1, (calls, launches)

@@ -527,10 +527,12 @@ def test_concurrent_host_calls(rslib, orc, torch_dev):
     assert not errors, errors
 
 
-def test_coalesced_host_calls(rslib, orc, torch_dev):
+@pytest.mark.parametrize("direct", [0, 1])
+def test_coalesced_host_calls(rslib, orc, torch_dev, direct):
     """Concurrent host calls of several shapes (Encode at two sizes, Update,
-    Replace, Reconst) from 16 threads share launches; every result must equal
-    the oracle's for that call alone."""
+    Replace, Reconst) from 16 threads; every result must equal the oracle's
+    for that call alone.  direct=0: they share coalesced launches; direct=1
+    (the default): each rings the resident engine itself, many in flight."""
     d, p = 10, 4
     r = rslib.New(d, p)
     errors = []
@@ -539,6 +541,7 @@ def test_coalesced_host_calls(rslib, orc, torch_dev):
     # a 2 ms group-commit window: concurrent calls reliably share launches
     # even when Python threads arrive staggered (GIL)
     assert L.rs_tune(b"host_coalesce_linger_us", 2000) == 0
+    assert L.rs_tune(b"host_engine_direct", direct) == 0
 
     def worker(t):
         try:
@@ -588,10 +591,16 @@ def test_coalesced_host_calls(rslib, orc, torch_dev):
             t.join()
     finally:
         assert L.rs_tune(b"host_coalesce_linger_us", 0) == 0
+        assert L.rs_tune(b"host_engine_direct", 1) == 0
     assert not errors, errors[:10]
     launches, calls = r.host_call_stats()
-    assert calls >= 16 * 12 * 2  # every Encode and Reconst went through the coalescer
-    assert launches < calls, (launches, calls)  # concurrent calls shared launches
+    if direct:
+        ecalls, _ = r.host_engine_stats()
+        assert ecalls >= 16 * 12 * 2, ecalls  # every Encode and Reconst rang the engine
+        assert calls == 0, calls
+    else:
+        assert calls >= 16 * 12 * 2  # every Encode and Reconst went through the coalescer
+        assert launches < calls, (launches, calls)  # concurrent calls shared launches
 
 
 def test_host_calls_on_registered_memory(rslib, orc, torch_dev):

@@ -10,6 +10,8 @@
  *
  * Prints one JSON object per thread count (after an untimed 8-thread warm-up
  * round that loads every path's kernels).
+ *   HL_REGISTER=1: each thread's vectors are page-aligned and registered with
+ *   rs_host_register (calls run over the caller's memory, no coalescing)
  */
 #define _POSIX_C_SOURCE 200112L
 #include <pthread.h>
@@ -91,6 +93,11 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));
     if (getenv("HL_ENGINE_MAX")) rs_tune("host_engine_max_bytes", atoi(getenv("HL_ENGINE_MAX")));
     if (getenv("HL_ENGINE_WAVES")) rs_tune("host_engine_waves", atoi(getenv("HL_ENGINE_WAVES")));
+    if (getenv("HL_CO_RUNNING")) rs_tune("host_coalesce_running", atoi(getenv("HL_CO_RUNNING")));
+    if (getenv("HL_ENGINE_IDLE")) rs_tune("host_engine_idle_us", atoi(getenv("HL_ENGINE_IDLE")));
+    if (getenv("HL_ENGINE_WG_UNITS")) rs_tune("host_engine_wg_units", atoi(getenv("HL_ENGINE_WG_UNITS")));
+    if (getenv("HL_ENGINE_DIRECT")) rs_tune("host_engine_direct", atoi(getenv("HL_ENGINE_DIRECT")));
+    if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &g_rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
@@ -100,7 +107,13 @@ int main(int argc, char** argv) {
         w->id = t;
         for (j = 0; j < N; ++j) {
             size_t b;
-            w->v[j] = (uint8_t*)malloc(g_vec);
+            if (getenv("HL_REGISTER") && atoi(getenv("HL_REGISTER"))) {
+                void* mem = NULL;
+                if (posix_memalign(&mem, 4096, g_vec) || rs_host_register(mem, g_vec) != RS_OK) return 8;
+                w->v[j] = (uint8_t*)mem;
+            } else {
+                w->v[j] = (uint8_t*)malloc(g_vec);
+            }
             w->want[j] = (uint8_t*)malloc(g_vec);
             w->lens[j] = g_vec;
             for (b = 0; b < g_vec; ++b) {

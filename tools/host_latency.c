@@ -10,6 +10,8 @@
  *   calls then run zero-copy over the caller's memory)
  *   HL_ENGINE=0/1: the resident host-call engine off / on (default on);
  *   HL_ENGINE_WAVES=n: its workgroups
+ *   HL_VEC=bytes: only this vector size; HL_OPS=mask: only these ops (bit 0
+ *   Encode, 1 Reconst lost=1, 2 Reconst lost=4, 3 Update, 4 Replace)
  *
  * Prints one JSON object per (op, size).
  */
@@ -59,12 +61,18 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));
     if (getenv("HL_ENGINE_MAX")) rs_tune("host_engine_max_bytes", atoi(getenv("HL_ENGINE_MAX")));  /* resident host-call engine on / off */
     if (getenv("HL_ENGINE_WAVES")) rs_tune("host_engine_waves", atoi(getenv("HL_ENGINE_WAVES")));
+    if (getenv("HL_ENGINE_WG_UNITS")) rs_tune("host_engine_wg_units", atoi(getenv("HL_ENGINE_WG_UNITS")));
+    if (getenv("HL_ENGINE_DIRECT")) rs_tune("host_engine_direct", atoi(getenv("HL_ENGINE_DIRECT")));
+    if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
     }
+    const long only_vec = getenv("HL_VEC") ? atol(getenv("HL_VEC")) : 0;
+    const int ops = getenv("HL_OPS") ? atoi(getenv("HL_OPS")) : 31;
     for (si = 0; si < sizeof sizes / sizeof sizes[0]; ++si) {
         const size_t vec = sizes[si];
+        if (only_vec && (size_t)only_vec != vec) continue;
         const int reps = vec >= 4194304 ? REPS / 8 : (vec >= 262144 ? REPS / 4 : REPS);
         uint8_t* v[N];
         size_t lens[N];
@@ -79,13 +87,15 @@ int main(int argc, char** argv) {
             if (reg && atoi(reg) && rs_host_register(v[i], vec) != RS_OK) return 8;
         }
         for (k = 0; k < 10; ++k) rs_encode(rs, v, lens, N);
-        for (k = 0; k < reps; ++k) {
-            double a = now_us();
-            if (rs_encode(rs, v, lens, N) != RS_OK) return 2;
-            t[k] = now_us() - a;
+        if (ops & 1) {
+            for (k = 0; k < reps; ++k) {
+                double a = now_us();
+                if (rs_encode(rs, v, lens, N) != RS_OK) return 2;
+                t[k] = now_us() - a;
+            }
+            report("Encode", vec, (double)N * vec, reps);
         }
-        report("Encode", vec, (double)N * vec, reps);
-        {
+        if (ops & 2) {
             int need[1] = {0};
             for (k = 0; k < reps; ++k) {
                 double a = now_us();
@@ -94,7 +104,7 @@ int main(int argc, char** argv) {
             }
             report("Reconst lost=1", vec, (double)(D + 1) * vec, reps);
         }
-        {
+        if (ops & 4) {
             int need[4] = {0, 3, 5, 9};
             for (k = 0; k < reps; ++k) {
                 double a = now_us();
@@ -103,13 +113,14 @@ int main(int argc, char** argv) {
             }
             report("Reconst lost=4", vec, (double)(D + 4) * vec, reps);
         }
+        if (ops & 8)
         for (k = 0; k < reps; ++k) {
             double a = now_us();
             if (rs_update(rs, v[2], vec, v[3], vec, 2, v + D, lens + D, P) != RS_OK) return 5;
             t[k] = now_us() - a;
         }
-        report("Update", vec, (double)(2 + 2 * P) * vec, reps);
-        {
+        if (ops & 8) report("Update", vec, (double)(2 + 2 * P) * vec, reps);
+        if (ops & 16) {
             int rows[1] = {1};
             for (k = 0; k < reps; ++k) {
                 double a = now_us();
