@@ -11,6 +11,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <initializer_list>
 #include <map>
@@ -23,6 +25,7 @@
 #include "../../include/rs_amd.h"
 #include "gf256.hpp"
 #include "kernels.hpp"
+#include "watchdog.hpp"
 
 #define RS_TRY(x)                 \
     do {                          \
@@ -236,10 +239,19 @@ inline void phase_add(HostPhase p, std::chrono::steady_clock::time_point a, std:
 inline void rs_codec::release_device() {
     {
         if (!device_ready) return;
+        static const bool trace = std::getenv("RSAMD_TEARDOWN_TRACE") != nullptr;  // diagnostics
+        auto step = [](const char* what) {
+            if (trace) std::fprintf(stderr, "rs_free: %s\n", what);
+        };
+        rsamd::detail::Region region("rs_free teardown");
+        step("engine shutdown");
         rsamd::detail::engine_shutdown(this);
         rsamd::detail::DeviceGuard g(device);
+        step("stream sync");
         if (stream) (void)hipStreamSynchronize(stream);
+        step("device sync");
         (void)hipDeviceSynchronize();
+        step("frees");
         for (auto& kv : tables) (void)hipFree(kv.second);
         for (UploadSlot& u : up) {
             if (u.host) (void)hipHostFree(u.host);
@@ -264,6 +276,7 @@ inline void rs_codec::release_device() {
         for (hipEvent_t e : chunk_ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
+        step("done");
     }
 }
 

@@ -126,17 +126,24 @@ static void engine_signal_stop(rs_t* rs) {  // every slot: a wave polls whicheve
 void engine_stop(rs_t* rs) {
     if (!rs->eng_running) return;
     engine_signal_stop(rs);
+    Region region("engine stop (instance leaving)");
+    // Watch the gone words (host memory, no runtime calls) until every
+    // workgroup of the latest instance has left, then one stream sync.
+    // (A busy loop of hipStreamQuery here left the process hanging in the
+    // runtime's teardown at exit, 1 run in 8: profiles/r02/exit_hang.log.)
     const auto t0 = std::chrono::steady_clock::now();
-    bool told = false;
-    for (;;) {
-        const hipError_t q = hipStreamQuery(rs->eng_stream);
-        if (q != hipErrorNotReady) break;
-        if (!told && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-            engine_dump(rs, "stop still waiting after 1 s");
-            told = true;
+    for (uint32_t spins = 0;; ++spins) {
+        bool all = true;
+        for (int w = 0; w < rs->eng_waves && all; ++w)
+            all = __atomic_load_n(&rs->eng_ring->gone[w], __ATOMIC_ACQUIRE) == rs->eng_epoch;
+        if (all) break;
+        _mm_pause();
+        if ((spins & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+            engine_dump(rs, "stop: workgroups still running after 1 s; waiting on the stream");
+            break;
         }
-        std::this_thread::yield();
     }
+    (void)hipStreamSynchronize(rs->eng_stream);
     rs->eng_running = false;
 }
 
@@ -177,6 +184,7 @@ static hipStream_t engine_stream() {
 static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     const uint64_t idle_ticks = static_cast<uint64_t>(g_engine_idle_us) * 100;  // 100 MHz realtime counter
     const uint64_t epoch = rs->eng_epoch + 1;
+    Region region("engine launch");
     RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks, rs->eng_stream),
                   "engine launch"));
     if (g_engine_trace) std::fprintf(stderr, "engine launch: epoch %llu start %llu\n",
@@ -190,10 +198,12 @@ static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     return RS_OK;
 }
 
-// Some workgroup of the running instance left (idle window): tell the rest
-// to leave too (they see the stop word at their next poll) and queue a new
-// instance behind it on the stream; each of its workgroups resumes after its
-// own done word.  Caller holds eng_mu.
+// Some workgroup of the running instance left (idle window): the rest leave
+// too (stop word), and once the instance is off the stream a new one starts;
+// each of its workgroups resumes after its own done word.  Never launch
+// behind a running instance: with kernels queued that way (or a
+// hipStreamQuery while one runs) the runtime's teardown deadlocked at
+// process exit, 1 run in 3 (profiles/r02/exit_hang.log).  Caller holds eng_mu.
 static int engine_relaunch_if_gone(rs_t* rs) {
     if (!rs->eng_running) return RS_OK;
     bool gone = false;
@@ -201,8 +211,7 @@ static int engine_relaunch_if_gone(rs_t* rs) {
         gone = __atomic_load_n(&rs->eng_ring->gone[w], __ATOMIC_ACQUIRE) == rs->eng_epoch;
     if (!gone) return RS_OK;
     if (g_engine_trace) engine_dump(rs, "gone");
-    engine_signal_stop(rs);
-    rs->eng_running = false;
+    engine_stop(rs);
     uint64_t start = ~uint64_t{0};
     for (int w = 0; w < rs->eng_waves; ++w) start = std::min<uint64_t>(start, rs->eng_ring->done[w]);
     return engine_launch(rs, rs->eng_waves, rs->eng_group_waves, start);
@@ -233,6 +242,7 @@ static bool all_done(const EngineRing* r, int waves, int w0, int n, uint64_t seq
 // it.  `locked`: the caller holds eng_mu (slot reuse wait); otherwise it is
 // taken only for a relaunch.
 static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool locked) {
+    Region region(locked ? "engine wait (slot reuse)" : "engine wait (call)");
     const EngineRing* r = rs->eng_ring;
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spins = 1; !all_done(r, waves, w0, n, seq); ++spins) {
@@ -248,10 +258,10 @@ static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool lo
             RS_TRY(engine_relaunch_if_gone(rs));  // (no-op when another waiter already relaunched)
         }
         if ((spins & 4095) != 0) continue;
+        // (no runtime calls while an instance runs: a hipStreamQuery here
+        // left the runtime's teardown deadlocked at process exit; a faulting
+        // instance ends the process through the runtime's fault handler)
         const auto now = std::chrono::steady_clock::now();
-        if (now - t0 < std::chrono::milliseconds(2)) continue;
-        const hipError_t q = hipStreamQuery(rs->eng_stream);  // a failed instance reports here
-        if (q != hipSuccess && q != hipErrorNotReady) return dev_fail(q, "engine call");
         if (now - t0 > std::chrono::seconds(10)) {
             if (g_engine_trace) engine_dump(rs, "no completion in 10 s");
             return dev_fail(hipErrorLaunchTimeOut, "engine call (no completion in 10 s)");
@@ -263,7 +273,11 @@ static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool lo
 static int engine_run(rs_t* rs, const EngineWork& wk) {
     const int rows = wk.rows, cols = wk.cols;
     const auto t_call = std::chrono::steady_clock::now();
-    std::unique_lock<std::mutex> lk(rs->eng_mu);
+    std::unique_lock<std::mutex> lk(rs->eng_mu, std::defer_lock);
+    {
+        Region region("engine submit lock");
+        lk.lock();
+    }
     if (!rs->eng_ring) {
         EngineRing* h = ring_get(rs->device);
         if (!h) return RS_ERR_NOMEM;

@@ -271,6 +271,7 @@ int rs_host_register(void* ptr, size_t bytes) {
     return abi_guard([&]() -> int {
         if (!ptr || !bytes) return RS_ERR_INVAL;
         // mapped: kernels may address it directly (zero-copy host batches and calls)
+        Region region("hipHostRegister");
         RS_TRY(hip_ok(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister"));
         void* dev = nullptr;
         if (hipHostGetDevicePointer(&dev, ptr, 0) == hipSuccess && dev) {

@@ -270,6 +270,7 @@ int pinned_get(size_t bytes, PinnedBlock* out) {
         }
     }
     void* h = nullptr;
+    Region region("hipHostMalloc (pinned pool block)");
     // default (coarse-grained) pinned memory: the zero-copy kernels and the
     // engine (system-scope acquire / release fences) read it faster than
     // coherent memory (10+4 @ 8 KiB host Encode 10.1 vs 11.1 us)
@@ -360,6 +361,7 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     uint8_t* out[kMaxVects];
     for (int i = 0; i < b.cols; ++i) in[i] = b.dev + static_cast<size_t>(i) * b.pitch;
     for (int r = 0; r < b.rows; ++r) out[r] = b.dev + static_cast<size_t>(b.cols + r) * b.pitch;
+    Region region("coalesced batch launch + sync");
     std::lock_guard<std::mutex> lk(rs->co_launch_mu);
     const int rc = matmul(rs, b.mat.data(), b.rows, b.cols, in, static_cast<int64_t>(b.stride), out,
                           static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
@@ -370,6 +372,7 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
 // Wait for the next batch state change: spin briefly on co_gen (a futex
 // wake costs several us, as much as a whole engine call), then block.
 static void co_wait(rs_t* rs, std::unique_lock<std::mutex>& lk) {
+    Region region("coalesce wait");
     const uint64_t g = rs->co_gen.load(std::memory_order_acquire);
     if (rs->co_active > g_co_spin_callers) {  // oversubscribed: spinners would take the copiers' CPUs
         rs->co_cv.wait(lk);
@@ -413,6 +416,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         for (int r = 0; r < rows && direct; ++r)
             direct = (out[r] = registered_device_ptr(dst[r], size)) && (reinterpret_cast<uintptr_t>(dst[r]) & 15) == 0;
         if (direct) {
+            Region region("registered-memory call");
             // small calls: the resident engine straight over the caller's memory
             const int erc = engine_call_addr(rs, mat, rows, cols, in, out, size, accumulate);
             if (erc != RS_ERR_INVAL) return erc;

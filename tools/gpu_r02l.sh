@@ -5,6 +5,7 @@ set -euo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"
 OUT="$REPO/gpurun_out"; mkdir -p "$OUT" tools/_build
+export RSAMD_TEARDOWN_TRACE=1 RSAMD_WATCHDOG=1 HL_PROGRESS=1
 echo "== engine + host-call tests"
 timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
     -p no:cacheprovider -k "engine or host or coalesc or concurrent or staging or registered" > "$OUT/pytest_engine.log" 2>&1 || { tail -40 "$OUT/pytest_engine.log"; exit 1; }

@@ -13,13 +13,16 @@
  *   HL_REGISTER=1: each thread's vectors are page-aligned and registered with
  *   rs_host_register (calls run over the caller's memory, no coalescing)
  */
-#define _POSIX_C_SOURCE 200112L
+#define _GNU_SOURCE
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
+#include <signal.h>
+#include <execinfo.h>
 
 #include "rs_amd.h"
 
@@ -78,8 +81,28 @@ static void* run(void* arg) {
     return NULL;
 }
 
+static void at_exit_last(void) { fprintf(stderr, "host_concurrency: atexit handlers done\n"); }
+
+/* diagnostics: SIGUSR1 prints the main thread's stack (stall analysis) */
+static pthread_t g_main_thread;
+static void on_usr1(int sig) {
+    void* frames[64];
+    int n;
+    (void)sig;
+    n = backtrace(frames, 64);
+    fprintf(stderr, "host_concurrency: %s thread stack:\n", pthread_equal(pthread_self(), g_main_thread) ? "main" : "other");
+    backtrace_symbols_fd(frames, n, 2);
+}
+
 int main(int argc, char** argv) {
     int a, t, j, nt;
+    atexit(at_exit_last);
+    {
+        void* warm[2];
+        g_main_thread = pthread_self();
+        backtrace(warm, 2); /* loads the unwinder before any signal */
+        signal(SIGUSR1, on_usr1);
+    }
     uint32_t seed = 12345;
     if (argc < 6) {
         fprintf(stderr, "usage: %s vec calls coalesce_max mixed T...\n", argv[0]);
@@ -123,8 +146,10 @@ int main(int argc, char** argv) {
         }
         /* expected result: the same call made alone (also leaves v in its final state) */
         if (rs_encode(g_rs, w->v, w->lens, N) != RS_OK) return 1;
+        if (getenv("HL_PROGRESS") && (t & 31) == 31) fprintf(stderr, "host_concurrency: %d workers ready\n", t + 1);
         for (j = 0; j < N; ++j) memcpy(w->want[j], w->v[j], g_vec);
     }
+    if (getenv("HL_PROGRESS")) fprintf(stderr, "host_concurrency: warm-up\n");
     {   /* untimed warm-up round at 8 threads: first launches of every path
          * (the engine, multi-stripe coalesced batches) load their kernels,
          * which costs milliseconds once per process and is not steady state */
@@ -174,6 +199,9 @@ int main(int argc, char** argv) {
         fflush(stdout);
         if (bad) return 3;
     }
+    fprintf(stderr, "host_concurrency: rs_free\n");
     rs_free(g_rs);
+    fprintf(stderr, "host_concurrency: exit\n");
+    if (getenv("HL_FAST_EXIT") && atoi(getenv("HL_FAST_EXIT"))) _exit(0); /* diagnostics: skip atexit handlers and static destructors */
     return 0;
 }

@@ -141,6 +141,8 @@ int main(int argc, char** argv) {
         printf("{\"engine_calls\": %llu, \"engine_launches\": %llu}\n", (unsigned long long)calls,
                (unsigned long long)launches);
     }
+    fprintf(stderr, "host_latency: rs_free\n");
     rs_free(rs);
+    fprintf(stderr, "host_latency: exit\n");
     return 0;
 }
