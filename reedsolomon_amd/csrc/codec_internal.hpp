@@ -186,6 +186,7 @@ struct rs_codec {
     uint32_t eng_slot_tab[rsamd::kEngineSlots] = {};  // table id each slot holds
     std::vector<uint8_t> eng_tab_key;
     std::atomic<uint64_t> eng_calls{0}, eng_launches{0};
+    std::atomic<int> eng_inflight{0};  // calls rung and not yet seen complete by their callers
 
     const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
 

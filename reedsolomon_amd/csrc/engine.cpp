@@ -318,9 +318,16 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     if (seq > static_cast<uint64_t>(kEngineSlots))  // the slot's previous call must be past every workgroup
         RS_TRY(engine_wait(rs, seq - kEngineSlots, inst_waves, 0, inst_waves, true));
     rs->eng_seq = seq;
-    // the call's workgroups: enough for one unit per lane, rotating, so
-    // small calls in flight run on different workgroups
+    // The call's workgroups, rotating.  A lone call (none other in flight)
+    // spreads over every workgroup's first wave: more loads over PCIe in
+    // flight at once (10+4 @ 8 KiB Encode 16.0 -> 11.0 us pageable, 14.0 ->
+    // 9.5 us registered, profiles/r02/engine_s.log).  Calls that overlap
+    // others take one unit per lane of one workgroup, so concurrent calls run
+    // on different workgroups (8 threads: 29 GiB/s against 14 when every call
+    // spreads).  rs_tune("host_engine_wg_units", n) fixes n units per workgroup.
+    const bool lone = rs->eng_inflight.load(std::memory_order_acquire) == 0;
     const uint64_t per_wg = g_engine_wg_units > 0 ? static_cast<uint64_t>(g_engine_wg_units)
+                            : lone                ? uint64_t{64}
                                                   : static_cast<uint64_t>(64 * rs->eng_group_waves);
     const uint64_t total = wk.units * static_cast<uint64_t>(wk.nstripes);
     const int nwg = static_cast<int>(std::min<uint64_t>(inst_waves, (total + per_wg - 1) / per_wg));
@@ -369,10 +376,13 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     std::atomic_thread_fence(std::memory_order_release);
     __atomic_store_n(&slot->hdr.seq0, seq, __ATOMIC_RELEASE);
     __atomic_store_n(&slot->hdr.seq1, seq, __ATOMIC_RELEASE);
+    rs->eng_inflight.fetch_add(1, std::memory_order_acq_rel);
     lk.unlock();
 
     const auto t_ring = std::chrono::steady_clock::now();
-    RS_TRY(engine_wait(rs, seq, inst_waves, wg0, nwg, false));
+    const int wrc = engine_wait(rs, seq, inst_waves, wg0, nwg, false);
+    rs->eng_inflight.fetch_sub(1, std::memory_order_acq_rel);
+    RS_TRY(wrc);
     const auto t_done = std::chrono::steady_clock::now();
     rs->eng_calls.fetch_add(1, std::memory_order_relaxed);
     if (g_engine_trace) {  // diagnostics: calls slower than 100 us, with where the time went
