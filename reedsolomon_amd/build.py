@@ -18,9 +18,9 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "librsamd.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("codec.cpp", "host_calls.cpp", "batches.cpp", "host_batches.cpp",
-                                           "engine.cpp", "watchdog.cpp", "kernels.hip")]
+                                           "engine.cpp", "watchdog.cpp", "jit.cpp", "kernels.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("gf256.hpp", "kernels.hpp", "codec_internal.hpp",
-                                                  "host_pool.hpp", "watchdog.hpp", "bitslice_gen.inc")] + [
+                                                  "host_pool.hpp", "watchdog.hpp", "jit.hpp", "bitslice_gen.inc")] + [
     os.path.join(ROOT, "include", "rs_amd.h")
 ]
 ARCH = os.environ.get("RSAMD_OFFLOAD_ARCH", "gfx950")
@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}",
         "-fvisibility=hidden", "-Wall", "-Wno-unused-result",
         "-I", os.path.join(ROOT, "include"),
-        *SOURCES, "-o", tmp,
+        *SOURCES, "-o", tmp, "-lhiprtc",
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -16,6 +16,7 @@
 #include <cstdlib>
 
 #include "codec_internal.hpp"
+#include "jit.hpp"
 
 using namespace rsamd;
 using namespace rsamd::detail;
@@ -515,6 +516,8 @@ int rs_tune(const char* name, int value) {
         else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
         else if (n == "block8") t.block8 = value == 128 ? 128 : 256;
         else if (n == "bitslice") t.bitslice = value ? 1 : 0;
+        else if (n == "jit") g_jit_mode = value < 0 ? 0 : value > 2 ? 2 : value;
+        else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
         else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
@@ -596,3 +599,14 @@ int rs_reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, 
 }
 
 }  // extern "C"
+
+int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms) {
+    return abi_guard([&]() -> int {
+        jit_stats(compiled, failed, launches, compile_ms);
+        return RS_OK;
+    });
+}
+
+int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms) {
+    return abi_guard([&]() -> int { return jit_compile_check(mat, rows, cols, accumulate != 0, ms); });
+}

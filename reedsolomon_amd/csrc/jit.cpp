@@ -1,0 +1,447 @@
+// jit.cpp — run-time generated bit-sliced kernels (hiprtc) for products with
+// 5-8 output rows whose matrix is only known at run time.
+//
+// Why: above 4 output rows the perm-table kernels are VALU-bound (10+8 @ 1 MiB
+// Reconst of 8: 5.05-5.18 TB/s, profiles/r02/pmc_sq_10_8.json), while the
+// bit-sliced networks generated at build time for fixed generator matrices
+// (tools/gen_bitslice.py, gf_bitslice in kernels.hip) need ~22 VALU per
+// (column, dword) against ~40 and run at 6.1-6.3 TB/s.  A network needs its
+// matrix at code-generation time: selecting subset XORs by a run-time index
+// costs a register gather per term (counted at ~40 VALU), so
+// the matrix is baked into the code instead — here, at run time.
+//
+// The generator is the C++ form of tools/gen_bitslice.py: a lane owns 32 bytes
+// of every vector as 8 bit-planes (8x8 SWAR transpose); multiplying by a
+// constant is GF(2)-linear, so output plane i of row r is a fixed XOR of input
+// planes; per column the XORs of each 4-plane half's subsets are formed once
+// and every output plane takes one subset of each half (xor3).  Accumulate
+// mode (Update / Replace) XORs the old output bytes in after the back
+// transpose.
+//
+// Flow: first sight of a (device, matrix, mode) in a launch moving at least
+// jit_min_bytes queues a compile on a worker thread (hiprtc only: the worker
+// makes no HIP runtime calls); launches keep taking the perm-table kernels
+// until the code object is ready; the launching thread then loads it
+// (hipModuleLoadData) and from there on launches the bit-sliced kernel.
+// rs_tune("jit", 2) compiles on the launching thread instead.
+#include "jit.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <thread>
+#include <vector>
+
+#include "rs_amd.h"
+
+namespace rsamd {
+
+int g_jit_mode = [] {
+    const char* e = std::getenv("RSAMD_JIT");
+    return e ? std::atoi(e) : 1;
+}();
+uint64_t g_jit_min_bytes = uint64_t{8} << 20;
+
+namespace {
+
+uint8_t gmul(uint8_t a, uint8_t b) {  // GF(2^8), polynomial 0x11d
+    uint8_t r = 0;
+    while (b) {
+        if (b & 1) r ^= a;
+        const bool hi = a & 0x80;
+        a = static_cast<uint8_t>(a << 1);
+        if (hi) a ^= 0x1d;
+        b >>= 1;
+    }
+    return r;
+}
+
+constexpr int kPF = 3;  // columns whose loads are in flight ahead of the one combined (as gen_bitslice.py)
+
+// Device prelude: the launch arguments (the layout of MatmulArgs, checked by
+// the static_asserts the generator appends) and the bit-slice helpers of
+// kernels.hip (bs_swap / bs_transpose8 / bs_x3, buffer nt dwordx2 accesses).
+const char* const kPrelude = R"RSJIT(
+typedef unsigned char u8;
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef long long i64;
+typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u8 g_u8;
+struct MatmulArgs {
+    const u32* tables; const u32* img4; const u8* host_mat;
+    int rows, cols, rows_pad; int nstripes; int accumulate; int units_per_chunk; int nt_store;
+    u64 len; u64 body; u64 tail_start; i64 ss[4]; const int* stripe_ids;
+    i64 chunks_per_stripe; i64 total_chunks; int cps_shift;
+    u64 ptr[260]; u32 sid[260];
+};
+__device__ __forceinline__ u32x2 ld8(const g_u8* base, u32 off, u32 nbytes) {
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, (int)nbytes, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 2);
+}
+__device__ __forceinline__ void st8(g_u8* base, u32 off, u32 nbytes, u32x2 v) {
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, (int)nbytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 2);
+}
+__device__ __forceinline__ void bs_swap(u32& a, u32& b, int s, u32 m) {
+    const u32 t = ((a >> s) ^ b) & m;
+    b ^= t;
+    a ^= t << s;
+}
+__device__ __forceinline__ void bs_transpose8(u32 (&w)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs_swap(w[i], w[i + 4], 4, 0x0F0F0F0Fu);
+    bs_swap(w[0], w[2], 2, 0x33333333u);
+    bs_swap(w[1], w[3], 2, 0x33333333u);
+    bs_swap(w[4], w[6], 2, 0x33333333u);
+    bs_swap(w[5], w[7], 2, 0x33333333u);
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) bs_swap(w[i], w[i + 1], 1, 0x55555555u);
+}
+__device__ __forceinline__ u32 bs_x3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// A workgroup covers 32*BS bytes of every vector; lane t's 32-byte unit is
+// four 8-byte pieces at 8t + 2048k (BS = 64) / 8t + 8*BS*k of the chunk.
+template <int BS>
+__device__ __forceinline__ void rs_bs_body(const MatmulArgs& a) {
+    const u32 chunk = blockIdx.x;
+    const u32 cps = (u32)a.chunks_per_stripe;
+    const u32 su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
+    const int s = a.stripe_ids ? a.stripe_ids[su] : (int)su;
+    const u32 cb = chunk - su * cps;
+    const u32 off = cb * (32u * BS) + 8u * threadIdx.x;
+    const u32 nbytes = (u32)a.body;
+    auto fetch = [&](int c, u32 (&w)[8]) {
+        const g_u8* p = (const g_u8*)a.ptr[c] + (i64)s * a.ss[a.sid[c] & 3];
+        u32 o32 = off;
+        asm volatile("" : "+v"(o32));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x2 v = ld8(p, o32 + (u32)(k * 8 * BS), nbytes);
+            w[2 * k] = v.x;
+            w[2 * k + 1] = v.y;
+        }
+    };
+    auto store = [&](int r, u32 (&o)[8]) {
+        bs_transpose8(o);
+        const int v = RSJ_COLS + r;
+        g_u8* q = (g_u8*)a.ptr[v] + (i64)s * a.ss[a.sid[v] & 3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u32x2 x = {o[2 * k], o[2 * k + 1]};
+            if (RSJ_ACC) x ^= ld8(q, off + (u32)(k * 8 * BS), nbytes);
+            st8(q, off + (u32)(k * 8 * BS), nbytes, x);
+        }
+    };
+    RSJ_NETWORK
+}
+extern "C" __global__ __launch_bounds__(64) void rs_bs_jit_64(const MatmulArgs a) { rs_bs_body<64>(a); }
+extern "C" __global__ __launch_bounds__(256) void rs_bs_jit_256(const MatmulArgs a) { rs_bs_body<256>(a); }
+)RSJIT";
+
+// The network for one matrix: the statements of BsNet<d, p>::run in
+// bitslice_gen.inc, for this matrix (same construction as
+// tools/gen_bitslice.py emit()).
+std::string network(const uint8_t* mat, int rows, int cols) {
+    std::string o;
+    char buf[160];
+#define line(...)                                      \
+    do {                                               \
+        std::snprintf(buf, sizeof buf, __VA_ARGS__);   \
+        o += buf;                                      \
+        o += '\n';                                     \
+    } while (0)
+    // mask[c][r][i]: input planes j of column c feeding plane i of row r
+    std::vector<uint8_t> mask(static_cast<size_t>(cols) * rows * 8);
+    for (int c = 0; c < cols; ++c)
+        for (int r = 0; r < rows; ++r) {
+            const uint8_t g = mat[static_cast<size_t>(r) * cols + c];
+            for (int i = 0; i < 8; ++i) {
+                uint8_t m = 0;
+                for (int j = 0; j < 8; ++j)
+                    if ((gmul(g, static_cast<uint8_t>(1u << j)) >> i) & 1) m |= static_cast<uint8_t>(1u << j);
+                mask[(static_cast<size_t>(c) * rows + r) * 8 + i] = m;
+            }
+        }
+    line("    u32 A[%d][8];", rows);
+    for (int k = 0; k < kPF && k < cols; ++k) {
+        line("    u32 N%d[8];", k);
+        line("    fetch(%d, N%d);", k, k);
+    }
+    for (int c = 0; c < cols; ++c) {
+        line("    {");
+        line("        u32 P[8];");
+        line("        for (int k = 0; k < 8; ++k) P[k] = N%d[k];", c % kPF);
+        if (c + kPF < cols) line("        fetch(%d, N%d);", c + kPF, c % kPF);
+        line("        bs_transpose8(P);");
+        std::string name[2][16];  // per half: expression naming subset m
+        for (int half = 0; half < 2; ++half) {
+            const int base = 4 * half;
+            const char h = half ? 'H' : 'L';
+            bool have[16] = {}, used[16] = {};
+            for (int b = 0; b < 4; ++b) {
+                have[1 << b] = true;
+                name[half][1 << b] = "P[" + std::to_string(base + b) + "]";
+            }
+            for (int r = 0; r < rows; ++r)
+                for (int i = 0; i < 8; ++i) used[(mask[(static_cast<size_t>(c) * rows + r) * 8 + i] >> base) & 15] = true;
+            used[0] = false;
+            bool need[16] = {};
+            // want(m): m and the chain m ^ lowbit(m), ... down to a single plane
+            for (int m = 1; m < 16; ++m)
+                if (used[m])
+                    for (int x = m; x && !have[x] && !need[x]; x ^= x & -x) need[x] = true;
+            for (int pc = 2; pc <= 4; ++pc)
+                for (int m = 1; m < 16; ++m) {
+                    if (!need[m] || __builtin_popcount(m) != pc) continue;
+                    const int low = m & -m, rest = m ^ low;
+                    line("        const u32 %c%d = %s ^ %s;", h, m, name[half][rest].c_str(), name[half][low].c_str());
+                    name[half][m] = std::string(1, h) + std::to_string(m);
+                    have[m] = true;
+                }
+        }
+        for (int r = 0; r < rows; ++r)
+            for (int i = 0; i < 8; ++i) {
+                const int m = mask[(static_cast<size_t>(c) * rows + r) * 8 + i];
+                const std::string* t[2];
+                int nt = 0;
+                if (m & 15) t[nt++] = &name[0][m & 15];
+                if (m >> 4) t[nt++] = &name[1][m >> 4];
+                if (c == 0) {
+                    if (nt == 0) line("        A[%d][%d] = 0u;", r, i);
+                    else if (nt == 1) line("        A[%d][%d] = %s;", r, i, t[0]->c_str());
+                    else line("        A[%d][%d] = %s ^ %s;", r, i, t[0]->c_str(), t[1]->c_str());
+                } else if (nt == 2) {
+                    line("        A[%d][%d] = bs_x3(A[%d][%d], %s, %s);", r, i, r, i, t[0]->c_str(), t[1]->c_str());
+                } else if (nt == 1) {
+                    line("        A[%d][%d] ^= %s;", r, i, t[0]->c_str());
+                }
+            }
+        line("    }");
+        // pin the running sums per column (no re-association across columns)
+        line("#pragma unroll");
+        line("    for (int r = 0; r < %d; ++r)", rows);
+        line("#pragma unroll");
+        line("        for (int i = 0; i < 8; ++i) asm volatile(\"\" : \"+v\"(A[r][i]));");
+        line("    __builtin_amdgcn_sched_barrier(0);");
+    }
+    line("    for (int r = 0; r < %d; ++r) store(r, A[r]);", rows);
+#undef line
+    return o;
+}
+
+struct Compiled {
+    std::vector<char> code;
+    double ms = 0;
+    bool ok = false;
+    std::string log;
+};
+
+Compiled compile(const std::string& src) {
+    Compiled out;
+    const auto t0 = std::chrono::steady_clock::now();
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "rs_bs_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        out.log = "hiprtcCreateProgram failed";
+        return out;
+    }
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        if (hiprtcGetProgramLogSize(prog, &n) == HIPRTC_SUCCESS && n > 1) {
+            out.log.resize(n);
+            hiprtcGetProgramLog(prog, &out.log[0]);
+        }
+        hiprtcDestroyProgram(&prog);
+        return out;
+    }
+    size_t n = 0;
+    if (hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n > 0) {
+        out.code.resize(n);
+        out.ok = hiprtcGetCode(prog, out.code.data()) == HIPRTC_SUCCESS;
+    }
+    hiprtcDestroyProgram(&prog);
+    out.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return out;
+}
+
+// ---------------------------------------------------------------- cache
+
+struct Entry {
+    enum State { kQueued, kCompiling, kReady, kLoaded, kFailed } state = kQueued;
+    std::string src;
+    std::vector<char> code;
+    hipModule_t module = nullptr;
+    hipFunction_t fn64 = nullptr, fn256 = nullptr;
+};
+
+constexpr size_t kMaxEntries = 64;
+
+struct Jit {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::string, std::shared_ptr<Entry>> entries;  // key: device, mode, rows, cols, matrix
+    std::deque<std::shared_ptr<Entry>> queue;
+    std::thread worker;
+    bool stop = false;
+    uint64_t compiled = 0, failed = 0;
+    double compile_ms = 0;
+    std::atomic<uint64_t> launches{0};
+
+    void run_one(const std::shared_ptr<Entry>& e) {  // caller does not hold mu
+        Compiled c = compile(e->src);
+        std::lock_guard<std::mutex> lk(mu);
+        if (c.ok) {
+            e->code = std::move(c.code);
+            e->state = Entry::kReady;
+            ++compiled;
+            compile_ms += c.ms;
+        } else {
+            e->state = Entry::kFailed;
+            ++failed;
+            std::fprintf(stderr, "librsamd: run-time kernel compile failed (perm-table kernels stay in use): %s\n",
+                         c.log.substr(0, 2000).c_str());
+        }
+        e->src.clear();
+        e->src.shrink_to_fit();
+    }
+
+    void work() {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return stop || !queue.empty(); });
+            if (stop) return;
+            std::shared_ptr<Entry> e = queue.front();
+            queue.pop_front();
+            e->state = Entry::kCompiling;
+            lk.unlock();
+            run_one(e);
+            lk.lock();
+        }
+    }
+
+    ~Jit() {  // process exit: finish the compile in flight (hiprtc only), drop the rest
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        if (worker.joinable()) worker.join();
+    }
+};
+
+Jit& jit() {
+    static Jit j;
+    return j;
+}
+
+}  // namespace
+
+std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) {
+    std::string s = "#define RSJ_COLS " + std::to_string(cols) + "\n#define RSJ_ACC " +
+                    std::string(accumulate ? "1" : "0") + "\n";
+    std::string pre(kPrelude);
+    const size_t at = pre.find("RSJ_NETWORK");
+    s += pre.substr(0, at) + "\n" + network(mat, rows, cols) + pre.substr(at + std::strlen("RSJ_NETWORK"));
+    // the kernel's argument layout must equal the host's
+    s += "static_assert(sizeof(MatmulArgs) == " + std::to_string(sizeof(MatmulArgs)) + ", \"MatmulArgs size\");\n";
+    s += "static_assert(__builtin_offsetof(MatmulArgs, ptr) == " + std::to_string(offsetof(MatmulArgs, ptr)) +
+         ", \"MatmulArgs ptr\");\n";
+    s += "static_assert(__builtin_offsetof(MatmulArgs, stripe_ids) == " +
+         std::to_string(offsetof(MatmulArgs, stripe_ids)) + ", \"MatmulArgs stripe_ids\");\n";
+    s += "static_assert(__builtin_offsetof(MatmulArgs, cps_shift) == " +
+         std::to_string(offsetof(MatmulArgs, cps_shift)) + ", \"MatmulArgs cps_shift\");\n";
+    return s;
+}
+
+int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
+    if (!mat || rows < kJitMinRows || rows > kJitMaxRows || cols < 1 || cols > kJitMaxCols) return RS_ERR_INVAL;
+    Compiled c = compile(jit_source(mat, rows, cols, accumulate));
+    if (ms) *ms = c.ms;
+    if (!c.ok) std::fprintf(stderr, "librsamd: jit compile check failed: %s\n", c.log.substr(0, 4000).c_str());
+    return c.ok ? RS_OK : RS_ERR_DEVICE;
+}
+
+void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms) {
+    Jit& j = jit();
+    std::lock_guard<std::mutex> lk(j.mu);
+    if (compiled) *compiled = j.compiled;
+    if (failed) *failed = j.failed;
+    if (launches) *launches = j.launches.load();
+    if (compile_ms) *compile_ms = j.compile_ms;
+}
+
+void jit_count_launch() { jit().launches.fetch_add(1, std::memory_order_relaxed); }
+
+hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
+    if (!g_jit_mode || !a.host_mat || a.rows < kJitMinRows || a.rows > kJitMaxRows || a.cols < 1 ||
+        a.cols > kJitMaxCols)
+        return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::string key(reinterpret_cast<const char*>(&dev), sizeof dev);
+    key += static_cast<char>(a.accumulate ? 1 : 0);
+    key += static_cast<char>(a.rows);
+    key += static_cast<char>(a.cols);
+    key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
+    Jit& j = jit();
+    std::shared_ptr<Entry> e;
+    {
+        std::unique_lock<std::mutex> lk(j.mu);
+        auto it = j.entries.find(key);
+        if (it == j.entries.end()) {
+            if (launch_bytes < g_jit_min_bytes && g_jit_mode != 2) return nullptr;
+            if (j.entries.size() >= kMaxEntries) return nullptr;
+            e = std::make_shared<Entry>();
+            e->src = jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
+            j.entries.emplace(key, e);
+            if (g_jit_mode == 2) {
+                e->state = Entry::kCompiling;
+                lk.unlock();
+                j.run_one(e);  // on this thread
+                lk.lock();
+            } else {
+                j.queue.push_back(e);
+                if (!j.worker.joinable()) j.worker = std::thread([&j] { j.work(); });
+                j.cv.notify_one();
+                return nullptr;
+            }
+        } else {
+            e = it->second;
+        }
+        if (e->state == Entry::kLoaded) return bs == 256 ? e->fn256 : e->fn64;
+        if (e->state != Entry::kReady) return nullptr;
+        // load the code object on this device (launching thread, under mu)
+        hipModule_t m = nullptr;
+        hipFunction_t f64 = nullptr, f256 = nullptr;
+        if (hipModuleLoadData(&m, e->code.data()) != hipSuccess ||
+            hipModuleGetFunction(&f64, m, "rs_bs_jit_64") != hipSuccess ||
+            hipModuleGetFunction(&f256, m, "rs_bs_jit_256") != hipSuccess) {
+            (void)hipGetLastError();
+            e->state = Entry::kFailed;
+            ++j.failed;
+            std::fprintf(stderr, "librsamd: run-time kernel load failed (perm-table kernels stay in use)\n");
+            return nullptr;
+        }
+        e->module = m;
+        e->fn64 = f64;
+        e->fn256 = f256;
+        e->state = Entry::kLoaded;
+        e->code.clear();
+        e->code.shrink_to_fit();
+        return bs == 256 ? f256 : f64;
+    }
+}
+
+}  // namespace rsamd

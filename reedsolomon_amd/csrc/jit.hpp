@@ -1,0 +1,38 @@
+// jit.hpp — run-time generated bit-sliced kernels for matrices with 5-8
+// output rows that are only known at run time (Reconst of 5-8 lost vectors,
+// Encode of codes without a generated network, Update / Replace with 5-8
+// parity rows).  See jit.cpp and DESIGN.md §3 "Run-time bit-sliced kernels".
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "kernels.hpp"
+
+namespace rsamd {
+
+constexpr int kJitMinRows = 5, kJitMaxRows = 8, kJitMaxCols = 32;
+
+// rs_tune("jit", 0 | 1 | 2): off / compile in the background on first sight
+// and launch the perm-table kernels until the code is ready (default) /
+// compile on the launching thread (tests, benchmarks).
+extern int g_jit_mode;
+// rs_tune("jit_min_bytes"): launches moving fewer bytes never start a compile
+// (a compile costs ~1 s of host time; a launch of 64 MiB ~10 us of GPU time).
+extern uint64_t g_jit_min_bytes;
+
+// The compiled kernel for this launch's matrix (a.host_mat, a.rows, a.cols,
+// a.accumulate) on the current device with `bs`-lane workgroups (64 or 256),
+// or nullptr (JIT off, shape not covered, not compiled yet, or failed).
+hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_bytes);
+void jit_count_launch();
+
+// The kernel source for one matrix (rows x cols, row-major); exposed for the
+// CPU tests (rs_jit_compile_check).
+std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate);
+// Compile only (hiprtc, no device needed): RS_OK or RS_ERR_DEVICE.
+int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms);
+void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
+
+}  // namespace rsamd

@@ -28,6 +28,7 @@
 //    vectors whose base/stride is not 16-byte aligned) go to a byte-granular
 //    kernel with identical arithmetic.
 #include "kernels.hpp"
+#include "jit.hpp"
 
 #include <cstdlib>
 #include <cstring>
@@ -1208,6 +1209,30 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
             bk = nullptr;
         }
         if (bk) a.body = 0;  // the vector path below is done; only the tail remains
+    }
+    // 5-8 output rows over a run-time matrix: the bit-sliced network compiled
+    // for this matrix (jit.cpp), once it is ready
+    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= kJitMinRows && a.rows <= kJitMaxRows) {
+        const int jbs = bs_block_for(a) == 256 ? 256 : 64;
+        const uint64_t bytes = a.body * static_cast<uint64_t>(a.nstripes) * static_cast<uint64_t>(a.rows + a.cols);
+        if (hipFunction_t f = jit_bitslice_for(a, jbs, bytes)) {
+            a.units_per_chunk = jbs;
+            a.nt_store = 1;
+            a.chunks_per_stripe = static_cast<int64_t>((a.body + 32 * jbs - 1) / (32 * jbs));
+            a.total_chunks = a.chunks_per_stripe * a.nstripes;
+            a.cps_shift = -1;
+            for (int sh = 0; sh < 31; ++sh)
+                if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
+            if (a.total_chunks <= 0x7fffffff) {
+                void* params[] = {&a};
+                (void)hipGetLastError();
+                const hipError_t e = hipModuleLaunchKernel(f, static_cast<unsigned>(a.total_chunks), 1, 1, jbs, 1, 1,
+                                                           0, stream, params, nullptr);
+                if (e != hipSuccess) return e;
+                jit_count_launch();
+                a.body = 0;
+            }
+        }
     }
 
     if (a.body) {

@@ -560,6 +560,23 @@ def inverse_cache_key(survived) -> int:
     return int(lib().rs_inverse_cache_key(s, ns))
 
 
+def jit_stats() -> dict:
+    """Run-time compiled bit-sliced kernels (rs_jit_stats): code objects
+    compiled, failures, launches, total compile time (ms)."""
+    c, f, n, ms = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+    _check(lib().rs_jit_stats(ctypes.byref(c), ctypes.byref(f), ctypes.byref(n), ctypes.byref(ms)))
+    return {"compiled": c.value, "failed": f.value, "launches": n.value, "compile_ms": ms.value}
+
+
+def jit_compile_check(mat, accumulate: bool = False) -> float:
+    """Generate and compile (no device needed) the run-time kernel for `mat`
+    (rows x cols, 5 <= rows <= 8); returns the compile time in ms."""
+    m = np.ascontiguousarray(mat, dtype=np.uint8)
+    ms = ctypes.c_double()
+    _check(lib().rs_jit_compile_check(m.ctypes.data, m.shape[0], m.shape[1], int(bool(accumulate)), ctypes.byref(ms)))
+    return ms.value
+
+
 def gf_mul(a: int, b: int) -> int:
     return int(lib().rs_gf_mul(a, b))
 

@@ -337,3 +337,23 @@ def test_multi_pattern_mask_validation_wide(rslib):
     assert fn == "rs_reconst_batch_multi" and m.dtype == np.uint64 and m.shape == (3,)
     m, fn = rslib.rs._masks_for([1 << 127, 0], 2, 128, "rs_reconst_batch_multi")
     assert fn == "rs_reconst_batch_multi256" and int(m[0, 1]) == 1 << 63
+
+
+def test_jit_compile_check(rslib, orc):
+    """The run-time bit-sliced kernel generator (jit.cpp) produces code that
+    hiprtc compiles for gfx950 (no device needed): a Reconst-of-8 matrix of
+    10+8 (overwrite) and a 16-column 5-row XOR-accumulate product; shapes
+    outside 5-8 rows / 1-32 columns are refused."""
+    import numpy as np
+
+    from reedsolomon_amd.rs import ErrInvalidArgument
+
+    r = rslib.New(10, 8)
+    survived = list(range(8, 18))
+    m = r.reconst_matrix(survived, list(range(8))).reshape(8, 10)  # rows of the inverse for data 0..7
+    assert rslib.jit_compile_check(m) > 0
+    rng = np.random.default_rng(3)
+    assert rslib.jit_compile_check(rng.integers(0, 256, (5, 16), dtype=np.uint8), accumulate=True) > 0
+    for shape in [(4, 10), (9, 10), (8, 33)]:
+        with pytest.raises(ErrInvalidArgument):
+            rslib.jit_compile_check(np.ones(shape, np.uint8))

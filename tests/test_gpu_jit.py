@@ -1,0 +1,210 @@
+"""Run-time compiled bit-sliced kernels (jit.cpp): products with 5-8 output
+rows over matrices known only at run time — the primitive (rs_gf_matmul_batch,
+gmu.go:4-9 / encodePart rs.go:175-203), Reconst of 5-8 lost vectors
+(rs.go:221-380), Update / Replace with 8 parity rows (rs.go:424-570) and the
+Encode of codes without a build-time network (matrix.go:37-54) — compared
+byte-for-byte with the CPU oracle.  rs_tune("jit", 2) compiles on the
+launching thread, so every launch below runs the compiled kernel (the
+counters say so); one test covers the default background compile.
+"""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    torch.cuda.init()
+    return torch
+
+
+@pytest.fixture
+def jit_sync(rslib):
+    L = rslib.lib()
+    assert L.rs_tune(b"jit", 2) == 0
+    yield
+    L.rs_tune(b"jit", 1)
+    L.rs_tune(b"jit_min_bytes", 8 << 20)
+
+
+def _padded(torch, rng, S, v, n, pad):
+    """[S, v, n] view of a [S, v, n + pad] device buffer (16-byte aligned rows
+    when n + pad is, so the vector body runs and n % 16 bytes take the tail)."""
+    host = rng.integers(0, 256, (S, v, n + pad), dtype=np.uint8)
+    t = torch.from_numpy(host).cuda()
+    return t[:, :, :n], host[:, :, :n]
+
+
+@pytest.mark.parametrize("rows,cols", [(5, 10), (6, 10), (7, 12), (8, 10), (8, 16), (8, 32), (5, 1), (8, 3)])
+def test_jit_matmul_vs_oracle(rslib, orc, torch_dev, jit_sync, rows, cols):
+    torch = torch_dev
+    rng = np.random.default_rng(rows * 100 + cols)
+    mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
+    r = rslib.New(10, 4)
+    before = rslib.jit_stats()["launches"]
+    for S, n, pad in [(3, 16, 0), (2, 2048 + 16, 0), (3, 4096 + 5, 11), (2, 65536 + 96, 0), (2, (1 << 20) + 3, 13)]:
+        src, hsrc = _padded(torch, rng, S, cols, n, pad)
+        dst, hdst = _padded(torch, rng, S, rows, n, pad)
+        r.gf_matmul_batch(mat, src, None, dst, None)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst.cpu().numpy(), orc.encode_numpy(mat, hsrc)), (rows, cols, S, n)
+        # accumulate (updateOnly): dst ^= mat x src
+        dst2, hdst2 = _padded(torch, rng, S, rows, n, pad)
+        r.gf_matmul_batch(mat, src, None, dst2, None, accumulate=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst2.cpu().numpy(), hdst2 ^ orc.encode_numpy(mat, hsrc)), (rows, cols, S, n, "acc")
+    st = rslib.jit_stats()
+    assert st["launches"] >= before + 8, st  # every aligned launch above ran the compiled kernel
+    assert st["failed"] == 0, st
+
+
+@pytest.mark.parametrize("d,p,lost", [(10, 8, [0, 1, 2, 3, 4, 5, 6, 7]), (10, 8, [1, 3, 5, 7, 9]),
+                                      (10, 8, [0, 2, 4, 11, 13, 17]), (10, 8, [12, 13, 14, 15, 16, 17]),
+                                      (16, 8, [0, 3, 6, 9, 12, 15, 18, 21]), (20, 7, [2, 4, 6, 8, 10, 12, 14])])
+def test_jit_reconst_5_to_8_lost(rslib, orc, torch_dev, jit_sync, d, p, lost):
+    """Reconst of 5-8 lost vectors (data and parity mixed) on a batch: the
+    rebuilt stripes equal the encoded originals, on both layouts."""
+    torch = torch_dev
+    rng = np.random.default_rng(d * 1000 + sum(lost))
+    r = rslib.New(d, p)
+    G = orc.gen_matrix(d, p).reshape(p, d)
+    S, n = 4, 65536 + 48
+    host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+    host[:, d:] = orc.encode_numpy(G, host[:, :d])
+    before = rslib.jit_stats()["launches"]
+    buf = torch.from_numpy(host).cuda()
+    buf[:, lost] = 0x5A
+    r.reconst_batch(buf, [], lost)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), host), (d, p, lost)
+    data = torch.from_numpy(np.ascontiguousarray(host[:, :d])).cuda()
+    par = torch.from_numpy(np.ascontiguousarray(host[:, d:])).cuda()
+    for v in lost:
+        (data[:, v] if v < d else par[:, v - d]).fill_(0x33)
+    r.reconst_batch_split(data, par, [], lost)
+    torch.cuda.synchronize()
+    assert np.array_equal(data.cpu().numpy(), host[:, :d]) and np.array_equal(par.cpu().numpy(), host[:, d:])
+    assert rslib.jit_stats()["launches"] > before
+
+
+def test_jit_multi_pattern_fallback(rslib, orc, torch_dev, jit_sync):
+    """rs_reconst_batch_multi with 5-8-output patterns on non-contiguous
+    stripes: each pattern's grouped launch maps its stripes through the
+    device stripe-id list; untouched stripes stay bit-identical."""
+    torch = torch_dev
+    d, p, S, n = 10, 8, 12, 8192
+    rng = np.random.default_rng(77)
+    r = rslib.New(d, p)
+    G = orc.gen_matrix(d, p).reshape(p, d)
+    host = rng.integers(0, 256, (S, d, n), dtype=np.uint8)
+    hpar = orc.encode_numpy(G, host)
+    pats = [[0, 1, 2, 3, 4, 5, 6, 7], [2, 5, 8, 10, 12, 16], [10, 11, 12, 13, 14], 0, [1, 9, 11, 15, 17]]
+    masks = np.zeros(S, np.uint64)
+    for s in range(S):
+        pt = pats[s % len(pats)]
+        masks[s] = 0 if pt == 0 else sum(1 << v for v in pt)
+    data = torch.from_numpy(host.copy()).cuda()
+    par = torch.from_numpy(hpar.copy()).cuda()
+    for s in range(S):
+        for v in range(d + p):
+            if (int(masks[s]) >> v) & 1:
+                (data[s, v] if v < d else par[s, v - d]).fill_(0xEE)
+    rslib.lib().rs_tune(b"jit_min_bytes", 0)
+    r.reconst_batch_multi(data, par, masks)
+    torch.cuda.synchronize()
+    assert np.array_equal(data.cpu().numpy(), host) and np.array_equal(par.cpu().numpy(), hpar)
+
+
+def test_jit_update_replace_8_parity(rslib, orc, torch_dev, jit_sync):
+    """Update and Replace on a 10+8 batch (8-row XOR-accumulate products)
+    equal re-encoding the new data."""
+    torch = torch_dev
+    d, p, S, n = 10, 8, 3, 65536 + 32
+    rng = np.random.default_rng(5)
+    r = rslib.New(d, p)
+    G = orc.gen_matrix(d, p).reshape(p, d)
+    host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+    host[:, d:] = orc.encode_numpy(G, host[:, :d])
+    buf = torch.from_numpy(host.copy()).cuda()
+    new = rng.integers(0, 256, (S, n), dtype=np.uint8)
+    before = rslib.jit_stats()["launches"]
+    r.update_batch(torch.from_numpy(np.ascontiguousarray(host[:, 4])).cuda(), torch.from_numpy(new).cuda(), 4, buf)
+    torch.cuda.synchronize()
+    host[:, 4] = new
+    exp = orc.encode_numpy(G, host[:, :d])
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[:, d:], exp)
+    rows = [1, 6, 8]
+    repl = rng.integers(0, 256, (S, len(rows), n), dtype=np.uint8)
+    r.replace_batch(torch.from_numpy(repl).cuda(), rows, buf)
+    torch.cuda.synchronize()
+    # Replace: the listed rows were zero when the parity was made (rs.go:492-529)
+    base = host[:, :d].copy()
+    base[:, rows] = 0
+    par0 = orc.encode_numpy(G, base)
+    base[:, rows] = repl
+    exp2 = exp ^ orc.encode_numpy(G, base) ^ par0
+    assert np.array_equal(buf.cpu().numpy()[:, d:], exp2)
+    assert rslib.jit_stats()["launches"] >= before + 2
+
+
+@pytest.mark.parametrize("d,p", [(16, 8), (9, 7), (14, 6)])
+def test_jit_encode_without_build_time_network(rslib, orc, torch_dev, jit_sync, d, p):
+    """Encode of codes whose generator has no generated network: interleaved
+    [S][d+p][n] (256-lane workgroups when d+p >= 18) and split layouts."""
+    torch = torch_dev
+    rng = np.random.default_rng(d * 10 + p)
+    r = rslib.New(d, p)
+    G = orc.gen_matrix(d, p).reshape(p, d)
+    for S, n in [(3, 16), (4, 65536 + 96), (2, 1 << 20)]:
+        host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+        host[:, d:] = 0xA5
+        exp = orc.encode_numpy(G, host[:, :d])
+        buf = torch.from_numpy(host).cuda()
+        r.encode_batch(buf)
+        data = torch.from_numpy(np.ascontiguousarray(host[:, :d])).cuda()
+        par = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device="cuda")
+        r.encode_batch_split(data, par)
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy()[:, d:], exp), (d, p, S, n)
+        assert np.array_equal(par.cpu().numpy(), exp), (d, p, S, n, "split")
+
+
+def test_jit_background_compile(rslib, orc, torch_dev):
+    """Default mode: the first launch of a new matrix runs the perm-table
+    kernels and queues a compile; once it is done the next launch runs the
+    compiled kernel; both give the same bytes."""
+    torch = torch_dev
+    L = rslib.lib()
+    assert L.rs_tune(b"jit", 1) == 0
+    L.rs_tune(b"jit_min_bytes", 0)
+    try:
+        rng = np.random.default_rng(4242)
+        mat = rng.integers(0, 256, (7, 11), dtype=np.uint8)
+        r = rslib.New(10, 4)
+        S, n = 2, 32768
+        src = torch.from_numpy(rng.integers(0, 256, (S, 11, n), dtype=np.uint8)).cuda()
+        exp = orc.encode_numpy(mat, src.cpu().numpy())
+        st0 = rslib.jit_stats()
+        dst = torch.zeros((S, 7, n), dtype=torch.uint8, device="cuda")
+        r.gf_matmul_batch(mat, src, None, dst, None)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst.cpu().numpy(), exp)
+        assert rslib.jit_stats()["launches"] == st0["launches"]  # not compiled yet: perm-table kernels
+        t0 = time.time()
+        while rslib.jit_stats()["compiled"] == st0["compiled"] and time.time() - t0 < 60:
+            time.sleep(0.05)
+        assert rslib.jit_stats()["compiled"] == st0["compiled"] + 1
+        dst.zero_()
+        r.gf_matmul_batch(mat, src, None, dst, None)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst.cpu().numpy(), exp)
+        assert rslib.jit_stats()["launches"] == st0["launches"] + 1
+    finally:
+        L.rs_tune(b"jit_min_bytes", 8 << 20)

@@ -6,6 +6,7 @@ rounds on the same device and buffers; reports median / min kernel time.
     python tools/ab.py "var=12" "var=14" "var=14,layout=inter" ...
     python tools/ab.py "op=rec1" "op=rec1,block8=256" "op=multi16" ...
 
+jit: 2 (default here: run-time bit-sliced kernels compiled before timing) | 0 (perm-table kernels).
 op: enc (Encode, default) | rec1 / rec2 / rec4 / rec5 / rec6 / rec8 (Reconst of
 1 / 2 / 4 / 5 / 6 / 8 lost data vectors, split layout; rec8p: 4 data + 4
 parity, needs AB_M >= 8) | multi16 (rs_reconst_batch_multi, 16 patterns) |
@@ -29,7 +30,7 @@ S = 256 * (1 << 20) // VEC
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
 DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "lane_bytes": 8, "block8": 128,
-            "bitslice": 1, "bs_block": 0, "wide_block": 256}
+            "bitslice": 1, "bs_block": 0, "wide_block": 256, "jit": 2}
 LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9], "rec5": [0, 2, 4, 6, 8], "rec6": [0, 1, 3, 5, 7, 9],
         "rec8": [0, 1, 2, 3, 4, 5, 6, 7], "rec8p": [0, 2, 4, 6, 10, 12, 14, 16]}
 
