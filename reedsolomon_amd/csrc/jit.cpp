@@ -51,6 +51,7 @@ int g_jit_mode = [] {
     return e ? std::atoi(e) : 1;
 }();
 uint64_t g_jit_min_bytes = uint64_t{8} << 20;
+int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 
 namespace {
 
@@ -66,7 +67,6 @@ uint8_t gmul(uint8_t a, uint8_t b) {  // GF(2^8), polynomial 0x11d
     return r;
 }
 
-constexpr int kPF = 3;  // columns whose loads are in flight ahead of the one combined (as gen_bitslice.py)
 
 // Device prelude: the launch arguments (the layout of MatmulArgs, checked by
 // the static_asserts the generator appends) and the bit-slice helpers of
@@ -153,6 +153,7 @@ extern "C" __global__ __launch_bounds__(256) void rs_bs_jit_256(const MatmulArgs
 // bitslice_gen.inc, for this matrix (same construction as
 // tools/gen_bitslice.py emit()).
 std::string network(const uint8_t* mat, int rows, int cols) {
+    const int kPF = g_jit_pf;
     std::string o;
     char buf[160];
 #define line(...)                                      \
@@ -394,6 +395,7 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
     key += static_cast<char>(a.accumulate ? 1 : 0);
     key += static_cast<char>(a.rows);
     key += static_cast<char>(a.cols);
+    key += static_cast<char>(g_jit_pf);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     Jit& j = jit();
     std::shared_ptr<Entry> e;

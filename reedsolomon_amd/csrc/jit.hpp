@@ -13,6 +13,7 @@
 namespace rsamd {
 
 constexpr int kJitMinRows = 5, kJitMaxRows = 8, kJitMaxCols = 32;
+constexpr int kJitMinAccCols = 8;  // XOR-accumulate launches (Update / Replace) with fewer columns are not compiled
 
 // rs_tune("jit", 0 | 1 | 2): off / compile in the background on first sight
 // and launch the perm-table kernels until the code is ready (default) /
@@ -21,6 +22,7 @@ extern int g_jit_mode;
 // rs_tune("jit_min_bytes"): launches moving fewer bytes never start a compile
 // (a compile costs ~1 s of host time; a launch of 64 MiB ~10 us of GPU time).
 extern uint64_t g_jit_min_bytes;
+extern int g_jit_pf;
 
 // The compiled kernel for this launch's matrix (a.host_mat, a.rows, a.cols,
 // a.accumulate) on the current device with `bs`-lane workgroups (64 or 256),

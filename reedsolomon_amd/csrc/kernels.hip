@@ -1212,7 +1212,11 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     }
     // 5-8 output rows over a run-time matrix: the bit-sliced network compiled
     // for this matrix (jit.cpp), once it is ready
-    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= kJitMinRows && a.rows <= kJitMaxRows) {
+    // (XOR-accumulate launches over few columns stay on the perm-table kernels:
+    // 10+8 Update 5.74 vs 5.20 TB/s, Replace of 3 rows 5.62 vs 5.11 compiled,
+    // profiles/r02/ab_jit.log)
+    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= kJitMinRows && a.rows <= kJitMaxRows &&
+        (!a.accumulate || a.cols >= kJitMinAccCols)) {
         const int jbs = bs_block_for(a) == 256 ? 256 : 64;
         const uint64_t bytes = a.body * static_cast<uint64_t>(a.nstripes) * static_cast<uint64_t>(a.rows + a.cols);
         if (hipFunction_t f = jit_bitslice_for(a, jbs, bytes)) {
