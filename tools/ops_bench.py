@@ -46,6 +46,10 @@ def rec(name, nbytes, t, **kw):
 
 def main():
     g = torch.Generator(device="cuda").manual_seed(42)
+    # run-time bit-sliced kernels (5-8 output rows) compile on first use here,
+    # so the timed calls run them (the library's default compiles in the
+    # background and uses the perm-table kernels until the code is ready)
+    rs.lib().rs_tune(b"jit", 2)
     # ---- encode, device-resident
     for k, m, vec, S in ((10, 4, 1 << 20, 256), (12, 4, 1 << 20, 256), (10, 4, 8 << 10, 32768), (10, 4, 8 << 10, 1)):
         r = rs.New(k, m)
@@ -54,13 +58,24 @@ def main():
         rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
         del buf
     # ---- other shapes (runtime-column kernels; 5-8 rows are VALU-bound)
-    for k, m in ((8, 4), (6, 3), (16, 4), (10, 6), (10, 8), (12, 8)):
+    for k, m in ((8, 4), (6, 3), (16, 4), (10, 6), (10, 8), (12, 8), (16, 8)):
         vec, S = 1 << 20, 256 * 14 // (k + m)
         r = rs.New(k, m)
         buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
         t = dev_time(lambda: r.encode_batch(buf))
         rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
         del buf
+    # ---- reconst of 5-8 lost at 10+8 @ 1 MiB (run-time matrices, > 4 outputs)
+    k, m, vec = 10, 8, 1 << 20
+    S = 256 * 14 // (k + m)
+    r = rs.New(k, m)
+    buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(buf)
+    for lost in ([0, 2, 4, 6, 8], list(range(8)), [0, 2, 4, 6, 10, 12, 14, 16]):
+        t = dev_time(lambda: r.reconst_batch(buf, [], lost))
+        rec(f"reconst 10+8 1MiB lost={len(lost)} ({'data' if max(lost) < k else 'data+parity'}) x{S}",
+            S * (k + len(lost)) * vec, t)
+    del buf
     # ---- reconst 10+4 @ 8 KiB, 1-4 lost data shards (config 3)
     k, m, vec, S = 10, 4, 8 << 10, 32768
     r = rs.New(k, m)
