@@ -145,33 +145,62 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         const int d = rs->d, p = rs->p;
         if (d + p > 64 * masks.words) return RS_ERR_INVAL;  // the mask cannot name every vector
         if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-        // Group stripes by erasure pattern (host, O(S)); validate every pattern before any launch.
-        std::unordered_map<Mask256, std::vector<int32_t>, Mask256Hash> groups;
+        // Group stripes by erasure pattern (host, O(S)); validate every pattern
+        // before any launch.  Batches hold few distinct patterns, often in runs:
+        // the previous stripe's pattern, then a scan of the first 16 patterns,
+        // then a hash map (32768 stripes through an unordered_map of vectors
+        // cost ~1 ms per call, more than the 0.55 ms kernel it feeds).
+        std::vector<int32_t> pat_of(static_cast<size_t>(nstripes), -1);
+        std::vector<Mask256> keys;
+        std::vector<size_t> counts;
+        std::unordered_map<Mask256, int, Mask256Hash> index;
+        int last = -1;
+        constexpr int kScan = 16;
         for (int s = 0; s < nstripes; ++s) {
             if (!masks.any(s)) continue;
             if (masks.beyond(s, d + p)) return RS_ERR_ILLEGAL_VECTS;
             Mask256 key{};
             for (int w = 0; w < masks.words; ++w) key[w] = masks.row(s)[w];
-            groups[key].push_back(s);
+            int gi = -1;
+            if (last >= 0 && keys[last] == key) {
+                gi = last;
+            } else {
+                const int n = static_cast<int>(keys.size());
+                for (int k = 0; k < n && k < kScan && gi < 0; ++k)
+                    if (keys[k] == key) gi = k;
+                if (gi < 0 && n > kScan) {
+                    auto it = index.find(key);
+                    if (it != index.end()) gi = it->second;
+                }
+                if (gi < 0) {
+                    gi = n;
+                    keys.push_back(key);
+                    counts.push_back(0);
+                    if (gi >= kScan) index.emplace(key, gi);
+                }
+            }
+            pat_of[s] = gi;
+            ++counts[gi];
+            last = gi;
         }
-        if (groups.empty()) return RS_OK;
+        if (keys.empty()) return RS_OK;
         struct Group {
             ReconstPlan pl;
             size_t off, n;
         };
         std::vector<Group> plan;
-        std::vector<int32_t> ids;
-        ids.reserve(nstripes);
-        for (auto& kv : groups) {
+        plan.reserve(keys.size());
+        size_t off = 0;
+        for (size_t gi = 0; gi < keys.size(); ++gi) {
             Group gr;
             int need[kMaxVects], nn = 0;
             for (int v = 0; v < d + p; ++v)
-                if (kv.first[v >> 6] >> (v & 63) & 1) need[nn++] = v;
+                if (keys[gi][v >> 6] >> (v & 63) & 1) need[nn++] = v;
             int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
             if (rc) return rc;  // RS_ERR_TOO_MANY_LOST for a pattern beyond p erasures
-            gr.off = ids.size();
-            gr.n = kv.second.size();
-            ids.insert(ids.end(), kv.second.begin(), kv.second.end());
+            gr.off = off;
+            gr.n = counts[gi];
+            off += gr.n;
             plan.push_back(gr);
         }
         if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
@@ -203,7 +232,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             uint32_t* tabs = reinterpret_cast<uint32_t*>(host);
             PatternDesc* descs = reinterpret_cast<PatternDesc*>(host + tab_bytes);
             int32_t* spat = reinterpret_cast<int32_t*>(host + tab_bytes + desc_bytes);
-            for (int s = 0; s < nstripes; ++s) spat[s] = -1;
+            std::memcpy(spat, pat_of.data(), pat_bytes);
             for (int gi = 0; gi < npat; ++gi) {
                 const Group& gr = plan[gi];
                 std::vector<uint8_t> m;
@@ -216,7 +245,6 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
                 pd.nout = static_cast<uint32_t>(gr.pl.nnr);
                 for (int i = 0; i < d; ++i) pd.in_idx[i] = static_cast<uint16_t>(gr.pl.vs[i]);
                 for (int r = 0; r < gr.pl.nnr; ++r) pd.out_idx[r] = static_cast<uint32_t>(gr.pl.nr[r]);
-                for (size_t t = 0; t < gr.n; ++t) spat[ids[gr.off + t]] = gi;
             }
             uint8_t* dev = nullptr;
             RS_TRY(lease.upload(st, &dev));
@@ -239,10 +267,17 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
                           "multi-pattern kernel launch");
         }
 
+        // stripe ids grouped by pattern, in stripe order within a pattern
         UploadLease lease(rs);
         uint8_t* hids = nullptr;
-        RS_TRY(lease.acquire(ids.size() * sizeof(int32_t), &hids));
-        std::memcpy(hids, ids.data(), ids.size() * sizeof(int32_t));
+        RS_TRY(lease.acquire(off * sizeof(int32_t), &hids));
+        {
+            int32_t* ids = reinterpret_cast<int32_t*>(hids);
+            std::vector<size_t> next(plan.size());
+            for (size_t gi = 0; gi < plan.size(); ++gi) next[gi] = plan[gi].off;
+            for (int s = 0; s < nstripes; ++s)
+                if (pat_of[s] >= 0) ids[next[pat_of[s]]++] = s;
+        }
         uint8_t* dev_ids = nullptr;
         RS_TRY(lease.upload(st, &dev_ids));
         const int32_t* dids = reinterpret_cast<const int32_t*>(dev_ids);

@@ -70,6 +70,8 @@ def main():
             assert L.rs_tune(k.encode(), v) == 0, k
         if op in LOST:
             lost = LOST[op]
+            if layout == "inter":  # in place in the [S][K+M][VEC] buffer
+                return (lambda: r.reconst_batch(buf, [], lost)), S * (K + len(lost)) * VEC
             return (lambda: r.reconst_batch_split(data, par, [], lost)), S * (K + len(lost)) * VEC
         if op == "upd":  # Update row 3 of every stripe: reads old, new, 4 parity; writes 4 parity
             return (lambda: r.update_batch(data[:, 0], data[:, 1], 3, buf)), S * (2 + 2 * M) * VEC
