@@ -366,8 +366,11 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * stripe in a pinned block of their own and ring the engine directly, several
  * callers' calls in flight at once | 0: they join coalesced batches),
  * "host_engine_wg_units" (16-byte units per workgroup a call is spread over;
- * 0 default = one per lane of a workgroup, so calls in flight run on
- * different workgroups),
+ * 0 default = adaptive: a lone call spreads over the first wave of every
+ * workgroup, calls that overlap others take one unit per lane of one
+ * workgroup, so calls in flight run on different workgroups),
+ * "host_engine_yield_us" (a caller waiting longer than this on its engine
+ * call yields its core between polls; 0 default = always spin),
  * "host_engine_idle_us" (the engine leaves after this long without a call,
  * default 200), "host_engine_max_bytes" (larger batches launch; default 1 MiB),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes

@@ -527,6 +527,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_engine_group_waves")
             g_engine_group_waves = value < 1 ? 1 : value > kEngineMaxGroupWaves ? kEngineMaxGroupWaves : value;
         else if (n == "host_engine_wg_units") g_engine_wg_units = value < 0 ? 0 : value;
+        else if (n == "host_engine_yield_us") g_engine_yield_us = value < 0 ? 0 : value;
         else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);

@@ -211,7 +211,7 @@ int engine_call_addr(rs_t* rs, const uint8_t* mat, int rows, int cols, const uin
 bool engine_accepts(int rows, int cols, size_t bytes);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
-extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_wg_units;
+extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_wg_units, g_engine_yield_us;
 extern size_t g_engine_max_bytes;
 
 // Diagnostics (env RSAMD_ENGINE_TRACE): where the time of the synchronous

@@ -51,6 +51,10 @@ size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
 // 16-byte units per workgroup a call is spread over (0: one per lane of a
 // workgroup); rs_tune("host_engine_wg_units")
 int g_engine_wg_units = 0;
+// Waiters spin this long, then yield the core between polls; rs_tune("host_engine_yield_us"), 0 = never
+// (default): 8-64 threads on the box measured the same either way and a lone
+// caller ~1 us slower with it (profiles/r02/engine_yield.log)
+int g_engine_yield_us = 0;
 static const bool g_engine_trace = std::getenv("RSAMD_ENGINE_TRACE") != nullptr;
 const bool g_phase_trace = g_engine_trace;
 
@@ -245,9 +249,17 @@ static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool lo
     Region region(locked ? "engine wait (slot reuse)" : "engine wait (call)");
     const EngineRing* r = rs->eng_ring;
     auto t0 = std::chrono::steady_clock::now();
+    bool yielding = false;
     for (uint32_t spins = 1; !all_done(r, waves, w0, n, seq); ++spins) {
-        _mm_pause();
+        // A call waited on this long (an 8 KiB call takes ~10 us) is queued
+        // behind others: give the core to threads that copy (with more callers
+        // than cores, spinning waiters starved the copiers).
+        if (yielding) std::this_thread::yield();
+        else _mm_pause();
         if ((spins & 63) != 0) continue;
+        if (!yielding && g_engine_yield_us > 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(g_engine_yield_us))
+            yielding = true;
         bool gone = false;
         for (int w = 0; w < waves && !gone; ++w)
             gone = __atomic_load_n(&r->done[w], __ATOMIC_ACQUIRE) < seq &&

@@ -27,6 +27,7 @@
 #include "jit.hpp"
 
 #include <hip/hiprtc.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <chrono>
@@ -332,19 +333,27 @@ struct Jit {
         }
     }
 
-    ~Jit() {  // process exit: finish the compile in flight (hiprtc only), drop the rest
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            stop = true;
-        }
-        cv.notify_all();
-        if (worker.joinable()) worker.join();
-    }
+    pid_t owner = 0;  // the process that started the worker
 };
 
+// Never destroyed (a std::thread destructor on a joinable thread aborts, and a
+// forked child inherits the object but not the thread); the process that
+// started the worker joins it at exit: the compile in flight finishes
+// (hiprtc only), queued ones are dropped.
 Jit& jit() {
-    static Jit j;
-    return j;
+    static Jit* j = new Jit;
+    return *j;
+}
+
+void jit_atexit() {
+    Jit& j = jit();
+    if (j.owner != getpid()) return;
+    {
+        std::lock_guard<std::mutex> lk(j.mu);
+        j.stop = true;
+    }
+    j.cv.notify_all();
+    if (j.worker.joinable()) j.worker.join();
 }
 
 }  // namespace
@@ -415,7 +424,13 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
                 lk.lock();
             } else {
                 j.queue.push_back(e);
-                if (!j.worker.joinable()) j.worker = std::thread([&j] { j.work(); });
+                if (!j.worker.joinable() || j.owner != getpid()) {  // (a forked child starts its own)
+                    if (j.worker.joinable()) j.worker.detach();
+                    static const bool registered = std::atexit(jit_atexit) == 0;
+                    (void)registered;
+                    j.owner = getpid();
+                    j.worker = std::thread([&j] { j.work(); });
+                }
                 j.cv.notify_one();
                 return nullptr;
             }
