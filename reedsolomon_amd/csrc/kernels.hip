@@ -63,6 +63,7 @@ LaunchTuning& tuning() {
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
         x.bs_block = 0;
         x.wide_block = 256;
+        x.xcd_remap = 0;
         return x;
     }();
     return t;
@@ -446,8 +447,14 @@ __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
         __syncthreads();
     };
     // stripe and chunk of this workgroup: a scalar shift when the chunk count
-    // per stripe is a power of two (the grid is < 2^31 chunks)
-    const uint32_t chunk = blockIdx.x;
+    // per stripe is a power of two (the grid is < 2^31 chunks).  xcd_remap:
+    // workgroups are dispatched round-robin over the 8 XCDs (b -> XCD b % 8);
+    // the remap gives XCD x the contiguous chunks [x * G/8, (x+1) * G/8).
+    uint32_t chunk = blockIdx.x;
+    if (a.xcd_remap) {
+        const uint32_t g8 = gridDim.x >> 3;
+        if (chunk < (g8 << 3)) chunk = (chunk & 7u) * g8 + (chunk >> 3);
+    }
     const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
     const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
     const int si = static_cast<int>(su);
@@ -1249,6 +1256,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         }
         a.units_per_chunk = var.bs * var.vpt;
         a.nt_store = tu.nt_store;
+        a.xcd_remap = var.one_chunk ? tu.xcd_remap : 0;
         const uint64_t nunits = a.body / (4 * var.lq);
         a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
         a.total_chunks = a.chunks_per_stripe * a.nstripes;
