@@ -209,3 +209,61 @@ def test_jit_background_compile(rslib, orc, torch_dev):
         assert rslib.jit_stats()["launches"] == st0["launches"] + 1
     finally:
         L.rs_tune(b"jit_min_bytes", 8 << 20)
+
+
+def test_jit_concurrent_threads_background(rslib, orc, torch_dev):
+    """Default (background) mode under concurrency: 4 threads, each with its
+    own handle, stream and matrix, launch repeatedly while their compiles are
+    queued, run and loaded; every launch's bytes equal the oracle's, whichever
+    kernel ran it."""
+    import threading
+
+    torch = torch_dev
+    L = rslib.lib()
+    assert L.rs_tune(b"jit", 1) == 0
+    L.rs_tune(b"jit_min_bytes", 0)
+    errors = []
+    try:
+        rng = np.random.default_rng(9090)
+        jobs = []
+        for t in range(4):
+            rows, cols = 5 + t, 9 + 2 * t
+            mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
+            src = rng.integers(0, 256, (3, cols, 16384 + 16 * t), dtype=np.uint8)
+            jobs.append((mat, src, orc.encode_numpy(mat, src)))
+        st0 = rslib.jit_stats()
+
+        def worker(i):
+            try:
+                mat, hsrc, exp = jobs[i]
+                r = rslib.New(10, 4)
+                s = torch.cuda.Stream()
+                src = torch.from_numpy(hsrc).cuda()
+                dst = torch.empty((hsrc.shape[0], mat.shape[0], hsrc.shape[2]), dtype=torch.uint8, device="cuda")
+                t0 = time.time()
+                n = 0
+                while time.time() - t0 < 60:
+                    dst.fill_(0x5A)
+                    torch.cuda.current_stream().synchronize()
+                    r.gf_matmul_batch(mat, src, None, dst, None, stream=s)
+                    s.synchronize()
+                    if not np.array_equal(dst.cpu().numpy(), exp):
+                        errors.append((i, n))
+                        return
+                    n += 1
+                    if n >= 8 and rslib.jit_stats()["compiled"] >= st0["compiled"] + 4:
+                        break
+            except Exception as e:  # noqa: BLE001
+                errors.append((i, repr(e)))
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors
+        st = rslib.jit_stats()
+        assert st["compiled"] == st0["compiled"] + 4 and st["failed"] == st0["failed"], (st0, st)
+        assert st["launches"] > st0["launches"], (st0, st)
+    finally:
+        L.rs_tune(b"jit_min_bytes", 8 << 20)
