@@ -389,8 +389,11 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
  * "jit" (run-time bit-sliced kernels for 5-8 output rows: 1 default = compile
  * in the background on first sight, perm-table kernels until ready | 2 =
- * compile on the launching thread | 0 = off), "jit_min_bytes" (launches moving
- * fewer bytes start no compile; default 8 MiB),
+ * compile on the launching thread | 0 = off), "jit_min_launches" (background
+ * mode compiles a matrix from its n-th launch on; default 2: one-off erasure
+ * patterns are never compiled), "jit_min_bytes" (... and once its launches
+ * moved this many bytes; default 8 MiB), "jit_pf" (columns loaded ahead in
+ * the compiled kernels, 1..6, default 3),
  * "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name. */

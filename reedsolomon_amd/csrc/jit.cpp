@@ -52,6 +52,7 @@ int g_jit_mode = [] {
     return e ? std::atoi(e) : 1;
 }();
 uint64_t g_jit_min_bytes = uint64_t{8} << 20;
+int g_jit_min_launches = 2;
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 
 namespace {
@@ -288,12 +289,20 @@ struct Entry {
     hipFunction_t fn64 = nullptr, fn256 = nullptr;
 };
 
-constexpr size_t kMaxEntries = 64;
+constexpr size_t kMaxEntries = 256;
+constexpr size_t kMaxSeen = 4096;  // matrices counted but not compiled yet (cleared when full)
+
+struct Seen {
+    uint64_t launches = 0, bytes = 0;
+};
+
+void jit_atexit_hook();
 
 struct Jit {
     std::mutex mu;
     std::condition_variable cv;
     std::map<std::string, std::shared_ptr<Entry>> entries;  // key: device, mode, rows, cols, matrix
+    std::map<std::string, Seen> seen;  // background mode: launches / bytes of matrices not compiled yet
     std::deque<std::shared_ptr<Entry>> queue;
     std::thread worker;
     bool stop = false;
@@ -303,6 +312,14 @@ struct Jit {
 
     void run_one(const std::shared_ptr<Entry>& e) {  // caller does not hold mu
         Compiled c = compile(e->src);
+        // The compiler libraries hiprtc loads on its first compile register
+        // their static destructors then, i.e. after jit_atexit: those ran
+        // first at exit and a compile still in flight on the worker crashed
+        // (SIGSEGV at exit of tools/gpu_stress.py).  Registering once more
+        // after the first compile puts the join ahead of them (atexit runs in
+        // reverse order); jit_atexit is idempotent.
+        static std::once_flag late;
+        std::call_once(late, [] { std::atexit(jit_atexit_hook); });
         std::lock_guard<std::mutex> lk(mu);
         if (c.ok) {
             e->code = std::move(c.code);
@@ -347,6 +364,7 @@ Jit& jit() {
 
 void jit_atexit() {
     Jit& j = jit();
+    if (!j.worker.joinable()) return;
     if (j.owner != getpid()) return;
     {
         std::lock_guard<std::mutex> lk(j.mu);
@@ -355,6 +373,8 @@ void jit_atexit() {
     j.cv.notify_all();
     if (j.worker.joinable()) j.worker.join();
 }
+
+void jit_atexit_hook() { jit_atexit(); }
 
 }  // namespace
 
@@ -412,8 +432,18 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
         std::unique_lock<std::mutex> lk(j.mu);
         auto it = j.entries.find(key);
         if (it == j.entries.end()) {
-            if (launch_bytes < g_jit_min_bytes && g_jit_mode != 2) return nullptr;
             if (j.entries.size() >= kMaxEntries) return nullptr;
+            if (g_jit_mode != 2) {
+                // compile only a matrix that recurs: a one-off erasure pattern
+                // would cost a compile (seconds of host time) and never pay it back
+                if (j.seen.size() >= kMaxSeen) j.seen.clear();
+                Seen& h = j.seen[key];
+                ++h.launches;
+                h.bytes += launch_bytes;
+                if (h.launches < static_cast<uint64_t>(g_jit_min_launches) || h.bytes < g_jit_min_bytes)
+                    return nullptr;
+                j.seen.erase(key);
+            }
             e = std::make_shared<Entry>();
             e->src = jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             j.entries.emplace(key, e);

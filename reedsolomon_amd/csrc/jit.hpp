@@ -19,10 +19,14 @@ constexpr int kJitMinAccCols = 8;  // XOR-accumulate launches (Update / Replace)
 // and launch the perm-table kernels until the code is ready (default) /
 // compile on the launching thread (tests, benchmarks).
 extern int g_jit_mode;
-// rs_tune("jit_min_bytes"): launches moving fewer bytes never start a compile
-// (a compile costs ~1 s of host time; a launch of 64 MiB ~10 us of GPU time).
+// rs_tune("jit_min_bytes"): a matrix whose launches moved fewer bytes in
+// total starts no compile (a compile costs 1.5-4.5 s of host time; a launch
+// of 64 MiB ~10 us of GPU time).
 extern uint64_t g_jit_min_bytes;
 extern int g_jit_pf;
+// rs_tune("jit_min_launches"): background mode compiles a matrix once it has
+// been launched this many times, moving jit_min_bytes in total (default 2)
+extern int g_jit_min_launches;
 
 // The compiled kernel for this launch's matrix (a.host_mat, a.rows, a.cols,
 // a.accumulate) on the current device with `bs`-lane workgroups (64 or 256),
