@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}",
         "-fvisibility=hidden", "-Wall", "-Wno-unused-result",
         "-I", os.path.join(ROOT, "include"),
-        *SOURCES, "-o", tmp, "-lhiprtc",
+        *SOURCES, "-o", tmp, "-lhiprtc", "-ldl",
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

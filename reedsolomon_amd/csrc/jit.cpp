@@ -27,6 +27,7 @@
 #include "jit.hpp"
 
 #include <hip/hiprtc.h>
+#include <dlfcn.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -456,6 +457,11 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
                 j.queue.push_back(e);
                 if (!j.worker.joinable() || j.owner != getpid()) {  // (a forked child starts its own)
                     if (j.worker.joinable()) j.worker.detach();
+                    // load the compiler library hiprtc would load on its first
+                    // compile now, so its static destructors are registered
+                    // before jit_atexit and run after it (atexit order)
+                    static void* const comgr = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
+                    (void)comgr;
                     static const bool registered = std::atexit(jit_atexit) == 0;
                     (void)registered;
                     j.owner = getpid();
