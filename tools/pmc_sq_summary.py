@@ -18,7 +18,8 @@ for d in sorted(glob.glob(os.path.join(out, "p*"))):
     files = glob.glob(os.path.join(d, "**", "pmc_counter_collection.csv"), recursive=True)
     if not files:
         continue
-    rows = [r for r in csv.DictReader(open(files[0])) if "gf_matmul" in r["Kernel_Name"] or "gf_bitslice" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(files[0]))
+            if any(k in r["Kernel_Name"] for k in ("gf_matmul", "gf_bitslice", "rs_bs_jit"))]
     if not rows:
         continue
     dom = statistics.mode(r["Kernel_Name"] for r in rows)
