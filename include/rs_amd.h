@@ -334,9 +334,9 @@ RS_API int rs_host_call_stats(const rs_t* rs, uint64_t* launches, uint64_t* call
  * idle period).  Either pointer may be NULL. */
 RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launches);
 
-/* Run-time compiled bit-sliced kernels (products with 5-8 output rows over a
- * matrix known only at run time: Reconst of 5-8 lost vectors, Encode of codes
- * without a build-time network, Update / Replace with 5-8 parity rows; see
+/* Run-time compiled bit-sliced kernels (products with 5-16 output rows over a
+ * matrix known only at run time: Reconst of 5-16 lost vectors, Encode of codes
+ * without a build-time network, Update / Replace with 5-16 parity rows; see
  * DESIGN.md §3).  Process-wide counters: code objects compiled, compiles or
  * loads that failed (the perm-table kernels then stay in use), launches of
  * compiled kernels, and the total compile time in ms.  Any pointer may be
@@ -344,7 +344,7 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
 RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
 
 /* Generate and compile (hiprtc, no device needed) the run-time kernel for a
- * rows x cols matrix (row-major, 5 <= rows <= 8, 1 <= cols <= 32), overwrite
+ * rows x cols matrix (row-major, 5 <= rows <= 16, 1 <= cols <= 32), overwrite
  * (accumulate 0) or XOR-into-outputs (1) mode.  RS_OK, RS_ERR_INVAL (shape)
  * or RS_ERR_DEVICE (compile failed: the log goes to stderr).  ms may be NULL.
  * For tests and warm-up. */
@@ -387,7 +387,7 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * batches in flight at once: 1 | 2 default),
  * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
  * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
- * "jit" (run-time bit-sliced kernels for 5-8 output rows: 1 default = compile
+ * "jit" (run-time bit-sliced kernels for 5-16 output rows: 1 default = compile
  * in the background on first sight, perm-table kernels until ready | 2 =
  * compile on the launching thread | 0 = off), "jit_min_launches" (background
  * mode compiles a matrix from its n-th launch on; default 2: one-off erasure

@@ -1,5 +1,5 @@
 // jit.cpp — run-time generated bit-sliced kernels (hiprtc) for products with
-// 5-8 output rows whose matrix is only known at run time.
+// 5-16 output rows whose matrix is only known at run time.
 //
 // Why: above 4 output rows the perm-table kernels are VALU-bound (10+8 @ 1 MiB
 // Reconst of 8: 5.05-5.18 TB/s, profiles/r02/pmc_sq_10_8.json), while the

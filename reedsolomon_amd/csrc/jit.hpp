@@ -1,6 +1,6 @@
-// jit.hpp — run-time generated bit-sliced kernels for matrices with 5-8
-// output rows that are only known at run time (Reconst of 5-8 lost vectors,
-// Encode of codes without a generated network, Update / Replace with 5-8
+// jit.hpp — run-time generated bit-sliced kernels for matrices with 5-16
+// output rows that are only known at run time (Reconst of 5-16 lost vectors,
+// Encode of codes without a generated network, Update / Replace with 5-16
 // parity rows).  See jit.cpp and DESIGN.md §3 "Run-time bit-sliced kernels".
 #pragma once
 #include <hip/hip_runtime.h>
@@ -12,7 +12,9 @@
 
 namespace rsamd {
 
-constexpr int kJitMinRows = 5, kJitMaxRows = 8, kJitMaxCols = 32;
+// 9-16 rows: 138-221 VGPRs, no scratch (16 x 16: 2 waves/SIMD); the perm-table
+// kernels run those in row groups of 8 that re-read every input
+constexpr int kJitMinRows = 5, kJitMaxRows = 16, kJitMaxCols = 32;
 constexpr int kJitMinAccCols = 8;  // XOR-accumulate launches (Update / Replace) with fewer columns are not compiled
 
 // rs_tune("jit", 0 | 1 | 2): off / compile in the background on first sight

@@ -1217,7 +1217,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         }
         if (bk) a.body = 0;  // the vector path below is done; only the tail remains
     }
-    // 5-8 output rows over a run-time matrix: the bit-sliced network compiled
+    // 5-16 output rows over a run-time matrix: the bit-sliced network compiled
     // for this matrix (jit.cpp), once it is ready
     // (XOR-accumulate launches over few columns stay on the perm-table kernels:
     // 10+8 Update 5.74 vs 5.20 TB/s, Replace of 3 rows 5.62 vs 5.11 compiled,

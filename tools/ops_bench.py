@@ -65,6 +65,21 @@ def main():
         t = dev_time(lambda: r.encode_batch(buf))
         rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
         del buf
+    # ---- > 4 outputs on the split layout (data [S][k][vec], parity [S][m][vec],
+    # as bench.py): 16+8 Encode (no build-time network: run-time compiled) and
+    # 10+8 Reconst of 5 / 8 lost data vectors
+    for k, m in ((16, 8), (10, 8)):
+        vec, S = 1 << 20, 256 * 14 // (k + m)
+        r = rs.New(k, m)
+        data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
+        par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
+        t = dev_time(lambda: r.encode_batch_split(data, par))
+        rec(f"encode {k}+{m} {vec >> 10}KiB x{S} split (device)", S * (k + m) * vec, t)
+        if k == 10:
+            for lost in ([0, 2, 4, 6, 8], list(range(8))):
+                t = dev_time(lambda: r.reconst_batch_split(data, par, [], lost))
+                rec(f"reconst {k}+{m} 1MiB lost={len(lost)} data x{S} split", S * (k + len(lost)) * vec, t)
+        del data, par
     # ---- reconst of 5-8 lost at 10+8 @ 1 MiB (run-time matrices, > 4 outputs)
     k, m, vec = 10, 8, 1 << 20
     S = 256 * 14 // (k + m)
