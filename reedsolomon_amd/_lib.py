@@ -98,6 +98,7 @@ SIGNATURES = {
     "rs_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
     "rs_jit_stats": (c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                              ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]),
+    "rs_jit_prepare": (c_int, [c_void, ctypes.c_void_p, c_int, c_int, c_int, c_int]),
     "rs_jit_compile_check": (c_int, [ctypes.c_void_p, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_double)]),
     "rs_tune": (c_int, [ctypes.c_char_p, c_int]),
 }

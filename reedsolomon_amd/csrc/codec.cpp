@@ -611,6 +611,16 @@ int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, doubl
     });
 }
 
+int rs_jit_prepare(rs_t* rs, const uint8_t* mat, int rows, int cols, int accumulate, int wait) {
+    return abi_guard([&]() -> int {
+        if (!rs || !mat || rows < kJitMinRows || rows > kJitMaxRows || cols < 1 || cols > kJitMaxCols)
+            return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        return jit_prepare(mat, rows, cols, accumulate != 0, wait != 0);
+    });
+}
+
 int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms) {
     return abi_guard([&]() -> int { return jit_compile_check(mat, rows, cols, accumulate != 0, ms); });
 }

@@ -415,8 +415,9 @@ void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double*
 
 void jit_count_launch() { jit().launches.fetch_add(1, std::memory_order_relaxed); }
 
-hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
-    if (!g_jit_mode || !a.host_mat || a.rows < kJitMinRows || a.rows > kJitMaxRows || a.cols < 1 ||
+// mode: 1 background after recurrence, 2 compile on this thread, 3 queue now
+static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int mode) {
+    if (!mode || !a.host_mat || a.rows < kJitMinRows || a.rows > kJitMaxRows || a.cols < 1 ||
         a.cols > kJitMaxCols)
         return nullptr;
     int dev = 0;
@@ -434,7 +435,7 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
         auto it = j.entries.find(key);
         if (it == j.entries.end()) {
             if (j.entries.size() >= kMaxEntries) return nullptr;
-            if (g_jit_mode != 2) {
+            if (mode == 1) {
                 // compile only a matrix that recurs: a one-off erasure pattern
                 // would cost a compile (seconds of host time) and never pay it back
                 if (j.seen.size() >= kMaxSeen) j.seen.clear();
@@ -448,7 +449,7 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
             e = std::make_shared<Entry>();
             e->src = jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             j.entries.emplace(key, e);
-            if (g_jit_mode == 2) {
+            if (mode == 2) {
                 e->state = Entry::kCompiling;
                 lk.unlock();
                 j.run_one(e);  // on this thread
@@ -495,6 +496,22 @@ hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_byte
         e->code.shrink_to_fit();
         return bs == 256 ? f256 : f64;
     }
+}
+
+hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
+    return lookup(a, bs, launch_bytes, g_jit_mode);
+}
+
+int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wait) {
+    if (!mat || rows < kJitMinRows || rows > kJitMaxRows || cols < 1 || cols > kJitMaxCols) return RS_ERR_INVAL;
+    MatmulArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.host_mat = mat;
+    a.rows = rows;
+    a.cols = cols;
+    a.accumulate = accumulate ? 1 : 0;
+    const hipFunction_t f = lookup(a, 64, ~uint64_t{0}, wait ? 2 : 3);
+    return (f || !wait) ? RS_OK : RS_ERR_DEVICE;
 }
 
 }  // namespace rsamd

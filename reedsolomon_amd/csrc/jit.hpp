@@ -41,6 +41,9 @@ void jit_count_launch();
 std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate);
 // Compile only (hiprtc, no device needed): RS_OK or RS_ERR_DEVICE.
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms);
+// Compile (wait: on this thread, and load on the current device) or queue
+// the kernel for a matrix now, whatever its launch history (rs_jit_prepare).
+int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wait);
 void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
 
 }  // namespace rsamd

@@ -410,6 +410,15 @@ class RS:
     def inverse_cache_size(self) -> int:
         return int(lib().rs_inverse_cache_size(self._h))
 
+    def jit_prepare(self, mat=None, accumulate: bool = False, wait: bool = True) -> None:
+        """Compile the run-time bit-sliced kernel for `mat` (rows x cols,
+        5 <= rows <= 16) on this codec's device now (rs_jit_prepare); default
+        mat = GenMatrix, i.e. this code's Encode."""
+        m = (self.GenMatrix.reshape(self.ParityNum, self.DataNum) if mat is None
+             else np.ascontiguousarray(mat, dtype=np.uint8))
+        _check(lib().rs_jit_prepare(self._h, m.ctypes.data, m.shape[0], m.shape[1], int(bool(accumulate)),
+                                    int(bool(wait))))
+
     def host_engine_stats(self) -> tuple:
         """(calls, launches) of the resident host-call engine since New (rs_host_engine_stats)."""
         a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)

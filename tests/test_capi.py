@@ -357,3 +357,5 @@ def test_jit_compile_check(rslib, orc):
     for shape in [(4, 10), (17, 10), (8, 33)]:
         with pytest.raises(ErrInvalidArgument):
             rslib.jit_compile_check(np.ones(shape, np.uint8))
+        with pytest.raises(ErrInvalidArgument):  # rs_jit_prepare checks the shape before any device work
+            r.jit_prepare(np.ones(shape, np.uint8))

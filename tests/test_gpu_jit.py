@@ -275,3 +275,23 @@ def test_jit_concurrent_threads_background(rslib, orc, torch_dev):
         assert st["launches"] > st0["launches"], (st0, st)
     finally:
         L.rs_tune(b"jit_min_bytes", 8 << 20)
+
+
+def test_jit_prepare_then_first_launch_runs_compiled(rslib, orc, torch_dev):
+    """rs_jit_prepare (default mode, no recurrence needed): after preparing the
+    16+8 Encode, its first launch (a small one, below jit_min_bytes) already
+    runs the compiled kernel; bytes equal the oracle's."""
+    torch = torch_dev
+    assert rslib.lib().rs_tune(b"jit", 1) == 0
+    d, p = 16, 8
+    r = rslib.New(d, p)
+    r.jit_prepare()
+    rng = np.random.default_rng(616)
+    host = rng.integers(0, 256, (3, d + p, 65536), dtype=np.uint8)
+    exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
+    buf = torch.from_numpy(host).cuda()
+    before = rslib.jit_stats()["launches"]
+    r.encode_batch(buf)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy()[:, d:], exp)
+    assert rslib.jit_stats()["launches"] == before + 1
