@@ -368,8 +368,6 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
  * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "wide_block" (128 | 256),
- * "xcd_remap" (0 default | 1: each XCD takes a contiguous eighth of the
- * one-chunk kernels' chunks instead of every eighth chunk),
  * "host_engine" (1 default: small synchronous host calls, coalesced or
  * alone, are served by a resident kernel through a doorbell in host memory |
  * 0: one launch + stream sync per call), "host_engine_waves" (1..64

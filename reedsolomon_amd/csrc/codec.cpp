@@ -522,7 +522,6 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
-        else if (n == "xcd_remap") t.xcd_remap = value ? 1 : 0;
         else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
         else if (n == "host_engine") g_engine = value ? 1 : 0;
         else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxGroups ? kEngineMaxGroups : value;

@@ -86,7 +86,7 @@ struct MatmulArgs {
     int rows, cols, rows_pad; int nstripes; int accumulate; int units_per_chunk; int nt_store;
     u64 len; u64 body; u64 tail_start; i64 ss[4]; const int* stripe_ids;
     i64 chunks_per_stripe; i64 total_chunks; int cps_shift;
-    u64 ptr[260]; u32 sid[260]; int xcd_remap;
+    u64 ptr[260]; u32 sid[260];
 };
 __device__ __forceinline__ u32x2 ld8(const g_u8* base, u32 off, u32 nbytes) {
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base), 0, (int)nbytes, 0x00020000);

@@ -63,7 +63,6 @@ LaunchTuning& tuning() {
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
         x.bs_block = 0;
         x.wide_block = 256;
-        x.xcd_remap = 0;
         return x;
     }();
     return t;
@@ -423,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void gf_matmul_vec(const MatmulArgs a) {
 // One chunk per workgroup, rows <= MC (grid = all chunks): the common case
 // without the row-group / grid-stride loops of gf_matmul_vec (less live state).
 template <int KB, bool KFIX, int MC, bool ACC, int WIN, bool STAGE_LATE = false, int LQ = 4, int VPT = 1,
-          int VAR = kVarDefault, int BS = kBlock>
+          int VAR = kVarDefault, int BS = kBlock, bool XCD = false>
 __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
     constexpr int COLD = ((MC * 5 + 3) / 4) * 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
@@ -447,11 +446,12 @@ __global__ __launch_bounds__(BS) void gf_matmul_vec1(const MatmulArgs a) {
         __syncthreads();
     };
     // stripe and chunk of this workgroup: a scalar shift when the chunk count
-    // per stripe is a power of two (the grid is < 2^31 chunks).  xcd_remap:
-    // workgroups are dispatched round-robin over the 8 XCDs (b -> XCD b % 8);
-    // the remap gives XCD x the contiguous chunks [x * G/8, (x+1) * G/8).
+    // per stripe is a power of two (the grid is < 2^31 chunks).  XCD
+    // (experiment, RSAMD_VAR=160): workgroups are dispatched round-robin over
+    // the 8 XCDs (b -> XCD b % 8); the remap gives XCD x the contiguous chunks
+    // [x * G/8, (x+1) * G/8) (measured slower).
     uint32_t chunk = blockIdx.x;
-    if (a.xcd_remap) {
+    if constexpr (XCD) {
         const uint32_t g8 = gridDim.x >> 3;
         if (chunk < (g8 << 3)) chunk = (chunk & 7u) * g8 + (chunk >> 3);
     }
@@ -991,6 +991,9 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
         case 159: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 2, 1, kVarDefault | kVarXorOnly, 128>, 10,
                                  4, 1, true, "vec1<10,8B,bs128,xor>", true, 2, 128}; return true;
         case 158: *out = RSAMD_BSV(false, 2, 1024, "vec1<10,8B,bs1024>"); return true;
+        // XCD-contiguous chunk order (each XCD streams its own eighth of the chunks)
+        case 160: *out = Variant{gf_matmul_vec1<10, true, 4, false, 0, false, 2, 1, kVarDefault, 128, true>, 10, 4, 1,
+                                 true, "vec1<10,8B,bs128,xcd>", true, 2, 128}; return true;
 #undef RSAMD_BSV
         default: break;
     }
@@ -1256,7 +1259,6 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         }
         a.units_per_chunk = var.bs * var.vpt;
         a.nt_store = tu.nt_store;
-        a.xcd_remap = var.one_chunk ? tu.xcd_remap : 0;
         const uint64_t nunits = a.body / (4 * var.lq);
         a.chunks_per_stripe = static_cast<int64_t>((nunits + a.units_per_chunk - 1) / a.units_per_chunk);
         a.total_chunks = a.chunks_per_stripe * a.nstripes;

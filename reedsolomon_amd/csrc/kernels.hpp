@@ -39,7 +39,6 @@ struct MatmulArgs {
     uint64_t ptr[kMaxPtrs];   // inputs [0, cols), outputs [cols, cols+rows)
     uint32_t sid[kMaxPtrs];   // stride selector of each vector (0..3); dwords so the
                               // kernel reads them with scalar loads
-    int xcd_remap;            // one-chunk kernels: workgroup b takes chunk (b % 8) * (G / 8) + b / 8
 };
 
 // Multi-pattern mode: one pattern of rs_reconst_batch_multi.  tab_off is the
@@ -122,7 +121,6 @@ struct LaunchTuning {
     int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
     int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
-    int xcd_remap;    // one-chunk kernels: each XCD streams its own contiguous eighth of the chunks (0 default | 1)
 };
 LaunchTuning& tuning();
 
