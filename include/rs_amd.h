@@ -344,7 +344,7 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
 RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
 
 /* Compile the run-time kernel for a rows x cols matrix (row-major, 5 <= rows
- * <= 16, 1 <= cols <= 32; accumulate 1 = the XOR-into-outputs form Update /
+ * <= 16, 1 <= cols <= 64; accumulate 1 = the XOR-into-outputs form Update /
  * Replace use) for the handle's device now, instead of on the matrix's
  * second large launch: wait 1 compiles and loads it on the calling thread
  * (RS_OK, or RS_ERR_DEVICE if the compile failed), wait 0 queues the compile
@@ -355,7 +355,7 @@ RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches
 RS_API int rs_jit_prepare(rs_t* rs, const uint8_t* mat, int rows, int cols, int accumulate, int wait);
 
 /* Generate and compile (hiprtc, no device needed) the run-time kernel for a
- * rows x cols matrix (row-major, 5 <= rows <= 16, 1 <= cols <= 32), overwrite
+ * rows x cols matrix (row-major, 5 <= rows <= 16, 1 <= cols <= 64), overwrite
  * (accumulate 0) or XOR-into-outputs (1) mode.  RS_OK, RS_ERR_INVAL (shape)
  * or RS_ERR_DEVICE (compile failed: the log goes to stderr).  ms may be NULL.
  * For tests and warm-up. */

@@ -14,7 +14,7 @@ namespace rsamd {
 
 // 9-16 rows: 138-221 VGPRs, no scratch (16 x 16: 2 waves/SIMD); the perm-table
 // kernels run those in row groups of 8 that re-read every input
-constexpr int kJitMinRows = 5, kJitMaxRows = 16, kJitMaxCols = 32;
+constexpr int kJitMinRows = 5, kJitMaxRows = 16, kJitMaxCols = 64;
 constexpr int kJitMinAccCols = 8;  // XOR-accumulate launches (Update / Replace) with fewer columns are not compiled
 
 // rs_tune("jit", 0 | 1 | 2): off / compile in the background on first sight

@@ -343,7 +343,7 @@ def test_jit_compile_check(rslib, orc):
     """The run-time bit-sliced kernel generator (jit.cpp) produces code that
     hiprtc compiles for gfx950 (no device needed): a Reconst-of-8 matrix of
     10+8 (overwrite) and a 16-column 5-row XOR-accumulate product; shapes
-    outside 5-16 rows / 1-32 columns are refused."""
+    outside 5-16 rows / 1-64 columns are refused."""
     import numpy as np
 
     from reedsolomon_amd.rs import ErrInvalidArgument
@@ -354,7 +354,7 @@ def test_jit_compile_check(rslib, orc):
     assert rslib.jit_compile_check(m) > 0
     rng = np.random.default_rng(3)
     assert rslib.jit_compile_check(rng.integers(0, 256, (5, 16), dtype=np.uint8), accumulate=True) > 0
-    for shape in [(4, 10), (17, 10), (8, 33)]:
+    for shape in [(4, 10), (17, 10), (8, 65)]:
         with pytest.raises(ErrInvalidArgument):
             rslib.jit_compile_check(np.ones(shape, np.uint8))
         with pytest.raises(ErrInvalidArgument):  # rs_jit_prepare checks the shape before any device work

@@ -42,7 +42,7 @@ def _padded(torch, rng, S, v, n, pad):
 
 
 @pytest.mark.parametrize("rows,cols", [(5, 10), (6, 10), (7, 12), (8, 10), (8, 16), (8, 32), (5, 1), (8, 3),
-                                       (9, 10), (12, 16), (16, 16), (16, 32)])
+                                       (9, 10), (12, 16), (16, 16), (16, 32), (8, 64)])
 def test_jit_matmul_vs_oracle(rslib, orc, torch_dev, jit_sync, rows, cols):
     torch = torch_dev
     rng = np.random.default_rng(rows * 100 + cols)
@@ -70,7 +70,8 @@ def test_jit_matmul_vs_oracle(rslib, orc, torch_dev, jit_sync, rows, cols):
 @pytest.mark.parametrize("d,p,lost", [(10, 8, [0, 1, 2, 3, 4, 5, 6, 7]), (10, 8, [1, 3, 5, 7, 9]),
                                       (10, 8, [0, 2, 4, 11, 13, 17]), (10, 8, [12, 13, 14, 15, 16, 17]),
                                       (16, 8, [0, 3, 6, 9, 12, 15, 18, 21]), (20, 7, [2, 4, 6, 8, 10, 12, 14]),
-                                      (20, 12, list(range(0, 24, 2))), (16, 16, list(range(16)))])
+                                      (20, 12, list(range(0, 24, 2))), (16, 16, list(range(16))),
+                                      (40, 8, [1, 5, 9, 13, 17, 21, 33, 45])])
 def test_jit_reconst_5_to_8_lost(rslib, orc, torch_dev, jit_sync, d, p, lost):
     """Reconst of 5-8 lost vectors (data and parity mixed) on a batch: the
     rebuilt stripes equal the encoded originals, on both layouts."""
