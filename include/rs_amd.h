@@ -380,6 +380,8 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * 0 default = adaptive: a lone call spreads over the first wave of every
  * workgroup, calls that overlap others take one unit per lane of one
  * workgroup, so calls in flight run on different workgroups),
+ * "host_engine_poll_gap" (0 default: the engine reads the doorbell once per
+ * PCIe round trip | n: two reads in flight, n x 10 ns apart),
  * "host_engine_yield_us" (a caller waiting longer than this on its engine
  * call yields its core between polls; 0 default = always spin),
  * "host_engine_idle_us" (the engine leaves after this long without a call,

@@ -528,6 +528,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_engine_group_waves")
             g_engine_group_waves = value < 1 ? 1 : value > kEngineMaxGroupWaves ? kEngineMaxGroupWaves : value;
         else if (n == "host_engine_wg_units") g_engine_wg_units = value < 0 ? 0 : value;
+        else if (n == "host_engine_poll_gap") g_engine_poll_gap = value < 0 ? 0 : value > 1000 ? 1000 : value;
         else if (n == "host_engine_yield_us") g_engine_yield_us = value < 0 ? 0 : value;
         else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);

@@ -46,6 +46,12 @@ int g_engine = [] {                     // rs_tune("host_engine", 0 | 1); env RS
 int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..64): workgroups (one polling wave each)
 int g_engine_group_waves = 8;           // rs_tune("host_engine_group_waves", 1..8): waves per workgroup
 int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
+// Doorbell polls: 0 = one read per PCIe round trip; n = a second read in
+// flight, issued n ticks (10 ns) after the first; rs_tune("host_engine_poll_gap")
+int g_engine_poll_gap = [] {  // (env RSAMD_ENGINE_POLL_GAP)
+    const char* e = std::getenv("RSAMD_ENGINE_POLL_GAP");
+    return e ? std::atoi(e) : 0;
+}();
 // Batches up to this many bytes go to the engine, larger ones launch.
 size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
 // 16-byte units per workgroup a call is spread over (0: one per lane of a
@@ -189,7 +195,8 @@ static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     const uint64_t idle_ticks = static_cast<uint64_t>(g_engine_idle_us) * 100;  // 100 MHz realtime counter
     const uint64_t epoch = rs->eng_epoch + 1;
     Region region("engine launch");
-    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks, rs->eng_stream),
+    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks,
+                                static_cast<uint32_t>(g_engine_poll_gap), rs->eng_stream),
                   "engine launch"));
     if (g_engine_trace) std::fprintf(stderr, "engine launch: epoch %llu start %llu\n",
                                      static_cast<unsigned long long>(epoch), static_cast<unsigned long long>(start));
@@ -198,6 +205,7 @@ static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     rs->eng_waves = waves;
     rs->eng_group_waves = group_waves;
     rs->eng_idle_us = g_engine_idle_us;
+    rs->eng_poll_gap = g_engine_poll_gap;
     rs->eng_launches.fetch_add(1, std::memory_order_relaxed);
     return RS_OK;
 }
@@ -319,7 +327,8 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
                        : g_engine_group_waves > kEngineMaxGroupWaves ? kEngineMaxGroupWaves
                                                                      : g_engine_group_waves;
     if (rs->eng_running &&
-        (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us))
+        (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us ||
+         rs->eng_poll_gap != g_engine_poll_gap))
         engine_stop(rs);  // new shape: the old instance must be gone before the next one reads done words
     RS_TRY(engine_relaunch_if_gone(rs));
     if (!rs->eng_running) RS_TRY(engine_launch(rs, waves, gwaves, rs->eng_seq));

@@ -770,7 +770,7 @@ __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t
 }
 
 __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t start, uint64_t epoch,
-                                                 uint64_t idle_ticks) {
+                                                 uint64_t idle_ticks, uint32_t poll_gap) {
     constexpr int kPollWords = 8 * (1 + kEnginePtrLines);  // a slot's header + address lines
     __shared__ __attribute__((aligned(16))) uint32_t tab[kEngineMaxCols * kEngineMaxRows * 5];
     __shared__ uint64_t s_raw[kPollWords];  // the lines wave 0 saw (s_raw[0] = 0: leave)
@@ -788,25 +788,47 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
             const uint64_t* lines = reinterpret_cast<const uint64_t*>(slot);
             uint64_t w = 0, seq = 0;
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t n = 1;; ++n) {
-                w = lane < kPollWords ? sys_load64(&lines[lane]) : 0;
-                const uint64_t s0 = lane_u64(w, 0), s1 = lane_u64(w, 7);
-                if (s0 == s1 && s0 == last + 1) {
-                    // address mode: the lines holding this call's addresses carry its tag
-                    const uint64_t w4 = lane_u64(w, 4), w5 = lane_u64(w, 5);
-                    const int nv = static_cast<int>((w4 >> 32) & 0xffff) + static_cast<int>(w4 >> 48);
-                    bool tagged = true;
-                    if (w5 & 8)
-                        for (int l = 1; l <= (nv + 6) / 7 && l <= kEnginePtrLines; ++l)
-                            tagged = tagged && lane_u64(w, 8 * l + 7) == s0;
-                    if (tagged) {
-                        seq = s0;
+            auto issue = [&]() -> uint64_t { return lane < kPollWords ? sys_load64(&lines[lane]) : 0; };
+            // the call number if the read shows call last + 1 complete, else 0
+            auto probe = [&](uint64_t x) -> uint64_t {
+                const uint64_t s0 = lane_u64(x, 0), s1 = lane_u64(x, 7);
+                if (s0 != s1 || s0 != last + 1) return 0;
+                // address mode: the lines holding this call's addresses carry its tag
+                const uint64_t w4 = lane_u64(x, 4), w5 = lane_u64(x, 5);
+                const int nv = static_cast<int>((w4 >> 32) & 0xffff) + static_cast<int>(w4 >> 48);
+                bool tagged = true;
+                if (w5 & 8)
+                    for (int l = 1; l <= (nv + 6) / 7 && l <= kEnginePtrLines; ++l)
+                        tagged = tagged && lane_u64(x, 8 * l + 7) == s0;
+                return tagged ? s0 : 0;
+            };
+            // stop word, or no call for idle_ticks: seq stays 0 and every wave leaves
+            auto leave = [&](uint64_t x, uint32_t n) {
+                return lane_u64(x, 6) >= epoch ||
+                       ((n & 31) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks);
+            };
+            if (poll_gap == 0) {  // one read per round trip
+                for (uint32_t n = 1;; ++n) {
+                    w = issue();
+                    if ((seq = probe(w)) != 0 || leave(w, n)) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            } else {  // two reads in flight, poll_gap ticks apart; the older is checked first
+                uint64_t wa = issue();
+                while (__builtin_amdgcn_s_memrealtime() - t0 < poll_gap) __builtin_amdgcn_s_sleep(1);
+                uint64_t wb = issue();
+                for (uint32_t n = 1;; ++n) {
+                    if ((seq = probe(wa)) != 0 || leave(wa, n)) {
+                        w = wa;
                         break;
                     }
+                    wa = issue();
+                    if ((seq = probe(wb)) != 0 || leave(wb, n)) {
+                        w = wb;
+                        break;
+                    }
+                    wb = issue();
                 }
-                if (lane_u64(w, 6) >= epoch || ((n & 31) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks))
-                    break;  // seq stays 0: every wave leaves
-                __builtin_amdgcn_s_sleep(2);
             }
             t_seen = __builtin_amdgcn_s_memrealtime();
             if (lane < kPollWords) s_raw[lane] = lane == 0 ? seq : w;
@@ -885,12 +907,12 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
 }
 
 hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
-                         uint64_t idle_ticks, hipStream_t stream) {
+                         uint64_t idle_ticks, uint32_t poll_gap_ticks, hipStream_t stream) {
     if (groups < 1 || groups > kEngineMaxGroups || waves_per_group < 1 || waves_per_group > kEngineMaxGroupWaves)
         return hipErrorInvalidValue;
     (void)hipGetLastError();
     hipLaunchKernelGGL(gf_engine, dim3(groups), dim3(64 * waves_per_group), 0, stream, ring_dev, start, epoch,
-                       idle_ticks);
+                       idle_ticks, poll_gap_ticks);
     return hipGetLastError();
 }
 

@@ -106,8 +106,10 @@ struct EngineRing {
 // its next call.  Each workgroup leaves when that slot's stop word reaches
 // its epoch or after `idle_ticks` of the 100 MHz realtime counter without a
 // call, and records `epoch` in its `gone` word.
+// poll_gap_ticks > 0: two doorbell reads in flight, the second issued that
+// many ticks after the first (pipelined polls); 0: one read per round trip.
 hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
-                         uint64_t idle_ticks, hipStream_t stream);
+                         uint64_t idle_ticks, uint32_t poll_gap_ticks, hipStream_t stream);
 
 // Launch tuning knobs (read from the environment once).
 struct LaunchTuning {

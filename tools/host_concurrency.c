@@ -119,6 +119,7 @@ int main(int argc, char** argv) {
     if (getenv("HL_CO_RUNNING")) rs_tune("host_coalesce_running", atoi(getenv("HL_CO_RUNNING")));
     if (getenv("HL_ENGINE_IDLE")) rs_tune("host_engine_idle_us", atoi(getenv("HL_ENGINE_IDLE")));
     if (getenv("HL_ENGINE_YIELD")) rs_tune("host_engine_yield_us", atoi(getenv("HL_ENGINE_YIELD")));
+    if (getenv("HL_ENGINE_POLL_GAP")) rs_tune("host_engine_poll_gap", atoi(getenv("HL_ENGINE_POLL_GAP")));
     if (getenv("HL_ENGINE_WG_UNITS")) rs_tune("host_engine_wg_units", atoi(getenv("HL_ENGINE_WG_UNITS")));
     if (getenv("HL_ENGINE_DIRECT")) rs_tune("host_engine_direct", atoi(getenv("HL_ENGINE_DIRECT")));
     if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
