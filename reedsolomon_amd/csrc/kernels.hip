@@ -1249,7 +1249,12 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     // profiles/r02/ab_jit.log)
     if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= kJitMinRows && a.rows <= kJitMaxRows &&
         (!a.accumulate || a.cols >= kJitMinAccCols)) {
-        const int jbs = bs_block_for(a) == 256 ? 256 : 64;
+        // 256-lane workgroups from 24 columns on whatever the layout (40+8
+        // Reconst of 8: 5.56-5.61 vs 4.98 TB/s, 24+8: 5.68 vs 5.29; 20+12
+        // Reconst of 12 5.83 vs 5.92 and 16+8 Encode 5.70-5.99 vs 5.90-6.02
+        // stay better at 64; profiles/r02/ab_jit_wide2.log, ab_jit_ao.log,
+        // ab_jit_pf.log), else the build-time kernels' per-layout rule
+        const int jbs = (bs_block_for(a) == 256 || (tuning().bs_block == 0 && a.cols >= 24)) ? 256 : 64;
         const uint64_t bytes = a.body * static_cast<uint64_t>(a.nstripes) * static_cast<uint64_t>(a.rows + a.cols);
         if (hipFunction_t f = jit_bitslice_for(a, jbs, bytes)) {
             a.units_per_chunk = jbs;
