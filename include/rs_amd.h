@@ -403,7 +403,9 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * compile on the launching thread | 0 = off), "jit_min_launches" (background
  * mode compiles a matrix from its n-th launch on; default 2: one-off erasure
  * patterns are never compiled), "jit_min_bytes" (... and once its launches
- * moved this many bytes; default 8 MiB), "jit_pf" (columns loaded ahead in
+ * moved this many bytes; default 8 MiB), "jit_min_acc_cols" (XOR-accumulate
+ * products over fewer columns stay on the table kernels; default 1),
+ * "jit_pf" (columns loaded ahead in
  * the compiled kernels, 1..6, default 3),
  * "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns

@@ -54,6 +54,7 @@ int g_jit_mode = [] {
 }();
 uint64_t g_jit_min_bytes = uint64_t{8} << 20;
 int g_jit_min_launches = 2;
+int g_jit_min_acc_cols = kJitMinAccCols;
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 
 namespace {
@@ -135,14 +136,17 @@ __device__ __forceinline__ void rs_bs_body(const MatmulArgs& a) {
             w[2 * k + 1] = v.y;
         }
     };
-    auto store = [&](int r, u32 (&o)[8]) {
+    // accumulate mode: the old output bytes are loaded up front (fetch_out,
+    // with the first columns) and XORed in after the back transpose
+    auto fetch_out = [&](int r, u32 (&w)[8]) { fetch(RSJ_COLS + r, w); };
+    auto store = [&](int r, u32 (&o)[8], const u32 (&old)[8]) {
         bs_transpose8(o);
         const int v = RSJ_COLS + r;
         g_u8* q = (g_u8*)a.ptr[v] + (i64)s * a.ss[a.sid[v] & 3];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             u32x2 x = {o[2 * k], o[2 * k + 1]};
-            if (RSJ_ACC) x ^= ld8(q, off + (u32)(k * 8 * BS), nbytes);
+            if (RSJ_ACC) x ^= u32x2{old[2 * k], old[2 * k + 1]};
             st8(q, off + (u32)(k * 8 * BS), nbytes, x);
         }
     };
@@ -155,7 +159,7 @@ extern "C" __global__ __launch_bounds__(256) void rs_bs_jit_256(const MatmulArgs
 // The network for one matrix: the statements of BsNet<d, p>::run in
 // bitslice_gen.inc, for this matrix (same construction as
 // tools/gen_bitslice.py emit()).
-std::string network(const uint8_t* mat, int rows, int cols) {
+std::string network(const uint8_t* mat, int rows, int cols, bool acc) {
     const int kPF = g_jit_pf;
     std::string o;
     char buf[160];
@@ -182,6 +186,8 @@ std::string network(const uint8_t* mat, int rows, int cols) {
         line("    u32 N%d[8];", k);
         line("    fetch(%d, N%d);", k, k);
     }
+    line("    u32 O[%d][8];", acc ? rows : 1);
+    if (acc) line("    for (int r = 0; r < %d; ++r) fetch_out(r, O[r]);", rows);
     for (int c = 0; c < cols; ++c) {
         line("    {");
         line("        u32 P[8];");
@@ -239,7 +245,7 @@ std::string network(const uint8_t* mat, int rows, int cols) {
         line("        for (int i = 0; i < 8; ++i) asm volatile(\"\" : \"+v\"(A[r][i]));");
         line("    __builtin_amdgcn_sched_barrier(0);");
     }
-    line("    for (int r = 0; r < %d; ++r) store(r, A[r]);", rows);
+    line("    for (int r = 0; r < %d; ++r) store(r, A[r], O[%s]);", rows, acc ? "r" : "0");
 #undef line
     return o;
 }
@@ -384,7 +390,7 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
                     std::string(accumulate ? "1" : "0") + "\n";
     std::string pre(kPrelude);
     const size_t at = pre.find("RSJ_NETWORK");
-    s += pre.substr(0, at) + "\n" + network(mat, rows, cols) + pre.substr(at + std::strlen("RSJ_NETWORK"));
+    s += pre.substr(0, at) + "\n" + network(mat, rows, cols, accumulate) + pre.substr(at + std::strlen("RSJ_NETWORK"));
     // the kernel's argument layout must equal the host's
     s += "static_assert(sizeof(MatmulArgs) == " + std::to_string(sizeof(MatmulArgs)) + ", \"MatmulArgs size\");\n";
     s += "static_assert(__builtin_offsetof(MatmulArgs, ptr) == " + std::to_string(offsetof(MatmulArgs, ptr)) +

@@ -15,7 +15,13 @@ namespace rsamd {
 // 9-16 rows: 138-221 VGPRs, no scratch (16 x 16: 2 waves/SIMD); the perm-table
 // kernels run those in row groups of 8 that re-read every input
 constexpr int kJitMinRows = 5, kJitMaxRows = 16, kJitMaxCols = 64;
-constexpr int kJitMinAccCols = 8;  // XOR-accumulate launches (Update / Replace) with fewer columns are not compiled
+// XOR-accumulate launches (Update / Replace) with fewer columns are not
+// compiled: 1 = every one (with the old outputs loaded up front the compiled
+// kernels measured 10+8 Update 6.08 vs 5.73 TB/s, Replace of 3 rows 6.13 vs
+// 5.60, 16+8 Replace 6.16 vs 6.09, 16+8 Update 6.07 vs 6.23;
+// profiles/r02/ab_jit_acc.log)
+constexpr int kJitMinAccCols = 1;
+extern int g_jit_min_acc_cols;     // rs_tune("jit_min_acc_cols"), default kJitMinAccCols
 
 // rs_tune("jit", 0 | 1 | 2): off / compile in the background on first sight
 // and launch the perm-table kernels until the code is ready (default) /

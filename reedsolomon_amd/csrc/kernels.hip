@@ -1244,11 +1244,9 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     }
     // 5-16 output rows over a run-time matrix: the bit-sliced network compiled
     // for this matrix (jit.cpp), once it is ready
-    // (XOR-accumulate launches over few columns stay on the perm-table kernels:
-    // 10+8 Update 5.74 vs 5.20 TB/s, Replace of 3 rows 5.62 vs 5.11 compiled,
-    // profiles/r02/ab_jit.log)
+    // (XOR-accumulate launches from jit_min_acc_cols columns on: jit.hpp)
     if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= kJitMinRows && a.rows <= kJitMaxRows &&
-        (!a.accumulate || a.cols >= kJitMinAccCols)) {
+        (!a.accumulate || a.cols >= g_jit_min_acc_cols)) {
         // 256-lane workgroups from 24 columns on whatever the layout (40+8
         // Reconst of 8: 5.56-5.61 vs 4.98 TB/s, 24+8: 5.68 vs 5.29; 20+12
         // Reconst of 12 5.83 vs 5.92 and 16+8 Encode 5.70-5.99 vs 5.90-6.02
