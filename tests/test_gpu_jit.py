@@ -1,6 +1,6 @@
-"""Run-time compiled bit-sliced kernels (jit.cpp): products with 5-8 output
+"""Run-time compiled bit-sliced kernels (jit.cpp): products with 5-16 output
 rows over matrices known only at run time — the primitive (rs_gf_matmul_batch,
-gmu.go:4-9 / encodePart rs.go:175-203), Reconst of 5-8 lost vectors
+gmu.go:4-9 / encodePart rs.go:175-203), Reconst of 5-16 lost vectors
 (rs.go:221-380), Update / Replace with 8 parity rows (rs.go:424-570) and the
 Encode of codes without a build-time network (matrix.go:37-54) — compared
 byte-for-byte with the CPU oracle.  rs_tune("jit", 2) compiles on the
@@ -72,7 +72,7 @@ def test_jit_matmul_vs_oracle(rslib, orc, torch_dev, jit_sync, rows, cols):
                                       (20, 12, list(range(0, 24, 2))), (16, 16, list(range(16))),
                                       (40, 8, [1, 5, 9, 13, 17, 21, 33, 45])])
 def test_jit_reconst_5_to_8_lost(rslib, orc, torch_dev, jit_sync, d, p, lost):
-    """Reconst of 5-8 lost vectors (data and parity mixed) on a batch: the
+    """Reconst of 5-16 lost vectors (data and parity mixed) on a batch: the
     rebuilt stripes equal the encoded originals, on both layouts."""
     torch = torch_dev
     rng = np.random.default_rng(d * 1000 + sum(lost))
