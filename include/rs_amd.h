@@ -405,6 +405,8 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * patterns are never compiled), "jit_min_bytes" (... and once its launches
  * moved this many bytes; default 8 MiB), "jit_min_acc_cols" (XOR-accumulate
  * products over fewer columns stay on the table kernels; default 1),
+ * "jit_min_rows" (launches with fewer output rows stay on the table kernels;
+ * default 5),
  * "jit_pf" (columns loaded ahead in
  * the compiled kernels, 1..6, default 3),
  * "table_registry_max" (distinct coefficient matrices

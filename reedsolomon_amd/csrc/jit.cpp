@@ -54,6 +54,7 @@ int g_jit_mode = [] {
 }();
 uint64_t g_jit_min_bytes = uint64_t{8} << 20;
 int g_jit_min_launches = 2;
+int g_jit_min_rows = kJitMinRows;
 int g_jit_min_acc_cols = kJitMinAccCols;
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 
@@ -423,7 +424,7 @@ void jit_count_launch() { jit().launches.fetch_add(1, std::memory_order_relaxed)
 
 // mode: 1 background after recurrence, 2 compile on this thread, 3 queue now
 static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int mode) {
-    if (!mode || !a.host_mat || a.rows < kJitMinRows || a.rows > kJitMaxRows || a.cols < 1 ||
+    if (!mode || !a.host_mat || a.rows < 1 || a.rows > kJitMaxRows || a.cols < 1 ||
         a.cols > kJitMaxCols)
         return nullptr;
     int dev = 0;

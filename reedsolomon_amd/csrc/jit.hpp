@@ -21,7 +21,8 @@ constexpr int kJitMinRows = 5, kJitMaxRows = 16, kJitMaxCols = 64;
 // 5.60, 16+8 Replace 6.16 vs 6.09, 16+8 Update 6.07 vs 6.23;
 // profiles/r02/ab_jit_acc.log)
 constexpr int kJitMinAccCols = 1;
-extern int g_jit_min_acc_cols;     // rs_tune("jit_min_acc_cols"), default kJitMinAccCols
+extern int g_jit_min_acc_cols;
+extern int g_jit_min_rows;         // rs_tune("jit_min_rows"): launches with fewer output rows stay on the table kernels     // rs_tune("jit_min_acc_cols"), default kJitMinAccCols
 
 // rs_tune("jit", 0 | 1 | 2): off / compile in the background on first sight
 // and launch the perm-table kernels until the code is ready (default) /

@@ -1245,7 +1245,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     // 5-16 output rows over a run-time matrix: the bit-sliced network compiled
     // for this matrix (jit.cpp), once it is ready
     // (XOR-accumulate launches from jit_min_acc_cols columns on: jit.hpp)
-    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= kJitMinRows && a.rows <= kJitMaxRows &&
+    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= g_jit_min_rows && a.rows <= kJitMaxRows &&
         (!a.accumulate || a.cols >= g_jit_min_acc_cols)) {
         // 256-lane workgroups from 24 columns on whatever the layout (40+8
         // Reconst of 8: 5.56-5.61 vs 4.98 TB/s, 24+8: 5.68 vs 5.29; 20+12
