@@ -362,12 +362,16 @@ RS_API int rs_jit_prepare(rs_t* rs, const uint8_t* mat, int rows, int cols, int 
 RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms);
 
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
- * tuned values): "max_grid", "vpt", "nt_store", "var", "lds_pad",
- * "lane_bytes" (8 default | 16), "block8" (lanes
+ * tuned values; every setting computes the same bytes, which
+ * tests/test_gpu_tune_sweep.py checks against the oracle): "max_grid", "vpt",
+ * "nt_store", "lds_pad", "lane_bytes" (8 default | 16), "block8" (lanes
  * per workgroup of the 8-byte-lane kernels: 128 default | 256), "bitslice"
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
  * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "wide_block" (128 | 256),
+ * "wide_single_pass" (1 default: products with more than 8 output rows and
+ * no compiled network read every input once, all rows of a chunk in one
+ * workgroup | 0: the looped kernel in row groups of 8, for A/B),
  * "host_engine" (1 default: small synchronous host calls, coalesced or
  * alone, are served by a resident kernel through a doorbell in host memory |
  * 0: one launch + stream sync per call), "host_engine_waves" (1..64
@@ -385,7 +389,10 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * "host_engine_yield_us" (a caller waiting longer than this on its engine
  * call yields its core between polls; 0 default = always spin),
  * "host_engine_idle_us" (the engine leaves after this long without a call,
- * default 200), "host_engine_max_bytes" (larger batches launch; default 1 MiB),
+ * default 200), "host_engine_life_us" (and once it has run this long, even
+ * while calls keep coming: a device-wide synchronisation waits at most about
+ * this long for it; default 4000), "host_engine_max_bytes" (larger batches
+ * launch; default 1 MiB),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;
@@ -411,7 +418,10 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * the compiled kernels, 1..6, default 3),
  * "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns
- * RS_OK, or RS_ERR_INVAL for an unknown name. */
+ * RS_OK, or RS_ERR_INVAL for an unknown name.  The code-shape experiments of
+ * earlier rounds (the knob named var, env RSAMD_VAR; some are XOR-only
+ * diagnostics) exist only in the separate experiments build librsamd_exp.so:
+ * this library returns RS_ERR_INVAL for var and ignores RSAMD_VAR. */
 RS_API int rs_tune(const char* name, int value);
 
 /* The calling thread's last RS_ERR_DEVICE cause ("where: hipErrorName (code)"),

@@ -12,7 +12,9 @@ import threading
 
 from . import build as _build
 
-LIB_PATH = _build.LIB
+# RSAMD_LIB_VARIANT=experiments loads librsamd_exp.so, the build with the A/B
+# code-shape experiments (tools/ab.py, tools/sweep.sh); never the product path.
+LIB_PATH = _build.LIB_EXP if os.environ.get("RSAMD_LIB_VARIANT") == "experiments" else _build.LIB
 
 _lock = threading.Lock()
 _lib = None

@@ -146,11 +146,27 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
     }
     const size_t main_dw = static_cast<size_t>(cols) * rows_pad * 5;
     const size_t img_dw = rows <= 4 ? rup(cols, 4) * 20 : 0;
-    std::vector<uint32_t> host(main_dw + img_dw, 0);
+    // wide kernels (rows > 8): [column pair][rows_pad][12] dwords, per (pair,
+    // row) T0a T2a T0b T2b | T1a T3a T1b T3b | T4a T4b 0 0 (the dwords v_perm
+    // takes from VGPRs first, as two 64-bit pairs); an odd last column's
+    // partner has zero tables
+    const size_t wide_dw = rows > 8 ? static_cast<size_t>((cols + 1) / 2) * rows_pad * 12 : 0;
+    std::vector<uint32_t> host(main_dw + img_dw + wide_dw, 0);
     for (int c = 0; c < cols; ++c)
         for (int r = 0; r < rows; ++r) {
-            perm_table(mat[static_cast<size_t>(r) * cols + c], &host[(static_cast<size_t>(c) * rows_pad + r) * 5]);
-            if (img_dw) perm_table(mat[static_cast<size_t>(r) * cols + c], &host[main_dw + static_cast<size_t>(c) * 20 + r * 5]);
+            uint32_t t[5];
+            perm_table(mat[static_cast<size_t>(r) * cols + c], t);
+            std::memcpy(&host[(static_cast<size_t>(c) * rows_pad + r) * 5], t, sizeof t);
+            if (img_dw) std::memcpy(&host[main_dw + static_cast<size_t>(c) * 20 + r * 5], t, sizeof t);
+            if (wide_dw) {
+                uint32_t* w = &host[main_dw + img_dw + (static_cast<size_t>(c / 2) * rows_pad + r) * 12];
+                const int h = c & 1;
+                w[2 * h] = t[0];
+                w[2 * h + 1] = t[2];
+                w[4 + 2 * h] = t[1];
+                w[5 + 2 * h] = t[3];
+                w[8 + h] = t[4];
+            }
         }
     uint32_t* dptr = nullptr;
     if (hipMalloc(&dptr, host.size() * 4) != hipSuccess) return RS_ERR_NOMEM;
@@ -179,6 +195,7 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     int rc = get_tables(rs, mat, rows, cols, &a.tables, &a.rows_pad);
     if (rc) return rc;
     a.img4 = rows <= 4 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
+    a.wide = rows > 8 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
     a.host_mat = mat;
     a.rows = rows;
     a.cols = cols;
@@ -511,7 +528,9 @@ int rs_tune(const char* name, int value) {
         if (n == "max_grid") t.max_grid = value;
         else if (n == "vpt") t.vpt = value == 2 ? 2 : 1;
         else if (n == "nt_store") t.nt_store = value;
+#ifdef RSAMD_EXPERIMENTS  // code-shape experiments: librsamd_exp.so only (the product has no "var")
         else if (n == "var") t.var = value;
+#endif
         else if (n == "lds_pad") t.lds_pad = value;
         else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
         else if (n == "block8") t.block8 = value == 128 ? 128 : 256;
@@ -524,6 +543,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
+        else if (n == "wide_single_pass") t.wide_single_pass = value ? 1 : 0;
         else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
         else if (n == "host_engine") g_engine = value ? 1 : 0;
         else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxGroups ? kEngineMaxGroups : value;
@@ -533,6 +553,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_engine_poll_gap") g_engine_poll_gap = value < 0 ? 0 : value > 1000 ? 1000 : value;
         else if (n == "host_engine_yield_us") g_engine_yield_us = value < 0 ? 0 : value;
         else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
+        else if (n == "host_engine_life_us") g_engine_life_us = value < 100 ? 100 : value > 1000000 ? 1000000 : value;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);

@@ -179,6 +179,8 @@ struct rs_codec {
     int eng_waves = 0;       // the running instance's workgroups
     int eng_group_waves = 0; // ... and waves per workgroup
     int eng_idle_us = 0;     // the running instance's idle window
+    int eng_life_us = 0;     // ... and its maximum life
+    bool eng_failed = false; // retired after a call timed out (calls take the launch paths)
     int eng_poll_gap = 0;    // ... and its doorbell poll gap
     uint64_t eng_seq = 0;
     int eng_next_wg = 0;     // first workgroup of the next call
@@ -212,8 +214,8 @@ int engine_call_addr(rs_t* rs, const uint8_t* mat, int rows, int cols, const uin
 bool engine_accepts(int rows, int cols, size_t bytes);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
-extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_wg_units, g_engine_yield_us,
-    g_engine_poll_gap;
+extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_life_us, g_engine_wg_units,
+    g_engine_yield_us, g_engine_poll_gap;
 extern size_t g_engine_max_bytes;
 
 // Diagnostics (env RSAMD_ENGINE_TRACE): where the time of the synchronous

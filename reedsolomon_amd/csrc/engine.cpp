@@ -17,14 +17,18 @@
 //         workgroup's done word holds the new value.
 //   kernel: each workgroup polls the header line, computes its share straight
 //         over the caller's pinned staging buffer, writes its done word.
-// The kernel leaves on the stop word or after host_engine_idle_us without a
+// The kernel leaves on the stop word, after host_engine_idle_us without a
 // doorbell (so it never outlives its callers, and never holds a hardware
-// queue that other streams share for long).  The host rings a running engine
-// only within half that window of its last call; otherwise it stops the old
-// instance and launches a new one.  If an instance is found gone while a call
-// is pending, a new one resumes it: workgroups that already finished the call
-// (done word) skip it, so no unit is computed twice (Update / Replace XOR
-// into their outputs).
+// queue that other streams share for long), or once it has run
+// host_engine_life_us even while calls keep coming (a device-wide
+// synchronisation - hipDeviceSynchronize, hipFree, torch.cuda.synchronize -
+// waits for a running instance, so that wait is bounded).  The host does not
+// predict either exit: it rings the running instance, and a workgroup that
+// left before seeing the call shows up in its gone word; the host (at the
+// next call, or a waiter) then stops what is left of the instance and
+// launches a new one, which resumes the pending calls: workgroups that
+// already finished a call (done word) skip it, so no unit is computed twice
+// (Update / Replace XOR into their outputs).
 #include <immintrin.h>
 
 #include <cstdio>
@@ -46,6 +50,10 @@ int g_engine = [] {                     // rs_tune("host_engine", 0 | 1); env RS
 int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..64): workgroups (one polling wave each)
 int g_engine_group_waves = 8;           // rs_tune("host_engine_group_waves", 1..8): waves per workgroup
 int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
+// Longest life of one instance (rs_tune("host_engine_life_us")): a relaunch
+// costs a stream sync and a launch (~20-30 us of stalled calls), so 4 ms
+// keeps that under 1 % of a busy engine's time.
+int g_engine_life_us = 4000;
 // Doorbell polls: 0 = one read per PCIe round trip; n = a second read in
 // flight, issued n ticks (10 ns) after the first; rs_tune("host_engine_poll_gap")
 int g_engine_poll_gap = [] {  // (env RSAMD_ENGINE_POLL_GAP)
@@ -191,11 +199,22 @@ static hipStream_t engine_stream() {
     return nullptr;
 }
 
+// Caller holds eng_mu; no instance is running.
 static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     const uint64_t idle_ticks = static_cast<uint64_t>(g_engine_idle_us) * 100;  // 100 MHz realtime counter
+    const uint64_t life_ticks = static_cast<uint64_t>(g_engine_life_us) * 100;
     const uint64_t epoch = rs->eng_epoch + 1;
     Region region("engine launch");
-    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks,
+    // Every workgroup of the new instance starts after call `start`.  A
+    // workgroup the previous instance did not have (host_engine_waves raised)
+    // holds a stale done word: bring it to `start` here, so the slot-reuse
+    // wait and a later relaunch (min over done words) never wait on a call
+    // that workgroup will never see.  No instance runs: the host is the only
+    // writer.
+    for (int w = 0; w < waves; ++w)
+        if (__atomic_load_n(&rs->eng_ring->done[w], __ATOMIC_ACQUIRE) < start)
+            __atomic_store_n(&rs->eng_ring->done[w], start, __ATOMIC_RELEASE);
+    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks, life_ticks,
                                 static_cast<uint32_t>(g_engine_poll_gap), rs->eng_stream),
                   "engine launch"));
     if (g_engine_trace) std::fprintf(stderr, "engine launch: epoch %llu start %llu\n",
@@ -205,6 +224,7 @@ static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     rs->eng_waves = waves;
     rs->eng_group_waves = group_waves;
     rs->eng_idle_us = g_engine_idle_us;
+    rs->eng_life_us = g_engine_life_us;
     rs->eng_poll_gap = g_engine_poll_gap;
     rs->eng_launches.fetch_add(1, std::memory_order_relaxed);
     return RS_OK;
@@ -249,6 +269,21 @@ static bool all_done(const EngineRing* r, int waves, int w0, int n, uint64_t seq
     return true;
 }
 
+// A call not complete after 10 s.  The instance is stopped before the error
+// is returned (workgroups serve the calls already rung before they read the
+// stop word, and the stream is synchronised), so once the caller has the
+// error the GPU can no longer write into the buffers it hands back (pinned
+// pool blocks, registered caller memory).  The handle's engine is then
+// retired: its later calls take the launch paths.
+static int engine_timeout(rs_t* rs, bool locked) {
+    std::unique_lock<std::mutex> lk(rs->eng_mu, std::defer_lock);
+    if (!locked) lk.lock();
+    engine_dump(rs, "no completion in 10 s; stopping the instance and retiring the handle's engine");
+    engine_stop(rs);
+    rs->eng_failed = true;
+    return dev_fail(hipErrorLaunchTimeOut, "engine call (no completion in 10 s)");
+}
+
 // Wait until workgroups [w0, w0 + n) completed call `seq`: spin (calls take
 // ~10 us), relaunching the engine if a workgroup left before the call reached
 // it.  `locked`: the caller holds eng_mu (slot reuse wait); otherwise it is
@@ -282,10 +317,7 @@ static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool lo
         // left the runtime's teardown deadlocked at process exit; a faulting
         // instance ends the process through the runtime's fault handler)
         const auto now = std::chrono::steady_clock::now();
-        if (now - t0 > std::chrono::seconds(10)) {
-            if (g_engine_trace) engine_dump(rs, "no completion in 10 s");
-            return dev_fail(hipErrorLaunchTimeOut, "engine call (no completion in 10 s)");
-        }
+        if (now - t0 > std::chrono::seconds(10)) return engine_timeout(rs, locked);
     }
     return RS_OK;
 }
@@ -298,6 +330,7 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
         Region region("engine submit lock");
         lk.lock();
     }
+    if (rs->eng_failed) return RS_ERR_INVAL;  // retired after a timeout: the caller launches instead
     if (!rs->eng_ring) {
         EngineRing* h = ring_get(rs->device);
         if (!h) return RS_ERR_NOMEM;
@@ -328,7 +361,7 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
                                                                      : g_engine_group_waves;
     if (rs->eng_running &&
         (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us ||
-         rs->eng_poll_gap != g_engine_poll_gap))
+         rs->eng_life_us != g_engine_life_us || rs->eng_poll_gap != g_engine_poll_gap))
         engine_stop(rs);  // new shape: the old instance must be gone before the next one reads done words
     RS_TRY(engine_relaunch_if_gone(rs));
     if (!rs->eng_running) RS_TRY(engine_launch(rs, waves, gwaves, rs->eng_seq));

@@ -84,7 +84,7 @@ typedef long long i64;
 typedef u32 u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) u8 g_u8;
 struct MatmulArgs {
-    const u32* tables; const u32* img4; const u8* host_mat;
+    const u32* tables; const u32* img4; const u32* wide; const u8* host_mat;
     int rows, cols, rows_pad; int nstripes; int accumulate; int units_per_chunk; int nt_store;
     u64 len; u64 body; u64 tail_start; i64 ss[4]; const int* stripe_ids;
     i64 chunks_per_stripe; i64 total_chunks; int cps_shift;

@@ -36,6 +36,7 @@
 namespace rsamd {
 
 constexpr int kBlock = 256;
+constexpr int kWideRows = 16;  // output rows per wave of the wide kernels
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;        // global (HBM) 16-byte word
@@ -51,8 +52,11 @@ LaunchTuning& tuning() {
         if (x.vpt != 2) x.vpt = 1;
         const char* n = std::getenv("RSAMD_NT_STORE");
         x.nt_store = n ? std::atoi(n) : 1;
+        x.var = -1;
+#ifdef RSAMD_EXPERIMENTS  // code-shape experiments exist only in librsamd_exp.so (tools/ab.py)
         const char* e = std::getenv("RSAMD_VAR");
         x.var = e ? std::atoi(e) : -1;
+#endif
         const char* l = std::getenv("RSAMD_LDS_PAD");
         x.lds_pad = l ? std::atoi(l) : 0;
         const char* lb = std::getenv("RSAMD_LANE_BYTES");
@@ -63,6 +67,7 @@ LaunchTuning& tuning() {
         x.bitslice = (bsl && std::atoi(bsl) == 0) ? 0 : 1;
         x.bs_block = 0;
         x.wide_block = 256;
+        x.wide_single_pass = 1;
         return x;
     }();
     return t;
@@ -105,8 +110,16 @@ __device__ __forceinline__ g_u8* out_ptr(const MatmulArgs& a, int cols, int row,
 //   VPT  16-byte units per lane per chunk
 //   VAR  code-shape flags (kVar* below); the default is kVarDefault
 // ---------------------------------------------------------------------------
+// kVarXorOnly is a DIAGNOSTIC (acc ^= x instead of the GF product: the memory
+// ceiling of the access pattern).  It exists only in the experiments build
+// (-DRSAMD_EXPERIMENTS, librsamd_exp.so); in the product library the flag is 0,
+// so no instantiation can compute anything but the GF product.
+#ifdef RSAMD_EXPERIMENTS
+constexpr int kVarXorOnly = 1;
+#else
+constexpr int kVarXorOnly = 0;
+#endif
 enum : int {
-    kVarXorOnly = 1,     // DIAGNOSTIC: acc ^= x instead of the GF product (memory ceiling of the pattern)
     kVarNtLoad = 2,      // non-temporal input loads
     kVarSingleTab = 4,   // no LDS table prefetch across columns (fewer VGPRs)
     kVarBitop3 = 8,      // explicit v_bitop3 (xor3) accumulation
@@ -526,6 +539,147 @@ __global__ __launch_bounds__(BS) void gf_matmul_multi(const MatmulArgs a, const 
 }
 
 // ---------------------------------------------------------------------------
+// Wide products: more than 8 output rows (Encode of wide codes such as 64+64
+// or 200+56, Reconst of 9-128 lost vectors, Update / Replace of wide codes)
+// over a run-time matrix, in ONE pass: every input byte is read from HBM once
+// whatever the row count (the looped kernel re-reads every input once per
+// 8-row group).
+//
+// A workgroup is NW waves over the same 1 KiB of every vector (lane t owns
+// bytes [16t, 16t+16) of the chunk in each); wave w computes up to 16 rows,
+// [row0 + 16w, row0 + 16w + 16).  With NW > 1 the waves of a workgroup load
+// the same input lines (cached loads: the first fetch goes to HBM, the others
+// hit the CU's L1 / the XCD's L2), so HBM still moves each input once.  The
+// accumulators of the wave's rows stay in VGPRs (16 B per row and lane).
+//
+// Coefficient tables come from the `wide` image ([column pair][rows_pad][12]
+// dwords, get_tables) through scalar loads: the matrix is the same for every
+// lane.  v_perm_b32 may read one SGPR (gfx9 constant-bus limit), so of each
+// column's perm pool (T0, T1) / (T2, T3) the dwords T0 and T2 come into VGPRs
+// with one v_mov_b64 per (row, column) and T1 / T3 / T4 stay scalar.
+// Columns are taken in pairs so the three partial products of two columns
+// fold into three xor3 per dword (4.5 VALU per (row, column, dword) without a
+// carried term), and the next pair's loads are in flight while this pair is
+// computed.  An odd last column is paired with itself against zero tables.
+// A wave's rows are computed in groups of 4 whose tables are read together
+// (one scalar-load wait per group); the body is specialised for the wave's
+// group count, so rows past the matrix cost at most 3 rows of zero tables.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(4))) const uint32_t c_u32;  // constant address space: scalar loads
+typedef __attribute__((address_space(4))) const uint64_t c_u64;
+
+template <int R, int LAUX, bool ACC>
+__device__ __forceinline__ void wide_body(const MatmulArgs& a, int s, int r0, int nr, uint32_t off) {
+    const uint32_t nbytes = static_cast<uint32_t>(a.body);
+    const int cols = a.cols;
+    uint32_t acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (ACC && r < nr) {
+            const u32x4 o = load16<0, 4>(out_ptr(a, cols, r0 + r, s), off, nbytes, false);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] = o[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] = 0;
+        }
+    }
+    auto load_col = [&](int c) { return load16<LAUX, 4>(in_ptr(a, c, s), off, nbytes, false); };
+    const int npairs = (cols + 1) >> 1;
+    u32x4 xa = load_col(0), xb = load_col(cols > 1 ? 1 : 0);
+    c_u32* tab = reinterpret_cast<c_u32*>(reinterpret_cast<uint64_t>(a.wide)) + static_cast<size_t>(r0) * 12;
+    for (int p = 0; p < npairs; ++p) {
+        // next pair's loads first: in flight while this pair is computed
+        const int cn = 2 * p + 2;
+        u32x4 na = xa, nb = xb;
+        if (cn < cols) {
+            na = load_col(cn);
+            nb = load_col(cn + 1 < cols ? cn + 1 : cn);
+        }
+        // bit groups {0-2}, {3-5}, {6-7} of both columns, shared by every row
+        uint32_t g[2][3][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const u32x4 x = h ? xb : xa;
+#pragma unroll
+            for (int q = 0; q < 4; q += 2) {
+                const uint64_t X = (static_cast<uint64_t>(x[q + 1]) << 32) | x[q];
+                uint64_t Y3, Y6;
+                asm("v_lshrrev_b64 %0, 3, %1" : "=v"(Y3) : "v"(X));
+                asm("v_lshrrev_b64 %0, 6, %1" : "=v"(Y6) : "v"(X));
+                g[h][0][q] = x[q] & 0x07070707u;
+                g[h][0][q + 1] = x[q + 1] & 0x07070707u;
+                g[h][1][q] = static_cast<uint32_t>(Y3) & 0x07070707u;
+                g[h][1][q + 1] = static_cast<uint32_t>(Y3 >> 32) & 0x07070707u;
+                g[h][2][q] = static_cast<uint32_t>(Y6) & 0x03030303u;
+                g[h][2][q + 1] = static_cast<uint32_t>(Y6 >> 32) & 0x03030303u;
+            }
+        }
+        c_u32* tp = tab + static_cast<size_t>(p) * a.rows_pad * 12;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            c_u32* t = tp + r * 12;
+            const uint64_t sa = *reinterpret_cast<c_u64*>(t), sb = *reinterpret_cast<c_u64*>(t + 2);
+            uint64_t va, vb;  // (T0, T2) of columns a / b into VGPRs: v_perm reads one SGPR
+            asm("v_mov_b64 %0, %1" : "=v"(va) : "s"(sa));
+            asm("v_mov_b64 %0, %1" : "=v"(vb) : "s"(sb));
+            const uint32_t t0a = static_cast<uint32_t>(va), t2a = static_cast<uint32_t>(va >> 32);
+            const uint32_t t0b = static_cast<uint32_t>(vb), t2b = static_cast<uint32_t>(vb >> 32);
+            const uint32_t t1a = t[4], t3a = t[5], t1b = t[6], t3b = t[7], t4a = t[8], t4b = t[9];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t p0a = __builtin_amdgcn_perm(t1a, t0a, g[0][0][q]);
+                const uint32_t p1a = __builtin_amdgcn_perm(t3a, t2a, g[0][1][q]);
+                const uint32_t p2a = __builtin_amdgcn_perm(t4a, t4a, g[0][2][q]);
+                const uint32_t p0b = __builtin_amdgcn_perm(t1b, t0b, g[1][0][q]);
+                const uint32_t p1b = __builtin_amdgcn_perm(t3b, t2b, g[1][1][q]);
+                const uint32_t p2b = __builtin_amdgcn_perm(t4b, t4b, g[1][2][q]);
+                acc[r][q] = xor3(xor3(xor3(acc[r][q], p0a, p1a), p2a, p0b), p1b, p2b);
+            }
+            // a scheduling fence per 4-row group: its tables are loaded
+            // together, and the next group's loads can issue under its math
+            if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        // pin the running sums per pair (no re-association across pairs)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(acc[r][q]));
+        xa = na;
+        xb = nb;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r < nr) {
+            const u32x4 v = {acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+            store16<kAuxNt, 4>(out_ptr(a, cols, r0 + r, s), off, nbytes, v, true);
+        }
+    }
+}
+
+template <int NW, bool ACC>
+__global__ __launch_bounds__(64 * NW) void gf_matmul_wide(const MatmulArgs a, int row0) {
+    constexpr int kLoadAux = NW > 1 ? 0 : kAuxNt;  // shared lines stay cached; a lone wave streams
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t chunk = blockIdx.x;
+    const uint32_t cps = static_cast<uint32_t>(a.chunks_per_stripe);
+    const uint32_t su = a.cps_shift >= 0 ? (chunk >> a.cps_shift) : chunk / cps;
+    const int s = a.stripe_ids ? a.stripe_ids[su] : static_cast<int>(su);
+    const uint32_t cb = chunk - su * cps;
+    const int r0 = row0 + wave * kWideRows;
+    const int nr = (a.rows - r0) < kWideRows ? (a.rows - r0) : kWideRows;
+    if (nr <= 0) return;  // uniform over the wave (no barrier in this kernel)
+    const uint32_t off = cb * 1024u + lane * 16u;
+    switch ((nr + 3) >> 2) {  // uniform
+        case 1: wide_body<4, kLoadAux, ACC>(a, s, r0, nr, off); break;
+        case 2: wide_body<8, kLoadAux, ACC>(a, s, r0, nr, off); break;
+        case 3: wide_body<12, kLoadAux, ACC>(a, s, r0, nr, off); break;
+        default: wide_body<16, kLoadAux, ACC>(a, s, r0, nr, off); break;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Byte kernel: any alignment, bytes [start, len) of every vector.  One lane
 // per (stripe, 4-byte group); tables are read straight from global memory.
 // ---------------------------------------------------------------------------
@@ -770,7 +924,7 @@ __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t
 }
 
 __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t start, uint64_t epoch,
-                                                 uint64_t idle_ticks, uint32_t poll_gap) {
+                                                 uint64_t idle_ticks, uint64_t life_ticks, uint32_t poll_gap) {
     constexpr int kPollWords = 8 * (1 + kEnginePtrLines);  // a slot's header + address lines
     __shared__ __attribute__((aligned(16))) uint32_t tab[kEngineMaxCols * kEngineMaxRows * 5];
     __shared__ uint64_t s_raw[kPollWords];  // the lines wave 0 saw (s_raw[0] = 0: leave)
@@ -780,6 +934,11 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
     // a relaunch resumes after the last call this workgroup completed
     uint64_t last = uniform_u64(sys_load64(&ring->done[blockIdx.x]));
     last = last > start ? last : start;
+    // bounded lifetime: a device-wide synchronisation (hipDeviceSynchronize,
+    // hipFree, torch.cuda.synchronize) waits for a running instance, so no
+    // instance outlives life_ticks even while calls keep arriving; the host
+    // sees the gone word and relaunches on the next call
+    const uint64_t t_birth = __builtin_amdgcn_s_memrealtime();
     uint32_t tab_have = 0xffffffffu;
     for (;;) {
         uint64_t t_seen = 0;
@@ -804,8 +963,10 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
             };
             // stop word, or no call for idle_ticks: seq stays 0 and every wave leaves
             auto leave = [&](uint64_t x, uint32_t n) {
-                return lane_u64(x, 6) >= epoch ||
-                       ((n & 31) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks);
+                if (lane_u64(x, 6) >= epoch) return true;
+                if ((n & 31) != 0) return false;
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                return now - t0 > idle_ticks || now - t_birth > life_ticks;
             };
             if (poll_gap == 0) {  // one read per round trip
                 for (uint32_t n = 1;; ++n) {
@@ -907,12 +1068,12 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
 }
 
 hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
-                         uint64_t idle_ticks, uint32_t poll_gap_ticks, hipStream_t stream) {
+                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t poll_gap_ticks, hipStream_t stream) {
     if (groups < 1 || groups > kEngineMaxGroups || waves_per_group < 1 || waves_per_group > kEngineMaxGroupWaves)
         return hipErrorInvalidValue;
     (void)hipGetLastError();
     hipLaunchKernelGGL(gf_engine, dim3(groups), dim3(64 * waves_per_group), 0, stream, ring_dev, start, epoch,
-                       idle_ticks, poll_gap_ticks);
+                       idle_ticks, life_ticks, poll_gap_ticks);
     return hipGetLastError();
 }
 
@@ -951,8 +1112,16 @@ struct Variant {
     Variant { gf_matmul_vec<10, true, 4, false, 1, VAR, LAUX, SAUX>, 10, 4, 1, true, \
               "gf_matmul_vec<10,true,4,false,1," #VAR "," #LAUX "," #SAUX ">" }
 
-// Experimental code shapes of the 10+4 encode kernel (RSAMD_VAR=<flags>),
-// used by tools/sweep.sh to A/B variants in separate processes.
+// Experimental code shapes of the 10+4 encode kernel (RSAMD_VAR=<flags> /
+// rs_tune("var")), used by tools/ab.py and tools/sweep.sh to A/B variants.
+// Compiled only into the experiments build (librsamd_exp.so,
+// -DRSAMD_EXPERIMENTS): some of them are XOR-only diagnostics whose output is
+// not the GF product, so the product library has no switch that reaches them.
+#ifndef RSAMD_EXPERIMENTS
+static bool pick_experimental(int, int, bool, int, Variant*) { return false; }
+static int exp_var() { return -1; }
+#else
+static int exp_var() { return tuning().var; }
 static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* out) {
     const int var = tuning().var;
     if (var < 0 || acc || cols != 10 || rows <= 2 || rows > 4) return false;
@@ -1033,6 +1202,7 @@ static bool pick_experimental(int rows, int cols, bool acc, int vpt, Variant* ou
     }
 #undef RSAMD_CASE
 }
+#endif  // RSAMD_EXPERIMENTS
 
 static Variant pick_global(int rows, bool acc) {  // global_* ops: vectors >= 2 GiB
     if (!acc) {
@@ -1090,8 +1260,8 @@ static bool pick_one_chunk(int rows, int cols, bool acc, bool lane16, Variant* o
         // the fixed-column 10 / 12 kernels, 1-2 rows and accumulate launches
         // stay on 8-byte units, profiles/r01/ab_lane_generic*.log).  var=201
         // keeps 8-byte units (A/B).
-        const bool wide34 = rows > 2 && rows <= 4 && cols > 4 && tuning().var != 201;
-        if (cols > 4 && (cols <= 8 || tuning().var == 200)) {
+        const bool wide34 = rows > 2 && rows <= 4 && cols > 4 && exp_var() != 201;
+        if (cols > 4 && (cols <= 8 || exp_var() == 200)) {
             if (rows == 1) { *out = RSAMD_VARIANT1(8, false, 1, false, 0); return true; }
             if (rows == 2) { *out = RSAMD_VARIANT1(8, false, 2, false, 0); return true; }
             if (wide34) { *out = RSAMD_VARIANT1_WIDE(8, false, 4, false, 0); return true; }
@@ -1103,7 +1273,7 @@ static bool pick_one_chunk(int rows, int cols, bool acc, bool lane16, Variant* o
         if (rows <= 4) { *out = RSAMD_VARIANT1(4, false, 4, false, 0); return true; }
         if (cols == 10 && rows <= 8) { *out = RSAMD_VARIANT1_WIDE(10, true, 8, false, 0); return true; }
         if (cols == 12 && rows <= 8) { *out = RSAMD_VARIANT1_WIDE(12, true, 8, false, 0); return true; }
-        if (rows <= 8 && cols > 4 && (cols <= 8 || tuning().var == 200)) {
+        if (rows <= 8 && cols > 4 && (cols <= 8 || exp_var() == 200)) {
             *out = RSAMD_VARIANT1_WIDE(8, false, 8, false, 0);
             return true;
         }
@@ -1157,6 +1327,23 @@ const char* vector_kernel_name(int rows, int cols, int accumulate) {
 }
 
 static bool aligned16(uint64_t v) { return (v & 15u) == 0; }
+
+// The wide kernel for `rows` (> 8) output rows: 16 rows per wave, NW waves
+// per workgroup; rows beyond 16*NW take further passes (> 128 rows only).
+using VecKernelRow = void (*)(const MatmulArgs, int);
+static VecKernelRow wide_kernel_for(int rows, bool acc, int* rw, int* nw) {
+#define RSAMD_WIDE(NW)                                                     \
+    do {                                                                   \
+        *rw = kWideRows;                                                   \
+        *nw = NW;                                                          \
+        return acc ? gf_matmul_wide<NW, true> : gf_matmul_wide<NW, false>; \
+    } while (0)
+    if (rows <= 16) RSAMD_WIDE(1);
+    if (rows <= 32) RSAMD_WIDE(2);
+    if (rows <= 64) RSAMD_WIDE(4);
+    RSAMD_WIDE(8);
+#undef RSAMD_WIDE
+}
 
 hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream) {
     if (a.len == 0 || a.nstripes <= 0) return hipSuccess;
@@ -1271,6 +1458,29 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
                 jit_count_launch();
                 a.body = 0;
             }
+        }
+    }
+
+    // More than 8 output rows and no compiled network: the single-pass wide
+    // kernels (every input read once), in passes of NW*RW rows
+    if (a.body && a.body < (uint64_t{1} << 31) && a.rows > 8 && a.wide && tuning().wide_single_pass) {
+        int rw = 16, nw = 1;
+        VecKernelRow fn = wide_kernel_for(a.rows, a.accumulate != 0, &rw, &nw);
+        a.units_per_chunk = 64;  // 16-byte units: 1 KiB of every vector per workgroup
+        a.nt_store = 1;
+        a.chunks_per_stripe = static_cast<int64_t>((a.body + 1023) / 1024);
+        a.total_chunks = a.chunks_per_stripe * a.nstripes;
+        a.cps_shift = -1;
+        for (int sh = 0; sh < 31; ++sh)
+            if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
+        if (a.total_chunks <= 0x7fffffff) {
+            for (int row0 = 0; row0 < a.rows; row0 += rw * nw) {
+                (void)hipGetLastError();
+                hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(a.total_chunks)), dim3(64 * nw), 0, stream, a, row0);
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            a.body = 0;
         }
     }
 

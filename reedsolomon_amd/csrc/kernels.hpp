@@ -22,6 +22,7 @@ constexpr int kMaxPtrs = 260;  // inputs + outputs of one launch (d+p <= 256, Up
 struct MatmulArgs {
     const uint32_t* tables;   // device perm tables, [cols][rows_pad][5] dwords
     const uint32_t* img4;     // the same as a 4-row LDS image [rup(cols, 4)][20] (rows <= 4), or null
+    const uint32_t* wide;     // the same for the wide kernels (rows > 8): [column pair][rows_pad][12], or null
     const uint8_t* host_mat;  // HOST copy of the rows x cols matrix (launch dispatch only; never read on device)
     int rows, cols, rows_pad;
     int nstripes;
@@ -104,12 +105,14 @@ struct EngineRing {
 // `waves_per_group` waves on `stream`; workgroup w serves the calls after
 // max(start, done[w]), in order.  Wave 0 of each workgroup polls the slot of
 // its next call.  Each workgroup leaves when that slot's stop word reaches
-// its epoch or after `idle_ticks` of the 100 MHz realtime counter without a
-// call, and records `epoch` in its `gone` word.
+// its epoch, after `idle_ticks` of the 100 MHz realtime counter without a
+// call, or once it has run `life_ticks` (checked between calls; bounds how
+// long a device-wide synchronisation can wait for the instance), and records
+// `epoch` in its `gone` word.
 // poll_gap_ticks > 0: two doorbell reads in flight, the second issued that
 // many ticks after the first (pipelined polls); 0: one read per round trip.
 hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
-                         uint64_t idle_ticks, uint32_t poll_gap_ticks, hipStream_t stream);
+                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t poll_gap_ticks, hipStream_t stream);
 
 // Launch tuning knobs (read from the environment once).
 struct LaunchTuning {
@@ -123,6 +126,7 @@ struct LaunchTuning {
     int bitslice;     // bit-sliced Encode for the generated fixed generator matrices (1 default | 0)
     int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
+    int wide_single_pass;  // > 8 rows without a compiled network: single-pass wide kernels (1) | row groups of 8 (0)
 };
 LaunchTuning& tuning();
 

@@ -293,6 +293,7 @@ def test_tune_accepts_every_documented_knob(rslib):
         "bad = [n for n in names if L.rs_tune(n.encode(), 1) != 0]\n"
         "assert not bad, bad\n"
         "assert L.rs_tune(b'no_such_knob', 1) == 13\n"
+        "assert L.rs_tune(b'var', 141) == 13  # experiments build only\n"
         "print('ok', len(names))\n"
     )
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)

@@ -30,6 +30,7 @@ def engine(rslib):
     L.rs_tune(b"host_engine_waves", 8)
     L.rs_tune(b"host_engine_group_waves", 8)
     L.rs_tune(b"host_engine_idle_us", 200)
+    L.rs_tune(b"host_engine_life_us", 4000)
     L.rs_tune(b"host_engine_max_bytes", 1 << 20)
     L.rs_tune(b"host_engine_wg_units", 0)
     L.rs_tune(b"host_engine_direct", 1)
@@ -112,6 +113,7 @@ def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
     calls, launches = r.host_engine_stats()
     assert calls == 6 and launches == 6, (calls, launches)
     assert engine.rs_tune(b"host_engine_idle_us", 100000) == 0
+    assert engine.rs_tune(b"host_engine_life_us", 1000000) == 0
     for k in range(50):  # a burst: one instance
         v = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
         r.Encode(v)
@@ -119,6 +121,74 @@ def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
     calls2, launches2 = r.host_engine_stats()
     assert calls2 == 56 and launches2 == launches + 1, (calls2, launches2)
     assert engine.rs_tune(b"host_engine_idle_us", 200) == 0
+
+
+def test_engine_waves_changed_on_live_handle(rslib, orc, torch_dev, engine):
+    """host_engine_waves raised (and lowered) on a handle that has made more
+    calls than the ring has slots: workgroups the old instance did not have
+    start at the new instance's first call, so the next calls neither stall
+    nor time out (advisor finding, engine.cpp slot-reuse wait)."""
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(71)
+    data = [_rand(rng, size) for _ in range(d)]
+    exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+    assert orc.encode(d, p, exp) == 0
+    for waves in (8, 16, 2, 64, 8):
+        assert engine.rs_tune(b"host_engine_waves", waves) == 0
+        for k in range(20):  # more calls than kEngineSlots (8) per setting
+            v = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+            t0 = time.perf_counter()
+            r.Encode(v)
+            assert time.perf_counter() - t0 < 1.0, (waves, k)
+            assert all(np.array_equal(v[j], exp[j]) for j in range(d, d + p)), (waves, k)
+    calls, launches = r.host_engine_stats()
+    assert calls == 100 and launches >= 5, (calls, launches)
+
+
+def test_engine_lifetime_bounds_device_sync(rslib, orc, torch_dev, engine):
+    """While another thread keeps the engine busy with calls, a device-wide
+    synchronisation still returns: each instance leaves after
+    host_engine_life_us and the next call relaunches it."""
+    torch = torch_dev
+    assert engine.rs_tune(b"host_engine_life_us", 2000) == 0
+    assert engine.rs_tune(b"host_engine_idle_us", 100000) == 0
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(72)
+    data = [_rand(rng, size) for _ in range(d)]
+    exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+    assert orc.encode(d, p, exp) == 0
+    stop, errors, count = threading.Event(), [], [0]
+
+    def caller():
+        try:
+            while not stop.is_set():
+                v = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                r.Encode(v)
+                if not all(np.array_equal(v[j], exp[j]) for j in range(d, d + p)):
+                    errors.append("mismatch")
+                count[0] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=caller)
+    th.start()
+    try:
+        time.sleep(0.05)
+        worst = 0.0
+        for _ in range(20):
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            worst = max(worst, time.perf_counter() - t0)
+            time.sleep(0.005)
+    finally:
+        stop.set()
+        th.join(30)
+    assert not th.is_alive() and not errors, errors[:3]
+    calls, launches = r.host_engine_stats()
+    assert count[0] > 20 and launches >= 2, (count[0], launches)
+    assert worst < 0.1, worst
 
 
 @pytest.mark.parametrize("direct", [1, 0])

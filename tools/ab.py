@@ -3,7 +3,7 @@
 rule 24): variants are switched with rs_tune() and timed in interleaved
 rounds on the same device and buffers; reports median / min kernel time.
 
-    python tools/ab.py "var=12" "var=14" "var=14,layout=inter" ...
+    python tools/ab.py "var=12" "var=14" "var=14,layout=inter" ...   (experiments build)
     python tools/ab.py "op=rec1" "op=rec1,block8=256" "op=multi16" ...
 
 jit: 2 (default here: run-time bit-sliced kernels compiled before timing) | 0 (perm-table kernels).
@@ -19,6 +19,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# "var=..." code-shape experiments live only in the experiments build
+# (librsamd_exp.so, -DRSAMD_EXPERIMENTS); the product library rejects "var".
+EXPERIMENTS = any("var=" in s for s in sys.argv[1:])
+if EXPERIMENTS:
+    os.environ["RSAMD_LIB_VARIANT"] = "experiments"
 
 import torch  # noqa: E402
 
@@ -29,7 +34,7 @@ VEC = int(os.environ.get("AB_VEC", str(1 << 20)))  # bytes per vector; stripes k
 S = 256 * (1 << 20) // VEC
 ROUNDS = int(os.environ.get("AB_ROUNDS", "12"))
 ITERS = int(os.environ.get("AB_ITERS", "20"))
-DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "var": -1, "lds_pad": 0, "lane_bytes": 8, "block8": 128,
+DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "lds_pad": 0, "lane_bytes": 8, "block8": 128,
             "bitslice": 1, "bs_block": 0, "wide_block": 256, "jit": 2, "jit_pf": 3, "jit_min_acc_cols": 1, "jit_min_rows": 5}
 LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9], "rec5": [0, 2, 4, 6, 8], "rec6": [0, 1, 3, 5, 7, 9],
         "rec8": [0, 1, 2, 3, 4, 5, 6, 7], "rec8p": [0, 2, 4, 6, 10, 12, 14, 16], "rec12": list(range(12)),
@@ -43,8 +48,15 @@ def parse(spec):
     return layout, op, {k: int(v) for k, v in kv.items()}
 
 
+if EXPERIMENTS:
+    DEFAULTS["var"] = -1
+
+
 def main():
-    specs = sys.argv[1:] or ["var=12"]
+    if EXPERIMENTS:
+        from reedsolomon_amd import build as rsbuild
+        rsbuild.build(experiments=True)
+    specs = sys.argv[1:] or ["jit=2"]
     dev = torch.device("cuda", 0)
     r = rs.New(K, M, device=0)
     L = rs.lib()

@@ -1,5 +1,8 @@
 #!/usr/bin/env bash
 # Launch-parameter sweep of the encode bench (one process per setting).
+# RSAMD_VAR=... experiments need RSAMD_LIB_VARIANT=experiments in the spec
+# (librsamd_exp.so, `python -m reedsolomon_amd.build --experiments`): the
+# product library ignores RSAMD_VAR.
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
