@@ -21,7 +21,8 @@ equal N and every rank must join, or the run exits non-zero (`ranks_seen`).
 Order per rank: self-check (encode -> erase -> reconst), pre-warm until the
 launch time has settled (at least 250 launches; 20 consecutive within 3 %
 and within 0.5 % of the 20 before; `prewarm` in the line), W counted
-warm-up steps queued right behind it, K timed steps.
+warm-up steps queued right behind it, K timed steps; then (`cold`) 50
+launches after a 100 ms idle, the rate a bursty caller sees.
 
 Rank 0 prints ONE JSON line.  `value` = (k+m)*vec*S*N*K / max-rank time in
 GiB/s.  `roofline` prices the encode kernel itself: algorithmic bytes per
@@ -70,6 +71,8 @@ def parse_args(argv=None):
     ap.add_argument("--prewarm-min", type=int, default=250,
                     help="pre-warm: at least this many launches before the counted warm-up")
     ap.add_argument("--prewarm-max", type=int, default=2000, help="pre-warm: at most this many launches")
+    ap.add_argument("--cold", type=int, default=1,
+                    help="after the timed region: 50 launches after a 100 ms idle (`cold` in the line)")
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="TEST ONLY: rehearse the launcher / rank / timing protocol on CPU (gloo, no GPU, "
                          "no kernel); the line it prints is not a measurement")
@@ -366,6 +369,32 @@ def prewarm(step, stream, min_launches: int, max_launches: int, window: int = 20
     return n, (time.perf_counter() - t0) * 1e3, last_mean, converged
 
 
+def cold_launches(step, stream, nbytes: int, max_over, idle_s: float = 0.1, n: int = 50):
+    """What a bursty caller sees: after `idle_s` of GPU idle,
+    `n` launches back to back, each bracketed by HIP events on the launch
+    stream; mean / max launch time over them (max over ranks) against the
+    steady state the timed region measures.  Runs after the timed region."""
+    import torch
+
+    torch.cuda.synchronize()
+    time.sleep(idle_s)
+    evs = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step(0)
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = [a.elapsed_time(b) for a, b in evs]
+    mean = max_over(sum(ms) / n)
+    return {"idle_ms": idle_s * 1e3, "launches": n, "mean_ms": round(mean, 4), "max_ms": round(max_over(max(ms)), 4),
+            "first10_ms": [round(x, 4) for x in ms[:10]],
+            "GiBps_per_gpu": round(nbytes / (mean / 1e3) / 2 ** 30, 1),
+            "rule": "after the timed region: GPU idle for idle_ms, then `launches` launches back to back, each "
+                    "bracketed by HIP events; mean over them (max over ranks)"}
+
+
 def metric_name(k: int, m: int, vec: int) -> str:
     """BASELINE.json's metric, with the shape of the config actually run."""
     size = f"{vec >> 20}MiB" if vec % (1 << 20) == 0 else f"{vec >> 10}KiB"
@@ -549,6 +578,7 @@ def main(argv=None):
 
     bytes_per_step_rank = S * (k + m) * vec
     value = throughput(bytes_per_step_rank, n_gpus, args.steps, elapsed)
+    cold = cold_launches(step, stream, bytes_per_step_rank, max_over) if args.cold else None
 
     e2e = None
     if args.e2e_stripes > 0:
@@ -601,6 +631,7 @@ def main(argv=None):
                                 "and their mean within 0.5 % of the 20 before; the counted warm-up is queued "
                                 "behind them with no idle gap"},
         }
+        result["cold"] = cold
         result["end_to_end"] = e2e
         if n_gpus == 1 and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(k, m, vec, args.cpu_seconds)

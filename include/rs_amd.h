@@ -84,6 +84,10 @@ RS_API int  rs_new(int data_num, int parity_num, int device, rs_t** out);
 RS_API void rs_free(rs_t* rs);
 RS_API int  rs_data_num(const rs_t* rs);                 /* RS.DataNum   rs.go:24 */
 RS_API int  rs_parity_num(const rs_t* rs);               /* RS.ParityNum rs.go:25 */
+/* The HIP device ordinal the handle launches on: the one given to rs_new,
+ * or -1 while it is "the current device at first use" and no call has bound
+ * it yet.  No device call. */
+RS_API int  rs_device(const rs_t* rs);
 /* Copies GenMatrix (p x d, row-major, G[j*d+i]) into out[p*d]. rs.go:31,65-68 */
 RS_API int  rs_gen_matrix(const rs_t* rs, uint8_t* out);
 /* Copies the (d+p) x d encoding matrix into out[(d+p)*d]. rs.go:30 */
@@ -231,6 +235,12 @@ RS_API int  rs_group_size(const rs_group_t* g);
 /* The codec of member i (borrowed; valid until rs_group_free), for
  * device-resident calls on that member's device. */
 RS_API rs_t* rs_group_codec(rs_group_t* g, int i);
+/* The slice [*lo, *hi) of stripes [0, nstripes) that member i takes in the
+ * group's batched calls: contiguous, in member order, sizes differing by at
+ * most one (lo = nstripes*i/n, hi = nstripes*(i+1)/n).  Device-resident
+ * callers splitting their own batches over rs_group_codec(g, i) use the same
+ * rule.  No device call. */
+RS_API int rs_group_slice(const rs_group_t* g, int nstripes, int i, int* lo, int* hi);
 /* rs_encode_host_batch over the group: stripes [0, nstripes) of one host
  * buffer split across the members. */
 RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
@@ -343,6 +353,14 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
  * NULL. */
 RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
 
+/* The run-time kernels' on-disk code-object cache (RSAMD_JIT_CACHE_DIR,
+ * default $XDG_CACHE_HOME/rsamd/jit or ~/.cache/rsamd/jit; knob
+ * "jit_disk_cache"), process-wide: first sights of a matrix whose code object
+ * was on disk (loaded, no compile), first sights that found none, code
+ * objects written, files rejected on load (corrupt or stale: recompiled).
+ * Any pointer may be NULL. */
+RS_API int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects);
+
 /* Compile the run-time kernel for a rows x cols matrix (row-major, 5 <= rows
  * <= 16, 1 <= cols <= 64; accumulate 1 = the XOR-into-outputs form Update /
  * Replace use) for the handle's device now, instead of on the matrix's
@@ -415,7 +433,9 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * "jit_min_rows" (launches with fewer output rows stay on the table kernels;
  * default 5),
  * "jit_pf" (columns loaded ahead in
- * the compiled kernels, 1..6, default 3),
+ * the compiled kernels, 1..6, default 3), "jit_disk_cache" (1 default: compiled
+ * code objects are kept in an on-disk cache shared by processes, see
+ * rs_jit_cache_stats | 0: compile in every process),
  * "table_registry_max" (distinct coefficient matrices
  * kept on the device per handle before the registry is recycled).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name.  The code-shape experiments of

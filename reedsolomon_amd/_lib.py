@@ -73,6 +73,8 @@ SIGNATURES = {
     "rs_group_free": (None, [c_void]),
     "rs_group_size": (c_int, [c_void]),
     "rs_group_codec": (c_void, [c_void, c_int]),
+    "rs_group_slice": (c_int, [c_void, c_int, c_int, c_intp, c_intp]),
+    "rs_device": (c_int, [c_void]),
     "rs_group_encode_host_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_int, c_int]),
     "rs_group_reconst_host_batch_multi": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
                                                   ctypes.POINTER(ctypes.c_uint64)]),
@@ -100,6 +102,7 @@ SIGNATURES = {
     "rs_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
     "rs_jit_stats": (c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                              ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]),
+    "rs_jit_cache_stats": (c_int, [ctypes.POINTER(ctypes.c_uint64)] * 4),
     "rs_jit_prepare": (c_int, [c_void, ctypes.c_void_p, c_int, c_int, c_int, c_int]),
     "rs_jit_compile_check": (c_int, [ctypes.c_void_p, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_double)]),
     "rs_tune": (c_int, [ctypes.c_char_p, c_int]),

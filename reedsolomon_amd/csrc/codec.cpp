@@ -502,6 +502,8 @@ int rs_data_num(const rs_t* rs) { return rs ? rs->d : 0; }
 
 int rs_parity_num(const rs_t* rs) { return rs ? rs->p : 0; }
 
+int rs_device(const rs_t* rs) { return rs ? rs->device : -1; }
+
 int rs_gen_matrix(const rs_t* rs, uint8_t* out) {
     return abi_guard([&]() -> int {
         if (!rs || !out) return RS_ERR_INVAL;
@@ -540,6 +542,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_min_acc_cols") g_jit_min_acc_cols = value < 1 ? 1 : value;
         else if (n == "jit_min_launches") g_jit_min_launches = value < 1 ? 1 : value;
         else if (n == "jit_pf") g_jit_pf = value < 1 ? 1 : value > 6 ? 6 : value;
+        else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
@@ -630,6 +633,13 @@ int rs_reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, 
 int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms) {
     return abi_guard([&]() -> int {
         jit_stats(compiled, failed, launches, compile_ms);
+        return RS_OK;
+    });
+}
+
+int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects) {
+    return abi_guard([&]() -> int {
+        jit_cache_stats(hits, misses, writes, rejects);
         return RS_OK;
     });
 }

@@ -511,6 +511,18 @@ void rs_group_free(rs_group_t* g) {
 
 int rs_group_size(const rs_group_t* g) { return g ? static_cast<int>(g->members.size()) : 0; }
 
+// Member i's contiguous slice of a batch (every group entry point splits this way).
+static void group_slice(int nstripes, int n, int i, int* lo, int* hi) {
+    *lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
+    *hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+}
+
+int rs_group_slice(const rs_group_t* g, int nstripes, int i, int* lo, int* hi) {
+    if (!g || !lo || !hi || nstripes < 0 || i < 0 || i >= static_cast<int>(g->members.size())) return RS_ERR_INVAL;
+    group_slice(nstripes, static_cast<int>(g->members.size()), i, lo, hi);
+    return RS_OK;
+}
+
 rs_t* rs_group_codec(rs_group_t* g, int i) {
     return g && i >= 0 && i < static_cast<int>(g->members.size()) ? g->members[i] : nullptr;
 }
@@ -524,8 +536,8 @@ int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stripe_stri
         std::vector<int> rc(n, RS_OK);
         std::vector<std::thread> th;
         for (int i = 0; i < n; ++i) {
-            const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
-            const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+            int lo = 0, hi = 0;
+            group_slice(nstripes, n, i, &lo, &hi);
             if (hi <= lo) continue;
             auto job = [&, i, lo, hi] {
                 rc[i] = rs_encode_host_batch(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride,
@@ -585,8 +597,8 @@ static int group_reconst_host_multi(rs_group_t* g, uint8_t* base, int64_t stripe
     std::vector<int> rc(n, RS_OK);
     std::vector<std::thread> th;
     for (int i = 0; i < n; ++i) {
-        const int lo = static_cast<int>(static_cast<int64_t>(nstripes) * i / n);
-        const int hi = static_cast<int>(static_cast<int64_t>(nstripes) * (i + 1) / n);
+        int lo = 0, hi = 0;
+        group_slice(nstripes, n, i, &lo, &hi);
         if (hi <= lo) continue;
         auto job = [&, i, lo, hi] {
             rc[i] = reconst_host_multi(g->members[i], base + static_cast<int64_t>(lo) * stripe_stride, stripe_stride,

@@ -24,16 +24,31 @@
 // until the code object is ready; the launching thread then loads it
 // (hipModuleLoadData) and from there on launches the bit-sliced kernel.
 // rs_tune("jit", 2) compiles on the launching thread instead.
+//
+// Code objects persist across processes in an on-disk cache
+// (RSAMD_JIT_CACHE_DIR, default $XDG_CACHE_HOME/rsamd/jit or
+// ~/.cache/rsamd/jit; rs_tune("jit_disk_cache", 0) turns it off): a file per
+// (device arch, hiprtc version, generator version, prelude, argument layout,
+// mode, prefetch distance, matrix).  The first sight of a matrix whose code
+// object is on disk loads it on the launching thread and launches the
+// compiled kernel right away, whatever the launch history: a restarted
+// server pays no compile for the matrices it has seen before.  Files are
+// written atomically (temporary file + rename) and checked on load (magic,
+// two independent key hashes, length, a checksum of the code, ELF magic);
+// anything else is ignored and recompiled.
 #include "jit.hpp"
 
 #include <hip/hiprtc.h>
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
+#include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -57,6 +72,10 @@ int g_jit_min_launches = 2;
 int g_jit_min_rows = kJitMinRows;
 int g_jit_min_acc_cols = kJitMinAccCols;
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
+int g_jit_disk_cache = [] {  // rs_tune("jit_disk_cache", 0 | 1); env RSAMD_JIT_DISK_CACHE
+    const char* e = std::getenv("RSAMD_JIT_DISK_CACHE");
+    return e ? (std::atoi(e) ? 1 : 0) : 1;
+}();
 
 namespace {
 
@@ -251,6 +270,145 @@ std::string network(const uint8_t* mat, int rows, int cols, bool acc) {
     return o;
 }
 
+// ---------------------------------------------------------------- on-disk cache
+
+// Bumped whenever network() or the launch contract changes in a way the
+// key below does not capture (the prelude text and the MatmulArgs layout are
+// hashed into the key).
+constexpr uint32_t kJitGenVersion = 3;
+constexpr char kDiskMagic[8] = {'R', 'S', 'A', 'M', 'D', 'J', 'I', 'T'};
+constexpr uint32_t kDiskFormat = 1;
+
+uint64_t fnv1a(const void* p, size_t n, uint64_t h) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+// Second, independent hash: splitmix64 over 8-byte words
+uint64_t hash2(const std::string& s) {
+    uint64_t h = 0x6a09e667f3bcc909ull ^ s.size();
+    size_t i = 0;
+    for (; i + 8 <= s.size(); i += 8) {
+        uint64_t w;
+        std::memcpy(&w, s.data() + i, 8);
+        h = mix64(h ^ w) + 0x9e3779b97f4a7c15ull;
+    }
+    uint64_t w = 0;
+    std::memcpy(&w, s.data() + i, s.size() - i);
+    return mix64(h ^ w ^ 0xff);
+}
+
+struct DiskStats {
+    std::atomic<uint64_t> hits{0}, misses{0}, writes{0}, rejects{0};
+};
+DiskStats& disk_stats() {
+    static DiskStats* d = new DiskStats;
+    return *d;
+}
+
+std::string cache_dir() {
+    static const std::string dir = [] {
+        if (const char* e = std::getenv("RSAMD_JIT_CACHE_DIR")) return std::string(e);
+        if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) return std::string(x) + "/rsamd/jit";
+        if (const char* h = std::getenv("HOME"); h && *h) return std::string(h) + "/.cache/rsamd/jit";
+        return std::string();
+    }();
+    return dir;
+}
+
+bool make_dirs(const std::string& d) {
+    if (d.empty()) return false;
+    std::string cur;
+    for (size_t i = 0; i <= d.size(); ++i) {
+        if (i == d.size() || d[i] == '/') {
+            if (!cur.empty() && mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+        }
+        if (i < d.size()) cur += d[i];
+    }
+    return true;
+}
+
+struct DiskKey {
+    std::string text;  // everything the code object depends on
+    uint64_t h1 = 0, h2 = 0;
+    std::string path() const {
+        char name[48];
+        std::snprintf(name, sizeof name, "%016llx%016llx.co", static_cast<unsigned long long>(h1),
+                      static_cast<unsigned long long>(h2));
+        return cache_dir() + "/" + name;
+    }
+};
+
+struct FileHeader {
+    char magic[8];
+    uint32_t format, gen;
+    uint64_t h1, h2, key_len, code_len, code_sum;
+};
+
+std::vector<char> disk_load(const DiskKey& k) {
+    std::vector<char> code;
+    const std::string path = k.path();
+    const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return code;
+    FileHeader h{};
+    bool ok = read(fd, &h, sizeof h) == static_cast<ssize_t>(sizeof h) &&
+              std::memcmp(h.magic, kDiskMagic, 8) == 0 && h.format == kDiskFormat && h.gen == kJitGenVersion &&
+              h.h1 == k.h1 && h.h2 == k.h2 && h.key_len == k.text.size() && h.code_len > 4 &&
+              h.code_len < (uint64_t{256} << 20);
+    if (ok) {
+        code.resize(h.code_len);
+        ok = read(fd, code.data(), code.size()) == static_cast<ssize_t>(code.size()) &&
+             fnv1a(code.data(), code.size(), 0xcbf29ce484222325ull) == h.code_sum && code[0] == 0x7f &&
+             code[1] == 'E' && code[2] == 'L' && code[3] == 'F';
+    }
+    close(fd);
+    if (!ok) {
+        code.clear();
+        disk_stats().rejects.fetch_add(1, std::memory_order_relaxed);
+    }
+    return code;
+}
+
+void disk_store(const DiskKey& k, const std::vector<char>& code) {
+    const std::string dir = cache_dir();
+    if (!make_dirs(dir)) return;
+    const std::string path = k.path();
+    char tmp_suffix[64];
+    std::snprintf(tmp_suffix, sizeof tmp_suffix, ".tmp.%d.%llx", static_cast<int>(getpid()),
+                  static_cast<unsigned long long>(mix64(reinterpret_cast<uintptr_t>(&code) ^ k.h1)));
+    const std::string tmp = path + tmp_suffix;
+    const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+    if (fd < 0) return;
+    FileHeader h{};
+    std::memcpy(h.magic, kDiskMagic, 8);
+    h.format = kDiskFormat;
+    h.gen = kJitGenVersion;
+    h.h1 = k.h1;
+    h.h2 = k.h2;
+    h.key_len = k.text.size();
+    h.code_len = code.size();
+    h.code_sum = fnv1a(code.data(), code.size(), 0xcbf29ce484222325ull);
+    bool ok = write(fd, &h, sizeof h) == static_cast<ssize_t>(sizeof h) &&
+              write(fd, code.data(), code.size()) == static_cast<ssize_t>(code.size());
+    ok = close(fd) == 0 && ok;
+    // rename is atomic: a reader sees the old file, no file, or this whole file
+    if (ok && rename(tmp.c_str(), path.c_str()) == 0) {
+        disk_stats().writes.fetch_add(1, std::memory_order_relaxed);
+    } else {
+        unlink(tmp.c_str());
+    }
+}
+
 struct Compiled {
     std::vector<char> code;
     double ms = 0;
@@ -266,8 +424,33 @@ Compiled compile(const std::string& src) {
         out.log = "hiprtcCreateProgram failed";
         return out;
     }
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+#ifdef RSAMD_EXPERIMENTS  // compile-option experiments (librsamd_exp.so only): RSAMD_JIT_OPTS="opt opt ..."
+    static std::vector<std::string> extra = [] {
+        std::vector<std::string> v;
+        if (const char* e = std::getenv("RSAMD_JIT_OPTS")) {
+            std::string cur;
+            for (const char* c = e;; ++c) {
+                if (*c == ' ' || *c == 0) {
+                    if (!cur.empty()) v.push_back(cur);
+                    cur.clear();
+                    if (!*c) break;
+                } else {
+                    cur += *c;
+                }
+            }
+        }
+        return v;
+    }();
+    for (const std::string& x : extra) opts.push_back(x.c_str());
+    if (const char* d = std::getenv("RSAMD_JIT_DUMP")) {  // the generated source, for offline profiling
+        if (FILE* f = std::fopen(d, "w")) {
+            std::fputs(src.c_str(), f);
+            std::fclose(f);
+        }
+    }
+#endif
+    const hiprtcResult rc = hiprtcCompileProgram(prog, static_cast<int>(opts.size()), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         if (hiprtcGetProgramLogSize(prog, &n) == HIPRTC_SUCCESS && n > 1) {
@@ -292,6 +475,7 @@ Compiled compile(const std::string& src) {
 struct Entry {
     enum State { kQueued, kCompiling, kReady, kLoaded, kFailed } state = kQueued;
     std::string src;
+    DiskKey disk;  // on-disk cache key (text empty: the disk cache is off)
     std::vector<char> code;
     hipModule_t module = nullptr;
     hipFunction_t fn64 = nullptr, fn256 = nullptr;
@@ -302,6 +486,7 @@ constexpr size_t kMaxSeen = 4096;  // matrices counted but not compiled yet (cle
 
 struct Seen {
     uint64_t launches = 0, bytes = 0;
+    bool disk_checked = false;  // no code object on disk for it at first sight
 };
 
 void jit_atexit_hook();
@@ -328,6 +513,7 @@ struct Jit {
         // reverse order); jit_atexit is idempotent.
         static std::once_flag late;
         std::call_once(late, [] { std::atexit(jit_atexit_hook); });
+        if (c.ok && !e->disk.text.empty()) disk_store(e->disk, c.code);
         std::lock_guard<std::mutex> lk(mu);
         if (c.ok) {
             e->code = std::move(c.code);
@@ -422,6 +608,48 @@ void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double*
 
 void jit_count_launch() { jit().launches.fetch_add(1, std::memory_order_relaxed); }
 
+void jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects) {
+    DiskStats& d = disk_stats();
+    if (hits) *hits = d.hits.load();
+    if (misses) *misses = d.misses.load();
+    if (writes) *writes = d.writes.load();
+    if (rejects) *rejects = d.rejects.load();
+}
+
+// gcnArchName of a device ("gfx950:sramecc+:xnack-"), cached; caller holds jit().mu
+static const std::string& device_arch(int dev) {
+    static std::map<int, std::string> archs;
+    auto it = archs.find(dev);
+    if (it != archs.end()) return it->second;
+    hipDeviceProp_t prop;
+    std::string name = hipGetDeviceProperties(&prop, dev) == hipSuccess ? std::string(prop.gcnArchName) : "";
+    return archs.emplace(dev, name).first->second;
+}
+
+// Everything the code object for this launch shape depends on.
+static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
+    static const std::string fixed = [] {
+        int maj = 0, mnr = 0;
+        (void)hiprtcVersion(&maj, &mnr);
+        char b[160];
+        std::snprintf(b, sizeof b, "gen %u hiprtc %d.%d args %zu/%zu/%zu/%zu prelude %016llx", kJitGenVersion, maj, mnr,
+                      sizeof(MatmulArgs), offsetof(MatmulArgs, ptr), offsetof(MatmulArgs, stripe_ids),
+                      offsetof(MatmulArgs, cps_shift),
+                      static_cast<unsigned long long>(fnv1a(kPrelude, std::strlen(kPrelude), 0xcbf29ce484222325ull)));
+        return std::string(b);
+    }();
+    DiskKey k;
+    k.text = arch + '\n' + fixed + '\n';
+    k.text += static_cast<char>(a.accumulate ? 1 : 0);
+    k.text += static_cast<char>(a.rows);
+    k.text += static_cast<char>(a.cols);
+    k.text += static_cast<char>(g_jit_pf);
+    k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
+    k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
+    k.h2 = hash2(k.text);
+    return k;
+}
+
 // mode: 1 background after recurrence, 2 compile on this thread, 3 queue now
 static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int mode) {
     if (!mode || !a.host_mat || a.rows < 1 || a.rows > kJitMaxRows || a.cols < 1 ||
@@ -429,6 +657,10 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
         return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    // the generated code is gfx950 code (v_bitop3, buffer nt): other devices
+    // keep the perm-table kernels (no compile is ever attempted for them)
+    const std::string& arch = device_arch(dev);
+    if (arch.compare(0, 6, "gfx950") != 0) return nullptr;
     std::string key(reinterpret_cast<const char*>(&dev), sizeof dev);
     key += static_cast<char>(a.accumulate ? 1 : 0);
     key += static_cast<char>(a.rows);
@@ -442,10 +674,35 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
         auto it = j.entries.find(key);
         if (it == j.entries.end()) {
             if (j.entries.size() >= kMaxEntries) return nullptr;
+            // a code object on disk (another process, an earlier run): load it
+            // now whatever the launch history; checked once per matrix
+            DiskKey dk;
+            Seen* h = nullptr;
+            if (mode == 1) {
+                if (j.seen.size() >= kMaxSeen) j.seen.clear();
+                h = &j.seen[key];
+            }
+            if (g_jit_disk_cache && !cache_dir().empty() && !(h && h->disk_checked)) {
+                dk = disk_key(arch, a);
+                std::vector<char> code = disk_load(dk);
+                if (h) h->disk_checked = true;
+                if (!code.empty()) {
+                    disk_stats().hits.fetch_add(1, std::memory_order_relaxed);
+                    if (h) j.seen.erase(key);
+                    e = std::make_shared<Entry>();
+                    e->code = std::move(code);
+                    e->state = Entry::kReady;
+                    e->disk = std::move(dk);
+                    it = j.entries.emplace(key, e).first;
+                } else {
+                    disk_stats().misses.fetch_add(1, std::memory_order_relaxed);
+                }
+            }
+        }
+        if (it == j.entries.end()) {
             if (mode == 1) {
                 // compile only a matrix that recurs: a one-off erasure pattern
                 // would cost a compile (seconds of host time) and never pay it back
-                if (j.seen.size() >= kMaxSeen) j.seen.clear();
                 Seen& h = j.seen[key];
                 ++h.launches;
                 h.bytes += launch_bytes;
@@ -455,6 +712,7 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
             }
             e = std::make_shared<Entry>();
             e->src = jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
+            if (g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
             j.entries.emplace(key, e);
             if (mode == 2) {
                 e->state = Entry::kCompiling;

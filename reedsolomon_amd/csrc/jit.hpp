@@ -52,5 +52,9 @@ int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, d
 // the kernel for a matrix now, whatever its launch history (rs_jit_prepare).
 int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wait);
 void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
+// On-disk code-object cache: first-sight lookups that found a valid file,
+// that found none, files written, files rejected on load (corrupt / stale).
+void jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects);
+extern int g_jit_disk_cache;  // rs_tune("jit_disk_cache", 0 | 1)
 
 }  // namespace rsamd

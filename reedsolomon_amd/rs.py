@@ -179,6 +179,10 @@ class RS:
         self.GenMatrix = g            # p x d, row-major: G[j*d+i]   (rs.go:31)
         self.encMatrix = e            # (d+p) x d                      (rs.go:30)
 
+    def device_ordinal(self) -> int:
+        """The device the handle launches on (rs_device; -1 = not bound yet)."""
+        return int(lib().rs_device(self._h))
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h and getattr(self, "_owner", None) is None:
@@ -513,6 +517,13 @@ class Group:
     def __len__(self) -> int:
         return lib().rs_group_size(self._g)
 
+    def slice(self, nstripes: int, i: int) -> tuple:
+        """(lo, hi): the stripes of a batch of `nstripes` that member i takes
+        in the group's batched calls (rs_group_slice)."""
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        _check(lib().rs_group_slice(self._g, int(nstripes), int(i), ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
     def encode_host_batch(self, buf, stripes_per_chunk: int = 4, streams: int = 3) -> None:
         """RS.encode_host_batch with the stripes split across the group's devices."""
         ptr, ss, vs, S, n = _host_batch(buf, self.DataNum + self.ParityNum)
@@ -575,6 +586,13 @@ def jit_stats() -> dict:
     c, f, n, ms = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
     _check(lib().rs_jit_stats(ctypes.byref(c), ctypes.byref(f), ctypes.byref(n), ctypes.byref(ms)))
     return {"compiled": c.value, "failed": f.value, "launches": n.value, "compile_ms": ms.value}
+
+
+def jit_cache_stats() -> dict:
+    """The run-time kernels' on-disk code-object cache (rs_jit_cache_stats)."""
+    v = [ctypes.c_uint64(0) for _ in range(4)]
+    _check(lib().rs_jit_cache_stats(*[ctypes.byref(x) for x in v]))
+    return dict(zip(("hits", "misses", "writes", "rejects"), (int(x.value) for x in v)))
 
 
 def jit_compile_check(mat, accumulate: bool = False) -> float:

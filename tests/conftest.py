@@ -7,6 +7,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# run-time compiled kernels: a test session has its own on-disk code-object
+# cache, so tests that count compiles do not depend on earlier runs
+if "RSAMD_JIT_CACHE_DIR" not in os.environ:
+    import tempfile
+
+    os.environ["RSAMD_JIT_CACHE_DIR"] = tempfile.mkdtemp(prefix="rsamd_jit_")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels through the C ABI)")

@@ -132,3 +132,81 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--rehearse-cpu"],
                        capture_output=True, text=True, env=env, timeout=100, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def _group_worker(rank, world, port, q):
+    """One rank of a 2-rank job that drives 2 GPUs per rank through a device
+    group (rs_group_*), the way an N-GPU storage node splits its stripes:
+    distinct device ordinals per rank (2r, 2r+1; no device call is made on
+    CPU, the handles bind lazily), the group's slice rule over this rank's
+    global stripe range, and the cross-GPU placement plan computed on every
+    rank from the same erasure masks."""
+    sys.path.insert(0, ROOT)
+    import hashlib
+
+    import torch.distributed as dist
+
+    import bench
+    import reedsolomon_amd as rs
+    from reedsolomon_amd import placement
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        d, p, S = 10, 4, 37
+        devs = [2 * rank, 2 * rank + 1]
+        g = rs.NewGroup(d, p, devs)
+        assert len(g) == 2
+        assert [m.device_ordinal() for m in g.members] == devs
+        lo, hi = bench.stripe_range(rank, S)
+        slices = [g.slice(S, i) for i in range(len(g))]
+        assert slices[0][0] == 0 and slices[-1][1] == S
+        assert all(a[1] == b[0] for a, b in zip(slices, slices[1:]))  # contiguous, in member order
+        assert max(h - l_ for l_, h in slices) - min(h - l_ for l_, h in slices) <= 1
+        # (global stripe range, device) per member; every rank collects all of them
+        mine = [(lo + a, lo + b, devs[i]) for i, (a, b) in enumerate(slices)]
+        allm = [None] * world
+        dist.all_gather_object(allm, mine)
+        # the placement plan every rank derives from the same masks
+        rng = np.random.default_rng(99)
+        n_total = S * world
+        masks = [0] * n_total
+        for s in range(n_total):
+            lost = rng.choice(d + p, int(rng.integers(0, p + 1)), replace=False)
+            masks[s] = sum(1 << int(v) for v in lost)
+        pl = placement.Placement(d, p, world, n_total)
+        plan = placement._plan(pl, np.asarray(masks, dtype=np.uint64))
+        digest = hashlib.sha256(repr(sorted(plan.items())).encode()).hexdigest()
+        digests = [None] * world
+        dist.all_gather_object(digests, digest)
+        owned = sorted(s for s in plan if pl.owner(s) == rank)
+        q.put((rank, allm, digests, len(owned), len(pl.local_shards(rank))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_gloo_device_groups_and_placement():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_group_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(150)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    allm0, allm1 = res[0][1], res[1][1]
+    assert allm0 == allm1  # both ranks see the same assignment
+    members = [m for per_rank in allm0 for m in per_rank]
+    # every global stripe is taken by exactly one member, every member is on its own device
+    covered = sorted((a, b) for a, b, _ in members)
+    assert covered[0][0] == 0 and covered[-1][1] == 2 * 37
+    assert all(x[1] == y[0] for x, y in zip(covered, covered[1:]))
+    assert sorted(dv for _, _, dv in members) == [0, 1, 2, 3]
+    # the decode plan is identical on every rank; owners split the stripes with erasures
+    assert res[0][2] == res[1][2] and res[0][2][0] == res[0][2][1]
+    assert res[0][3] > 0 and res[1][3] > 0
+    assert res[0][4] + res[1][4] == 2 * 37 * 14  # every shard has exactly one home

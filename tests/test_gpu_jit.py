@@ -297,3 +297,62 @@ def test_jit_prepare_then_first_launch_runs_compiled(rslib, orc, torch_dev):
     torch.cuda.synchronize()
     assert np.array_equal(buf.cpu().numpy()[:, d:], exp)
     assert rslib.jit_stats()["launches"] == before + 1
+
+
+_DISK_SCRIPT = r'''
+import json, os, sys
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+import reedsolomon_amd as rs
+from oracle import oracle
+L = rs.lib()
+assert L.rs_tune(b"jit", int(sys.argv[1])) == 0
+rng = np.random.default_rng(5151)
+mat = rng.integers(0, 256, (12, 20), dtype=np.uint8)
+src_h = rng.integers(0, 256, (2, 20, 65536), dtype=np.uint8)
+exp = oracle.encode_numpy(mat, src_h)
+r = rs.New(10, 4)
+src = torch.from_numpy(src_h).cuda()
+dst = torch.zeros((2, 12, 65536), dtype=torch.uint8, device="cuda")
+r.gf_matmul_batch(mat, src, None, dst, None)
+torch.cuda.synchronize()
+print(json.dumps({"ok": bool(np.array_equal(dst.cpu().numpy(), exp)), "jit": rs.jit_stats(),
+                  "cache": rs.jit_cache_stats()}))
+'''
+
+
+def test_jit_disk_cache_across_processes(rslib, tmp_path):
+    """The on-disk code-object cache: process A compiles a 12 x 20 matrix and
+    writes its code object; process B's FIRST launch of the same matrix (the
+    default background mode, which would otherwise only count it) loads the
+    file and runs the compiled kernel with no compile; a corrupted file is
+    rejected and recompiled.  Every launch's bytes equal the oracle's."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RSAMD_JIT_CACHE_DIR=str(tmp_path / "jit"), RSAMD_JIT_DISK_CACHE="1")
+    script = "ROOT = %r\n" % root + _DISK_SCRIPT
+
+    def run(mode):
+        out = subprocess.run([sys.executable, "-c", script, str(mode)], env=env, capture_output=True, text=True,
+                             timeout=240)
+        assert out.returncode == 0, out.stderr[-3000:]
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    a = run(2)  # compile on the launching thread
+    assert a["ok"] and a["jit"]["compiled"] == 1 and a["jit"]["launches"] == 1, a
+    assert a["cache"]["misses"] == 1 and a["cache"]["writes"] == 1, a
+    files = list((tmp_path / "jit").glob("*.co"))
+    assert len(files) == 1, files
+    b = run(1)  # default mode: first sight, loaded from disk, compiled kernel runs
+    assert b["ok"] and b["jit"]["compiled"] == 0 and b["jit"]["launches"] == 1, b
+    assert b["cache"]["hits"] == 1 and b["cache"]["writes"] == 0, b
+    raw = bytearray(files[0].read_bytes())
+    raw[len(raw) // 2] ^= 0xFF  # corrupt the code: the checksum rejects it
+    files[0].write_bytes(bytes(raw))
+    c = run(2)
+    assert c["ok"] and c["cache"]["rejects"] == 1 and c["jit"]["compiled"] == 1 and c["cache"]["writes"] == 1, c

@@ -260,26 +260,49 @@ def test_reconst_host_round_trip(rslib, orc, torch_dev):  # TestRS_Reconst rs_te
             assert np.array_equal(act[i], ora[i])
 
 
-def test_reconst_batch_every_pattern(rslib, torch_dev):
-    """All C(14,1..4) erasure patterns of 10+4 (8 KiB, BASELINE config 3)."""
+def _oracle_stripes(orc, rng, d, p, S, n):
+    """[S, d+p, n] host stripes: random data, parity from the oracle's AVX2
+    restatement of the reference's encode (pinned to the table path by
+    tests/test_oracle.py), one stripe at a time."""
+    host = np.empty((S, d + p, n), np.uint8)
+    host[:, :d] = rng.integers(0, 256, (S, d, n), dtype=np.uint8)
+    host[:, d:] = 0
+    for s in range(S):
+        v = list(host[s])
+        assert orc.encode_avx2(d, p, v) or orc.encode(d, p, v) == 0
+    return host
+
+
+def test_reconst_batch_every_pattern(rslib, orc, torch_dev):
+    """All C(14,1..4) = 1470 erasure patterns of 10+4 @ 8 KiB (BASELINE
+    config 3) over a 32,768-stripe batch (the ops_bench size): stripe s loses
+    pattern s % 1470 (garbage in the lost vectors), one rs_reconst_batch
+    launch per pattern over its strided stripe set; every byte of every
+    stripe equals the oracle-encoded original, and the oracle's own Reconst
+    (rs.go:221-380 restated) of every stripe gives the same bytes."""
     torch = torch_dev
-    d, p, S, n = 10, 4, 4, 8192
+    d, p, S, n = 10, 4, 32768, 8192
+    rng = np.random.default_rng(263)
     r = rslib.New(d, p)
-    g = torch.Generator(device="cuda").manual_seed(7)
-    ref = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
-    r.encode_batch(ref)
-    work = torch.empty_like(ref)
-    npat = 0
-    for k in range(1, p + 1):
-        for lost in itertools.combinations(range(d + p), k):
-            work.copy_(ref)
-            work[:, list(lost)] = 0x3C
-            r.reconst_batch(work, [], list(lost))
-            npat += 1
-            if npat % 64 == 0:
-                torch.cuda.synchronize()
-            assert torch.equal(work, ref), lost
-    assert npat == 14 + 91 + 364 + 1001
+    host = _oracle_stripes(orc, rng, d, p, S, n)
+    pats = [list(c) for k in range(1, p + 1) for c in itertools.combinations(range(d + p), k)]
+    assert len(pats) == 14 + 91 + 364 + 1001
+    work = torch.from_numpy(host).cuda()
+    for i, lost in enumerate(pats):
+        work[i::len(pats), lost] = 0x3C
+    for i, lost in enumerate(pats):
+        r.reconst_batch(work[i::len(pats)], [], lost)
+    torch.cuda.synchronize()
+    got = work.cpu().numpy()
+    for s0 in range(0, S, 4096):
+        assert np.array_equal(got[s0:s0 + 4096], host[s0:s0 + 4096]), s0
+    for s in range(S):  # the restated reference, per stripe
+        lost = pats[s % len(pats)]
+        v = [x.copy() for x in host[s]]
+        for i in lost:
+            v[i][:] = 0x3C
+        assert orc.reconst(d, p, v, [], lost) == 0
+        assert all(np.array_equal(v[i], got[s, i]) for i in lost), s
 
 
 def test_reconst_dev_and_explicit_survived(rslib, orc, torch_dev):
@@ -340,22 +363,28 @@ def test_update_every_row(rslib, orc, torch_dev):  # TestRS_Update rs_test.go:21
             assert np.array_equal(dv[d + j].cpu().numpy(), exp2[d + j])
 
 
-def test_update_batch(rslib, orc, torch_dev):
+@pytest.mark.parametrize("S,rows", [(32768, [3]), (4096, list(range(10)))])
+def test_update_batch(rslib, orc, torch_dev, S, rows):
+    """rs_update_batch (BASELINE config 5, 10+4 @ 8 KiB) at the ops_bench batch
+    size for one row and on 4,096 stripes for every row; every stripe's parity
+    equals the oracle's Update (rs.go:424-449 restated)."""
     torch = torch_dev
-    d, p, S, n = 10, 4, 16, 8192
+    d, p, n = 10, 4, 8192
+    rng = np.random.default_rng(343 + S)
     r = rslib.New(d, p)
-    g = torch.Generator(device="cuda").manual_seed(8)
-    buf = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
-    r.encode_batch(buf)
-    for row in range(d):
-        new = torch.randint(0, 256, (S, n), dtype=torch.uint8, device="cuda", generator=g)
-        old = buf[:, row].clone()
-        r.update_batch(old, new, row, buf)
-        buf[:, row] = new
-        exp = buf.clone()
-        r.encode_batch(exp)
+    host = _oracle_stripes(orc, rng, d, p, S, n)
+    buf = torch.from_numpy(host).cuda()
+    for row in rows:
+        new = rng.integers(0, 256, (S, n), dtype=np.uint8)
+        r.update_batch(buf[:, row].clone(), torch.from_numpy(new).cuda(), row, buf)
         torch.cuda.synchronize()
-        assert torch.equal(buf, exp), row
+        got = buf[:, d:].cpu().numpy()
+        for s in range(S):
+            par = list(host[s, d:])
+            assert orc.update(d, p, host[s, row], new[s], row, par) == 0
+            assert all(np.array_equal(got[s, j], par[j]) for j in range(p)), (row, s)
+        host[:, row] = new
+        buf[:, row] = torch.from_numpy(new).cuda()
 
 
 def _replace_rows(rng, d):  # makeReplaceRowRandom rs_test.go:333-353
@@ -394,22 +423,28 @@ def test_replace_host(rslib, orc, torch_dev, to_zero):  # TestRS_Replace rs_test
             assert np.array_equal(act[d + j], ora[j])
 
 
-def test_replace_batch_1_to_6_rows(rslib, torch_dev):  # BASELINE config 5 (rn = 1..6)
+@pytest.mark.parametrize("S,rns", [(32768, [3]), (4096, [1, 2, 3, 4, 5, 6])])
+def test_replace_batch_1_to_6_rows(rslib, orc, torch_dev, S, rns):  # BASELINE config 5 (rn = 1..6)
+    """rs_replace_batch with 1-6 replaced rows (rs.go:492-529) at the
+    ops_bench batch size (rn = 3) and on 4,096 stripes for rn = 1..6: every
+    stripe's parity equals the oracle's Replace of the same rows."""
     torch = torch_dev
-    d, p, S, n = 10, 4, 32, 8192
+    d, p, n = 10, 4, 8192
+    rng = np.random.default_rng(397 + S)
     r = rslib.New(d, p)
-    g = torch.Generator(device="cuda").manual_seed(9)
-    for rn in range(1, 7):
-        full = torch.randint(0, 256, (S, d + p, n), dtype=torch.uint8, device="cuda", generator=g)
-        rows = list(range(rn))
-        zeroed = full.clone()
-        zeroed[:, rows] = 0
-        r.encode_batch(full)
-        r.encode_batch(zeroed)
-        data = full[:, rows].contiguous()
-        r.replace_batch(data, rows, zeroed)  # zero -> data
+    host = _oracle_stripes(orc, rng, d, p, S, n)
+    for rn in rns:
+        rows = sorted(int(x) for x in rng.choice(d, rn, replace=False))
+        data = rng.integers(0, 256, (S, rn, n), dtype=np.uint8)
+        buf = torch.from_numpy(host).cuda()
+        r.replace_batch(torch.from_numpy(data).cuda(), rows, buf)
         torch.cuda.synchronize()
-        assert torch.equal(zeroed[:, d:], full[:, d:]), rn
+        got = buf[:, d:].cpu().numpy()
+        del buf
+        for s in range(S):
+            par = [x.copy() for x in host[s, d:]]
+            assert orc.replace(d, p, list(data[s]), rows, par) == 0
+            assert all(np.array_equal(got[s, j], par[j]) for j in range(p)), (rn, s)
 
 
 def test_replace_dev(rslib, torch_dev):

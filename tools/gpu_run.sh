@@ -12,6 +12,7 @@
 #   tools/gpu_run.sh "ops:--only wide"                          # tools/ops_bench.py with args
 #   tools/gpu_run.sh "ab:AB_K=16,AB_M=16:op=rec16,jit=0:op=rec16,jit=2"   # tools/ab.py: env, then specs
 #   tools/gpu_run.sh "py:tools/some_probe.py args"              # any python script
+#   tools/gpu_run.sh "bin:tools/_build/valu_probe"              # a prebuilt probe binary
 #   tools/gpu_run.sh "prof:<tag>:<python args>"                 # rocprofv3 kernel trace + stats of a python command
 #   tools/gpu_run.sh "pmc:<tag>:<counters>:<python args>"       # one rocprofv3 --pmc pass (own run)
 set -uo pipefail
@@ -56,6 +57,10 @@ for step in "$@"; do
       IFS=',' read -ra ev <<< "$envs"
       timeout -k 10 600 env "${ev[@]}" python -u tools/ab.py "${sp[@]}" > "$log" 2>&1 || fail "$step" $? "$log"
       cat "$log" ;;
+    bin)
+      # shellcheck disable=SC2086
+      timeout -k 10 300 $arg > "$log" 2>&1 || fail "$step" $? "$log"
+      tail -40 "$log" ;;
     py)
       # shellcheck disable=SC2086
       timeout -k 10 900 python -u $arg > "$log" 2>&1 || fail "$step" $? "$log"

@@ -8,6 +8,11 @@ rs_test.go:450,489,556,598):
   Update   (2+2m)*vec         Replace  (rn+2m)*vec
 Device-resident numbers time HIP events around back-to-back launches on one
 stream; end-to-end numbers time host wall clock around the pinned pipeline.
+
+    python tools/ops_bench.py                    # every section
+    python tools/ops_bench.py --only wide,api    # some sections
+
+Sections: encode, shapes, split, rec8, rec4, multi, upd, wide, host, api.
 """
 import json
 import os
@@ -44,188 +49,248 @@ def rec(name, nbytes, t, **kw):
     print(f"{name:44s} {nbytes / t / GiB:10.2f} GiB/s  {t * 1e6:10.2f} us/call", flush=True)
 
 
+SECTIONS = ["encode", "shapes", "split", "rec8", "rec4", "multi", "upd", "wide", "host", "api"]
+
+
+def want(name):
+    only = None
+    if "--only" in sys.argv:
+        only = sys.argv[sys.argv.index("--only") + 1].split(",")
+    return only is None or name in only
+
+
+def wide(g):
+    """> 8 output rows: the single-pass wide kernels (and the run-time
+    compiled networks where they apply), ~3.5 GiB of stripes per launch."""
+    L = rs.lib()
+    for k, m, vec in ((16, 16, 1 << 20), (32, 32, 1 << 20), (64, 64, 1 << 20), (128, 128, 1 << 20), (200, 56, 1 << 20)):
+        S = max(1, (3584 << 20) // ((k + m) * vec))
+        r = rs.New(k, m)
+        data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
+        par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
+        for jit in ((0, 2) if m <= 16 else (0,)):
+            L.rs_tune(b"jit", jit)
+            t = dev_time(lambda: r.encode_batch_split(data, par), iters=10, warm=5)
+            rec(f"encode {k}+{m} {vec >> 10}KiB x{S} split, jit={jit} (device)", S * (k + m) * vec, t)
+        del data, par
+    for k, m, vec, lost in ((16, 16, 1 << 20, list(range(16))), (20, 12, 1 << 20, list(range(12))),
+                            (48, 16, 256 << 10, list(range(16))), (100, 28, 256 << 10, list(range(0, 40, 2))),
+                            (100, 28, 256 << 10, list(range(0, 84, 3)))):
+        S = max(1, (3584 << 20) // ((k + m) * vec))
+        r = rs.New(k, m)
+        data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
+        par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
+        r.encode_batch_split(data, par)
+        for jit, sp in (((0, 1), (0, 0), (2, 1)) if len(lost) <= 16 else ((0, 1), (0, 0))):
+            L.rs_tune(b"jit", jit)
+            L.rs_tune(b"wide_single_pass", sp)
+            t = dev_time(lambda: r.reconst_batch_split(data, par, [], lost), iters=10, warm=5)
+            rec(f"reconst {k}+{m} {vec >> 10}KiB lost={len(lost)} x{S} split, jit={jit} single_pass={sp}",
+                S * (k + len(lost)) * vec, t)
+        del data, par
+    L.rs_tune(b"jit", 2)
+    L.rs_tune(b"wide_single_pass", 1)
+
+
 def main():
     g = torch.Generator(device="cuda").manual_seed(42)
     # run-time bit-sliced kernels (5-8 output rows) compile on first use here,
     # so the timed calls run them (the library's default compiles in the
     # background and uses the perm-table kernels until the code is ready)
     rs.lib().rs_tune(b"jit", 2)
-    # ---- encode, device-resident
-    for k, m, vec, S in ((10, 4, 1 << 20, 256), (12, 4, 1 << 20, 256), (10, 4, 8 << 10, 32768), (10, 4, 8 << 10, 1)):
+    if want("wide"):
+        wide(g)
+    if want("encode"):
+        # ---- encode, device-resident
+        for k, m, vec, S in ((10, 4, 1 << 20, 256), (12, 4, 1 << 20, 256), (10, 4, 8 << 10, 32768), (10, 4, 8 << 10, 1)):
+            r = rs.New(k, m)
+            buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+            t = dev_time(lambda: r.encode_batch(buf))
+            rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
+            del buf
+    if want("shapes"):
+        # ---- other shapes (runtime-column kernels; 5-8 rows are VALU-bound)
+        for k, m in ((8, 4), (6, 3), (16, 4), (10, 6), (10, 8), (12, 8), (16, 8)):
+            vec, S = 1 << 20, 256 * 14 // (k + m)
+            r = rs.New(k, m)
+            buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+            t = dev_time(lambda: r.encode_batch(buf))
+            rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
+            del buf
+    if want("split"):
+        # ---- > 4 outputs on the split layout (data [S][k][vec], parity [S][m][vec],
+        # as bench.py): 16+8 Encode (no build-time network: run-time compiled) and
+        # 10+8 Reconst of 5 / 8 lost data vectors
+        for k, m in ((16, 8), (10, 8)):
+            vec, S = 1 << 20, 256 * 14 // (k + m)
+            r = rs.New(k, m)
+            data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
+            par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
+            t = dev_time(lambda: r.encode_batch_split(data, par))
+            rec(f"encode {k}+{m} {vec >> 10}KiB x{S} split (device)", S * (k + m) * vec, t)
+            if k == 10:
+                for lost in ([0, 2, 4, 6, 8], list(range(8))):
+                    t = dev_time(lambda: r.reconst_batch_split(data, par, [], lost))
+                    rec(f"reconst {k}+{m} 1MiB lost={len(lost)} data x{S} split", S * (k + len(lost)) * vec, t)
+            del data, par
+    if want("rec8"):
+        # ---- reconst of 5-8 lost at 10+8 @ 1 MiB (run-time matrices, > 4 outputs)
+        k, m, vec = 10, 8, 1 << 20
+        S = 256 * 14 // (k + m)
         r = rs.New(k, m)
         buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
-        t = dev_time(lambda: r.encode_batch(buf))
-        rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
+        r.encode_batch(buf)
+        for lost in ([0, 2, 4, 6, 8], list(range(8)), [0, 2, 4, 6, 10, 12, 14, 16]):
+            t = dev_time(lambda: r.reconst_batch(buf, [], lost))
+            rec(f"reconst 10+8 1MiB lost={len(lost)} ({'data' if max(lost) < k else 'data+parity'}) x{S}",
+                S * (k + len(lost)) * vec, t)
         del buf
-    # ---- other shapes (runtime-column kernels; 5-8 rows are VALU-bound)
-    for k, m in ((8, 4), (6, 3), (16, 4), (10, 6), (10, 8), (12, 8), (16, 8)):
-        vec, S = 1 << 20, 256 * 14 // (k + m)
+    if want("rec4") or want("multi") or want("upd"):
+        # ---- reconst 10+4 @ 8 KiB, 1-4 lost data shards (config 3)
+        k, m, vec, S = 10, 4, 8 << 10, 32768
         r = rs.New(k, m)
         buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
-        t = dev_time(lambda: r.encode_batch(buf))
-        rec(f"encode {k}+{m} {vec >> 10}KiB x{S} (device)", S * (k + m) * vec, t)
-        del buf
-    # ---- > 4 outputs on the split layout (data [S][k][vec], parity [S][m][vec],
-    # as bench.py): 16+8 Encode (no build-time network: run-time compiled) and
-    # 10+8 Reconst of 5 / 8 lost data vectors
-    for k, m in ((16, 8), (10, 8)):
-        vec, S = 1 << 20, 256 * 14 // (k + m)
-        r = rs.New(k, m)
-        data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
-        par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
-        t = dev_time(lambda: r.encode_batch_split(data, par))
-        rec(f"encode {k}+{m} {vec >> 10}KiB x{S} split (device)", S * (k + m) * vec, t)
-        if k == 10:
-            for lost in ([0, 2, 4, 6, 8], list(range(8))):
-                t = dev_time(lambda: r.reconst_batch_split(data, par, [], lost))
-                rec(f"reconst {k}+{m} 1MiB lost={len(lost)} data x{S} split", S * (k + len(lost)) * vec, t)
-        del data, par
-    # ---- reconst of 5-8 lost at 10+8 @ 1 MiB (run-time matrices, > 4 outputs)
-    k, m, vec = 10, 8, 1 << 20
-    S = 256 * 14 // (k + m)
-    r = rs.New(k, m)
-    buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
-    r.encode_batch(buf)
-    for lost in ([0, 2, 4, 6, 8], list(range(8)), [0, 2, 4, 6, 10, 12, 14, 16]):
-        t = dev_time(lambda: r.reconst_batch(buf, [], lost))
-        rec(f"reconst 10+8 1MiB lost={len(lost)} ({'data' if max(lost) < k else 'data+parity'}) x{S}",
-            S * (k + len(lost)) * vec, t)
-    del buf
-    # ---- reconst 10+4 @ 8 KiB, 1-4 lost data shards (config 3)
-    k, m, vec, S = 10, 4, 8 << 10, 32768
-    r = rs.New(k, m)
-    buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
-    r.encode_batch(buf)
-    for lost in ([0], [0, 5], [0, 5, 9], [0, 3, 5, 9]):
-        t = dev_time(lambda: r.reconst_batch(buf, [], lost))
-        rec(f"reconst 10+4 8KiB lost={len(lost)} data x{S}", S * (k + len(lost)) * vec, t)
-        t1 = dev_time(lambda: r.reconst_batch(buf[:1], [], lost))
-        rec(f"reconst 10+4 8KiB lost={len(lost)} data x1", (k + len(lost)) * vec, t1)
-    # ---- multi-pattern reconst: every stripe its own 1-4 erasures (16 distinct patterns)
-    import numpy as np
+        r.encode_batch(buf)
+        for lost in ([0], [0, 5], [0, 5, 9], [0, 3, 5, 9]):
+            t = dev_time(lambda: r.reconst_batch(buf, [], lost))
+            rec(f"reconst 10+4 8KiB lost={len(lost)} data x{S}", S * (k + len(lost)) * vec, t)
+            t1 = dev_time(lambda: r.reconst_batch(buf[:1], [], lost))
+            rec(f"reconst 10+4 8KiB lost={len(lost)} data x1", (k + len(lost)) * vec, t1)
+        # ---- multi-pattern reconst: every stripe its own 1-4 erasures (16 distinct patterns)
+        import numpy as np
 
-    rng = np.random.default_rng(5)
-    pats = []
-    for _ in range(16):
-        lost = rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False)
-        pats.append(sum(1 << int(v) for v in lost))
-    masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
-    nrec = sum(bin(int(x)).count("1") for x in masks)
-    # full warm-up: the single-stripe calls above leave the GPU idle enough to
-    # drop its clocks, and 5 warm-up calls did not bring them back (4,934 GiB/s
-    # with warm=5 vs ~5,700 in tools/multi_mix.py on the same box)
-    t = dev_time(lambda: r.reconst_batch_multi(buf[:, :k], buf[:, k:], masks))
-    rec(f"reconst_multi 10+4 8KiB 16 patterns x{S}", (S * k + nrec) * vec, t)
-    # ---- update / replace 10+4 @ 8 KiB (config 5)
-    old = buf[:, 3].clone()
-    new = torch.randint(0, 256, (S, vec), dtype=torch.uint8, device="cuda", generator=g)
-    t = dev_time(lambda: r.update_batch(old, new, 3, buf))
-    rec(f"update 10+4 8KiB x{S}", S * (2 + 2 * m) * vec, t)
-    for rn in range(1, 7):
-        data = torch.randint(0, 256, (S, rn, vec), dtype=torch.uint8, device="cuda", generator=g)
-        t = dev_time(lambda: r.replace_batch(data, list(range(rn)), buf))
-        rec(f"replace 10+4 8KiB rn={rn} x{S}", S * (rn + 2 * m) * vec, t)
-    del buf
-    torch.cuda.empty_cache()
-    # ---- host-resident end-to-end (pinned), 10+4 @ 1 MiB
-    k, m, vec, S = 10, 4, 1 << 20, 128
-    r = rs.New(k, m)
-    host = torch.empty((S, k + m, vec), dtype=torch.uint8, pin_memory=True)
-    host.copy_(torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g).cpu())
-    L = rs.lib()
-    r.encode_host_batch(host)  # warm (zero-copy: pinned memory is device-mapped)
-    t0 = time.perf_counter()
-    for _ in range(3):
-        r.encode_host_batch(host)
-    rec(f"encode 10+4 1MiB x{S} host->host pinned, zero-copy", S * (k + m) * vec, (time.perf_counter() - t0) / 3)
-    L.rs_tune(b"host_batch_zc", 0)
-    for spc, nst in ((2, 3), (4, 3), (8, 3), (8, 4), (16, 3)):
-        r.encode_host_batch(host, spc, nst)  # warm
-        t0 = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            r.encode_host_batch(host, spc, nst)
-        t = (time.perf_counter() - t0) / reps
-        rec(f"encode 10+4 1MiB x{S} host->host pinned, DMA pipeline spc={spc} streams={nst}", S * (k + m) * vec, t)
-    L.rs_tune(b"host_batch_zc", 1)
-    # pageable (ordinary) host memory: staged through the pinned mirror
-    for pv, pS in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64)):
-        pg = np.random.default_rng(3).integers(0, 256, (pS, k + m, pv), dtype=np.uint8)
-        r.encode_host_batch(pg)  # warm
+        rng = np.random.default_rng(5)
+        pats = []
+        for _ in range(16):
+            lost = rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False)
+            pats.append(sum(1 << int(v) for v in lost))
+        masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
+        nrec = sum(bin(int(x)).count("1") for x in masks)
+        # full warm-up: the single-stripe calls above leave the GPU idle enough to
+        # drop its clocks, and 5 warm-up calls did not bring them back (4,934 GiB/s
+        # with warm=5 vs ~5,700 in tools/multi_mix.py on the same box)
+        t = dev_time(lambda: r.reconst_batch_multi(buf[:, :k], buf[:, k:], masks))
+        rec(f"reconst_multi 10+4 8KiB 16 patterns x{S}", (S * k + nrec) * vec, t)
+        # ---- update / replace 10+4 @ 8 KiB (config 5)
+        old = buf[:, 3].clone()
+        new = torch.randint(0, 256, (S, vec), dtype=torch.uint8, device="cuda", generator=g)
+        t = dev_time(lambda: r.update_batch(old, new, 3, buf))
+        rec(f"update 10+4 8KiB x{S}", S * (2 + 2 * m) * vec, t)
+        for rn in range(1, 7):
+            data = torch.randint(0, 256, (S, rn, vec), dtype=torch.uint8, device="cuda", generator=g)
+            t = dev_time(lambda: r.replace_batch(data, list(range(rn)), buf))
+            rec(f"replace 10+4 8KiB rn={rn} x{S}", S * (rn + 2 * m) * vec, t)
+        del buf
+        torch.cuda.empty_cache()
+    if want("host"):
+        # ---- host-resident end-to-end (pinned), 10+4 @ 1 MiB
+        k, m, vec, S = 10, 4, 1 << 20, 128
+        r = rs.New(k, m)
+        host = torch.empty((S, k + m, vec), dtype=torch.uint8, pin_memory=True)
+        host.copy_(torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g).cpu())
+        L = rs.lib()
+        r.encode_host_batch(host)  # warm (zero-copy: pinned memory is device-mapped)
         t0 = time.perf_counter()
         for _ in range(3):
-            r.encode_host_batch(pg)
-        rec(f"encode 10+4 {pv >> 10}KiB x{pS} host->host pageable (staged)", pS * (k + m) * pv,
-            (time.perf_counter() - t0) / 3)
-        del pg
-    # PCIe reference rates (one direction at a time, then both at once)
-    dbuf = torch.empty((S * k * vec,), dtype=torch.uint8, device="cuda")
-    hflat = host.view(-1)[: S * k * vec]
-    t0 = time.perf_counter()
-    dbuf.copy_(hflat, non_blocking=True)
-    torch.cuda.synchronize()
-    rec("H2D pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
-    t0 = time.perf_counter()
-    hflat.copy_(dbuf, non_blocking=True)
-    torch.cuda.synchronize()
-    rec("D2H pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    half = host.numel() // 2
-    ha, hb = host.view(-1)[:half], host.view(-1)[half: 2 * half]
-    da, db = torch.empty(half, dtype=torch.uint8, device="cuda"), torch.empty(half, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(s1):
-        da.copy_(ha, non_blocking=True)
-    with torch.cuda.stream(s2):
-        hb.copy_(db, non_blocking=True)
-    torch.cuda.synchronize()
-    rec("H2D + D2H concurrently (torch, sum of both)", 2 * half, time.perf_counter() - t0)
-    del da, db
-    # verify the pipelined parity against a device encode of the same stripes
-    chk = host[:4].cuda()
-    ref = chk.clone()
-    r.encode_batch(ref)
-    torch.cuda.synchronize()
-    assert torch.equal(chk, ref), "host pipeline parity mismatch"
-    # ---- host-memory Go-API calls (pageable numpy buffers), per-call latency
-    import numpy as np
-
-    L = rs.lib()
-    modes = (("default: chunked zero-copy pipeline", 256 << 10, -1),
-             ("staged: pinned mirror + DMA <= 4MiB", 4 << 20, 0),
-             ("staged: pageable per-vector copies", 0, 0))
-    for label, pinned_max, zc_max in modes:
-        L.rs_tune(b"host_pinned_max", pinned_max)
-        L.rs_tune(b"host_zc_max", zc_max)
-        for vec in (8 << 10, 64 << 10, 256 << 10, 1 << 20):
-            rng = np.random.default_rng(1)
-            v = [rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] + [np.zeros(vec, np.uint8)
-                                                                                 for _ in range(m)]
-            for _ in range(5):
-                r.Encode(v)
-            n = 50 if vec > 65536 else 500
+            r.encode_host_batch(host)
+        rec(f"encode 10+4 1MiB x{S} host->host pinned, zero-copy", S * (k + m) * vec, (time.perf_counter() - t0) / 3)
+        L.rs_tune(b"host_batch_zc", 0)
+        for spc, nst in ((2, 3), (4, 3), (8, 3), (8, 4), (16, 3)):
+            r.encode_host_batch(host, spc, nst)  # warm
             t0 = time.perf_counter()
-            for _ in range(n):
-                r.Encode(v)
-            t = (time.perf_counter() - t0) / n
-            rec(f"Encode() host API 10+4 {vec >> 10}KiB ({label})", (k + m) * vec, t)
-            if vec == 8 << 10:
-                full = [x.copy() for x in v]
-                for lost in ([0], [0, 1, 2, 3]):
-                    w = [x.copy() for x in full]
-                    for _ in range(5):
-                        r.Reconst(w, [], lost)
-                    t0 = time.perf_counter()
-                    for _ in range(n):
-                        r.Reconst(w, [], lost)
-                    t = (time.perf_counter() - t0) / n
-                    assert all(np.array_equal(a, b) for a, b in zip(w, full))
-                    rec(f"Reconst() host API 10+4 8KiB lost={len(lost)} ({label})", (k + len(lost)) * vec, t)
-    L.rs_tune(b"host_pinned_max", 256 << 10)
-    L.rs_tune(b"host_zc_max", -1)
+            reps = 3
+            for _ in range(reps):
+                r.encode_host_batch(host, spc, nst)
+            t = (time.perf_counter() - t0) / reps
+            rec(f"encode 10+4 1MiB x{S} host->host pinned, DMA pipeline spc={spc} streams={nst}", S * (k + m) * vec, t)
+        L.rs_tune(b"host_batch_zc", 1)
+        # pageable (ordinary) host memory: staged through the pinned mirror
+        for pv, pS in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64)):
+            pg = np.random.default_rng(3).integers(0, 256, (pS, k + m, pv), dtype=np.uint8)
+            r.encode_host_batch(pg)  # warm
+            t0 = time.perf_counter()
+            for _ in range(3):
+                r.encode_host_batch(pg)
+            rec(f"encode 10+4 {pv >> 10}KiB x{pS} host->host pageable (staged)", pS * (k + m) * pv,
+                (time.perf_counter() - t0) / 3)
+            del pg
+        # PCIe reference rates (one direction at a time, then both at once)
+        dbuf = torch.empty((S * k * vec,), dtype=torch.uint8, device="cuda")
+        hflat = host.view(-1)[: S * k * vec]
+        t0 = time.perf_counter()
+        dbuf.copy_(hflat, non_blocking=True)
+        torch.cuda.synchronize()
+        rec("H2D pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        hflat.copy_(dbuf, non_blocking=True)
+        torch.cuda.synchronize()
+        rec("D2H pinned copy (torch)", S * k * vec, time.perf_counter() - t0)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        half = host.numel() // 2
+        ha, hb = host.view(-1)[:half], host.view(-1)[half: 2 * half]
+        da, db = torch.empty(half, dtype=torch.uint8, device="cuda"), torch.empty(half, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s1):
+            da.copy_(ha, non_blocking=True)
+        with torch.cuda.stream(s2):
+            hb.copy_(db, non_blocking=True)
+        torch.cuda.synchronize()
+        rec("H2D + D2H concurrently (torch, sum of both)", 2 * half, time.perf_counter() - t0)
+        del da, db
+        # verify the pipelined parity against a device encode of the same stripes
+        chk = host[:4].cuda()
+        ref = chk.clone()
+        r.encode_batch(ref)
+        torch.cuda.synchronize()
+        assert torch.equal(chk, ref), "host pipeline parity mismatch"
+    if want("api"):
+        # ---- host-memory Go-API calls (pageable numpy buffers), per-call latency
+        import numpy as np
+
+        L = rs.lib()
+        k, m = 10, 4
+        r = rs.New(k, m)
+        # (label, host_pinned_max, host_zc_max, host_engine); the library's
+        # defaults are 256 KiB / 2 MiB / engine on
+        modes = (("default: host-call engine up to 1 MiB", 256 << 10, 2 << 20, 1),
+                 ("engine off: chunked zero-copy pipeline", 256 << 10, 2 << 20, 0),
+                 ("engine off, staged: pinned mirror + DMA <= 4MiB", 4 << 20, 0, 0),
+                 ("engine off, staged: pageable per-vector copies", 0, 0, 0))
+        for label, pinned_max, zc_max, engine in modes:
+            L.rs_tune(b"host_pinned_max", pinned_max)
+            L.rs_tune(b"host_zc_max", zc_max)
+            L.rs_tune(b"host_engine", engine)
+            for vec in (8 << 10, 64 << 10, 256 << 10, 1 << 20):
+                rng = np.random.default_rng(1)
+                v = [rng.integers(0, 256, vec, dtype=np.uint8) for _ in range(k)] + [np.zeros(vec, np.uint8)
+                                                                                     for _ in range(m)]
+                for _ in range(5):
+                    r.Encode(v)
+                n = 50 if vec > 65536 else 500
+                t0 = time.perf_counter()
+                for _ in range(n):
+                    r.Encode(v)
+                t = (time.perf_counter() - t0) / n
+                rec(f"Encode() host API 10+4 {vec >> 10}KiB ({label})", (k + m) * vec, t)
+                if vec == 8 << 10:
+                    full = [x.copy() for x in v]
+                    for lost in ([0], [0, 1, 2, 3]):
+                        w = [x.copy() for x in full]
+                        for _ in range(5):
+                            r.Reconst(w, [], lost)
+                        t0 = time.perf_counter()
+                        for _ in range(n):
+                            r.Reconst(w, [], lost)
+                        t = (time.perf_counter() - t0) / n
+                        assert all(np.array_equal(a, b) for a, b in zip(w, full))
+                        rec(f"Reconst() host API 10+4 8KiB lost={len(lost)} ({label})", (k + len(lost)) * vec, t)
+        L.rs_tune(b"host_pinned_max", 256 << 10)
+        L.rs_tune(b"host_zc_max", 2 << 20)
+        L.rs_tune(b"host_engine", 1)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ops_bench.json"), "w"), indent=1)
+    tag = "_".join(sys.argv[sys.argv.index("--only") + 1].split(",")) if "--only" in sys.argv else "all"
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"ops_bench_{tag}.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
