@@ -362,7 +362,8 @@ RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches
 RS_API int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects);
 
 /* Compile the run-time kernel for a rows x cols matrix (row-major, 5 <= rows
- * <= 16, 1 <= cols <= 64; accumulate 1 = the XOR-into-outputs form Update /
+ * <= 128 and 1 <= cols <= 256 with the assembly backend, <= 16 x 64 with
+ * hiprtc; accumulate 1 = the XOR-into-outputs form Update /
  * Replace use) for the handle's device now, instead of on the matrix's
  * second large launch: wait 1 compiles and loads it on the calling thread
  * (RS_OK, or RS_ERR_DEVICE if the compile failed), wait 0 queues the compile
@@ -372,12 +373,20 @@ RS_API int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes
  * (rs_reconst_matrix).  RS_ERR_INVAL for shapes outside those bounds. */
 RS_API int rs_jit_prepare(rs_t* rs, const uint8_t* mat, int rows, int cols, int accumulate, int wait);
 
-/* Generate and compile (hiprtc, no device needed) the run-time kernel for a
- * rows x cols matrix (row-major, 5 <= rows <= 16, 1 <= cols <= 64), overwrite
+/* Generate and compile (comgr / hiprtc, no device needed) the run-time kernel
+ * for a rows x cols matrix (row-major, bounds as rs_jit_prepare), overwrite
  * (accumulate 0) or XOR-into-outputs (1) mode.  RS_OK, RS_ERR_INVAL (shape)
  * or RS_ERR_DEVICE (compile failed: the log goes to stderr).  ms may be NULL.
  * For tests and warm-up. */
 RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms);
+
+/* The gfx950 assembly the run-time kernel generator emits for a rows x cols
+ * matrix (row-major, 1 <= rows <= 128, 1 <= cols <= 256), overwrite
+ * (accumulate 0) or XOR-into-outputs (1): copied NUL-terminated into
+ * buf[len] (truncated if short).  Returns the length needed including the
+ * NUL, or -RS_ERR_INVAL.  For tests (a CPU emulator runs it against the
+ * oracle) and inspection; no device needed. */
+RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int accumulate, char* buf, size_t len);
 
 /* Expert launch knobs, process-wide (for A/B experiments; defaults are the
  * tuned values; every setting computes the same bytes, which
@@ -433,7 +442,10 @@ RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accu
  * "jit_min_rows" (launches with fewer output rows stay on the table kernels;
  * default 5),
  * "jit_pf" (columns loaded ahead in
- * the compiled kernels, 1..6, default 3), "jit_disk_cache" (1 default: compiled
+ * the compiled kernels, 1..6 (1..4 for assembly kernels), default 3),
+ * "jit_backend" (1 default: kernels emitted as gfx950 assembly and assembled
+ * by comgr, tens of ms per matrix, up to 128 output rows x 256 columns | 0:
+ * C++ compiled by hiprtc, seconds per matrix, up to 16 x 64), "jit_disk_cache" (1 default: compiled
  * code objects are kept in an on-disk cache shared by processes, see
  * rs_jit_cache_stats | 0: compile in every process),
  * "table_registry_max" (distinct coefficient matrices

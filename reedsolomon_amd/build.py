@@ -26,9 +26,11 @@ LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "librsamd.so")
 LIB_EXP = os.path.join(LIB_DIR, "librsamd_exp.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("codec.cpp", "host_calls.cpp", "batches.cpp", "host_batches.cpp",
-                                           "engine.cpp", "watchdog.cpp", "jit.cpp", "kernels.hip")]
+                                           "engine.cpp", "watchdog.cpp", "jit.cpp", "jit_asm.cpp",
+                                           "kernels.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("gf256.hpp", "kernels.hpp", "codec_internal.hpp",
-                                                  "host_pool.hpp", "watchdog.hpp", "jit.hpp", "bitslice_gen.inc")] + [
+                                                  "host_pool.hpp", "watchdog.hpp", "jit.hpp", "jit_asm.hpp",
+                                                  "bitslice_gen.inc")] + [
     os.path.join(ROOT, "include", "rs_amd.h")
 ]
 ARCH = os.environ.get("RSAMD_OFFLOAD_ARCH", "gfx950")
@@ -59,7 +61,7 @@ def build(force: bool = False, verbose: bool = False, experiments: bool = False)
         "-fvisibility=hidden", "-Wall", "-Wno-unused-result",
         *(["-DRSAMD_EXPERIMENTS"] if experiments else []),
         "-I", os.path.join(ROOT, "include"),
-        *SOURCES, "-o", tmp, "-lhiprtc", "-ldl",
+        *SOURCES, "-o", tmp, "-lhiprtc", "-lamd_comgr", "-ldl",
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

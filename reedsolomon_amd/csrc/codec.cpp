@@ -543,6 +543,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_min_launches") g_jit_min_launches = value < 1 ? 1 : value;
         else if (n == "jit_pf") g_jit_pf = value < 1 ? 1 : value > 6 ? 6 : value;
         else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;
+        else if (n == "jit_backend") g_jit_backend = value ? 1 : 0;
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
@@ -646,12 +647,28 @@ int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint6
 
 int rs_jit_prepare(rs_t* rs, const uint8_t* mat, int rows, int cols, int accumulate, int wait) {
     return abi_guard([&]() -> int {
-        if (!rs || !mat || rows < kJitMinRows || rows > kJitMaxRows || cols < 1 || cols > kJitMaxCols)
+        if (!rs || !mat || rows < kJitMinRows || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols())
             return RS_ERR_INVAL;
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         return jit_prepare(mat, rows, cols, accumulate != 0, wait != 0);
     });
+}
+
+int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int accumulate, char* buf, size_t len) {
+    try {
+        std::string s;
+        const int rc = jit_asm_source_text(mat, rows, cols, accumulate != 0, &s);
+        if (rc) return -rc;
+        if (buf && len) {
+            const size_t n = s.size() < len - 1 ? s.size() : len - 1;
+            std::memcpy(buf, s.data(), n);
+            buf[n] = 0;
+        }
+        return static_cast<int64_t>(s.size()) + 1;
+    } catch (...) {
+        return -RS_ERR_NOMEM;
+    }
 }
 
 int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms) {

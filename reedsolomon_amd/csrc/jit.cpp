@@ -59,6 +59,7 @@
 #include <thread>
 #include <vector>
 
+#include "jit_asm.hpp"
 #include "rs_amd.h"
 
 namespace rsamd {
@@ -72,6 +73,12 @@ int g_jit_min_launches = 2;
 int g_jit_min_rows = kJitMinRows;
 int g_jit_min_acc_cols = kJitMinAccCols;
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
+int g_jit_backend = [] {  // rs_tune("jit_backend", 1 | 0): assembly (jit_asm.cpp) | hiprtc C++; env RSAMD_JIT_BACKEND
+    const char* e = std::getenv("RSAMD_JIT_BACKEND");
+    return e ? (std::atoi(e) ? 1 : 0) : 1;
+}();
+int jit_max_rows() { return g_jit_backend ? kAsmMaxRows : kJitMaxRows; }
+int jit_max_cols() { return g_jit_backend ? kAsmMaxCols : kJitMaxCols; }
 int g_jit_disk_cache = [] {  // rs_tune("jit_disk_cache", 0 | 1); env RSAMD_JIT_DISK_CACHE
     const char* e = std::getenv("RSAMD_JIT_DISK_CACHE");
     return e ? (std::atoi(e) ? 1 : 0) : 1;
@@ -416,6 +423,12 @@ struct Compiled {
     std::string log;
 };
 
+Compiled compile_asm(const std::string& src) {
+    Compiled out;
+    out.ok = asm_assemble(src, &out.code, &out.log, &out.ms);
+    return out;
+}
+
 Compiled compile(const std::string& src) {
     Compiled out;
     const auto t0 = std::chrono::steady_clock::now();
@@ -474,6 +487,8 @@ Compiled compile(const std::string& src) {
 
 struct Entry {
     enum State { kQueued, kCompiling, kReady, kLoaded, kFailed } state = kQueued;
+    bool is_asm = false;  // generated assembly (rs_bs_asm) or hiprtc C++ (rs_bs_jit_64 / _256)
+    int nw = 1;           // assembly kernels: waves per workgroup
     std::string src;
     DiskKey disk;  // on-disk cache key (text empty: the disk cache is off)
     std::vector<char> code;
@@ -504,7 +519,7 @@ struct Jit {
     std::atomic<uint64_t> launches{0};
 
     void run_one(const std::shared_ptr<Entry>& e) {  // caller does not hold mu
-        Compiled c = compile(e->src);
+        Compiled c = e->is_asm ? compile_asm(e->src) : compile(e->src);
         // The compiler libraries hiprtc loads on its first compile register
         // their static destructors then, i.e. after jit_atexit: those ran
         // first at exit and a compile still in flight on the worker crashed
@@ -590,8 +605,10 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
 }
 
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
-    if (!mat || rows < kJitMinRows || rows > kJitMaxRows || cols < 1 || cols > kJitMaxCols) return RS_ERR_INVAL;
-    Compiled c = compile(jit_source(mat, rows, cols, accumulate));
+    if (!mat || rows < 1 || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
+    Compiled c = g_jit_backend
+                     ? compile_asm(asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, nullptr))
+                     : compile(jit_source(mat, rows, cols, accumulate));
     if (ms) *ms = c.ms;
     if (!c.ok) std::fprintf(stderr, "librsamd: jit compile check failed: %s\n", c.log.substr(0, 4000).c_str());
     return c.ok ? RS_OK : RS_ERR_DEVICE;
@@ -639,7 +656,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
         return std::string(b);
     }();
     DiskKey k;
-    k.text = arch + '\n' + fixed + '\n';
+    k.text = arch + '\n' + fixed + (g_jit_backend ? " asm " : " hiprtc ") + '\n';
     k.text += static_cast<char>(a.accumulate ? 1 : 0);
     k.text += static_cast<char>(a.rows);
     k.text += static_cast<char>(a.cols);
@@ -651,29 +668,32 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
 }
 
 // mode: 1 background after recurrence, 2 compile on this thread, 3 queue now
-static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int mode) {
-    if (!mode || !a.host_mat || a.rows < 1 || a.rows > kJitMaxRows || a.cols < 1 ||
-        a.cols > kJitMaxCols)
-        return nullptr;
+static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int mode) {
+    const int backend = g_jit_backend;
+    if (!mode || !a.host_mat || a.rows < 1 || a.rows > jit_max_rows() || a.cols < 1 || a.cols > jit_max_cols())
+        return {};
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (hipGetDevice(&dev) != hipSuccess) return {};
+    Jit& j = jit();
+    std::shared_ptr<Entry> e;
+    std::unique_lock<std::mutex> lk(j.mu);
     // the generated code is gfx950 code (v_bitop3, buffer nt): other devices
     // keep the perm-table kernels (no compile is ever attempted for them)
     const std::string& arch = device_arch(dev);
-    if (arch.compare(0, 6, "gfx950") != 0) return nullptr;
+    if (arch.compare(0, 6, "gfx950") != 0) return {};
     std::string key(reinterpret_cast<const char*>(&dev), sizeof dev);
+    key += static_cast<char>(backend);
     key += static_cast<char>(a.accumulate ? 1 : 0);
     key += static_cast<char>(a.rows);
+    key += static_cast<char>(a.rows >> 8);
     key += static_cast<char>(a.cols);
+    key += static_cast<char>(a.cols >> 8);
     key += static_cast<char>(g_jit_pf);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
-    Jit& j = jit();
-    std::shared_ptr<Entry> e;
     {
-        std::unique_lock<std::mutex> lk(j.mu);
         auto it = j.entries.find(key);
         if (it == j.entries.end()) {
-            if (j.entries.size() >= kMaxEntries) return nullptr;
+            if (j.entries.size() >= kMaxEntries) return {};
             // a code object on disk (another process, an earlier run): load it
             // now whatever the launch history; checked once per matrix
             DiskKey dk;
@@ -690,6 +710,8 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
                     disk_stats().hits.fetch_add(1, std::memory_order_relaxed);
                     if (h) j.seen.erase(key);
                     e = std::make_shared<Entry>();
+                    e->is_asm = backend != 0;
+                    e->nw = asm_waves(a.rows);
                     e->code = std::move(code);
                     e->state = Entry::kReady;
                     e->disk = std::move(dk);
@@ -707,11 +729,14 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
                 ++h.launches;
                 h.bytes += launch_bytes;
                 if (h.launches < static_cast<uint64_t>(g_jit_min_launches) || h.bytes < g_jit_min_bytes)
-                    return nullptr;
+                    return {};
                 j.seen.erase(key);
             }
             e = std::make_shared<Entry>();
-            e->src = jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
+            e->is_asm = backend != 0;
+            e->nw = asm_waves(a.rows);
+            e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->nw, g_jit_pf, nullptr)
+                               : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             if (g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
             j.entries.emplace(key, e);
             if (mode == 2) {
@@ -734,24 +759,33 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
                     j.worker = std::thread([&j] { j.work(); });
                 }
                 j.cv.notify_one();
-                return nullptr;
+                return {};
             }
         } else {
             e = it->second;
         }
-        if (e->state == Entry::kLoaded) return bs == 256 ? e->fn256 : e->fn64;
-        if (e->state != Entry::kReady) return nullptr;
+        auto result = [&]() -> JitKernel {
+            JitKernel k;
+            k.is_asm = e->is_asm;
+            k.nw = e->nw;
+            k.fn = e->is_asm ? e->fn64 : (bs == 256 ? e->fn256 : e->fn64);
+            return k;
+        };
+        if (e->state == Entry::kLoaded) return result();
+        if (e->state != Entry::kReady) return {};
         // load the code object on this device (launching thread, under mu)
         hipModule_t m = nullptr;
         hipFunction_t f64 = nullptr, f256 = nullptr;
-        if (hipModuleLoadData(&m, e->code.data()) != hipSuccess ||
-            hipModuleGetFunction(&f64, m, "rs_bs_jit_64") != hipSuccess ||
-            hipModuleGetFunction(&f256, m, "rs_bs_jit_256") != hipSuccess) {
+        const bool ok = hipModuleLoadData(&m, e->code.data()) == hipSuccess &&
+                        (e->is_asm ? hipModuleGetFunction(&f64, m, "rs_bs_asm") == hipSuccess
+                                   : hipModuleGetFunction(&f64, m, "rs_bs_jit_64") == hipSuccess &&
+                                         hipModuleGetFunction(&f256, m, "rs_bs_jit_256") == hipSuccess);
+        if (!ok) {
             (void)hipGetLastError();
             e->state = Entry::kFailed;
             ++j.failed;
             std::fprintf(stderr, "librsamd: run-time kernel load failed (perm-table kernels stay in use)\n");
-            return nullptr;
+            return {};
         }
         e->module = m;
         e->fn64 = f64;
@@ -759,24 +793,30 @@ static hipFunction_t lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, 
         e->state = Entry::kLoaded;
         e->code.clear();
         e->code.shrink_to_fit();
-        return bs == 256 ? f256 : f64;
+        return result();
     }
 }
 
-hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
+JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
     return lookup(a, bs, launch_bytes, g_jit_mode);
 }
 
+int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out) {
+    if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
+    *out = asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, nullptr);
+    return RS_OK;
+}
+
 int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wait) {
-    if (!mat || rows < kJitMinRows || rows > kJitMaxRows || cols < 1 || cols > kJitMaxCols) return RS_ERR_INVAL;
+    if (!mat || rows < kJitMinRows || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
     MatmulArgs a;
     std::memset(&a, 0, sizeof a);
     a.host_mat = mat;
     a.rows = rows;
     a.cols = cols;
     a.accumulate = accumulate ? 1 : 0;
-    const hipFunction_t f = lookup(a, 64, ~uint64_t{0}, wait ? 2 : 3);
-    return (f || !wait) ? RS_OK : RS_ERR_DEVICE;
+    const JitKernel k = lookup(a, 64, ~uint64_t{0}, wait ? 2 : 3);
+    return (k.fn || !wait) ? RS_OK : RS_ERR_DEVICE;
 }
 
 }  // namespace rsamd

@@ -37,10 +37,29 @@ extern int g_jit_pf;
 // been launched this many times, moving jit_min_bytes in total (default 2)
 extern int g_jit_min_launches;
 
+// rs_tune("jit_backend", 1 | 0): kernels generated as gfx950 assembly and
+// assembled by comgr (jit_asm.cpp; default: tens of ms per matrix, up to 128
+// rows x 256 columns) | C++ compiled by hiprtc (1-16 s, up to 16 x 64)
+extern int g_jit_backend;
+int jit_max_rows();
+int jit_max_cols();
+
+// A compiled kernel for a launch: the hiprtc kernels take MatmulArgs and a
+// 1-D grid of chunks (rs_bs_jit_64 / _256); the assembly kernel takes AsmArgs
+// (jit_asm.hpp), grid (2 KiB chunks, stripes) and nw waves per workgroup.
+struct JitKernel {
+    hipFunction_t fn = nullptr;
+    bool is_asm = false;
+    int nw = 1;
+};
 // The compiled kernel for this launch's matrix (a.host_mat, a.rows, a.cols,
-// a.accumulate) on the current device with `bs`-lane workgroups (64 or 256),
-// or nullptr (JIT off, shape not covered, not compiled yet, or failed).
-hipFunction_t jit_bitslice_for(const MatmulArgs& a, int bs, uint64_t launch_bytes);
+// a.accumulate) on the current device (hiprtc kernels: `bs`-lane
+// workgroups, 64 or 256), or fn == nullptr (JIT off, shape not covered, not
+// compiled yet, or failed).
+JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes);
+// The assembly source the generator emits for a matrix (tests: the CPU
+// emulator in tests/asm_emu.py runs it against the oracle).
+int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out);
 void jit_count_launch();
 
 // The kernel source for one matrix (rows x cols, row-major); exposed for the

@@ -1,0 +1,41 @@
+// jit_asm.hpp — run-time bit-sliced kernels emitted as gfx950 assembly
+// (jit_asm.cpp): the kernel-argument block and the generator / assembler.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+namespace rsamd {
+
+// Kernel arguments of the generated kernels (by value, 3,136 bytes).  Vector v
+// (inputs [0, cols), outputs [cols, cols + rows)) of stripe s is at
+// ptr[v] + s * 16 * stride16[v]; launch stripe y (grid y, offset by stripe0
+// for launches of more than 65,535 stripes) is stripe stripe_ids[stripe0 + y]
+// (stripe_ids == 0: stripe0 + y).  `body` bytes of each vector are processed
+// (a multiple of 16; the rest is the byte kernel's).
+struct AsmArgs {
+    uint32_t body;
+    uint32_t stripe0;
+    uint64_t stripe_ids;
+    uint64_t ptr[kMaxPtrs];
+    uint32_t stride16[kMaxPtrs];
+};
+static_assert(offsetof(AsmArgs, ptr) == 16 && offsetof(AsmArgs, stride16) == 16 + 8 * kMaxPtrs, "AsmArgs layout");
+
+constexpr int kAsmMaxRows = 128, kAsmMaxCols = 256;  // (up to 8 waves of 16 rows)
+constexpr int kAsmChunk = 2048;                      // bytes of each vector per workgroup
+
+// Waves per workgroup for a rows-row matrix (16 rows per wave at most).
+inline int asm_waves(int rows) { return rows <= 16 ? 1 : (rows + 15) / 16; }
+
+// The assembly source of the kernel for a rows x cols matrix (row-major),
+// accumulate (XOR into the outputs) or overwrite, nw waves per workgroup,
+// pf columns of loads in flight.  *vgprs receives the VGPRs per lane.
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int* vgprs);
+// Assemble + link (comgr) into a code object; false with the log on failure.
+bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* log, double* ms);
+
+}  // namespace rsamd

@@ -29,6 +29,7 @@
 //    kernel with identical arithmetic.
 #include "kernels.hpp"
 #include "jit.hpp"
+#include "jit_asm.hpp"
 
 #include <cstdlib>
 #include <cstring>
@@ -1429,19 +1430,50 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         }
         if (bk) a.body = 0;  // the vector path below is done; only the tail remains
     }
-    // 5-16 output rows over a run-time matrix: the bit-sliced network compiled
-    // for this matrix (jit.cpp), once it is ready
+    // 5-128 output rows over a run-time matrix: the bit-sliced network
+    // generated for this matrix (jit.cpp / jit_asm.cpp), once it is ready
     // (XOR-accumulate launches from jit_min_acc_cols columns on: jit.hpp)
-    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= g_jit_min_rows && a.rows <= kJitMaxRows &&
-        (!a.accumulate || a.cols >= g_jit_min_acc_cols)) {
-        // 256-lane workgroups from 24 columns on whatever the layout (40+8
-        // Reconst of 8: 5.56-5.61 vs 4.98 TB/s, 24+8: 5.68 vs 5.29; 20+12
-        // Reconst of 12 5.83 vs 5.92 and 16+8 Encode 5.70-5.99 vs 5.90-6.02
-        // stay better at 64; profiles/r02/ab_jit_wide2.log, ab_jit_ao.log,
-        // ab_jit_pf.log), else the build-time kernels' per-layout rule
+    if (a.body && a.body < (uint64_t{1} << 31) && a.rows >= g_jit_min_rows && a.rows <= jit_max_rows() &&
+        a.cols <= jit_max_cols() && (!a.accumulate || a.cols >= g_jit_min_acc_cols)) {
+        // hiprtc kernels: 256-lane workgroups from 24 columns on whatever the
+        // layout (40+8 Reconst of 8: 5.56-5.61 vs 4.98 TB/s, 24+8: 5.68 vs
+        // 5.29; 20+12 Reconst of 12 5.83 vs 5.92 and 16+8 Encode 5.70-5.99 vs
+        // 5.90-6.02 stay better at 64; profiles/r02/ab_jit_wide2.log,
+        // ab_jit_ao.log, ab_jit_pf.log), else the build-time kernels' per-layout rule
         const int jbs = (bs_block_for(a) == 256 || (tuning().bs_block == 0 && a.cols >= 24)) ? 256 : 64;
         const uint64_t bytes = a.body * static_cast<uint64_t>(a.nstripes) * static_cast<uint64_t>(a.rows + a.cols);
-        if (hipFunction_t f = jit_bitslice_for(a, jbs, bytes)) {
+        const JitKernel k = jit_kernel_for(a, jbs, bytes);
+        if (k.fn && k.is_asm) {
+            // assembly kernel: grid (2 KiB chunks, stripes), nw waves per
+            // workgroup; vector v of stripe s at ptr[v] + s * 16 * stride16[v]
+            AsmArgs x;
+            std::memset(&x, 0, sizeof x);
+            x.body = static_cast<uint32_t>(a.body);
+            x.stripe_ids = reinterpret_cast<uint64_t>(a.stripe_ids);
+            bool ok = true;
+            for (int v = 0; v < a.cols + a.rows && ok; ++v) {
+                const int64_t ss = a.nstripes > 1 ? a.ss[a.sid[v] & 3] : 0;
+                ok = ss >= 0 && ss % 16 == 0 && (ss >> 4) <= 0xffffffffll;
+                x.ptr[v] = a.ptr[v];
+                x.stride16[v] = static_cast<uint32_t>(ss >> 4);
+            }
+            if (ok) {
+                const unsigned gx = static_cast<unsigned>((a.body + kAsmChunk - 1) / kAsmChunk);
+                for (int y0 = 0; y0 < a.nstripes; y0 += 65535) {
+                    x.stripe0 = static_cast<uint32_t>(y0);
+                    const unsigned gy = static_cast<unsigned>(a.nstripes - y0 < 65535 ? a.nstripes - y0 : 65535);
+                    size_t sz = sizeof x;
+                    void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &x, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                                     HIP_LAUNCH_PARAM_END};
+                    (void)hipGetLastError();
+                    const hipError_t e = hipModuleLaunchKernel(k.fn, gx, gy, 1, 64 * k.nw, 1, 1, 0, stream, nullptr,
+                                                               extra);
+                    if (e != hipSuccess) return e;
+                }
+                jit_count_launch();
+                a.body = 0;
+            }
+        } else if (k.fn) {
             a.units_per_chunk = jbs;
             a.nt_store = 1;
             a.chunks_per_stripe = static_cast<int64_t>((a.body + 32 * jbs - 1) / (32 * jbs));
@@ -1452,8 +1484,8 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
             if (a.total_chunks <= 0x7fffffff) {
                 void* params[] = {&a};
                 (void)hipGetLastError();
-                const hipError_t e = hipModuleLaunchKernel(f, static_cast<unsigned>(a.total_chunks), 1, 1, jbs, 1, 1,
-                                                           0, stream, params, nullptr);
+                const hipError_t e = hipModuleLaunchKernel(k.fn, static_cast<unsigned>(a.total_chunks), 1, 1, jbs, 1,
+                                                           1, 0, stream, params, nullptr);
                 if (e != hipSuccess) return e;
                 jit_count_launch();
                 a.body = 0;

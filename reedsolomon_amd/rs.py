@@ -595,6 +595,17 @@ def jit_cache_stats() -> dict:
     return dict(zip(("hits", "misses", "writes", "rejects"), (int(x.value) for x in v)))
 
 
+def jit_asm_source(mat, accumulate: bool = False) -> str:
+    """The gfx950 assembly of the run-time kernel for `mat` (rs_jit_asm_source)."""
+    m = np.ascontiguousarray(mat, dtype=np.uint8)
+    n = lib().rs_jit_asm_source(m.ctypes.data, m.shape[0], m.shape[1], int(bool(accumulate)), None, 0)
+    if n < 0:
+        _check(int(-n))
+    buf = ctypes.create_string_buffer(int(n))
+    lib().rs_jit_asm_source(m.ctypes.data, m.shape[0], m.shape[1], int(bool(accumulate)), buf, int(n))
+    return buf.value.decode()
+
+
 def jit_compile_check(mat, accumulate: bool = False) -> float:
     """Generate and compile (no device needed) the run-time kernel for `mat`
     (rows x cols, 5 <= rows <= 8); returns the compile time in ms."""

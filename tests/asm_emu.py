@@ -1,0 +1,260 @@
+"""A small CPU emulator for the gfx950 assembly the run-time kernel generator
+emits (reedsolomon_amd/csrc/jit_asm.cpp): test infrastructure, so the
+generated kernels' arithmetic and addressing can be checked against the
+oracle without a GPU (tests/test_jit_asm.py).
+
+Only the instruction subset the generator uses is implemented, with the
+semantics of the CDNA ISA: scalar loads from the kernel-argument block and
+from device memory, SALU integer ops and branches (s_getpc / s_setpc long
+jumps included), VALU bitwise ops on 64 lanes (numpy vectors), and
+buffer_load / buffer_store_dwordx2 through 128-bit buffer descriptors with
+range checking (out-of-range lanes read 0, their stores are dropped).  Wait
+counts and hazards have no effect here (every access completes at once).
+"""
+from __future__ import annotations
+
+import re
+
+import numpy as np
+
+M32 = 0xFFFFFFFF
+
+
+class Memory:
+    """Flat device memory: a byte array starting at `base`."""
+
+    def __init__(self, size: int, base: int = 0x100000):
+        self.base = base
+        self.buf = np.zeros(size, np.uint8)
+        self.top = 0
+
+    def alloc(self, n: int, align: int = 256) -> int:
+        self.top = (self.top + align - 1) // align * align
+        addr = self.base + self.top
+        self.top += n
+        assert self.top <= self.buf.size, "emulated memory full"
+        return addr
+
+    def view(self, addr: int, n: int) -> np.ndarray:
+        o = addr - self.base
+        assert 0 <= o and o + n <= self.buf.size, hex(addr)
+        return self.buf[o:o + n]
+
+
+def _parse(src: str):
+    prog, labels = [], {}
+    for raw in src.splitlines():
+        line = raw.split(";")[0].strip()
+        if not line or line.startswith("."):
+            m = re.match(r"^(\.L\w+|\w+):$", line)
+            if m:
+                labels[m.group(1)] = len(prog)
+            continue
+        m = re.match(r"^(\.L\w+|\w+):$", line)
+        if m:
+            labels[m.group(1)] = len(prog)
+            continue
+        op, _, rest = line.partition(" ")
+        prog.append((op, rest.strip()))
+    return prog, labels
+
+
+def _regs(tok: str):
+    """'v[4:5]' -> ('v', 4, 2); 's12' -> ('s', 12, 1)"""
+    m = re.match(r"^([sv])\[(\d+):(\d+)\]$", tok)
+    if m:
+        a, b = int(m.group(2)), int(m.group(3))
+        return m.group(1), a, b - a + 1
+    m = re.match(r"^([sv])(\d+)$", tok)
+    if m:
+        return m.group(1), int(m.group(2)), 1
+    return None
+
+
+class Wave:
+    def __init__(self, emu, karg_addr, wg, tid0):
+        self.emu = emu
+        self.s = [0] * 128
+        self.v = np.zeros((256, 64), np.uint64)
+        self.s[0], self.s[1] = karg_addr & M32, karg_addr >> 32
+        self.s[2], self.s[3] = wg
+        self.v[0] = np.arange(tid0, tid0 + 64, dtype=np.uint64)
+        self.scc = 0
+
+    # operand values
+    def sval(self, tok: str) -> int:
+        r = _regs(tok)
+        if r and r[0] == "s":
+            if r[2] == 1:
+                return self.s[r[1]]
+            return self.s[r[1]] | (self.s[r[1] + 1] << 32)
+        return int(tok, 0) & 0xFFFFFFFFFFFFFFFF
+
+    def vval(self, tok: str) -> np.ndarray:
+        r = _regs(tok)
+        if r and r[0] == "v":
+            return self.v[r[1]] & M32
+        return np.full(64, self.sval(tok) & M32, np.uint64)
+
+    def run(self, prog, labels):
+        pc = 0
+        emu = self.emu
+        while True:
+            op, rest = prog[pc]
+            pc += 1
+            ops = [t.strip() for t in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
+            if op == "s_endpgm":
+                return
+            if op in ("s_waitcnt", "s_nop"):
+                continue
+            if op == "s_load_dword" or op == "s_load_dwordx2":
+                d, base, off = ops[0], ops[1], int(ops[2], 0)
+                addr = self.sval(base) + off
+                n = 1 if op == "s_load_dword" else 2
+                r = _regs(d)
+                for k in range(n):
+                    self.s[r[1] + k] = emu.read32(addr + 4 * k)
+                continue
+            if op == "s_mov_b32":
+                self.s[_regs(ops[0])[1]] = self.sval(ops[1]) & M32
+                continue
+            if op in ("s_add_u32", "s_addc_u32", "s_mul_i32", "s_mul_hi_u32", "s_and_b32", "s_lshl_b32"):
+                d = _regs(ops[0])[1]
+                a = self.sval(ops[1]) & M32
+                b = self._imm_expr(ops[2], labels, pc) if op in ("s_add_u32", "s_addc_u32") else self.sval(ops[2]) & M32
+                b &= M32
+                if op == "s_add_u32":
+                    t = a + b
+                    self.s[d], self.scc = t & M32, int(t >> 32)
+                elif op == "s_addc_u32":
+                    t = a + b + self.scc
+                    self.s[d], self.scc = t & M32, int(t >> 32)
+                elif op == "s_mul_i32":
+                    self.s[d] = (a * b) & M32
+                elif op == "s_mul_hi_u32":
+                    self.s[d] = (a * b) >> 32
+                elif op == "s_and_b32":
+                    self.s[d] = a & b
+                    self.scc = int(self.s[d] != 0)
+                else:
+                    self.s[d] = (a << (b & 31)) & M32
+                    self.scc = int(self.s[d] != 0)
+                continue
+            if op == "s_lshl_b64":
+                r = _regs(ops[0])
+                x = (self.sval(ops[1]) << int(ops[2], 0)) & 0xFFFFFFFFFFFFFFFF
+                self.s[r[1]], self.s[r[1] + 1] = x & M32, x >> 32
+                continue
+            if op == "s_cmp_eq_u64":
+                self.scc = int(self.sval(ops[0]) == (int(ops[1], 0) & 0xFFFFFFFFFFFFFFFF))
+                continue
+            if op == "s_cmp_eq_u32":
+                self.scc = int((self.sval(ops[0]) & M32) == (self.sval(ops[1]) & M32))
+                continue
+            if op == "s_cbranch_scc1":
+                if self.scc:
+                    pc = labels[ops[0]]
+                continue
+            if op == "s_cbranch_scc0":
+                if not self.scc:
+                    pc = labels[ops[0]]
+                continue
+            if op == "s_branch":
+                pc = labels[ops[0]]
+                continue
+            if op == "s_getpc_b64":  # the "pc" of the next instruction, as an index
+                r = _regs(ops[0])
+                self.s[r[1]], self.s[r[1] + 1] = pc, 0
+                continue
+            if op == "s_setpc_b64":
+                pc = self.sval(ops[0])
+                continue
+            # ---- VALU (64 lanes)
+            if op == "v_readfirstlane_b32":
+                self.s[_regs(ops[0])[1]] = int(self.vval(ops[1])[0])
+                continue
+            if op in ("v_and_b32", "v_xor_b32", "v_add_u32", "v_lshlrev_b32", "v_lshrrev_b32", "v_mov_b32"):
+                d = _regs(ops[0])[1]
+                if op == "v_mov_b32":
+                    self.v[d] = self.vval(ops[1])
+                    continue
+                a, b = self.vval(ops[1]), self.vval(ops[2])
+                if op == "v_and_b32":
+                    x = a & b
+                elif op == "v_xor_b32":
+                    x = a ^ b
+                elif op == "v_add_u32":
+                    x = (a + b) & M32
+                elif op == "v_lshlrev_b32":
+                    x = (b << (a & 31)) & M32
+                else:
+                    x = b >> (a & 31)
+                self.v[d] = x
+                continue
+            if op == "v_bfi_b32":
+                d = _regs(ops[0])[1]
+                m, x, y = self.vval(ops[1]), self.vval(ops[2]), self.vval(ops[3])
+                self.v[d] = (m & x) | ((~m & M32) & y)
+                continue
+            if op == "v_bitop3_b32":
+                d = _regs(ops[0])[1]
+                parts = ops[3].split()
+                assert parts[1] == "bitop3:0x96", ops
+                self.v[d] = self.vval(ops[1]) ^ self.vval(ops[2]) ^ self.vval(parts[0])
+                continue
+            if op in ("buffer_load_dwordx2", "buffer_store_dwordx2"):
+                vr = _regs(ops[0])
+                voff = self.vval(ops[1]).astype(np.int64)
+                sr = _regs(ops[2])
+                d0, d1, d2 = self.s[sr[1]], self.s[sr[1] + 1], self.s[sr[1] + 2]
+                base = d0 | ((d1 & 0xFFFF) << 32)
+                nrec = d2
+                mods = ops[3].split()[1:]
+                imm = 0
+                for m_ in mods:
+                    if m_.startswith("offset:"):
+                        imm = int(m_.split(":")[1])
+                off = voff + imm
+                for lane in range(64):
+                    o = int(off[lane])
+                    inr = o + 8 <= nrec
+                    if op == "buffer_load_dwordx2":
+                        if inr:
+                            w = emu.mem.view(base + o, 8).view(np.uint32)
+                            self.v[vr[1], lane], self.v[vr[1] + 1, lane] = int(w[0]), int(w[1])
+                        else:
+                            self.v[vr[1], lane] = self.v[vr[1] + 1, lane] = 0
+                    elif inr:
+                        w = np.array([self.v[vr[1], lane], self.v[vr[1] + 1, lane]], np.uint32)
+                        emu.mem.view(base + o, 8)[:] = w.view(np.uint8)
+                continue
+            raise NotImplementedError(f"{op} {rest}")
+
+    def _imm_expr(self, tok, labels, pc):
+        m = re.match(r"^\((\.L\w+)-(\.L\w+)\)(&4294967295|>>32)$", tok)
+        if m:
+            # long jumps: the emulator's "pc" is an instruction index and
+            # s_getpc gave the index after it (the .Lpc label's position)
+            delta = labels[m.group(1)] - labels[m.group(2)]
+            return delta & M32 if m.group(3) == "&4294967295" else (delta >> 32) & M32
+        return self.sval(tok)
+
+
+class Emu:
+    def __init__(self, mem: Memory):
+        self.mem = mem
+        self.karg = None
+
+    def read32(self, addr: int) -> int:
+        if self.karg is not None and self.karg[0] <= addr < self.karg[0] + len(self.karg[1]):
+            o = addr - self.karg[0]
+            return int.from_bytes(self.karg[1][o:o + 4], "little")
+        return int(self.mem.view(addr, 4).view(np.uint32)[0])
+
+    def launch(self, src: str, karg: bytes, grid, nw: int):
+        prog, labels = _parse(src)
+        self.karg = (0x7F0000000000, karg)
+        for y in range(grid[1]):
+            for x in range(grid[0]):
+                for w in range(nw):
+                    Wave(self, self.karg[0], (x, y), 64 * w).run(prog, labels)

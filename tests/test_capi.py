@@ -341,22 +341,35 @@ def test_multi_pattern_mask_validation_wide(rslib):
 
 
 def test_jit_compile_check(rslib, orc):
-    """The run-time bit-sliced kernel generator (jit.cpp) produces code that
-    hiprtc compiles for gfx950 (no device needed): a Reconst-of-8 matrix of
-    10+8 (overwrite) and a 16-column 5-row XOR-accumulate product; shapes
-    outside 5-16 rows / 1-64 columns are refused."""
+    """The run-time bit-sliced kernel generators produce code that assembles
+    (jit_asm.cpp, comgr; the default backend) or compiles (jit.cpp, hiprtc)
+    for gfx950 with no device: a Reconst-of-8 matrix of 10+8 (overwrite) and
+    a 16-column 5-row XOR-accumulate product, plus a 64 x 64 product for the
+    assembly backend; shapes outside each backend's bounds are refused
+    (assembly: 1-128 rows, 1-256 columns; hiprtc: 5-16 rows, 1-64 columns;
+    rs_jit_prepare: from 5 rows)."""
     import numpy as np
 
     from reedsolomon_amd.rs import ErrInvalidArgument
 
+    L = rslib.lib()
     r = rslib.New(10, 8)
     survived = list(range(8, 18))
     m = r.reconst_matrix(survived, list(range(8))).reshape(8, 10)  # rows of the inverse for data 0..7
-    assert rslib.jit_compile_check(m) > 0
     rng = np.random.default_rng(3)
-    assert rslib.jit_compile_check(rng.integers(0, 256, (5, 16), dtype=np.uint8), accumulate=True) > 0
-    for shape in [(4, 10), (17, 10), (8, 65)]:
-        with pytest.raises(ErrInvalidArgument):
-            rslib.jit_compile_check(np.ones(shape, np.uint8))
-        with pytest.raises(ErrInvalidArgument):  # rs_jit_prepare checks the shape before any device work
-            r.jit_prepare(np.ones(shape, np.uint8))
+    try:
+        for backend, bad, extra in ((1, [(129, 10), (8, 257)], [(64, 64)]), (0, [(17, 10), (8, 65)], [])):
+            assert L.rs_tune(b"jit_backend", backend) == 0
+            assert rslib.jit_compile_check(m) > 0
+            assert rslib.jit_compile_check(rng.integers(0, 256, (5, 16), dtype=np.uint8), accumulate=True) > 0
+            for shape in extra:
+                assert rslib.jit_compile_check(rng.integers(0, 256, shape, dtype=np.uint8)) > 0
+            for shape in bad:
+                with pytest.raises(ErrInvalidArgument):
+                    rslib.jit_compile_check(np.ones(shape, np.uint8))
+            for shape in bad + [(4, 10)]:
+                with pytest.raises(ErrInvalidArgument):  # rs_jit_prepare checks the shape before any device work
+                    r.jit_prepare(np.ones(shape, np.uint8))
+    finally:
+        L.rs_tune(b"jit_backend", 1)
+

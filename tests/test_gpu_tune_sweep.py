@@ -60,6 +60,7 @@ SWEEP = {
     "jit_min_rows": [1, 5],
     "jit_pf": [1, 2, 4, 6, 3],
     "jit_disk_cache": [0, 1],
+    "jit_backend": [0, 1],
     "table_registry_max": [1, 1 << 14],
 }
 

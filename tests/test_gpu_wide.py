@@ -190,3 +190,65 @@ def test_wide_matches_row_groups(rslib, torch_dev, no_jit):
         torch.cuda.synchronize()
         out.append(dst.cpu())
     assert torch.equal(out[0], out[1])
+
+
+@pytest.fixture
+def asm_jit(rslib):
+    L = rslib.lib()
+    assert L.rs_tune(b"jit", 2) == 0 and L.rs_tune(b"jit_backend", 1) == 0
+    yield L
+    L.rs_tune(b"jit", 1)
+
+
+@pytest.mark.parametrize("rows,cols", [(9, 10), (16, 64), (17, 5), (24, 33), (56, 200), (64, 64), (100, 100),
+                                       (128, 128), (128, 1)])
+def test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols):
+    """The assembly-generated bit-sliced kernels (jit_asm.cpp) for 9-128
+    output rows: 1-8 waves per workgroup, each wave up to 16 rows, all over
+    the same input lines; overwrite and XOR-accumulate, aligned and ragged
+    sizes, against the oracle.  The compiled kernel really runs (launch
+    counter)."""
+    torch = torch_dev
+    rng = np.random.default_rng(rows * 7000 + cols)
+    mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
+    r = rslib.New(10, 4)
+    before = rslib.jit_stats()["launches"]
+    for S, n, pad in [(3, 2048, 0), (2, 4096 + 5, 11), (2, 65536 + 48, 16)]:
+        src, hsrc = _padded(torch, rng, S, cols, n, pad)
+        dst, _ = _padded(torch, rng, S, rows, n, pad)
+        r.gf_matmul_batch(mat, src, None, dst, None)
+        torch.cuda.synchronize()
+        exp = orc.encode_numpy(mat, hsrc)
+        assert np.array_equal(dst.cpu().numpy(), exp), (rows, cols, S, n)
+        dst2, hdst2 = _padded(torch, rng, S, rows, n, pad)
+        r.gf_matmul_batch(mat, src, None, dst2, None, accumulate=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst2.cpu().numpy(), hdst2 ^ exp), (rows, cols, S, n, "acc")
+    st = rslib.jit_stats()
+    assert st["launches"] >= before + 6 and st["failed"] == 0, st
+
+
+@pytest.mark.parametrize("d,p,lost", [(100, 28, list(range(0, 84, 3))), (64, 64, list(range(0, 128, 2))),
+                                      (16, 16, list(range(16)))])
+def test_wide_asm_jit_reconst(rslib, orc, torch_dev, asm_jit, d, p, lost):
+    """Reconst of 16-64 lost vectors through the assembly kernels, in place
+    on the interleaved layout and on the split layout."""
+    torch = torch_dev
+    rng = np.random.default_rng(d + 10 * len(lost))
+    S, n = 3, 8192 + 48
+    r = rslib.New(d, p)
+    G = orc.gen_matrix(d, p).reshape(p, d)
+    host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+    host[:, d:] = orc.encode_numpy(G, host[:, :d])
+    buf = torch.from_numpy(host).cuda()
+    buf[:, lost] = 0x5A
+    r.reconst_batch(buf, [], lost)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), host), (d, p, len(lost))
+    data = torch.from_numpy(np.ascontiguousarray(host[:, :d])).cuda()
+    par = torch.from_numpy(np.ascontiguousarray(host[:, d:])).cuda()
+    for v in lost:
+        (data[:, v] if v < d else par[:, v - d]).fill_(0x33)
+    r.reconst_batch_split(data, par, [], lost)
+    torch.cuda.synchronize()
+    assert np.array_equal(data.cpu().numpy(), host[:, :d]) and np.array_equal(par.cpu().numpy(), host[:, d:])

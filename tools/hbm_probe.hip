@@ -345,3 +345,98 @@ extern "C" int probe_calib(int kind, void* a, uint64_t bytes, void* stream) {
     else return -1;
     return hipGetLastError();
 }
+
+// In-place Reconst access pattern: stripes
+// of NV vectors `vec` bytes apart in one buffer (the interleaved
+// [S][d+p][len] layout), KR survivors read and KW lost vectors written in
+// place; 8-byte lanes, 128-lane workgroups (1 KiB of every vector per chunk),
+// buffer nt, XOR instead of the GF math.  DEFER: 0 = read a chunk, write it;
+// 1 = each workgroup takes two chunks G/2 apart in the grid (different
+// stripes) and stores the first only after the second's loads are issued;
+// 2 = the same with adjacent chunks (1 KiB apart).
+struct IdxList {
+    uint32_t rd[32], wr[32];
+};
+template <int KR, int KW, int DEFER>
+__global__ __launch_bounds__(128) void kin_inplace(uint8_t* base, uint64_t vec, uint64_t sstride, uint32_t cps,
+                                                   uint32_t nchunks, IdxList L) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    auto chunk_of = [&](uint32_t c, uint64_t& sb, uint32_t& off) {
+        const uint32_t s = c / cps, cb = c % cps;
+        sb = (uint64_t)s * sstride;
+        off = cb * 1024u + threadIdx.x * 8u;
+    };
+    auto load = [&](uint64_t sb, uint32_t off, u32x2 (&x)[KR]) {
+#pragma unroll
+        for (int i = 0; i < KR; ++i)
+            x[i] = __builtin_amdgcn_raw_buffer_load_b64(rsrc(base + sb + L.rd[i] * vec, (uint32_t)vec), off, 0, 2);
+    };
+    auto store = [&](uint64_t sb, uint32_t off, const u32x2 (&x)[KR]) {
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+            u32x2 a = {(uint32_t)j, 0u};
+#pragma unroll
+            for (int i = 0; i < KR; ++i) a ^= x[i];
+            __builtin_amdgcn_raw_buffer_store_b64(a, rsrc(base + sb + L.wr[j] * vec, (uint32_t)vec), off, 0, 2);
+        }
+    };
+    if (DEFER == 0) {
+        uint64_t sb;
+        uint32_t off;
+        chunk_of(blockIdx.x, sb, off);
+        u32x2 x[KR];
+        load(sb, off, x);
+        store(sb, off, x);
+        return;
+    }
+    const uint32_t c0 = DEFER == 1 ? blockIdx.x : 2 * blockIdx.x;
+    const uint32_t c1 = DEFER == 1 ? blockIdx.x + nchunks / 2 : 2 * blockIdx.x + 1;
+    uint64_t sb0, sb1;
+    uint32_t off0, off1;
+    chunk_of(c0, sb0, off0);
+    chunk_of(c1, sb1, off1);
+    u32x2 x0[KR], x1[KR];
+    load(sb0, off0, x0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    load(sb1, off1, x1);
+    store(sb0, off0, x0);
+    store(sb1, off1, x1);
+}
+
+// kind: 0/1/2 = DEFER; shape: 0 = 10+8 lost 0-7 (reads 8..17), 1 = 10+8
+// lost 0,2,4,6,8 (5 writes), 2 = 10+4 lost 0-3, 3 = 10+8 Encode-like (reads
+// 0..9, writes 10..17; the same in-place buffer)
+extern "C" int probe_inplace(int kind, int shape, void* a, uint64_t vec, int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    IdxList L{};
+    const uint32_t cps = static_cast<uint32_t>(vec / 1024);
+    const uint32_t nchunks = cps * static_cast<uint32_t>(nstripes);
+    const dim3 grid(kind == 0 ? nchunks : nchunks / 2);
+#define KIN(KR, KW, NV)                                                                                        \
+    do {                                                                                                      \
+        const uint64_t ss = (uint64_t)(NV) * vec;                                                              \
+        if (kind == 0) hipLaunchKernelGGL((kin_inplace<KR, KW, 0>), grid, dim3(128), 0, st, (uint8_t*)a, vec, ss, cps, nchunks, L); \
+        else if (kind == 1) hipLaunchKernelGGL((kin_inplace<KR, KW, 1>), grid, dim3(128), 0, st, (uint8_t*)a, vec, ss, cps, nchunks, L); \
+        else hipLaunchKernelGGL((kin_inplace<KR, KW, 2>), grid, dim3(128), 0, st, (uint8_t*)a, vec, ss, cps, nchunks, L); \
+    } while (0)
+    if (shape == 0) {
+        for (int i = 0; i < 10; ++i) L.rd[i] = 8 + i;
+        for (int j = 0; j < 8; ++j) L.wr[j] = j;
+        KIN(10, 8, 18);
+    } else if (shape == 1) {
+        const uint32_t w[5] = {0, 2, 4, 6, 8}, r[10] = {1, 3, 5, 7, 9, 10, 11, 12, 13, 14};
+        for (int i = 0; i < 10; ++i) L.rd[i] = r[i];
+        for (int j = 0; j < 5; ++j) L.wr[j] = w[j];
+        KIN(10, 5, 18);
+    } else if (shape == 2) {
+        for (int i = 0; i < 10; ++i) L.rd[i] = 4 + i;
+        for (int j = 0; j < 4; ++j) L.wr[j] = j;
+        KIN(10, 4, 14);
+    } else {
+        for (int i = 0; i < 10; ++i) L.rd[i] = i;
+        for (int j = 0; j < 8; ++j) L.wr[j] = 10 + j;
+        KIN(10, 8, 18);
+    }
+#undef KIN
+    return hipGetLastError();
+}

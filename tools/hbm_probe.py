@@ -113,6 +113,20 @@ def pattern_probes(L, a, n, vp, sp, timeit):
                    lambda: L.probe_buf(8, vp(a), vp(b), ctypes.c_uint64(0), ctypes.c_uint64(vec), S, sp),
                    S * 14 * vec)
         return
+    if os.environ.get("PROBE_INPLACE", "0") == "1":
+        # in-place Reconst ceilings (interleaved [S][d+p][1 MiB]), XOR for the math:
+        # plain, stores deferred behind a far chunk's loads, or behind the next chunk's
+        L.probe_inplace.restype = ctypes.c_int
+        vec = 1 << 20
+        for shape, nv, kr, kw, name in ((0, 18, 10, 8, "10+8 lost 0-7"), (1, 18, 10, 5, "10+8 lost 5 data"),
+                                        (2, 14, 10, 4, "10+4 lost 0-3"), (3, 18, 10, 8, "10+8 encode in place")):
+            S = min(256, int(n // (nv * vec)) // 2 * 2)
+            for _ in range(2):
+                for kind, kname in ((0, "plain"), (1, "defer far"), (2, "defer next")):
+                    timeit(f"in place {name} {kname}",
+                           lambda: L.probe_inplace(kind, shape, vp(a), ctypes.c_uint64(vec), S, sp),
+                           S * (kr + kw) * vec, iters=20)
+        return
     if os.environ.get("PROBE_BUF", "0") == "1":
         import torch
         half = (n // 2) // 4096 * 4096

@@ -68,7 +68,7 @@ def wide(g):
         r = rs.New(k, m)
         data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
         par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
-        for jit in ((0, 2) if m <= 16 else (0,)):
+        for jit in (0, 2):
             L.rs_tune(b"jit", jit)
             t = dev_time(lambda: r.encode_batch_split(data, par), iters=10, warm=5)
             rec(f"encode {k}+{m} {vec >> 10}KiB x{S} split, jit={jit} (device)", S * (k + m) * vec, t)
@@ -81,7 +81,7 @@ def wide(g):
         data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
         par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
         r.encode_batch_split(data, par)
-        for jit, sp in (((0, 1), (0, 0), (2, 1)) if len(lost) <= 16 else ((0, 1), (0, 0))):
+        for jit, sp in ((0, 1), (0, 0), (2, 1)):
             L.rs_tune(b"jit", jit)
             L.rs_tune(b"wide_single_pass", sp)
             t = dev_time(lambda: r.reconst_batch_split(data, par, [], lost), iters=10, warm=5)
