@@ -62,7 +62,7 @@ def counter_rows(d):
     raise SystemExit(f"no counter_collection.csv under {d}")
 
 
-def per_launch(d, want=("gf_matmul", "rs_bs_jit", "gf_bitslice")):
+def per_launch(d, want=("gf_matmul", "rs_bs_jit", "rs_bs_asm", "gf_bitslice")):
     rows = [r for r in counter_rows(d) if any(w in r["Kernel_Name"] for w in want)]
     by = {}
     for r in rows:
@@ -80,8 +80,9 @@ def calib(d, kernel, nbytes=2 << 30):
 def summarize(tag, dfetch, dwrite, cfetch, cwrite, algorithmic):
     kf, fetch = per_launch(dfetch)
     kw, write = per_launch(dwrite)
-    # the wide / bit-sliced kernels read and write with 16- or 8-byte lanes:
-    # use the calibration of the kernel's width (gf_matmul_wide: 16 B)
+    # the kernels read and write with 16- or 8-byte lanes: use the
+    # calibration of the kernel's width (gf_matmul_wide: 16 B; the bit-sliced
+    # and one-chunk kernels: 8 B)
     w = 16 if ("gf_matmul_wide" in kf or "16B" in kf) else 8
     cr, cw = calib(cfetch, f"kc_read{w}"), calib(cwrite, f"kc_write{w}")
     f_b = statistics.median(fetch[2:] or fetch) * 1024 * cr["unit"]
