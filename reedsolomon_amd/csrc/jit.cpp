@@ -282,7 +282,7 @@ std::string network(const uint8_t* mat, int rows, int cols, bool acc) {
 // Bumped whenever network() or the launch contract changes in a way the
 // key below does not capture (the prelude text and the MatmulArgs layout are
 // hashed into the key).
-constexpr uint32_t kJitGenVersion = 3;
+constexpr uint32_t kJitGenVersion = 4;
 constexpr char kDiskMagic[8] = {'R', 'S', 'A', 'M', 'D', 'J', 'I', 'T'};
 constexpr uint32_t kDiskFormat = 1;
 

@@ -157,7 +157,14 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
     A.line("v_lshlrev_b32 v%d, 3, v%d", kVOff, kVOff);
     A.line("s_lshl_b32 s%d, s%d, 11", kSTmp + 2, kSWgX);
     A.line("v_add_u32 v%d, s%d, v%d", kVOff, kSTmp + 2, kVOff);
-    A.line("v_lshrrev_b32 v%d, 6, v%d", kVT0, kVTid);
+    // wave id = bits 6-9 of the work-item id (packed work-item ids: y / z sit
+    // in bits 10-29; zero for these 1-D launches, masked anyway)
+    A.line("v_and_b32 v%d, 0x3c0, v%d", kVT0, kVTid);
+    A.line("v_lshrrev_b32 v%d, 6, v%d", kVT0, kVT0);
+    // a VALU write of a VGPR followed at once by v_readfirstlane of it reads
+    // the OLD value (one wait state required; measured: the wave id came out
+    // as 64, not 1, tools/asm_probe/wave_id.s)
+    A.line("s_nop 1");
     A.line("v_readfirstlane_b32 s%d, v%d", kSWave, kVT0);
     A.line("s_waitcnt lgkmcnt(0)");
     A.line("s_mov_b32 s%d, s%d", kSDescOut + 2, kSDescIn + 2);

@@ -8,8 +8,15 @@ semantics of the CDNA ISA: scalar loads from the kernel-argument block and
 from device memory, SALU integer ops and branches (s_getpc / s_setpc long
 jumps included), VALU bitwise ops on 64 lanes (numpy vectors), and
 buffer_load / buffer_store_dwordx2 through 128-bit buffer descriptors with
-range checking (out-of-range lanes read 0, their stores are dropped).  Wait
-counts and hazards have no effect here (every access completes at once).
+range checking (out-of-range lanes read 0, their stores are dropped).
+Every access completes at once, but the wait counts are checked: vector
+memory operations retire in issue order at `s_waitcnt vmcnt(N)` (loads and
+stores share the counter on gfx9), scalar loads only at `lgkmcnt(0)` (they
+may return out of order), and reading or overwriting a register whose load
+has not been waited for raises `WaitcntError` — the hardware would have
+used stale data.  So does `v_readfirstlane` of a VGPR the instruction just
+before it wrote: the hardware needs one wait state there and otherwise reads
+the old value (measured on MI355X, tools/asm_probe/wave_id.s).
 """
 from __future__ import annotations
 
@@ -71,6 +78,10 @@ def _regs(tok: str):
     return None
 
 
+class WaitcntError(AssertionError):
+    pass
+
+
 class Wave:
     def __init__(self, emu, karg_addr, wg, tid0):
         self.emu = emu
@@ -78,12 +89,32 @@ class Wave:
         self.v = np.zeros((256, 64), np.uint64)
         self.s[0], self.s[1] = karg_addr & M32, karg_addr >> 32
         self.s[2], self.s[3] = wg
-        self.v[0] = np.arange(tid0, tid0 + 64, dtype=np.uint64)
+        # work-item id x in bits 0-9; the bits above (packed y / z ids) hold
+        # junk here, so code that depends on them fails
+        self.v[0] = np.arange(tid0, tid0 + 64, dtype=np.uint64) | (0x2A5 << 10)
         self.scc = 0
+        self.vm = []        # outstanding vector memory ops, issue order: set of load-destination VGPRs
+        self.lgkm = set()   # SGPRs of outstanding scalar loads
+        self.pc = 0
+        self.prev_vdst = None  # VGPR the previous instruction wrote (VALU), for the readlane hazard
+
+    # wait-count checks
+    def _chk(self, kind, idx, n, write=False):
+        for i in range(idx, idx + n):
+            if kind == "v" and any(i in d for d in self.vm):
+                raise WaitcntError(f"pc {self.pc}: v{i} {'written' if write else 'read'} before its load was waited for")
+            if kind == "s" and i in self.lgkm:
+                raise WaitcntError(f"pc {self.pc}: s{i} {'written' if write else 'read'} before its load was waited for")
+
+    def _use(self, tok, write=False):
+        r = _regs(tok)
+        if r:
+            self._chk(r[0], r[1], r[2], write)
 
     # operand values
     def sval(self, tok: str) -> int:
         r = _regs(tok)
+        self._use(tok)
         if r and r[0] == "s":
             if r[2] == 1:
                 return self.s[r[1]]
@@ -92,6 +123,7 @@ class Wave:
 
     def vval(self, tok: str) -> np.ndarray:
         r = _regs(tok)
+        self._use(tok)
         if r and r[0] == "v":
             return self.v[r[1]] & M32
         return np.full(64, self.sval(tok) & M32, np.uint64)
@@ -101,12 +133,26 @@ class Wave:
         emu = self.emu
         while True:
             op, rest = prog[pc]
+            self.pc = pc
             pc += 1
+            prev, self.prev_vdst = self.prev_vdst, None
             ops = [t.strip() for t in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
             if op == "s_endpgm":
                 return
-            if op in ("s_waitcnt", "s_nop"):
+            if op == "s_waitcnt":
+                for m_ in re.finditer(r"(vmcnt|lgkmcnt)\((\d+)\)", rest):
+                    n = int(m_.group(2))
+                    if m_.group(1) == "vmcnt":
+                        while len(self.vm) > n:
+                            self.vm.pop(0)
+                    elif n == 0:
+                        self.lgkm.clear()
                 continue
+            if op == "s_nop":
+                continue
+            if ops and op not in ("s_cbranch_scc1", "s_cbranch_scc0", "s_branch", "s_cmp_eq_u64", "s_cmp_eq_u32",
+                                  "s_setpc_b64", "buffer_store_dwordx2"):
+                self._use(ops[0], write=True)  # the destination
             if op == "s_load_dword" or op == "s_load_dwordx2":
                 d, base, off = ops[0], ops[1], int(ops[2], 0)
                 addr = self.sval(base) + off
@@ -114,6 +160,7 @@ class Wave:
                 r = _regs(d)
                 for k in range(n):
                     self.s[r[1] + k] = emu.read32(addr + 4 * k)
+                    self.lgkm.add(r[1] + k)
                 continue
             if op == "s_mov_b32":
                 self.s[_regs(ops[0])[1]] = self.sval(ops[1]) & M32
@@ -171,12 +218,15 @@ class Wave:
                 continue
             # ---- VALU (64 lanes)
             if op == "v_readfirstlane_b32":
+                if prev is not None and _regs(ops[1])[1] == prev:
+                    raise WaitcntError(f"pc {self.pc}: v_readfirstlane of v{prev} right after a VALU wrote it")
                 self.s[_regs(ops[0])[1]] = int(self.vval(ops[1])[0])
                 continue
             if op in ("v_and_b32", "v_xor_b32", "v_add_u32", "v_lshlrev_b32", "v_lshrrev_b32", "v_mov_b32"):
                 d = _regs(ops[0])[1]
                 if op == "v_mov_b32":
                     self.v[d] = self.vval(ops[1])
+                    self.prev_vdst = d
                     continue
                 a, b = self.vval(ops[1]), self.vval(ops[2])
                 if op == "v_and_b32":
@@ -190,22 +240,29 @@ class Wave:
                 else:
                     x = b >> (a & 31)
                 self.v[d] = x
+                self.prev_vdst = d
                 continue
             if op == "v_bfi_b32":
                 d = _regs(ops[0])[1]
                 m, x, y = self.vval(ops[1]), self.vval(ops[2]), self.vval(ops[3])
                 self.v[d] = (m & x) | ((~m & M32) & y)
+                self.prev_vdst = d
                 continue
             if op == "v_bitop3_b32":
                 d = _regs(ops[0])[1]
                 parts = ops[3].split()
                 assert parts[1] == "bitop3:0x96", ops
                 self.v[d] = self.vval(ops[1]) ^ self.vval(ops[2]) ^ self.vval(parts[0])
+                self.prev_vdst = d
                 continue
             if op in ("buffer_load_dwordx2", "buffer_store_dwordx2"):
                 vr = _regs(ops[0])
                 voff = self.vval(ops[1]).astype(np.int64)
                 sr = _regs(ops[2])
+                self._chk("s", sr[1], 4)
+                if op == "buffer_store_dwordx2":
+                    self._chk("v", vr[1], 2)
+                self.vm.append({vr[1], vr[1] + 1} if op == "buffer_load_dwordx2" else set())
                 d0, d1, d2 = self.s[sr[1]], self.s[sr[1] + 1], self.s[sr[1] + 2]
                 base = d0 | ((d1 & 0xFFFF) << 32)
                 nrec = d2

@@ -26,7 +26,7 @@ def _karg(body, stripe0, stripe_ids, ptrs, strides16):
 
 
 @pytest.mark.parametrize("rows,cols,acc", [(5, 10, 0), (8, 10, 1), (3, 7, 0), (16, 16, 0), (12, 5, 1),
-                                           (20, 4, 0), (33, 3, 1), (9, 1, 0)])
+                                           (20, 4, 0), (33, 3, 1), (9, 1, 0), (17, 5, 0)])
 def test_asm_kernel_matches_oracle(rslib, orc, rows, cols, acc):
     rng = np.random.default_rng(rows * 1000 + cols * 10 + acc)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
