@@ -1452,7 +1452,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
             x.stripe_ids = reinterpret_cast<uint64_t>(a.stripe_ids);
             bool ok = true;
             for (int v = 0; v < a.cols + a.rows && ok; ++v) {
-                const int64_t ss = a.nstripes > 1 ? a.ss[a.sid[v] & 3] : 0;
+                const int64_t ss = (a.nstripes > 1 || a.stripe_ids) ? a.ss[a.sid[v] & 3] : 0;  // (a listed stripe may be > 0)
                 ok = ss >= 0 && ss % 16 == 0 && (ss >> 4) <= 0xffffffffll;
                 x.ptr[v] = a.ptr[v];
                 x.stride16[v] = static_cast<uint32_t>(ss >> 4);

@@ -134,7 +134,7 @@ __device__ __forceinline__ u4 coef(u4 x, int c, int r) {
 // stripe (16 B per lane); WAVES == 1: each lane all 4 rows, WAVES == 4: wave
 // w row w (the same input lines loaded by each wave); stores to host memory,
 // then its done word
-template <int WAVES, bool HEAVY>
+template <int WAVES, bool HEAVY, bool RELEASE>
 __global__ __launch_bounds__(64 * WAVES) void call_sim(const uint64_t* bell, const u4* in, u4* out, uint64_t* done,
                                                         int n) {
     __shared__ int s_ok;
@@ -170,7 +170,10 @@ __global__ __launch_bounds__(64 * WAVES) void call_sim(const uint64_t* bell, con
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) sys_store(&done[16 * blockIdx.x], i);
+        if (threadIdx.x == 0) {
+            if (RELEASE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // write back the L2 before the done word
+            sys_store(&done[16 * blockIdx.x], i);
+        }
         __syncthreads();
     }
 }
@@ -232,7 +235,7 @@ static void run_pingpong(const char* name, uint64_t* bell, uint64_t* done, int n
                 failed ? "FAILED (time-out)" : "ok");
 }
 
-template <int WAVES, bool HEAVY>
+template <int WAVES, bool HEAVY, bool RELEASE = true>
 static void run_call(const char* name, uint64_t* bell, uint8_t* in, uint8_t* out, uint64_t* done, int n) {
     std::vector<uint8_t> src(kIn * kLen), dst(kOut * kLen), want(kOut * kLen);
     for (size_t i = 0; i < src.size(); ++i) src[i] = static_cast<uint8_t>(i * 131 + 7);
@@ -240,7 +243,7 @@ static void run_call(const char* name, uint64_t* bell, uint8_t* in, uint8_t* out
     for (int g = 0; g < kGroups; ++g) reinterpret_cast<volatile uint64_t*>(done)[16 * g] = 0;
     _mm_sfence();
     CHECK(hipDeviceSynchronize());
-    hipLaunchKernelGGL((call_sim<WAVES, HEAVY>), dim3(kGroups), dim3(64 * WAVES), 0, 0, bell, reinterpret_cast<const u4*>(in),
+    hipLaunchKernelGGL((call_sim<WAVES, HEAVY, RELEASE>), dim3(kGroups), dim3(64 * WAVES), 0, 0, bell, reinterpret_cast<const u4*>(in),
                        reinterpret_cast<u4*>(out), done, n);
     const double start = now_us();
     while (now_us() - start < 20000) {}
@@ -274,8 +277,10 @@ static void run_call(const char* name, uint64_t* bell, uint8_t* in, uint8_t* out
                 size_t k = 0, nbad = 0;
                 while (dst[k] == want[k]) ++k;
                 for (size_t q = 0; q < dst.size(); ++q) nbad += dst[q] != want[q];
-                std::printf("  call %d: %zu of %zu bytes differ, first at %zu (got %02x want %02x)\n", i, nbad,
-                            dst.size(), k, dst[k], want[k]);
+                size_t zeros = 0;
+                for (size_t q = 0; q < dst.size(); ++q) zeros += dst[q] == 0;
+                std::printf("  call %d: %zu of %zu bytes differ, first at %zu (got %02x want %02x), %zu zero bytes\n",
+                            i, nbad, dst.size(), k, dst[k], want[k], zeros);
             }
         }
     }
@@ -304,6 +309,7 @@ int main() {
 
     const int n = 400;
     run_pingpong("bell in host memory", hbell, hdone, n);
+    run_call<1, false, false>("inputs+bell in host memory (no release)", hbell, hin, hout, hdone, n);
     run_call<1, false>("inputs+bell in host memory", hbell, hin, hout, hdone, n);
     run_call<1, true>("inputs+bell in host memory", hbell, hin, hout, hdone, n);
     run_call<4, true>("inputs+bell in host memory", hbell, hin, hout, hdone, n);
