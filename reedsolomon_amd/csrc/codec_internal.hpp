@@ -174,6 +174,9 @@ struct rs_codec {
     std::mutex eng_mu;
     rsamd::EngineRing* eng_ring = nullptr;   // host address (fine-grained pinned)
     rsamd::EngineRing* eng_dring = nullptr;  // its device address
+    // the call slots in device memory the host writes through the BAR (the
+    // engine polls local HBM), or nullptr: the slots of eng_ring
+    rsamd::EngineSlot* eng_vslots = nullptr;
     hipStream_t eng_stream = nullptr;
     bool eng_running = false;
     int eng_waves = 0;       // the running instance's workgroups
@@ -215,7 +218,13 @@ bool engine_accepts(int rows, int cols, size_t bytes);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
 extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_life_us, g_engine_wg_units,
-    g_engine_yield_us, g_engine_poll_gap;
+    g_engine_yield_us, g_engine_poll_gap, g_engine_vram;
+// Device memory the host can write through the BAR (uncached for the GPU:
+// its loads always see the host's latest bytes), or nullptr when the
+// platform maps no such memory for the CPU (engine.cpp).  Blocks are pooled
+// per device and never freed while the process runs.
+uint8_t* host_writable_vram_get(int device, size_t bytes, size_t* cap);
+void host_writable_vram_put(int device, uint8_t* p, size_t cap);
 extern size_t g_engine_max_bytes;
 
 // Diagnostics (env RSAMD_ENGINE_TRACE): where the time of the synchronous

@@ -30,10 +30,12 @@
 // already finished a call (done word) skip it, so no unit is computed twice
 // (Update / Replace XOR into their outputs).
 #include <immintrin.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <algorithm>
 #include <cstdlib>
+#include <map>
 #include <thread>
 
 #include <hip/hip_ext.h>
@@ -59,6 +61,17 @@ int g_engine_life_us = 4000;
 int g_engine_poll_gap = [] {  // (env RSAMD_ENGINE_POLL_GAP)
     const char* e = std::getenv("RSAMD_ENGINE_POLL_GAP");
     return e ? std::atoi(e) : 0;
+}();
+// Call slots (and the pageable calls' input staging, host_calls.cpp) in
+// device memory the host writes through the BAR: the engine polls and reads
+// local HBM instead of paying a PCIe read round trip per poll and per input
+// batch (tools/bar_probe.hip, profiles/r03/bar_probe.log).  Taken by handles
+// whose engine starts after the change; rs_tune("host_engine_vram", 0 | 1),
+// env RSAMD_ENGINE_VRAM.  Platforms that map no device memory for the CPU
+// keep everything in host memory.
+int g_engine_vram = [] {
+    const char* e = std::getenv("RSAMD_ENGINE_VRAM");
+    return e ? (std::atoi(e) ? 1 : 0) : 1;
 }();
 // Batches up to this many bytes go to the engine, larger ones launch.
 size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
@@ -124,6 +137,73 @@ static void ring_put(int device, EngineRing* r) {
     g_ring_pool.emplace_back(device, r);
 }
 
+// ---- device memory the host writes through the BAR
+namespace {
+std::mutex g_vram_mu;
+std::multimap<std::pair<int, size_t>, uint8_t*> g_vram_free;  // (device, size class) -> idle blocks
+std::vector<int> g_vram_state;                                // per device: 0 unknown, 1 usable, 2 not mapped for the CPU
+}  // namespace
+
+// Can this process read and write [p, p + 8) from the CPU?  Asked of the
+// kernel through a pipe (EFAULT instead of a signal when it is not mapped).
+static bool cpu_can_access(void* p) {
+    int fd[2];
+    if (pipe(fd) != 0) return false;
+    const uint64_t probe = 0x5253414d44564d31ull;
+    uint64_t back = 0;
+    bool ok = write(fd[1], &probe, 8) == 8 && read(fd[0], p, 8) == 8;  // the kernel stores into p
+    ok = ok && write(fd[1], p, 8) == 8 && read(fd[0], &back, 8) == 8 && back == probe;  // ... and loads from it
+    close(fd[0]);
+    close(fd[1]);
+    return ok;
+}
+
+uint8_t* host_writable_vram_get(int device, size_t bytes, size_t* cap) {
+    size_t cls = size_t{64} << 10;
+    while (cls < bytes) cls <<= 1;
+    std::lock_guard<std::mutex> lk(g_vram_mu);
+    if (device < 0) return nullptr;
+    if (g_vram_state.size() <= static_cast<size_t>(device)) g_vram_state.resize(static_cast<size_t>(device) + 1, 0);
+    if (g_vram_state[static_cast<size_t>(device)] == 2) return nullptr;
+    auto it = g_vram_free.find({device, cls});
+    if (it != g_vram_free.end()) {
+        uint8_t* p = it->second;
+        g_vram_free.erase(it);
+        *cap = cls;
+        return p;
+    }
+    void* d = nullptr;
+    Region region("hipExtMallocWithFlags (host-writable device block)");
+    if (hipExtMallocWithFlags(&d, cls, hipDeviceMallocUncached) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    uint8_t* p = static_cast<uint8_t*>(d);
+    if (g_vram_state[static_cast<size_t>(device)] == 0) {
+        const bool ok = cpu_can_access(p) && cpu_can_access(p + cls - 8);
+        g_vram_state[static_cast<size_t>(device)] = ok ? 1 : 2;
+        if (!ok) {
+            (void)hipFree(d);
+            return nullptr;
+        }
+    }
+    *cap = cls;
+    return p;
+}
+
+void host_writable_vram_put(int device, uint8_t* p, size_t cap) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_vram_mu);
+    g_vram_free.emplace(std::make_pair(device, cap), p);
+}
+
+static EngineSlot* slots_of(rs_t* rs) { return rs->eng_vslots ? rs->eng_vslots : rs->eng_ring->slot; }
+static size_t vslots_cap() {
+    size_t cls = size_t{64} << 10;
+    while (cls < sizeof(EngineSlot) * kEngineSlots) cls <<= 1;
+    return cls;
+}
+
 static void engine_dump(const rs_t* rs, const char* what) {  // diagnostics
     const EngineRing* r = rs->eng_ring;
     std::fprintf(stderr, "engine %s: epoch %llu seq %llu running %d waves %d | done/gone:", what,
@@ -136,7 +216,9 @@ static void engine_dump(const rs_t* rs, const char* what) {  // diagnostics
 }
 
 static void engine_signal_stop(rs_t* rs) {  // every slot: a wave polls whichever holds its next call
-    for (int i = 0; i < kEngineSlots; ++i) __atomic_store_n(&rs->eng_ring->slot[i].hdr.stop, rs->eng_epoch, __ATOMIC_RELEASE);
+    EngineSlot* slots = slots_of(rs);
+    for (int i = 0; i < kEngineSlots; ++i) __atomic_store_n(&slots[i].hdr.stop, rs->eng_epoch, __ATOMIC_RELEASE);
+    _mm_sfence();  // (device-memory slots: write-combined stores leave now)
 }
 
 // Caller holds eng_mu.  Calls already rung are served first (a wave checks
@@ -171,9 +253,13 @@ void engine_shutdown(rs_t* rs) {
     DeviceGuard g(rs->device);
     engine_stop(rs);
     if (rs->eng_stream) (void)hipStreamDestroy(rs->eng_stream);
-    if (!rs->eng_running) ring_put(rs->device, rs->eng_ring);  // (a ring an instance may still read is dropped)
+    if (!rs->eng_running) {  // (a ring an instance may still read is dropped)
+        ring_put(rs->device, rs->eng_ring);
+        if (rs->eng_vslots) host_writable_vram_put(rs->device, reinterpret_cast<uint8_t*>(rs->eng_vslots), vslots_cap());
+    }
     rs->eng_stream = nullptr;
     rs->eng_ring = rs->eng_dring = nullptr;
+    rs->eng_vslots = nullptr;
 }
 
 // The engine's stream must own its hardware queue: HIP maps streams onto a
@@ -214,8 +300,8 @@ static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     for (int w = 0; w < waves; ++w)
         if (__atomic_load_n(&rs->eng_ring->done[w], __ATOMIC_ACQUIRE) < start)
             __atomic_store_n(&rs->eng_ring->done[w], start, __ATOMIC_RELEASE);
-    RS_TRY(hip_ok(launch_engine(rs->eng_dring, waves, group_waves, start, epoch, idle_ticks, life_ticks,
-                                static_cast<uint32_t>(g_engine_poll_gap), rs->eng_stream),
+    RS_TRY(hip_ok(launch_engine(rs->eng_dring, rs->eng_vslots, waves, group_waves, start, epoch, idle_ticks,
+                                life_ticks, static_cast<uint32_t>(g_engine_poll_gap), rs->eng_stream),
                   "engine launch"));
     if (g_engine_trace) std::fprintf(stderr, "engine launch: epoch %llu start %llu\n",
                                      static_cast<unsigned long long>(epoch), static_cast<unsigned long long>(start));
@@ -349,6 +435,15 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
         rs->eng_ring = h;
         rs->eng_dring = static_cast<EngineRing*>(d);
         rs->eng_stream = st;
+        rs->eng_vslots = nullptr;
+        if (g_engine_vram) {
+            size_t cap = 0;
+            if (uint8_t* v = host_writable_vram_get(rs->device, sizeof(EngineSlot) * kEngineSlots, &cap)) {
+                std::memset(v, 0, sizeof(EngineSlot) * kEngineSlots);
+                _mm_sfence();
+                rs->eng_vslots = reinterpret_cast<EngineSlot*>(v);
+            }
+        }
         rs->eng_seq = 0;
         rs->eng_epoch = 0;
         rs->eng_tab_key.clear();
@@ -368,7 +463,7 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     const int inst_waves = rs->eng_waves;
 
     const uint64_t seq = rs->eng_seq + 1;
-    EngineSlot* slot = &ring->slot[seq % kEngineSlots];
+    EngineSlot* slot = &slots_of(rs)[seq % kEngineSlots];
     if (seq > static_cast<uint64_t>(kEngineSlots))  // the slot's previous call must be past every workgroup
         RS_TRY(engine_wait(rs, seq - kEngineSlots, inst_waves, 0, inst_waves, true));
     rs->eng_seq = seq;
@@ -427,9 +522,13 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     h->flags = (wk.accumulate ? 1u : 0u) | (wk.coherent ? 2u : 0u) | (g_engine_trace ? 4u : 0u) | (wk.addr ? 8u : 0u) |
                (static_cast<uint32_t>(wg0) << 8) | (static_cast<uint32_t>(nwg) << 16);
     h->tab_id = rs->eng_tab_id;
-    std::atomic_thread_fence(std::memory_order_release);
+    // (write-combined device-memory slots and staging blocks: sfence makes
+    // every store before it visible first, tables, addresses and inputs
+    // included; for host memory it costs nothing measurable)
+    _mm_sfence();
     __atomic_store_n(&slot->hdr.seq0, seq, __ATOMIC_RELEASE);
     __atomic_store_n(&slot->hdr.seq1, seq, __ATOMIC_RELEASE);
+    _mm_sfence();
     rs->eng_inflight.fetch_add(1, std::memory_order_acq_rel);
     lk.unlock();
 

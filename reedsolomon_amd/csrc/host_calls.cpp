@@ -439,19 +439,41 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
             using clk = std::chrono::steady_clock;
             clk::time_point t0, t1, t2;
             if (g_phase_trace) t0 = clk::now();
+            // inputs into device memory the host writes through the BAR when
+            // the platform has it (posted writes; the engine reads them from
+            // HBM), outputs (and an Update / Replace's old parity) in a pinned
+            // block; else the whole stripe in the pinned block
+            const size_t in_bytes = pitch * static_cast<size_t>(cols);
+            size_t vcap = 0;
+            uint8_t* vin = g_engine_vram ? host_writable_vram_get(rs->device, in_bytes, &vcap) : nullptr;
             PinnedBlock blk;
-            RS_TRY(pinned_get(stride, &blk));
-            for (int i = 0; i < cols; ++i) std::memcpy(blk.host + static_cast<size_t>(i) * pitch, src[i], size);
+            const int prc = pinned_get(vin ? stride - in_bytes : stride, &blk);
+            if (prc) {
+                host_writable_vram_put(rs->device, vin, vcap);
+                return prc;
+            }
+            uint8_t* in_host = vin ? vin : blk.host;
+            uint8_t* out_host = vin ? blk.host : blk.host + in_bytes;
+            for (int i = 0; i < cols; ++i) std::memcpy(in_host + static_cast<size_t>(i) * pitch, src[i], size);
             if (accumulate)
-                for (int r = 0; r < rows; ++r)
-                    std::memcpy(blk.host + static_cast<size_t>(cols + r) * pitch, dst[r], size);
+                for (int r = 0; r < rows; ++r) std::memcpy(out_host + static_cast<size_t>(r) * pitch, dst[r], size);
             if (g_phase_trace) t1 = clk::now();
-            const int rc = engine_call(rs, mat, rows, cols, blk.dev, pitch, stride, 1, accumulate, false);
+            int rc;
+            if (vin) {
+                const uint8_t* in[kMaxVects];
+                uint8_t* out[kMaxVects];
+                uint8_t* out_dev = blk.dev;
+                for (int i = 0; i < cols; ++i) in[i] = vin + static_cast<size_t>(i) * pitch;
+                for (int r = 0; r < rows; ++r) out[r] = out_dev + static_cast<size_t>(r) * pitch;
+                rc = engine_call_addr(rs, mat, rows, cols, in, out, pitch, accumulate);
+            } else {
+                rc = engine_call(rs, mat, rows, cols, blk.dev, pitch, stride, 1, accumulate, false);
+            }
             if (g_phase_trace) t2 = clk::now();
             if (rc == RS_OK)
-                for (int r = 0; r < rows; ++r)
-                    std::memcpy(dst[r], blk.host + static_cast<size_t>(cols + r) * pitch, size);
+                for (int r = 0; r < rows; ++r) std::memcpy(dst[r], out_host + static_cast<size_t>(r) * pitch, size);
             pinned_put(blk);
+            host_writable_vram_put(rs->device, vin, vcap);
             if (g_phase_trace && rc == RS_OK) {
                 phase_add(kPhCopyIn, t0, t1);
                 phase_add(kPhCopyOut, t2, clk::now());

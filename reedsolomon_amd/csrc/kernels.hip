@@ -924,8 +924,12 @@ __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t
     }
 }
 
-__global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t start, uint64_t epoch,
-                                                 uint64_t idle_ticks, uint64_t life_ticks, uint32_t poll_gap) {
+__global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineSlot* vslots, uint64_t start,
+                                                 uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks,
+                                                 uint32_t poll_gap) {
+    // the call slots: in device memory the host writes through the BAR
+    // (vslots: polls and table loads stay in local HBM) or in the ring
+    const EngineSlot* const slots = vslots ? vslots : ring->slot;
     constexpr int kPollWords = 8 * (1 + kEnginePtrLines);  // a slot's header + address lines
     __shared__ __attribute__((aligned(16))) uint32_t tab[kEngineMaxCols * kEngineMaxRows * 5];
     __shared__ uint64_t s_raw[kPollWords];  // the lines wave 0 saw (s_raw[0] = 0: leave)
@@ -943,7 +947,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
     uint32_t tab_have = 0xffffffffu;
     for (;;) {
         uint64_t t_seen = 0;
-        const EngineSlot* slot = &ring->slot[(last + 1) % kEngineSlots];
+        const EngineSlot* slot = &slots[(last + 1) % kEngineSlots];
         if (poller) {
             const uint64_t* lines = reinterpret_cast<const uint64_t*>(slot);
             uint64_t w = 0, seq = 0;
@@ -1068,12 +1072,13 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, uint64_t star
     }
 }
 
-hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
-                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t poll_gap_ticks, hipStream_t stream) {
+hipError_t launch_engine(EngineRing* ring_dev, const EngineSlot* vslots, int groups, int waves_per_group,
+                         uint64_t start, uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks,
+                         uint32_t poll_gap_ticks, hipStream_t stream) {
     if (groups < 1 || groups > kEngineMaxGroups || waves_per_group < 1 || waves_per_group > kEngineMaxGroupWaves)
         return hipErrorInvalidValue;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(gf_engine, dim3(groups), dim3(64 * waves_per_group), 0, stream, ring_dev, start, epoch,
+    hipLaunchKernelGGL(gf_engine, dim3(groups), dim3(64 * waves_per_group), 0, stream, ring_dev, vslots, start, epoch,
                        idle_ticks, life_ticks, poll_gap_ticks);
     return hipGetLastError();
 }

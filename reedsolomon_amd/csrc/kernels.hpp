@@ -111,8 +111,11 @@ struct EngineRing {
 // `epoch` in its `gone` word.
 // poll_gap_ticks > 0: two doorbell reads in flight, the second issued that
 // many ticks after the first (pipelined polls); 0: one read per round trip.
-hipError_t launch_engine(EngineRing* ring_dev, int groups, int waves_per_group, uint64_t start, uint64_t epoch,
-                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t poll_gap_ticks, hipStream_t stream);
+// vslots != nullptr: the call slots live there (device memory the host
+// writes through the BAR, engine.cpp) instead of in ring->slot.
+hipError_t launch_engine(EngineRing* ring_dev, const EngineSlot* vslots, int groups, int waves_per_group,
+                         uint64_t start, uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks,
+                         uint32_t poll_gap_ticks, hipStream_t stream);
 
 // Launch tuning knobs (read from the environment once).
 struct LaunchTuning {

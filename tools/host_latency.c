@@ -12,8 +12,14 @@
  *   HL_ENGINE_WAVES=n: its workgroups
  *   HL_VEC=bytes: only this vector size; HL_OPS=mask: only these ops (bit 0
  *   Encode, 1 Reconst lost=1, 2 Reconst lost=4, 3 Update, 4 Replace)
+ *   HL_VRAM=0/1: engine call slots and input staging in host-writable device
+ *   memory (default 1 where the platform has it)
  *
- * Prints one JSON object per (op, size).
+ * Every call's result is checked outside the timed region: Encode's parity
+ * and Update / Replace's new parity against a plain GF(2^8)/0x11d product
+ * over the library's generator matrix (rs_gen_matrix), Reconst's rebuilt
+ * vectors (overwritten with junk before each call) against their bytes.
+ * Prints one JSON object per (op, size); "checked" counts verified calls.
  */
 #define _POSIX_C_SOURCE 200112L
 #include <stdint.h>
@@ -38,6 +44,36 @@ static int cmp(const void* a, const void* b) {
 }
 
 static double t[REPS];
+static uint8_t gexp[512], glog[256], gen[P * D];
+static long checked;
+
+static void gf_init(void) {
+    int x = 1, i;
+    for (i = 0; i < 255; ++i) {
+        gexp[i] = gexp[i + 255] = (uint8_t)x;
+        glog[x] = (uint8_t)i;
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11d;
+    }
+}
+static uint8_t gmul(uint8_t a, uint8_t b) { return a && b ? gexp[glog[a] + glog[b]] : 0; }
+
+/* parity row j of data vectors v[0..D) at byte k */
+static uint8_t par_byte(uint8_t* const* v, int j, size_t k) {
+    uint8_t x = 0;
+    int c;
+    for (c = 0; c < D; ++c) x ^= gmul(gen[j * D + c], v[c][k]);
+    return x;
+}
+static int check_parity(uint8_t* const* v, size_t vec) {
+    size_t k;
+    int j;
+    for (j = 0; j < P; ++j)
+        for (k = 0; k < vec; ++k)
+            if (v[D + j][k] != par_byte(v, j, k)) return 0;
+    ++checked;
+    return 1;
+}
 
 static void report(const char* op, size_t vec, double bytes, int reps) {
     double med;
@@ -65,10 +101,13 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE_DIRECT")) rs_tune("host_engine_direct", atoi(getenv("HL_ENGINE_DIRECT")));
     if (getenv("HL_ENGINE_POLL_GAP")) rs_tune("host_engine_poll_gap", atoi(getenv("HL_ENGINE_POLL_GAP")));
     if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
+    if (getenv("HL_VRAM")) rs_tune("host_engine_vram", atoi(getenv("HL_VRAM")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
     }
+    gf_init();
+    if (rs_gen_matrix(rs, gen) != RS_OK) return 11;
     const long only_vec = getenv("HL_VEC") ? atol(getenv("HL_VEC")) : 0;
     const int ops = getenv("HL_OPS") ? atoi(getenv("HL_OPS")) : 31;
     for (si = 0; si < sizeof sizes / sizeof sizes[0]; ++si) {
@@ -76,6 +115,7 @@ int main(int argc, char** argv) {
         if (only_vec && (size_t)only_vec != vec) continue;
         const int reps = vec >= 4194304 ? REPS / 8 : (vec >= 262144 ? REPS / 4 : REPS);
         uint8_t* v[N];
+        uint8_t* saved[N];
         size_t lens[N];
         int i, k;
         const char* reg = getenv("HL_REGISTER");
@@ -86,61 +126,95 @@ int main(int argc, char** argv) {
             lens[i] = vec;
             for (k = 0; k < (int)vec; ++k) v[i][k] = (uint8_t)(k * 31 + i * 7);
             if (reg && atoi(reg) && rs_host_register(v[i], vec) != RS_OK) return 8;
+            if (!(saved[i] = (uint8_t*)malloc(vec))) return 7;
         }
         for (k = 0; k < 10; ++k) rs_encode(rs, v, lens, N);
+        if (!check_parity(v, vec)) return 12;
         if (ops & 1) {
             for (k = 0; k < reps; ++k) {
-                double a = now_us();
+                double a;
+                for (i = D; i < N; ++i) memset(v[i], 0x5a, vec);
+                a = now_us();
                 if (rs_encode(rs, v, lens, N) != RS_OK) return 2;
                 t[k] = now_us() - a;
+                if (!check_parity(v, vec)) return 13;
             }
             report("Encode", vec, (double)N * vec, reps);
         }
+        for (i = 0; i < N; ++i) memcpy(saved[i], v[i], vec);
         if (ops & 2) {
             int need[1] = {0};
             for (k = 0; k < reps; ++k) {
-                double a = now_us();
+                double a;
+                memset(v[0], 0x77, vec);
+                a = now_us();
                 if (rs_reconst(rs, v, lens, N, NULL, 0, need, 1) != RS_OK) return 3;
                 t[k] = now_us() - a;
+                if (memcmp(v[0], saved[0], vec)) return 14;
+                ++checked;
             }
             report("Reconst lost=1", vec, (double)(D + 1) * vec, reps);
         }
         if (ops & 4) {
             int need[4] = {0, 3, 5, 9};
             for (k = 0; k < reps; ++k) {
-                double a = now_us();
+                double a;
+                for (i = 0; i < 4; ++i) memset(v[need[i]], 0x77, vec);
+                a = now_us();
                 if (rs_reconst(rs, v, lens, N, NULL, 0, need, 4) != RS_OK) return 4;
                 t[k] = now_us() - a;
+                for (i = 0; i < 4; ++i)
+                    if (memcmp(v[need[i]], saved[need[i]], vec)) return 15;
+                ++checked;
             }
             report("Reconst lost=4", vec, (double)(D + 4) * vec, reps);
         }
-        if (ops & 8)
-        for (k = 0; k < reps; ++k) {
-            double a = now_us();
-            if (rs_update(rs, v[2], vec, v[3], vec, 2, v + D, lens + D, P) != RS_OK) return 5;
-            t[k] = now_us() - a;
+        if (ops & 8) {
+            /* data row 2 alternates between its bytes and row 3's: the
+             * parity after each Update is that of the data as it now is */
+            for (k = 0; k < reps; ++k) {
+                double a;
+                uint8_t* nw = (k & 1) ? saved[2] : saved[3];
+                a = now_us();
+                if (rs_update(rs, v[2], vec, nw, vec, 2, v + D, lens + D, P) != RS_OK) return 5;
+                t[k] = now_us() - a;
+                memcpy(v[2], nw, vec);
+                if (!check_parity(v, vec)) return 16;
+            }
+            report("Update", vec, (double)(2 + 2 * P) * vec, reps);
+            memcpy(v[2], saved[2], vec);
+            for (i = D; i < N; ++i) memcpy(v[i], saved[i], vec);
         }
-        if (ops & 8) report("Update", vec, (double)(2 + 2 * P) * vec, reps);
         if (ops & 16) {
+            /* parity ^= G[:, 1] x data (rs.go:492-529): from the parity before */
             int rows[1] = {1};
             for (k = 0; k < reps; ++k) {
-                double a = now_us();
+                double a;
+                size_t b;
+                int j;
+                for (j = 0; j < P; ++j) memcpy(saved[D + j], v[D + j], vec);
+                a = now_us();
                 if (rs_replace(rs, (const uint8_t* const*)v, lens, 1, rows, 1, v + D, lens + D, P) != RS_OK)
                     return 6;
                 t[k] = now_us() - a;
+                for (j = 0; j < P; ++j)
+                    for (b = 0; b < vec; ++b)
+                        if (v[D + j][b] != (uint8_t)(saved[D + j][b] ^ gmul(gen[j * D + 1], v[0][b]))) return 17;
+                ++checked;
             }
             report("Replace rn=1", vec, (double)(1 + 2 * P) * vec, reps);
         }
         for (i = 0; i < N; ++i) {
             if (reg && atoi(reg)) rs_host_unregister(v[i]);
             free(v[i]);
+            free(saved[i]);
         }
     }
     {
         uint64_t calls = 0, launches = 0;
         rs_host_engine_stats(rs, &calls, &launches);
-        printf("{\"engine_calls\": %llu, \"engine_launches\": %llu}\n", (unsigned long long)calls,
-               (unsigned long long)launches);
+        printf("{\"engine_calls\": %llu, \"engine_launches\": %llu, \"checked\": %ld}\n",
+               (unsigned long long)calls, (unsigned long long)launches, checked);
     }
     fprintf(stderr, "host_latency: rs_free\n");
     rs_free(rs);
