@@ -419,10 +419,11 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * default 200), "host_engine_life_us" (and once it has run this long, even
  * while calls keep coming: a device-wide synchronisation waits at most about
  * this long for it; default 4000), "host_engine_max_bytes" (larger batches
- * launch; default 1 MiB), "host_engine_vram" (1 default: the engine's call
- * slots and the small calls' input staging live in device memory the host
- * writes through the BAR, where the platform maps it for the CPU | 0: pinned
- * host memory; taken by handles whose engine starts after the change),
+ * launch; default 1 MiB), "host_engine_vram" (1: the engine's call slots and
+ * the small calls' input staging live in device memory the host writes
+ * through the BAR, where the platform maps it for the CPU | 0 default: pinned
+ * host memory, measured faster; taken by handles whose engine starts after
+ * the change),
  * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;

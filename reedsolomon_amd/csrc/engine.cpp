@@ -63,15 +63,19 @@ int g_engine_poll_gap = [] {  // (env RSAMD_ENGINE_POLL_GAP)
     return e ? std::atoi(e) : 0;
 }();
 // Call slots (and the pageable calls' input staging, host_calls.cpp) in
-// device memory the host writes through the BAR: the engine polls and reads
-// local HBM instead of paying a PCIe read round trip per poll and per input
-// batch (tools/bar_probe.hip, profiles/r03/bar_probe.log).  Taken by handles
-// whose engine starts after the change; rs_tune("host_engine_vram", 0 | 1),
-// env RSAMD_ENGINE_VRAM.  Platforms that map no device memory for the CPU
-// keep everything in host memory.
+// device memory the host writes through the BAR, so that the engine polls and
+// reads local memory instead of host memory over PCIe.  Off by default:
+// measured slower on MI355X (profiles/r03/host_latency_vram.log, 10+4 @ 8 KiB
+// Encode 13.8 us against 11.0 pageable, 9.7 against 9.2 registered): an
+// uncached device-memory read round trip is ~2.1 us against ~2.4 us for host
+// memory over PCIe (tools/bar_probe.hip, profiles/r03/bar_probe.log), while
+// the host's copy of 80 KiB of inputs through the BAR takes 1.5 us against
+// 0.55 us into pinned host memory.  Taken by handles whose engine starts after
+// the change; rs_tune("host_engine_vram", 0 | 1), env RSAMD_ENGINE_VRAM.
+// Platforms that map no device memory for the CPU keep host memory.
 int g_engine_vram = [] {
     const char* e = std::getenv("RSAMD_ENGINE_VRAM");
-    return e ? (std::atoi(e) ? 1 : 0) : 1;
+    return e ? (std::atoi(e) ? 1 : 0) : 0;
 }();
 // Batches up to this many bytes go to the engine, larger ones launch.
 size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
