@@ -105,6 +105,8 @@ struct rs_codec {
     size_t stage_bytes = 0;
     uint8_t* hstage = nullptr;  // pinned host mirror of `stage` (small-vector fast path)
     size_t hstage_bytes = 0;
+    uint8_t* bounce = nullptr;  // pinned bounce buffer of the staged path's pageable copies (two halves)
+    hipEvent_t bounce_ev[2] = {nullptr, nullptr};
     uint8_t* slots = nullptr;   // device staging slots of the staged (non-zero-copy) host path
     bool zc_pending = false;    // a zero-copy kernel may still be using hstage
     hipEvent_t chunk_ev[3] = {nullptr, nullptr, nullptr};  // host-call chunk pipeline slots
@@ -276,6 +278,9 @@ inline void rs_codec::release_device() {
         if (up_stream) (void)hipStreamDestroy(up_stream);
         if (stage) (void)hipFree(stage);
         if (hstage) (void)hipHostFree(hstage);
+        if (bounce) (void)hipHostFree(bounce);
+        for (hipEvent_t e : bounce_ev)
+            if (e) (void)hipEventDestroy(e);
         for (CoBatch& b : co)
             if (b.blk.host) rsamd::detail::pinned_put(b.blk);
         for (hipStream_t s : dma_stream)

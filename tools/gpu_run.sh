@@ -39,7 +39,7 @@ for step in "$@"; do
     tests)
       paths="${arg:-tests}"
       # shellcheck disable=SC2086
-      timeout -k 10 1000 python -u -m pytest $paths -m gpu -x -v -p no:cacheprovider --timeout 300 \
+      timeout -k 10 1000 python -u -m pytest $paths -m gpu -x -v -l -p no:cacheprovider --timeout 300 \
           --timeout-method thread > "$log" 2>&1 || fail "$step" $? "$log"
       tail -3 "$log" ;;
     bench)
