@@ -70,7 +70,7 @@ for step in "$@"; do
       cmd="${arg#*:}"
       export TMPDIR=/tmp
       # shellcheck disable=SC2086
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$tag" -o "$tag" -- python3 -u $cmd \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$tag" -o "$tag" -- python3 -u $cmd \
           > "$log" 2>&1 || fail "$step" $? "$log"
       tail -5 "$log" ;;
     pmc)
@@ -80,7 +80,7 @@ for step in "$@"; do
       cmd="${rest#*:}"
       export TMPDIR=/tmp
       # shellcheck disable=SC2086
-      timeout -s KILL 240 rocprofv3 --pmc $counters -d "$OUT/pmc_$tag" -o "$tag" -- python3 -u $cmd \
+      timeout -s KILL 240 rocprofv3 --pmc $counters -f csv -d "$OUT/pmc_$tag" -o "$tag" -- python3 -u $cmd \
           > "$log" 2>&1 || fail "$step" $? "$log"
       tail -5 "$log" ;;
     *)
