@@ -220,7 +220,7 @@ bool engine_accepts(int rows, int cols, size_t bytes);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
 void engine_shutdown(rs_t* rs);
 extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_life_us, g_engine_wg_units,
-    g_engine_yield_us, g_engine_poll_gap, g_engine_vram;
+    g_engine_yield_us, g_engine_poll_gap, g_engine_vram, g_engine_split_rows;
 // Device memory the host can write through the BAR (uncached for the GPU:
 // its loads always see the host's latest bytes), or nullptr when the
 // platform maps no such memory for the CPU (engine.cpp).  Blocks are pooled

@@ -82,6 +82,9 @@ size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
 // 16-byte units per workgroup a call is spread over (0: one per lane of a
 // workgroup); rs_tune("host_engine_wg_units")
 int g_engine_wg_units = 0;
+// A lone call's output rows computed by separate waves of each workgroup
+// (1) or all by its first wave (0); rs_tune("host_engine_split_rows")
+int g_engine_split_rows = 1;
 // Waiters spin this long, then yield the core between polls; rs_tune("host_engine_yield_us"), 0 = never
 // (default): 8-64 threads on the box measured the same either way and a lone
 // caller ~1 us slower with it (profiles/r02/engine_yield.log)
@@ -523,8 +526,11 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     h->nstripes = static_cast<uint32_t>(wk.nstripes);
     h->rows = static_cast<uint16_t>(rows);
     h->cols = static_cast<uint16_t>(cols);
+    // a lone call with all its units on the workgroups' first waves also
+    // spreads its rows over their waves (host_engine_split_rows)
+    const bool split = g_engine_split_rows && lone && per_wg == 64 && rows > 1 && rows <= rs->eng_group_waves;
     h->flags = (wk.accumulate ? 1u : 0u) | (wk.coherent ? 2u : 0u) | (g_engine_trace ? 4u : 0u) | (wk.addr ? 8u : 0u) |
-               (static_cast<uint32_t>(wg0) << 8) | (static_cast<uint32_t>(nwg) << 16);
+               (split ? 16u : 0u) | (static_cast<uint32_t>(wg0) << 8) | (static_cast<uint32_t>(nwg) << 16);
     h->tab_id = rs->eng_tab_id;
     // (write-combined device-memory slots and staging blocks: sfence makes
     // every store before it visible first, tables, addresses and inputs

@@ -924,6 +924,44 @@ __device__ __forceinline__ void engine_units(const EngineCall& e, const uint32_t
     }
 }
 
+// A lone call's rows spread over the waves of each workgroup: wave `row`
+// computes that one row over the workgroup's units (every wave loads the same
+// input lines; one row is ~1/ROWS of the VALU work, which bounds a lone call
+// at one wave per workgroup: ~720 dependent VALU for 10 x 4 at ~4-5 cycles).
+__device__ __forceinline__ void engine_units_row(const EngineCall& e, const uint32_t* tab, int row) {
+    typedef __attribute__((address_space(1))) u32x4 gq;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t step = e.nwg * 64u;
+    for (uint32_t u = e.local * 64u + lane; u < e.total; u += step) {
+        const uint32_t si = u / e.units, k = u - si * e.units;
+        const uint64_t sb = static_cast<uint64_t>(si) * e.stride + static_cast<uint64_t>(k) * 16;
+        u32x4 acc = e.accumulate ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(e.vaddr[e.cols + row] + sb))
+                                 : u32x4{0, 0, 0, 0};
+        for (int c0 = 0; c0 < e.cols; c0 += kEngineColBatch) {
+            const int nb = (e.cols - c0) < kEngineColBatch ? (e.cols - c0) : kEngineColBatch;
+            u32x4 x[kEngineColBatch];
+#pragma unroll
+            for (int b = 0; b < kEngineColBatch; ++b)
+                if (b < nb) x[b] = __builtin_nontemporal_load(reinterpret_cast<const gq*>(e.vaddr[c0 + b] + sb));
+#pragma unroll
+            for (int b = 0; b < kEngineColBatch; ++b) {
+                if (b < nb) {
+                    uint32_t t[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) t[i] = tab[((c0 + b) * kEngineMaxRows + row) * 5 + i];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t g0, g1, g2;
+                        split_groups(x[b][q], g0, g1, g2);
+                        acc[q] ^= gf_mul_packed(g0, g1, g2, t);
+                    }
+                }
+            }
+        }
+        __builtin_nontemporal_store(acc, reinterpret_cast<gq*>(e.vaddr[e.cols + row] + sb));
+    }
+}
+
 __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineSlot* vslots, uint64_t start,
                                                  uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks,
                                                  uint32_t poll_gap) {
@@ -1022,8 +1060,10 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
             s_vaddr[i] = addressed ? s_raw[8 * (1 + i / 7) + i % 7] : base + static_cast<uint64_t>(i) * pitch;
         }
         // system-scope acquire, always: without it the first call on a fresh
-        // coherent block read zeros (lines the runtime's clear left in L2)
-        if (works) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // coherent block read zeros (lines the runtime's clear left in L2).
+        // One wave's invalidate covers the workgroup: its waves share the
+        // CU's L1 and the XCD's L2, and they load only after the barrier below
+        if (works && poller) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
         if (works && tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords, every load in flight at once (one PCIe trip)
             if (poller) {
@@ -1042,7 +1082,11 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
         __syncthreads();  // tables and addresses ready; s_raw read by every wave
         const uint64_t t_tab = __builtin_amdgcn_s_memrealtime();
         const EngineCall call{s_vaddr, stride, units, works ? nstripes * units : 0u, cols, accumulate, local, nwg};
-        if (works) switch (rows) {
+        const bool split_rows = (w5 & 16) != 0 && rows <= static_cast<int>(blockDim.x >> 6);
+        if (works && split_rows) {
+            const int wave = static_cast<int>(threadIdx.x >> 6);
+            if (wave < rows) engine_units_row(call, tab, wave);
+        } else if (works) switch (rows) {
             case 1: engine_units<1>(call, tab); break;
             case 2: engine_units<2>(call, tab); break;
             case 3: engine_units<3>(call, tab); break;

@@ -79,6 +79,8 @@ struct EngineHeader {      // one 64-byte line; the host writes seq0 and seq1 LA
                            // bit 2: workgroup 0 writes EngineRing::stamp (diagnostics);
                            // bit 3: address mode: vector i of the (single) stripe is at
                            // EngineSlot::ptr[i / 7][i % 7] instead of base + i * pitch;
+                           // bit 4: rows across waves (wave r of each workgroup computes row r;
+                           // a lone call, rows <= waves per workgroup);
                            // bits 8-15: first workgroup of the call, 16-23: its workgroups
                            // (wrapping; the others pass the call without work)
     uint32_t tab_id;       // identity of the slot's tables (reloaded into LDS when it changes)

@@ -13,7 +13,8 @@
  *   HL_VEC=bytes: only this vector size; HL_OPS=mask: only these ops (bit 0
  *   Encode, 1 Reconst lost=1, 2 Reconst lost=4, 3 Update, 4 Replace)
  *   HL_VRAM=0/1: engine call slots and input staging in host-writable device
- *   memory (default 1 where the platform has it)
+ *   memory (default 0); HL_SPLIT_ROWS=0/1: a lone call's rows on separate
+ *   waves (default 1)
  *
  * Every call's result is checked outside the timed region: Encode's parity
  * and Update / Replace's new parity against a plain GF(2^8)/0x11d product
@@ -102,6 +103,7 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE_POLL_GAP")) rs_tune("host_engine_poll_gap", atoi(getenv("HL_ENGINE_POLL_GAP")));
     if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
     if (getenv("HL_VRAM")) rs_tune("host_engine_vram", atoi(getenv("HL_VRAM")));
+    if (getenv("HL_SPLIT_ROWS")) rs_tune("host_engine_split_rows", atoi(getenv("HL_SPLIT_ROWS")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
