@@ -117,7 +117,7 @@ void transpose8(Asm& A, const int (&r)[8]) {
 
 }  // namespace
 
-std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int* vgprs_out) {
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int* vgprs_out) {
     const int rw = (rows + nw - 1) / nw;  // rows per wave
     Layout L;
     L.pf = pf < 1 ? 1 : pf > 4 ? 4 : pf;
@@ -238,15 +238,20 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
         };
         auto slot_reg = [&](int c, int j) { return kVSlots + 8 * (c % L.pf) + j; };
         std::vector<int> col_id(static_cast<size_t>(cols), -1);  // last VMEM op of each column's loads
+        // a lone wave streams its inputs (nt); the waves of a multi-wave
+        // workgroup read the same lines, so those loads keep them cached for
+        // the other waves (measured with nt: 64+64 Encode fetched 1.45x its
+        // input bytes from HBM, 128+128 2.8x; profiles/r03/pmc_traffic_*.json)
+        const char* in_aux = nw > 1 ? "" : " nt";
         auto issue_col = [&](int c) {  // stage(c) was issued into slot c & 1
             desc(c & 1, kSDescIn);
             if (c + 1 < cols) stage(c + 1, (c + 1) & 1);
             for (int k = 0; k < 4; ++k) {
                 const int v = slot_reg(c, 2 * k);
-                if (k) A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen offset:%d nt", v, v + 1, kVOff,
-                              kSDescIn, kSDescIn + 3, 512 * k);
-                else A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen nt", v, v + 1, kVOff, kSDescIn,
-                            kSDescIn + 3);
+                if (k) A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen offset:%d%s", v, v + 1, kVOff,
+                              kSDescIn, kSDescIn + 3, 512 * k, in_aux);
+                else A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen%s", v, v + 1, kVOff, kSDescIn,
+                            kSDescIn + 3, in_aux);
                 vq.push_back(next_id);
                 col_id[static_cast<size_t>(c)] = next_id++;
             }
@@ -304,6 +309,9 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
                     }
                 }
             if (c + L.pf < cols) issue_col(c + L.pf);  // the slot is free again
+            // keep the waves within `sync` columns of each other, so the lines
+            // the first wave fetched are still cached when the others load them
+            if (nw > 1 && sync > 0 && (c + 1) % sync == 0 && c + 1 < cols) A.line("s_barrier");
         }
         // ---- outputs: transpose back, (accumulate: XOR the old bytes), store
         int ostage = 0;

@@ -34,7 +34,10 @@ inline int asm_waves(int rows) { return rows <= 16 ? 1 : (rows + 15) / 16; }
 // The assembly source of the kernel for a rows x cols matrix (row-major),
 // accumulate (XOR into the outputs) or overwrite, nw waves per workgroup,
 // pf columns of loads in flight.  *vgprs receives the VGPRs per lane.
-std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int* vgprs);
+// sync > 0: the waves of a multi-wave workgroup meet at s_barrier every
+// `sync` columns.
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int sync,
+                       int* vgprs);
 // Assemble + link (comgr) into a code object; false with the log on failure.
 bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* log, double* ms);
 

@@ -148,7 +148,7 @@ class Wave:
                     elif n == 0:
                         self.lgkm.clear()
                 continue
-            if op == "s_nop":
+            if op == "s_nop" or op == "s_barrier":  # waves run one after another here
                 continue
             if ops and op not in ("s_cbranch_scc1", "s_cbranch_scc0", "s_branch", "s_cmp_eq_u64", "s_cmp_eq_u32",
                                   "s_setpc_b64", "buffer_store_dwordx2"):

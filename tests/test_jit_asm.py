@@ -28,6 +28,24 @@ def _karg(body, stripe0, stripe_ids, ptrs, strides16):
 @pytest.mark.parametrize("rows,cols,acc", [(5, 10, 0), (8, 10, 1), (3, 7, 0), (16, 16, 0), (12, 5, 1),
                                            (20, 4, 0), (33, 3, 1), (9, 1, 0), (17, 5, 0)])
 def test_asm_kernel_matches_oracle(rslib, orc, rows, cols, acc):
+    _check_kernel(rslib, orc, rows, cols, acc)
+
+
+@pytest.mark.parametrize("rows,cols,sync", [(33, 7, 2), (40, 9, 4), (17, 5, 1)])
+def test_asm_kernel_with_barriers(rslib, orc, rows, cols, sync):
+    """rs_tune("jit_sync", n): the waves of a multi-wave kernel meet at
+    s_barrier every n columns; the same number of barriers in every wave."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_sync", sync) == 0
+    try:
+        src = _check_kernel(rslib, orc, rows, cols, 0)
+    finally:
+        L.rs_tune(b"jit_sync", 0)
+    nw = (rows + 15) // 16
+    assert src.count("s_barrier") == nw * ((cols - 1) // sync)
+
+
+def _check_kernel(rslib, orc, rows, cols, acc):
     rng = np.random.default_rng(rows * 1000 + cols * 10 + acc)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
     src = rslib.jit_asm_source(mat, bool(acc))
@@ -56,3 +74,4 @@ def test_asm_kernel_matches_oracle(rslib, orc, rows, cols, acc):
     assert np.array_equal(got[:, cols:, :body], exp)
     assert np.array_equal(got[:, :cols], host[:, :cols])             # inputs untouched
     assert np.array_equal(got[:, cols:, body:], host[:, cols:, body:])  # past the body untouched
+    return src
