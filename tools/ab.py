@@ -70,8 +70,10 @@ def main():
     import numpy as np
 
     rng = np.random.default_rng(5)
-    pats = [sum(1 << int(v) for v in rng.choice(K + M, int(rng.integers(1, M + 1)), replace=False))
-            for _ in range(16)]
+    # multi16 patterns over the first 64 vectors (64-bit masks)
+    pats = [sum(1 << int(v) for v in rng.choice(min(K + M, 64), int(rng.integers(1, min(M, 64 - K) + 1)),
+                                                replace=False))
+            for _ in range(16)] if K < 64 else [1] * 16
     masks = np.array([pats[i % 16] for i in range(S)], dtype=np.uint64)
     masks_sorted = np.array([pats[i * 16 // S] for i in range(S)], dtype=np.uint64)  # runs of one pattern
     nrec16 = sum(bin(int(x)).count("1") for x in masks)

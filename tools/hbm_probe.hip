@@ -403,6 +403,75 @@ __global__ __launch_bounds__(128) void kin_inplace(uint8_t* base, uint64_t vec, 
     store(sb1, off1, x1);
 }
 
+// Geometry of the run-time assembly kernels (jit_asm.cpp) against the
+// perm-table kernels' (in-place Reconst): GEO 0 = 128 lanes x
+// 8 B over a 1 KiB chunk; GEO 1 = 64 lanes, each owning four 8-byte pieces
+// 512 B apart of a 2 KiB chunk.  SPLIT: the lost vectors are written into a
+// separate [S][KW][vec] region (`wbase`) instead of in place.  Every load is
+// issued before any store; XOR for the math.
+template <int KR, int KW, int GEO, bool SPLIT>
+__global__ __launch_bounds__(GEO ? 64 : 128) void kin_geo(uint8_t* base, uint8_t* wbase, uint64_t vec, uint64_t sstride,
+                                                           uint32_t cps, IdxList L) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    constexpr int P = GEO ? 4 : 1;
+    const uint32_t s = blockIdx.x / cps, cb = blockIdx.x % cps;
+    const uint64_t sb = (uint64_t)s * sstride;
+    const uint32_t off = cb * (GEO ? 2048u : 1024u) + threadIdx.x * 8u;
+    u32x2 x[KR][P];
+#pragma unroll
+    for (int i = 0; i < KR; ++i)
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            x[i][k] = __builtin_amdgcn_raw_buffer_load_b64(rsrc(base + sb + L.rd[i] * vec, (uint32_t)vec), off + 512 * k,
+                                                           0, 2);
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        uint8_t* w = SPLIT ? wbase + ((uint64_t)s * KW + j) * vec : base + sb + L.wr[j] * vec;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            u32x2 a = {(uint32_t)j, 0u};
+#pragma unroll
+            for (int i = 0; i < KR; ++i) a ^= x[i][k];
+            __builtin_amdgcn_raw_buffer_store_b64(a, rsrc(w, (uint32_t)vec), off + 512 * k, 0, 2);
+        }
+    }
+}
+
+// kind: 0 = 1 KiB / 128 lanes in place, 1 = 2 KiB / 64 lanes (assembly-kernel
+// geometry) in place, 2 / 3 = the same with the writes into `w` (split)
+extern "C" int probe_geo(int kind, int shape, void* a, void* w, uint64_t vec, int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    IdxList L{};
+    const int geo = kind & 1;
+    const uint32_t cps = static_cast<uint32_t>(vec / (geo ? 2048 : 1024));
+    const dim3 grid(cps * static_cast<uint32_t>(nstripes)), block(geo ? 64 : 128);
+#define KG(KR, KW, NV)                                                                                          \
+    do {                                                                                                        \
+        const uint64_t ss = (uint64_t)(NV) * vec;                                                              \
+        uint8_t *pa = (uint8_t*)a, *pw = (uint8_t*)w;                                                           \
+        if (kind == 0) hipLaunchKernelGGL((kin_geo<KR, KW, 0, false>), grid, block, 0, st, pa, pw, vec, ss, cps, L); \
+        else if (kind == 1) hipLaunchKernelGGL((kin_geo<KR, KW, 1, false>), grid, block, 0, st, pa, pw, vec, ss, cps, L); \
+        else if (kind == 2) hipLaunchKernelGGL((kin_geo<KR, KW, 0, true>), grid, block, 0, st, pa, pw, vec, ss, cps, L); \
+        else hipLaunchKernelGGL((kin_geo<KR, KW, 1, true>), grid, block, 0, st, pa, pw, vec, ss, cps, L);       \
+    } while (0)
+    if (shape == 0) {
+        for (int i = 0; i < 10; ++i) L.rd[i] = 8 + i;
+        for (int j = 0; j < 8; ++j) L.wr[j] = j;
+        KG(10, 8, 18);
+    } else if (shape == 1) {
+        const uint32_t wr[5] = {0, 2, 4, 6, 8}, rd[10] = {1, 3, 5, 7, 9, 10, 11, 12, 13, 14};
+        for (int i = 0; i < 10; ++i) L.rd[i] = rd[i];
+        for (int j = 0; j < 5; ++j) L.wr[j] = wr[j];
+        KG(10, 5, 18);
+    } else {
+        for (int i = 0; i < 10; ++i) L.rd[i] = 4 + i;
+        for (int j = 0; j < 4; ++j) L.wr[j] = j;
+        KG(10, 4, 14);
+    }
+#undef KG
+    return hipGetLastError();
+}
+
 // kind: 0/1/2 = DEFER; shape: 0 = 10+8 lost 0-7 (reads 8..17), 1 = 10+8
 // lost 0,2,4,6,8 (5 writes), 2 = 10+4 lost 0-3, 3 = 10+8 Encode-like (reads
 // 0..9, writes 10..17; the same in-place buffer)

@@ -127,6 +127,23 @@ def pattern_probes(L, a, n, vp, sp, timeit):
                            lambda: L.probe_inplace(kind, shape, vp(a), ctypes.c_uint64(vec), S, sp),
                            S * (kr + kw) * vec, iters=20)
         return
+    if os.environ.get("PROBE_GEO", "0") == "1":
+        # the assembly kernels' 2 KiB / 64-lane geometry against the 1 KiB /
+        # 128-lane one, in place and with the lost vectors written elsewhere
+        L.probe_geo.restype = ctypes.c_int
+        vec = 1 << 20
+        for shape, nv, kr, kw, name in ((1, 18, 10, 5, "10+8 lost 5 data"), (0, 18, 10, 8, "10+8 lost 0-7"),
+                                        (2, 14, 10, 4, "10+4 lost 0-3")):
+            S = min(256, int(n // (nv * vec)))
+            import torch
+            b = torch.empty(S * kw * vec, dtype=torch.uint8, device="cuda")
+            for _ in range(2):
+                for kind, kname in ((0, "1KiB/128 in place"), (1, "2KiB/64 in place"), (2, "1KiB/128 split"),
+                                    (3, "2KiB/64 split")):
+                    timeit(f"geo {name} {kname}",
+                           lambda: L.probe_geo(kind, shape, vp(a), vp(b), ctypes.c_uint64(vec), S, sp),
+                           S * (kr + kw) * vec, iters=20)
+        return
     if os.environ.get("PROBE_BUF", "0") == "1":
         import torch
         half = (n // 2) // 4096 * 4096
