@@ -83,8 +83,11 @@ size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
 // workgroup); rs_tune("host_engine_wg_units")
 int g_engine_wg_units = 0;
 // A lone call's output rows computed by separate waves of each workgroup
-// (1) or all by its first wave (0); rs_tune("host_engine_split_rows")
-int g_engine_split_rows = 1;
+// (1) or all by its first wave (0, default); rs_tune("host_engine_split_rows").
+// Measured slower: each wave reads every input over PCIe again (host memory is
+// not cached), 10+4 @ 8 KiB Encode 10.8 -> 20.5 us, Reconst of 4 10.9 -> 20.4
+// (profiles/r03/host_latency_split_rows.log)
+int g_engine_split_rows = 0;
 // Waiters spin this long, then yield the core between polls; rs_tune("host_engine_yield_us"), 0 = never
 // (default): 8-64 threads on the box measured the same either way and a lone
 // caller ~1 us slower with it (profiles/r02/engine_yield.log)

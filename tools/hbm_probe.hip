@@ -404,56 +404,84 @@ __global__ __launch_bounds__(128) void kin_inplace(uint8_t* base, uint64_t vec, 
 }
 
 // Geometry of the run-time assembly kernels (jit_asm.cpp) against the
-// perm-table kernels' (in-place Reconst): GEO 0 = 128 lanes x
-// 8 B over a 1 KiB chunk; GEO 1 = 64 lanes, each owning four 8-byte pieces
-// 512 B apart of a 2 KiB chunk.  SPLIT: the lost vectors are written into a
-// separate [S][KW][vec] region (`wbase`) instead of in place.  Every load is
-// issued before any store; XOR for the math.
+// perm-table kernels' (in-place Reconst).  GEO (lanes per
+// workgroup, bytes a workgroup covers per vector, 8-byte pieces per lane):
+//   0: 128 lanes, 1 KiB, 1 piece at 8t          (perm-table kernels)
+//   1:  64 lanes, 2 KiB, 4 pieces at 8t + 512k  (assembly kernels, round 3)
+//   2: 256 lanes, 2 KiB, 1 piece at 8t
+//   3: 128 lanes, 2 KiB, 2 pieces at 8t + 1024k
+//   4:  64 lanes, 512 B of 4 stripes: piece k at 8t of stripe 4g + k
+// SPLIT: the lost vectors are written into a separate [S][KW][vec] region
+// (`wbase`) instead of in place.  Every load is issued before any store;
+// XOR for the math.
+template <int GEO>
+struct Geo {
+    static constexpr int lanes = GEO == 0 ? 128 : GEO == 2 ? 256 : GEO == 3 ? 128 : 64;
+    static constexpr int P = GEO == 1 || GEO == 4 ? 4 : GEO == 3 ? 2 : 1;
+    static constexpr uint32_t chunk = GEO == 0 ? 1024 : GEO == 4 ? 512 : 2048;
+    static constexpr uint32_t step = GEO == 1 ? 512 : GEO == 3 ? 1024 : 0;  // piece spacing within a stripe
+    static constexpr int spp = GEO == 4 ? 4 : 1;                             // stripes per workgroup
+};
 template <int KR, int KW, int GEO, bool SPLIT>
-__global__ __launch_bounds__(GEO ? 64 : 128) void kin_geo(uint8_t* base, uint8_t* wbase, uint64_t vec, uint64_t sstride,
-                                                           uint32_t cps, IdxList L) {
+__global__ __launch_bounds__(Geo<GEO>::lanes) void kin_geo(uint8_t* base, uint8_t* wbase, uint64_t vec,
+                                                            uint64_t sstride, uint32_t cps, IdxList L) {
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    constexpr int P = GEO ? 4 : 1;
-    const uint32_t s = blockIdx.x / cps, cb = blockIdx.x % cps;
-    const uint64_t sb = (uint64_t)s * sstride;
-    const uint32_t off = cb * (GEO ? 2048u : 1024u) + threadIdx.x * 8u;
-    u32x2 x[KR][P];
+    typedef Geo<GEO> G;
+    const uint32_t sg = blockIdx.x / cps, cb = blockIdx.x % cps;
+    const uint32_t off0 = cb * G::chunk + threadIdx.x * 8u;
+    auto stripe = [&](int k) { return (uint64_t)(sg * G::spp + (G::spp > 1 ? k : 0)); };
+    auto offk = [&](int k) { return off0 + (G::spp > 1 ? 0u : G::step * k); };
+    u32x2 x[KR][G::P];
 #pragma unroll
     for (int i = 0; i < KR; ++i)
 #pragma unroll
-        for (int k = 0; k < P; ++k)
-            x[i][k] = __builtin_amdgcn_raw_buffer_load_b64(rsrc(base + sb + L.rd[i] * vec, (uint32_t)vec), off + 512 * k,
-                                                           0, 2);
+        for (int k = 0; k < G::P; ++k)
+            x[i][k] = __builtin_amdgcn_raw_buffer_load_b64(
+                rsrc(base + stripe(k) * sstride + L.rd[i] * vec, (uint32_t)vec), offk(k), 0, 2);
 #pragma unroll
     for (int j = 0; j < KW; ++j) {
-        uint8_t* w = SPLIT ? wbase + ((uint64_t)s * KW + j) * vec : base + sb + L.wr[j] * vec;
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
+        for (int k = 0; k < G::P; ++k) {
+            uint8_t* w = SPLIT ? wbase + (stripe(k) * KW + j) * vec : base + stripe(k) * sstride + L.wr[j] * vec;
             u32x2 a = {(uint32_t)j, 0u};
 #pragma unroll
             for (int i = 0; i < KR; ++i) a ^= x[i][k];
-            __builtin_amdgcn_raw_buffer_store_b64(a, rsrc(w, (uint32_t)vec), off + 512 * k, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b64(a, rsrc(w, (uint32_t)vec), offk(k), 0, 2);
         }
     }
 }
 
-// kind: 0 = 1 KiB / 128 lanes in place, 1 = 2 KiB / 64 lanes (assembly-kernel
-// geometry) in place, 2 / 3 = the same with the writes into `w` (split)
+// kind = GEO + 8 * SPLIT (GEO 0-4 above); nstripes a multiple of 4
 extern "C" int probe_geo(int kind, int shape, void* a, void* w, uint64_t vec, int nstripes, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     IdxList L{};
-    const int geo = kind & 1;
-    const uint32_t cps = static_cast<uint32_t>(vec / (geo ? 2048 : 1024));
-    const dim3 grid(cps * static_cast<uint32_t>(nstripes)), block(geo ? 64 : 128);
-#define KG(KR, KW, NV)                                                                                          \
-    do {                                                                                                        \
-        const uint64_t ss = (uint64_t)(NV) * vec;                                                              \
-        uint8_t *pa = (uint8_t*)a, *pw = (uint8_t*)w;                                                           \
-        if (kind == 0) hipLaunchKernelGGL((kin_geo<KR, KW, 0, false>), grid, block, 0, st, pa, pw, vec, ss, cps, L); \
-        else if (kind == 1) hipLaunchKernelGGL((kin_geo<KR, KW, 1, false>), grid, block, 0, st, pa, pw, vec, ss, cps, L); \
-        else if (kind == 2) hipLaunchKernelGGL((kin_geo<KR, KW, 0, true>), grid, block, 0, st, pa, pw, vec, ss, cps, L); \
-        else hipLaunchKernelGGL((kin_geo<KR, KW, 1, true>), grid, block, 0, st, pa, pw, vec, ss, cps, L);       \
+    const int geo = kind & 7;
+    const bool split = kind >= 8;
+    if (geo > 4 || nstripes % 4) return -1;
+    const uint32_t chunk = geo == 0 ? 1024 : geo == 4 ? 512 : 2048;
+    const uint32_t cps = static_cast<uint32_t>(vec / chunk);
+    const uint32_t groups = geo == 4 ? nstripes / 4 : nstripes;
+    const dim3 grid(cps * groups);
+#define KG1(KR, KW, G, SP)                                                                                     \
+    hipLaunchKernelGGL((kin_geo<KR, KW, G, SP>), grid, dim3(Geo<G>::lanes), 0, st, (uint8_t*)a, (uint8_t*)w, vec, \
+                       ss, cps, L)
+#define KG(KR, KW, NV)                                                          \
+    do {                                                                        \
+        const uint64_t ss = (uint64_t)(NV) * vec;                               \
+        switch (kind) {                                                         \
+            case 0: KG1(KR, KW, 0, false); break;                               \
+            case 1: KG1(KR, KW, 1, false); break;                               \
+            case 2: KG1(KR, KW, 2, false); break;                               \
+            case 3: KG1(KR, KW, 3, false); break;                               \
+            case 4: KG1(KR, KW, 4, false); break;                               \
+            case 8: KG1(KR, KW, 0, true); break;                                \
+            case 9: KG1(KR, KW, 1, true); break;                                \
+            case 10: KG1(KR, KW, 2, true); break;                               \
+            case 11: KG1(KR, KW, 3, true); break;                               \
+            default: KG1(KR, KW, 4, true); break;                               \
+        }                                                                       \
     } while (0)
+    (void)split;
     if (shape == 0) {
         for (int i = 0; i < 10; ++i) L.rd[i] = 8 + i;
         for (int j = 0; j < 8; ++j) L.wr[j] = j;
@@ -469,6 +497,7 @@ extern "C" int probe_geo(int kind, int shape, void* a, void* w, uint64_t vec, in
         KG(10, 4, 14);
     }
 #undef KG
+#undef KG1
     return hipGetLastError();
 }
 

@@ -132,17 +132,18 @@ def pattern_probes(L, a, n, vp, sp, timeit):
         # 128-lane one, in place and with the lost vectors written elsewhere
         L.probe_geo.restype = ctypes.c_int
         vec = 1 << 20
+        geos = ((0, "1KiB/128"), (1, "2KiB/64 x4"), (2, "2KiB/256"), (3, "2KiB/128 x2"), (4, "512B x 4 stripes/64"))
         for shape, nv, kr, kw, name in ((1, 18, 10, 5, "10+8 lost 5 data"), (0, 18, 10, 8, "10+8 lost 0-7"),
                                         (2, 14, 10, 4, "10+4 lost 0-3")):
-            S = min(256, int(n // (nv * vec)))
+            S = min(256, int(n // (nv * vec))) // 4 * 4
             import torch
             b = torch.empty(S * kw * vec, dtype=torch.uint8, device="cuda")
             for _ in range(2):
-                for kind, kname in ((0, "1KiB/128 in place"), (1, "2KiB/64 in place"), (2, "1KiB/128 split"),
-                                    (3, "2KiB/64 split")):
-                    timeit(f"geo {name} {kname}",
-                           lambda: L.probe_geo(kind, shape, vp(a), vp(b), ctypes.c_uint64(vec), S, sp),
-                           S * (kr + kw) * vec, iters=20)
+                for split in (0, 8):
+                    for geo, gname in geos:
+                        timeit(f"geo {name} {gname} {'split' if split else 'in place'}",
+                               lambda: L.probe_geo(geo + split, shape, vp(a), vp(b), ctypes.c_uint64(vec), S, sp),
+                               S * (kr + kw) * vec, iters=20)
         return
     if os.environ.get("PROBE_BUF", "0") == "1":
         import torch
