@@ -411,15 +411,17 @@ __global__ __launch_bounds__(128) void kin_inplace(uint8_t* base, uint64_t vec, 
 //   2: 256 lanes, 2 KiB, 1 piece at 8t
 //   3: 128 lanes, 2 KiB, 2 pieces at 8t + 1024k
 //   4:  64 lanes, 512 B of 4 stripes: piece k at 8t of stripe 4g + k
+//   5: 256 lanes, 8 KiB, 4 pieces at 512w + 8l + 2048k (wave w, lane l)
+//   6: 128 lanes, 4 KiB, 4 pieces at 512w + 8l + 1024k
 // SPLIT: the lost vectors are written into a separate [S][KW][vec] region
 // (`wbase`) instead of in place.  Every load is issued before any store;
 // XOR for the math.
 template <int GEO>
 struct Geo {
-    static constexpr int lanes = GEO == 0 ? 128 : GEO == 2 ? 256 : GEO == 3 ? 128 : 64;
-    static constexpr int P = GEO == 1 || GEO == 4 ? 4 : GEO == 3 ? 2 : 1;
-    static constexpr uint32_t chunk = GEO == 0 ? 1024 : GEO == 4 ? 512 : 2048;
-    static constexpr uint32_t step = GEO == 1 ? 512 : GEO == 3 ? 1024 : 0;  // piece spacing within a stripe
+    static constexpr int lanes = GEO == 0 ? 128 : GEO == 2 ? 256 : GEO == 3 ? 128 : GEO == 5 ? 256 : GEO == 6 ? 128 : 64;
+    static constexpr int P = GEO == 1 || GEO == 4 || GEO >= 5 ? 4 : GEO == 3 ? 2 : 1;
+    static constexpr uint32_t chunk = GEO == 0 ? 1024 : GEO == 4 ? 512 : GEO == 5 ? 8192 : GEO == 6 ? 4096 : 2048;
+    static constexpr uint32_t step = GEO == 1 ? 512 : GEO == 3 ? 1024 : GEO == 5 ? 2048 : GEO == 6 ? 1024 : 0;
     static constexpr int spp = GEO == 4 ? 4 : 1;                             // stripes per workgroup
 };
 template <int KR, int KW, int GEO, bool SPLIT>
@@ -428,7 +430,8 @@ __global__ __launch_bounds__(Geo<GEO>::lanes) void kin_geo(uint8_t* base, uint8_
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef Geo<GEO> G;
     const uint32_t sg = blockIdx.x / cps, cb = blockIdx.x % cps;
-    const uint32_t off0 = cb * G::chunk + threadIdx.x * 8u;
+    const uint32_t off0 = GEO >= 5 ? cb * G::chunk + (threadIdx.x >> 6) * 512u + (threadIdx.x & 63) * 8u
+                                   : cb * G::chunk + threadIdx.x * 8u;
     auto stripe = [&](int k) { return (uint64_t)(sg * G::spp + (G::spp > 1 ? k : 0)); };
     auto offk = [&](int k) { return off0 + (G::spp > 1 ? 0u : G::step * k); };
     u32x2 x[KR][G::P];
@@ -451,20 +454,53 @@ __global__ __launch_bounds__(Geo<GEO>::lanes) void kin_geo(uint8_t* base, uint8_
     }
 }
 
-// kind = GEO + 8 * SPLIT (GEO 0-4 above); nstripes a multiple of 4
+// 16-byte pieces, 64 lanes over 2 KiB: GEO 7 = two dwordx4 at 16l + 1024k
+// (each wave instruction covers 1 KiB), GEO 8 = two dwordx4 at 32l + 16k
+// (a lane's 32 bytes contiguous; each instruction touches every other 16 B)
+template <int KR, int KW, int GEO, bool SPLIT>
+__global__ __launch_bounds__(64) void kin_geo16(uint8_t* base, uint8_t* wbase, uint64_t vec, uint64_t sstride,
+                                                uint32_t cps, IdxList L) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t s = blockIdx.x / cps, cb = blockIdx.x % cps;
+    const uint64_t sb = (uint64_t)s * sstride;
+    auto offk = [&](int k) {
+        return GEO == 7 ? cb * 2048u + threadIdx.x * 16u + 1024u * k : cb * 2048u + threadIdx.x * 32u + 16u * k;
+    };
+    u32x4 x[KR][2];
+#pragma unroll
+    for (int i = 0; i < KR; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            x[i][k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base + sb + L.rd[i] * vec, (uint32_t)vec), offk(k), 0, 2);
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        uint8_t* w = SPLIT ? wbase + ((uint64_t)s * KW + j) * vec : base + sb + L.wr[j] * vec;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            u32x4 a = {(uint32_t)j, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < KR; ++i) a ^= x[i][k];
+            __builtin_amdgcn_raw_buffer_store_b128(a, rsrc(w, (uint32_t)vec), offk(k), 0, 2);
+        }
+    }
+}
+
+// kind = GEO + 16 * SPLIT (GEO 0-8 above); nstripes a multiple of 4
 extern "C" int probe_geo(int kind, int shape, void* a, void* w, uint64_t vec, int nstripes, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     IdxList L{};
-    const int geo = kind & 7;
-    const bool split = kind >= 8;
-    if (geo > 4 || nstripes % 4) return -1;
-    const uint32_t chunk = geo == 0 ? 1024 : geo == 4 ? 512 : 2048;
+    const int geo = kind & 15;
+    const bool split = kind >= 16;
+    if (geo > 8 || nstripes % 4) return -1;
+    const uint32_t chunk = geo == 0 ? 1024 : geo == 4 ? 512 : geo == 5 ? 8192 : geo == 6 ? 4096 : 2048;
     const uint32_t cps = static_cast<uint32_t>(vec / chunk);
     const uint32_t groups = geo == 4 ? nstripes / 4 : nstripes;
     const dim3 grid(cps * groups);
 #define KG1(KR, KW, G, SP)                                                                                     \
     hipLaunchKernelGGL((kin_geo<KR, KW, G, SP>), grid, dim3(Geo<G>::lanes), 0, st, (uint8_t*)a, (uint8_t*)w, vec, \
                        ss, cps, L)
+#define KG16(KR, KW, G, SP)                                                                                    \
+    hipLaunchKernelGGL((kin_geo16<KR, KW, G, SP>), grid, dim3(64), 0, st, (uint8_t*)a, (uint8_t*)w, vec, ss, cps, L)
 #define KG(KR, KW, NV)                                                          \
     do {                                                                        \
         const uint64_t ss = (uint64_t)(NV) * vec;                               \
@@ -474,11 +510,19 @@ extern "C" int probe_geo(int kind, int shape, void* a, void* w, uint64_t vec, in
             case 2: KG1(KR, KW, 2, false); break;                               \
             case 3: KG1(KR, KW, 3, false); break;                               \
             case 4: KG1(KR, KW, 4, false); break;                               \
-            case 8: KG1(KR, KW, 0, true); break;                                \
-            case 9: KG1(KR, KW, 1, true); break;                                \
-            case 10: KG1(KR, KW, 2, true); break;                               \
-            case 11: KG1(KR, KW, 3, true); break;                               \
-            default: KG1(KR, KW, 4, true); break;                               \
+            case 5: KG1(KR, KW, 5, false); break;                               \
+            case 6: KG1(KR, KW, 6, false); break;                               \
+            case 7: KG16(KR, KW, 7, false); break;                              \
+            case 8: KG16(KR, KW, 8, false); break;                              \
+            case 16: KG1(KR, KW, 0, true); break;                               \
+            case 17: KG1(KR, KW, 1, true); break;                               \
+            case 18: KG1(KR, KW, 2, true); break;                               \
+            case 19: KG1(KR, KW, 3, true); break;                               \
+            case 20: KG1(KR, KW, 4, true); break;                               \
+            case 21: KG1(KR, KW, 5, true); break;                               \
+            case 22: KG1(KR, KW, 6, true); break;                               \
+            case 23: KG16(KR, KW, 7, true); break;                              \
+            default: KG16(KR, KW, 8, true); break;                              \
         }                                                                       \
     } while (0)
     (void)split;
@@ -498,6 +542,7 @@ extern "C" int probe_geo(int kind, int shape, void* a, void* w, uint64_t vec, in
     }
 #undef KG
 #undef KG1
+#undef KG16
     return hipGetLastError();
 }
 

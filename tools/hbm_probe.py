@@ -132,14 +132,19 @@ def pattern_probes(L, a, n, vp, sp, timeit):
         # 128-lane one, in place and with the lost vectors written elsewhere
         L.probe_geo.restype = ctypes.c_int
         vec = 1 << 20
-        geos = ((0, "1KiB/128"), (1, "2KiB/64 x4"), (2, "2KiB/256"), (3, "2KiB/128 x2"), (4, "512B x 4 stripes/64"))
+        geos = ((0, "1KiB/128"), (1, "2KiB/64 x4"), (2, "2KiB/256"), (3, "2KiB/128 x2"), (4, "512B x 4 stripes/64"),
+                (5, "8KiB/256 x4 wave-interleaved"), (6, "4KiB/128 x4 wave-interleaved"),
+                (7, "2KiB/64 x2 dwordx4 1KiB apart"), (8, "2KiB/64 x2 dwordx4 contiguous"))
+        if os.environ.get("PROBE_GEOS"):
+            keep = {int(x) for x in os.environ["PROBE_GEOS"].split(",")}
+            geos = tuple(g for g in geos if g[0] in keep)
         for shape, nv, kr, kw, name in ((1, 18, 10, 5, "10+8 lost 5 data"), (0, 18, 10, 8, "10+8 lost 0-7"),
                                         (2, 14, 10, 4, "10+4 lost 0-3")):
             S = min(256, int(n // (nv * vec))) // 4 * 4
             import torch
             b = torch.empty(S * kw * vec, dtype=torch.uint8, device="cuda")
             for _ in range(2):
-                for split in (0, 8):
+                for split in (0, 16):
                     for geo, gname in geos:
                         timeit(f"geo {name} {gname} {'split' if split else 'in place'}",
                                lambda: L.probe_geo(geo + split, shape, vp(a), vp(b), ctypes.c_uint64(vec), S, sp),
