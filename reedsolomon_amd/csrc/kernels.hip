@@ -69,7 +69,10 @@ LaunchTuning& tuning() {
         x.bs_block = 0;
         x.wide_block = 256;
         x.wide_single_pass = 1;
-        x.bs_waves = 0;
+        // 2 waves per SIMD: fewer 32 * bs-byte chunks in flight per CU; +3-8 %
+        // on every generated shape, split and interleaved (10+8 Encode 6.04 ->
+        // 6.28 TB/s, 8+5 interleaved 6.06 -> 6.53; profiles/r03/ab_bs_waves.log)
+        x.bs_waves = 2;
         return x;
     }();
     return t;
