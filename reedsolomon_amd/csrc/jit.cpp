@@ -48,6 +48,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
+#include <cstdlib>
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
@@ -77,7 +78,10 @@ int g_jit_sync = 0;
 // most n waves per SIMD (0: as many as their registers allow).  Default 2:
 // fewer 2 KiB chunks in flight per CU; 4-15 % faster on every shape measured,
 // in-place Reconst most (10+8 of 5: 5.34 -> 6.13 TB/s, profiles/r03/ab_jit_waves.log)
-int g_jit_waves = 2;  // rs_tune("jit_sync", n): multi-wave assembly kernels meet at a barrier every n columns (0: never)
+int g_jit_waves = [] {
+    const char* e = std::getenv("RSAMD_JIT_WAVES");
+    return e ? std::atoi(e) : 2;
+}();  // rs_tune("jit_sync", n): multi-wave assembly kernels meet at a barrier every n columns (0: never)
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 int g_jit_backend = [] {  // rs_tune("jit_backend", 1 | 0): assembly (jit_asm.cpp) | hiprtc C++; env RSAMD_JIT_BACKEND
     const char* e = std::getenv("RSAMD_JIT_BACKEND");

@@ -30,7 +30,6 @@ SWEEP = {
     "block8": [256, 128],
     "bitslice": [0, 1],
     "bs_block": [64, 128, 256, 0],
-    "bs_waves": [0, 4, 2],
     "wide_block": [128, 256],
     "wide_single_pass": [0, 1],
     "host_engine": [0, 1],
