@@ -452,8 +452,6 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * the compiled kernels, 1..6 (1..4 for assembly kernels), default 3),
  * "jit_sync" (assembly kernels of more than 16 rows: the waves of a
  * workgroup meet at a barrier every n columns, 0 = never; default 0),
- * "jit_waves" (assembly kernels hold at most n waves per SIMD, 2..8, by
- * declaring more registers; 0 = as many as fit; default 2),
  * "jit_backend" (1 default: kernels emitted as gfx950 assembly and assembled
  * by comgr, tens of ms per matrix, up to 128 output rows x 256 columns | 0:
  * C++ compiled by hiprtc, seconds per matrix, up to 16 x 64), "jit_disk_cache" (1 default: compiled

@@ -62,7 +62,6 @@ SWEEP = {
     "jit_min_rows": [1, 5],
     "jit_pf": [1, 2, 4, 6, 3],
     "jit_sync": [1, 4, 0],
-    "jit_waves": [0, 4, 2],
     "jit_disk_cache": [0, 1],
     "jit_backend": [0, 1],
     "table_registry_max": [1, 1 << 14],
