@@ -32,8 +32,20 @@ def _has_gpu() -> bool:
 def _gpu_required(request):
     # A gpu-marked test must run on a GPU: it fails (never skips) without one,
     # so a green `-m gpu` run always means the HIP path executed.
-    if request.node.get_closest_marker("gpu") and not _has_gpu():
+    gpu = request.node.get_closest_marker("gpu") is not None
+    if gpu and not _has_gpu():
         pytest.fail("gpu test needs a visible HIP device")
+    yield
+    if gpu and "torch" in sys.modules:
+        # the test's handles freed (resident engines stopped) and the device
+        # drained: an asynchronous GPU fault is reported against the test
+        # that caused it, not a later one
+        import gc
+
+        torch = sys.modules["torch"]
+        gc.collect()
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
 
 
 @pytest.fixture(scope="session")
@@ -51,3 +63,23 @@ def rslib():
 
     build.build()
     return reedsolomon_amd
+
+
+_ARENAS = []
+
+
+def host_arena(nbytes: int):
+    """A page-aligned uint8 numpy array over its own anonymous mapping, kept
+    for the whole session, for tests that rs_host_register memory.  The HIP
+    runtime's pageable-copy path faulted (hipErrorIllegalAddress at a later
+    torch `.cuda()` of a new numpy array) when registered-then-unregistered
+    ranges shared pages with, or were freed and reused by, ordinary heap
+    arrays; a mapping of its own that is never unmapped rules both out."""
+    import mmap
+
+    import numpy as np
+
+    size = max(4096, (nbytes + 4095) // 4096 * 4096)
+    m = mmap.mmap(-1, size)
+    _ARENAS.append(m)
+    return np.frombuffer(m, dtype=np.uint8, count=nbytes)

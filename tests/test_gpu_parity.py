@@ -646,10 +646,10 @@ def test_host_calls_on_registered_memory(rslib, orc, torch_dev):
     r = rslib.New(d, p)
     rng = np.random.default_rng(404)
     for size in (4096, 65536, 1 << 20, 1000):
+        from conftest import host_arena
+
         pitch = (size + 4095) // 4096 * 4096
-        arena = np.zeros((d + p + 1) * pitch + 4096, np.uint8)
-        off = (-arena.ctypes.data) % 4096
-        base = arena[off: off + (d + p + 1) * pitch]
+        base = host_arena((d + p + 1) * pitch)
         rslib.host_register(base.ctypes.data, base.nbytes)
         try:
             v = [base[i * pitch: i * pitch + size] for i in range(d + p)]
@@ -728,8 +728,12 @@ def test_host_batch_zero_copy(rslib, orc, torch_dev):
     rng = np.random.default_rng(122)
     host = _rand(rng, S, d + p, n)
     exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
-    # registered pageable numpy buffer -> device-mapped
-    reg = host.copy()
+    # registered pageable numpy buffer -> device-mapped (a mapping of its own,
+    # kept for the session: conftest.host_arena)
+    from conftest import host_arena
+
+    reg = host_arena(host.nbytes).reshape(host.shape)
+    reg[:] = host
     rslib.host_register(reg.ctypes.data, reg.nbytes)
     try:
         dp = rslib.host_device_pointer(reg.ctypes.data, reg.nbytes)
