@@ -395,7 +395,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * per workgroup of the 8-byte-lane kernels: 128 default | 256), "bitslice"
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
- * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "wide_block" (128 | 256),
+ * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "bs_waves"
+ * (bit-sliced kernels hold at most n waves per SIMD, 1..7, through LDS
+ * padding; 0 = as many as fit; default 2), "wide_block" (128 | 256),
  * "wide_single_pass" (1 default: products with more than 8 output rows and
  * no compiled network read every input once, all rows of a chunk in one
  * workgroup | 0: the looped kernel in row groups of 8, for A/B),
@@ -452,6 +454,8 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * the compiled kernels, 1..6 (1..4 for assembly kernels), default 3),
  * "jit_sync" (assembly kernels of more than 16 rows: the waves of a
  * workgroup meet at a barrier every n columns, 0 = never; default 0),
+ * "jit_waves" (assembly kernels hold at most n waves per SIMD, 2..8, by
+ * declaring more registers; 0 = as many as fit; default 2),
  * "jit_backend" (1 default: kernels emitted as gfx950 assembly and assembled
  * by comgr, tens of ms per matrix, up to 128 output rows x 256 columns | 0:
  * C++ compiled by hiprtc, seconds per matrix, up to 16 x 64), "jit_disk_cache" (1 default: compiled

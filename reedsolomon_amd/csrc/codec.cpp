@@ -537,12 +537,14 @@ int rs_tune(const char* name, int value) {
         else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
         else if (n == "block8") t.block8 = value == 128 ? 128 : 256;
         else if (n == "bitslice") t.bitslice = value ? 1 : 0;
+        else if (n == "bs_waves") t.bs_waves = value < 0 ? 0 : value > 8 ? 8 : value;
         else if (n == "jit") g_jit_mode = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (n == "jit_min_rows") g_jit_min_rows = value < 1 ? 1 : value;
         else if (n == "jit_min_acc_cols") g_jit_min_acc_cols = value < 1 ? 1 : value;
         else if (n == "jit_min_launches") g_jit_min_launches = value < 1 ? 1 : value;
         else if (n == "jit_pf") g_jit_pf = value < 1 ? 1 : value > 6 ? 6 : value;
         else if (n == "jit_sync") g_jit_sync = value < 0 ? 0 : value > 64 ? 64 : value;
+        else if (n == "jit_waves") g_jit_waves = value < 0 ? 0 : value > 8 ? 8 : value;
         else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;
         else if (n == "jit_backend") g_jit_backend = value ? 1 : 0;
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);

@@ -73,8 +73,16 @@ uint64_t g_jit_min_bytes = uint64_t{8} << 20;
 int g_jit_min_launches = 2;
 int g_jit_min_rows = kJitMinRows;
 int g_jit_min_acc_cols = kJitMinAccCols;
-int g_jit_sync = 0;
-  // rs_tune("jit_sync", n): multi-wave assembly kernels meet at a barrier every n columns (0: never)
+int g_jit_sync = 0;  // rs_tune("jit_sync", n): multi-wave assembly kernels meet at a barrier every n columns (0: never)
+// rs_tune("jit_waves", n): assembly kernels declare enough VGPRs to hold at
+// most n waves per SIMD (0: as many as their registers allow).  Default 2:
+// fewer 2 KiB chunks in flight per CU; 4-15 % faster on every shape measured,
+// in-place Reconst most (10+8 of 5: 5.34 -> 6.13 TB/s, profiles/r03/ab_jit_waves.log)
+// (env RSAMD_JIT_WAVES)
+int g_jit_waves = [] {
+    const char* e = std::getenv("RSAMD_JIT_WAVES");
+    return e ? std::atoi(e) : 2;
+}();
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 int g_jit_backend = [] {  // rs_tune("jit_backend", 1 | 0): assembly (jit_asm.cpp) | hiprtc C++; env RSAMD_JIT_BACKEND
     const char* e = std::getenv("RSAMD_JIT_BACKEND");
@@ -610,7 +618,7 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
     if (!mat || rows < 1 || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
     Compiled c = g_jit_backend
-                     ? compile_asm(asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync, nullptr))
+                     ? compile_asm(asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync, g_jit_waves, nullptr))
                      : compile(jit_source(mat, rows, cols, accumulate));
     if (ms) *ms = c.ms;
     if (!c.ok) std::fprintf(stderr, "librsamd: jit compile check failed: %s\n", c.log.substr(0, 4000).c_str());
@@ -665,6 +673,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(a.cols);
     k.text += static_cast<char>(g_jit_pf);
     k.text += static_cast<char>(g_jit_backend ? g_jit_sync : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_waves : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -694,6 +703,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(a.cols >> 8);
     key += static_cast<char>(g_jit_pf);
     key += static_cast<char>(backend ? g_jit_sync : 0);
+    key += static_cast<char>(backend ? g_jit_waves : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);
@@ -740,7 +750,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
             e = std::make_shared<Entry>();
             e->is_asm = backend != 0;
             e->nw = asm_waves(a.rows);
-            e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->nw, g_jit_pf, g_jit_sync, nullptr)
+            e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->nw, g_jit_pf, g_jit_sync, g_jit_waves, nullptr)
                                : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             if (g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
             j.entries.emplace(key, e);
@@ -808,7 +818,7 @@ JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
 
 int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out) {
     if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
-    *out = asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync, nullptr);
+    *out = asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync, g_jit_waves, nullptr);
     return RS_OK;
 }
 

@@ -34,6 +34,7 @@ extern int g_jit_mode;
 extern uint64_t g_jit_min_bytes;
 extern int g_jit_pf;
 extern int g_jit_sync;
+extern int g_jit_waves;
 // rs_tune("jit_min_launches"): background mode compiles a matrix once it has
 // been launched this many times, moving jit_min_bytes in total (default 2)
 extern int g_jit_min_launches;

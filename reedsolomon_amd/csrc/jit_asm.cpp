@@ -117,7 +117,8 @@ void transpose8(Asm& A, const int (&r)[8]) {
 
 }  // namespace
 
-std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int* vgprs_out) {
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int max_waves,
+                       int* vgprs_out) {
     const int rw = (rows + nw - 1) / nw;  // rows per wave
     Layout L;
     L.pf = pf < 1 ? 1 : pf > 4 ? 4 : pf;
@@ -359,7 +360,9 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
     A.line("s_endpgm");
     A.out += ".Lfunc_end0:\n\t.size\trs_bs_asm, .Lfunc_end0-rs_bs_asm\n";
     // ---- kernel descriptor and metadata (code object v6)
-    const int accum = (L.vgprs + 3) / 4 * 4;
+    int accum = (L.vgprs + 3) / 4 * 4;
+    // occupancy cap: 512 VGPRs per SIMD lane, allocated in granules of 8
+    if (max_waves > 1 && max_waves <= 8) accum = std::max(accum, std::min(256, 512 / max_waves / 8 * 8));
     char kd[2048];
     std::snprintf(kd, sizeof kd,
                   "\t.rodata\n\t.p2align\t6\n\t.amdhsa_kernel rs_bs_asm\n"

@@ -35,9 +35,10 @@ inline int asm_waves(int rows) { return rows <= 16 ? 1 : (rows + 15) / 16; }
 // accumulate (XOR into the outputs) or overwrite, nw waves per workgroup,
 // pf columns of loads in flight.  *vgprs receives the VGPRs per lane.
 // sync > 0: the waves of a multi-wave workgroup meet at s_barrier every
-// `sync` columns.
+// `sync` columns; max_waves > 1: the kernel declares enough VGPRs that at
+// most that many waves share a SIMD (0: as many as its registers allow).
 std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int sync,
-                       int* vgprs);
+                       int max_waves, int* vgprs);
 // Assemble + link (comgr) into a code object; false with the log on failure.
 bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* log, double* ms);
 

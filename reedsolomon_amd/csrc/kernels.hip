@@ -69,6 +69,11 @@ LaunchTuning& tuning() {
         x.bs_block = 0;
         x.wide_block = 256;
         x.wide_single_pass = 1;
+        // 2 waves per SIMD: fewer 32 * bs-byte chunks in flight per CU; +3-8 %
+        // on every generated shape, split and interleaved (10+8 Encode 6.04 ->
+        // 6.28 TB/s, 8+5 interleaved 6.06 -> 6.53; profiles/r03/ab_bs_waves.log)
+        const char* bw = std::getenv("RSAMD_BS_WAVES");
+        x.bs_waves = bw ? std::atoi(bw) : 2;
         return x;
     }();
     return t;
@@ -1470,8 +1475,16 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         for (int sh = 0; sh < 31; ++sh)
             if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
         if (a.total_chunks <= 0x7fffffff && a.body < (uint64_t{1} << 31)) {
+            // occupancy cap (rs_tune("bs_waves", n)): dynamic LDS the kernel
+            // does not use, so at most n waves per SIMD share a CU's 160 KiB
+            size_t lds = 0;
+            const int bw = tuning().bs_waves;
+            if (bw > 0 && bw < 8) {
+                const int wgs = std::max(1, bw * 4 / (bs / 64));
+                lds = std::min<size_t>(65536, 163840 / wgs);
+            }
             (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
-            hipLaunchKernelGGL(bk, dim3(static_cast<unsigned>(a.total_chunks)), dim3(bs), 0, stream, a);
+            hipLaunchKernelGGL(bk, dim3(static_cast<unsigned>(a.total_chunks)), dim3(bs), lds, stream, a);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         } else {  // too large for one grid / 31-bit buffer offsets: the perm-table kernels

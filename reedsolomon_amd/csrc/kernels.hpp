@@ -132,6 +132,7 @@ struct LaunchTuning {
     int bs_block;     // bit-sliced Encode: lanes per workgroup (64 | 128 | 256; 0 = per-layout rule)
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
     int wide_single_pass;  // > 8 rows without a compiled network: single-pass wide kernels (1) | row groups of 8 (0)
+    int bs_waves;     // bit-sliced Encode: at most this many waves per SIMD (LDS padding; 0 = as many as fit; default 2)
 };
 LaunchTuning& tuning();
 

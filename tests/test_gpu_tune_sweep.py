@@ -30,6 +30,7 @@ SWEEP = {
     "block8": [256, 128],
     "bitslice": [0, 1],
     "bs_block": [64, 128, 256, 0],
+    "bs_waves": [0, 4, 2],
     "wide_block": [128, 256],
     "wide_single_pass": [0, 1],
     "host_engine": [0, 1],
@@ -62,6 +63,7 @@ SWEEP = {
     "jit_min_rows": [1, 5],
     "jit_pf": [1, 2, 4, 6, 3],
     "jit_sync": [1, 4, 0],
+    "jit_waves": [0, 4, 2],
     "jit_disk_cache": [0, 1],
     "jit_backend": [0, 1],
     "table_registry_max": [1, 1 << 14],

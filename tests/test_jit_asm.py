@@ -76,3 +76,22 @@ def _check_kernel(rslib, orc, rows, cols, acc):
     assert np.array_equal(got[:, cols:, body:], host[:, cols:, body:])  # past the body untouched
     return src
 
+
+@pytest.mark.parametrize("waves,vgprs", [(2, 256), (4, 128), (0, None)])
+def test_asm_kernel_occupancy_cap(rslib, waves, vgprs):
+    """rs_tune("jit_waves", n): the kernel declares 512 / n VGPRs (granule 8,
+    at most 256) so at most n waves share a SIMD; 0 declares what it uses."""
+    import re
+
+    L = rslib.lib()
+    mat = np.random.default_rng(3).integers(0, 256, (5, 10), dtype=np.uint8)
+    assert L.rs_tune(b"jit_waves", waves) == 0
+    try:
+        src = rslib.jit_asm_source(mat, False)
+    finally:
+        L.rs_tune(b"jit_waves", 2)
+    declared = int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", src).group(1))
+    if vgprs is None:
+        assert declared < 128  # 5 rows x 8 planes + slots + subsets
+    else:
+        assert declared == vgprs
