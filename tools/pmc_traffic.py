@@ -4,6 +4,7 @@
 
     python tools/pmc_traffic.py run enc:64+64                  # the workload (5 launches)
     python tools/pmc_traffic.py run rec:16+16:16 --jit 0        # Reconst of 16 lost
+    python tools/pmc_traffic.py run inrec:10+8:8                # the same in place (interleaved layout)
     python tools/pmc_traffic.py summarize <tag> <dir_FETCH> <dir_WRITE> <calib_FETCH> <calib_WRITE>
 
 `run` encodes (or rebuilds) ~3.5 GiB of 1 MiB-vector stripes on the split
@@ -42,6 +43,11 @@ def run(spec, jit):
     r.encode_batch_split(data, par)
     if op == "enc":
         fn, nbytes = (lambda: r.encode_batch_split(data, par)), S * (k + m) * vec
+    elif op == "inrec":  # Reconst in place on the interleaved [S][k+m][vec] buffer
+        buf = torch.cat([data, par], dim=1).contiguous()
+        del data, par
+        lost = list(range(int(rest[0])))
+        fn, nbytes = (lambda: r.reconst_batch(buf, [], lost)), S * (k + len(lost)) * vec
     else:
         lost = list(range(int(rest[0])))
         fn, nbytes = (lambda: r.reconst_batch_split(data, par, [], lost)), S * (k + len(lost)) * vec
