@@ -397,7 +397,8 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
  * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "bs_waves"
  * (bit-sliced kernels hold at most n waves per SIMD, 1..7, through LDS
- * padding; 0 = as many as fit; default 2), "wide_block" (128 | 256),
+ * padding of at most 64 KiB per workgroup, so 256-lane workgroups keep at
+ * least 2; 0 = as many as fit; default 2), "wide_block" (128 | 256),
  * "wide_single_pass" (1 default: products with more than 8 output rows and
  * no compiled network read every input once, all rows of a chunk in one
  * workgroup | 0: the looped kernel in row groups of 8, for A/B),
