@@ -250,8 +250,33 @@ RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stri
  * Registered (or hipHostMalloc'd) memory is device-addressable: the host
  * batch entry points then run their kernels straight over it (zero-copy,
  * no staging): 72 GiB/s for 10+4 encode on one MI355X vs 20-57 GiB/s for
- * pageable memory (staged through a pinned mirror by host threads). */
+ * pageable memory (staged through a pinned mirror by host threads).
+ * Any address and length: the range is rounded out to whole pages, and pages
+ * already registered by an earlier call (a neighbouring buffer sharing a
+ * page) are shared by reference rather than registered twice.
+ * rs_host_unregister(ptr) takes the address given to rs_host_register
+ * (RS_ERR_INVAL for any other); a page leaves the runtime when the last
+ * registration holding it goes, after every device this process launched on
+ * has been drained.  The caller may then free the memory and reuse the range
+ * like any other (the reference retains nothing after a call: rs.go:101-111).
+ * No rs_host_register equivalent exists in the reference; it replaces the
+ * pinning a cgo caller would otherwise do per call. */
 RS_API int rs_host_register(void* ptr, size_t bytes);
+/* Library-owned page-locked buffers (mmap + hipHostRegister), for callers
+ * that allocate and release stripe buffers continually (a Go server's
+ * per-request buffers): rs_host_alloc hands out a block of at least `bytes`
+ * (page-aligned; size classes of powers of two from 64 KiB), device-mapped
+ * like registered memory; rs_host_free returns it to the library, which keeps
+ * it registered and mapped for reuse and never gives the pages back while the
+ * process runs (no register / unregister / unmap churn, so no freed range is
+ * ever reused by the runtime's own pageable copies).  A reused block holds its
+ * previous bytes.  rs_host_free(NULL) is a no-op; any other pointer that is
+ * not a live block gives RS_ERR_INVAL.  Thread-safe. */
+RS_API int rs_host_alloc(size_t bytes, void** out);
+RS_API int rs_host_free(void* ptr);
+/* Pool bytes mapped / handed out, pool blocks, and registered page spans
+ * (pool blocks and caller registrations); any pointer may be NULL. */
+RS_API int rs_host_pool_stats(size_t* mapped, size_t* in_use, size_t* blocks, size_t* spans);
 /* Bind the calling thread to the CPUs local to `device` (its PCI function's
  * NUMA node, from sysfs), within the process's affinity, so page-locked
  * buffers and staging copies stay near the GPU.  Device-group workers do
@@ -358,7 +383,10 @@ RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches
  * "jit_disk_cache"), process-wide: first sights of a matrix whose code object
  * was on disk (loaded, no compile), first sights that found none, code
  * objects written, files rejected on load (corrupt or stale: recompiled).
- * Any pointer may be NULL. */
+ * The directory must be the user's own and not group / world-writable (the
+ * library creates it 0700 and its files 0600), since the cache holds GPU code
+ * the process runs; otherwise it is neither read nor written.  Any pointer
+ * may be NULL. */
 RS_API int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects);
 
 /* Compile the run-time kernel for a rows x cols matrix (row-major, 5 <= rows

@@ -87,6 +87,9 @@ SIGNATURES = {
     "rs_host_device_pointer": (c_int, [c_void, c_sz, ctypes.POINTER(c_void)]),
     "rs_host_register": (c_int, [c_void, c_sz]),
     "rs_host_unregister": (c_int, [c_void]),
+    "rs_host_alloc": (c_int, [c_sz, ctypes.POINTER(c_void)]),
+    "rs_host_free": (c_int, [c_void]),
+    "rs_host_pool_stats": (c_int, [ctypes.POINTER(c_sz)] * 4),
     "rs_bind_thread_to_device": (c_int, [c_int]),
     "rs_last_device_error": (ctypes.c_char_p, []),
     "rs_xor_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_void, c_i64, c_int, c_sz, c_void]),

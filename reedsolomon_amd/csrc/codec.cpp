@@ -101,9 +101,12 @@ int ensure_device(rs_t* rs) {
         rs->device = cur;
     }
     if (rs->device >= count) return dev_fail(hipErrorInvalidDevice, "device ordinal");
+    if (rs->device < 64) g_devices_used.fetch_or(uint64_t{1} << rs->device, std::memory_order_acq_rel);
     rs->device_ready = true;
     return RS_OK;
 }
+
+std::atomic<uint64_t> g_devices_used{0};
 
 size_t g_registry_max = size_t{1} << 14;
 
@@ -139,6 +142,7 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
         // Bounded registry: drain the device before recycling table memory
         // (the resident host-call engine first: a device sync waits for it)
         std::lock_guard<std::mutex> elk(rs->eng_mu);
+        RS_TRY(engine_drain(rs));  // calls in flight complete first (a stopped instance would strand them)
         engine_stop(rs);
         RS_TRY(hip_ok(hipDeviceSynchronize(), "table registry drain"));
         for (auto& kv : rs->tables) (void)hipFree(kv.second);

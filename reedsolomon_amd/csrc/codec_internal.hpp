@@ -181,7 +181,8 @@ struct rs_codec {
     rsamd::EngineSlot* eng_vslots = nullptr;
     hipStream_t eng_stream = nullptr;
     bool eng_running = false;
-    int eng_waves = 0;       // the running instance's workgroups
+    int eng_waves = 0;       // the latest instance's workgroups (kept once it stops: calls still
+                             // pending resume on this shape, engine_drain)
     int eng_group_waves = 0; // ... and waves per workgroup
     int eng_idle_us = 0;     // the running instance's idle window
     int eng_life_us = 0;     // ... and its maximum life
@@ -218,6 +219,10 @@ int engine_call_addr(rs_t* rs, const uint8_t* mat, int rows, int cols, const uin
 // Would the engine take a call of this shape moving `bytes` in all?
 bool engine_accepts(int rows, int cols, size_t bytes);
 void engine_stop(rs_t* rs);  // caller holds eng_mu
+// Every call rung so far complete (relaunching the latest shape if needed);
+// caller holds eng_mu.  Precedes an engine_stop that no same-shape relaunch
+// follows.
+int engine_drain(rs_t* rs);
 void engine_shutdown(rs_t* rs);
 extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_life_us, g_engine_wg_units,
     g_engine_yield_us, g_engine_poll_gap, g_engine_vram, g_engine_split_rows;
@@ -502,6 +507,9 @@ int host_device_range(const void* p, size_t bytes, uint8_t** dev);
 // rs_host_register, or nullptr.
 uint8_t* registered_device_ptr(const void* p, size_t bytes);
 extern std::atomic<int> g_reg_count;
+// Devices some handle of this process has launched on (bit per ordinal < 64):
+// rs_host_unregister drains them before a range leaves the runtime.
+extern std::atomic<uint64_t> g_devices_used;
 size_t batch_extent(int64_t ss, int64_t vs, int nstripes, int nvec, size_t len);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -295,19 +295,37 @@ static hipStream_t engine_stream() {
     return nullptr;
 }
 
-// Caller holds eng_mu; no instance is running.
+// Oldest call some workgroup of the latest instance's shape has not completed
+// yet, minus one (= eng_seq when every rung call is complete).
+static uint64_t engine_low_done(const rs_t* rs) {
+    uint64_t lo = rs->eng_seq;
+    for (int w = 0; w < rs->eng_waves; ++w)
+        lo = std::min<uint64_t>(lo, __atomic_load_n(&rs->eng_ring->done[w], __ATOMIC_ACQUIRE));
+    return lo;
+}
+
+// Caller holds eng_mu; no instance is running.  `start` <= every done word of
+// the workgroups [0, rs->eng_waves) of the previous shape (a relaunch passes
+// their minimum; a new shape is launched only after engine_drain, when all of
+// them equal eng_seq).
 static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     const uint64_t idle_ticks = static_cast<uint64_t>(g_engine_idle_us) * 100;  // 100 MHz realtime counter
     const uint64_t life_ticks = static_cast<uint64_t>(g_engine_life_us) * 100;
     const uint64_t epoch = rs->eng_epoch + 1;
     Region region("engine launch");
-    // Every workgroup of the new instance starts after call `start`.  A
-    // workgroup the previous instance did not have (host_engine_waves raised)
-    // holds a stale done word: bring it to `start` here, so the slot-reuse
-    // wait and a later relaunch (min over done words) never wait on a call
-    // that workgroup will never see.  No instance runs: the host is the only
-    // writer.
-    for (int w = 0; w < waves; ++w)
+    // Every workgroup of the new instance starts after max(call `start`, its
+    // own done word).  A workgroup the previous shape did not have
+    // (host_engine_waves raised) may hold a stale done word from an older
+    // instance: every call rung since was served by the previous shape's
+    // workgroups alone (calls name workgroups of their own instance's grid),
+    // so bring it to `start` here, so the slot-reuse wait and a later relaunch
+    // (min over done words) never wait on a call that workgroup will never
+    // see.  Workgroups of the previous shape keep their done words: one that
+    // left before a call reached it resumes at that call (raising its word
+    // would report the call complete with its units never written).  No
+    // instance runs: the host is the only writer.
+    const int prev = rs->eng_ring ? rs->eng_waves : 0;
+    for (int w = prev; w < waves; ++w)
         if (__atomic_load_n(&rs->eng_ring->done[w], __ATOMIC_ACQUIRE) < start)
             __atomic_store_n(&rs->eng_ring->done[w], start, __ATOMIC_RELEASE);
     RS_TRY(hip_ok(launch_engine(rs->eng_dring, rs->eng_vslots, waves, group_waves, start, epoch, idle_ticks,
@@ -418,6 +436,19 @@ static int engine_wait(rs_t* rs, uint64_t seq, int waves, int w0, int n, bool lo
     return RS_OK;
 }
 
+// Caller holds eng_mu.  Every call rung so far completed by every workgroup,
+// on the shape it was rung for (calls name workgroups of their instance's
+// grid, so another shape cannot serve them): the instance is relaunched with
+// the same shape if it is gone or stopped while calls are pending.  Needed
+// before any engine_stop that is not followed by a relaunch of the same shape
+// (a new shape, the table registry's recycle): without it a workgroup that
+// left before a pending call reached it would never serve that call.
+int engine_drain(rs_t* rs) {
+    if (!rs->eng_ring || rs->eng_waves <= 0 || engine_low_done(rs) >= rs->eng_seq) return RS_OK;
+    if (!rs->eng_running) RS_TRY(engine_launch(rs, rs->eng_waves, rs->eng_group_waves, engine_low_done(rs)));
+    return engine_wait(rs, rs->eng_seq, rs->eng_waves, 0, rs->eng_waves, true);
+}
+
 static int engine_run(rs_t* rs, const EngineWork& wk) {
     const int rows = wk.rows, cols = wk.cols;
     const auto t_call = std::chrono::steady_clock::now();
@@ -464,12 +495,19 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     const int gwaves = g_engine_group_waves < 1                      ? 1
                        : g_engine_group_waves > kEngineMaxGroupWaves ? kEngineMaxGroupWaves
                                                                      : g_engine_group_waves;
-    if (rs->eng_running &&
+    if (rs->eng_waves > 0 &&
         (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us ||
-         rs->eng_life_us != g_engine_life_us || rs->eng_poll_gap != g_engine_poll_gap))
-        engine_stop(rs);  // new shape: the old instance must be gone before the next one reads done words
+         rs->eng_life_us != g_engine_life_us || rs->eng_poll_gap != g_engine_poll_gap)) {
+        // new shape: the calls in flight finish on the old one, and the old
+        // instance is gone before the next one reads done words
+        RS_TRY(engine_drain(rs));
+        engine_stop(rs);
+    }
     RS_TRY(engine_relaunch_if_gone(rs));
-    if (!rs->eng_running) RS_TRY(engine_launch(rs, waves, gwaves, rs->eng_seq));
+    if (!rs->eng_running) {
+        RS_TRY(engine_drain(rs));  // (a stopped instance with calls pending relaunches on its own shape)
+        if (!rs->eng_running) RS_TRY(engine_launch(rs, waves, gwaves, rs->eng_seq));
+    }
     const int inst_waves = rs->eng_waves;
 
     const uint64_t seq = rs->eng_seq + 1;

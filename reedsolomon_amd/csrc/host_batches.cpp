@@ -3,6 +3,8 @@
 // pageable memory, and device groups (one process, several GPUs).
 #include <pthread.h>
 #include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cctype>
@@ -43,28 +45,118 @@ int host_device_range(const void* p, size_t bytes, uint8_t** dev) {
     return RS_OK;
 }
 
-// Ranges registered through rs_host_register: host base -> (bytes, device
-// address).  Host calls look their vectors up here (registered_device_ptr)
-// and, when every vector is registered, run the kernel straight over the
-// caller's memory.
+// Host memory registered with the HIP runtime, as disjoint page spans.
+// rs_host_register rounds the caller's range out to whole pages and takes a
+// reference on every span that covers part of it, registering only the pages
+// no span covers yet, so two caller ranges that share a page (heap buffers
+// side by side) never register that page twice and neither unregister pulls
+// it from under the other.  A span leaves the runtime when its last reference
+// goes, after every device this process launched on has been drained (a
+// kernel the caller queued over the range may still be reading it).  The
+// library-owned pool (rs_host_alloc) holds a permanent reference on its
+// blocks: they are registered once and stay registered and mapped while the
+// process runs, however often they are handed out again.  Host calls look
+// their vectors up here (registered_device_ptr) and, when every vector lies
+// inside one span, run the kernel straight over the caller's memory.
 namespace {
-struct RegRange {
+struct Span {
+    uintptr_t hi;   // [key, hi): whole pages
+    uint8_t* dev;   // device address of the span's first byte
+    int refs;
+};
+struct PoolBlock {
     size_t bytes;
-    uint8_t* dev;
+    bool free;
 };
 std::mutex g_reg_mu;
-std::map<uintptr_t, RegRange> g_reg;
+std::map<uintptr_t, Span> g_spans;                      // disjoint page spans, by first address
+struct UserReg {
+    size_t bytes;
+    std::vector<uintptr_t> spans;  // the spans it holds a reference on
+};
+std::map<uintptr_t, UserReg> g_user;                    // rs_host_register'ed ranges, by address
+std::map<uintptr_t, PoolBlock> g_pool;                  // every pool block ever mapped
+std::multimap<size_t, uintptr_t> g_pool_free;           // size class -> free pool block
+size_t g_pool_mapped = 0, g_pool_in_use = 0;
+
+uintptr_t page_bytes() {
+    static const uintptr_t ps = [] {
+        const long v = sysconf(_SC_PAGESIZE);
+        return v > 0 ? static_cast<uintptr_t>(v) : uintptr_t{4096};
+    }();
+    return ps;
+}
+
+// Caller holds g_reg_mu.  Registers [lo, hi) with the runtime as a new span
+// holding one reference.
+int span_register(uintptr_t lo, uintptr_t hi) {
+    void* p = reinterpret_cast<void*>(lo);
+    {
+        Region region("hipHostRegister");
+        RS_TRY(hip_ok(hipHostRegister(p, hi - lo, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister"));
+    }
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+        (void)hipGetLastError();
+        (void)hipHostUnregister(p);
+        return dev_fail(hipErrorInvalidValue, "hipHostGetDevicePointer (registered span)");
+    }
+    g_spans.emplace(lo, Span{hi, static_cast<uint8_t*>(dev), 1});
+    return RS_OK;
+}
+
+// Every device this process launched on has finished its queued work.
+void drain_used_devices() {
+    const uint64_t used = g_devices_used.load(std::memory_order_acquire);
+    for (int dv = 0; dv < 64; ++dv)
+        if (used & (uint64_t{1} << dv)) {
+            DeviceGuard g(dv);
+            (void)hipDeviceSynchronize();
+        }
+}
+
+// Drops one reference on each span in `spans` (caller holds g_reg_mu);
+// spans whose last reference went are removed from the lookup and returned.
+std::vector<uintptr_t> spans_release(const std::vector<uintptr_t>& spans) {
+    std::vector<uintptr_t> dead;
+    for (uintptr_t lo : spans) {
+        auto it = g_spans.find(lo);
+        if (it != g_spans.end() && --it->second.refs == 0) {
+            dead.push_back(lo);
+            g_spans.erase(it);
+        }
+    }
+    g_reg_count.store(static_cast<int>(g_spans.size()));
+    return dead;
+}
 }  // namespace
 std::atomic<int> g_reg_count{0};
 
+// [p, p + bytes) inside one span AND inside a live registration or a pool
+// block: pages a span keeps for another registration (a shared page's whole
+// span) do not make a range the caller unregistered zero-copy again.  The
+// registration is searched among the 8 nearest starting at or below p (a
+// range under a registration that starts further back takes the staged path:
+// same bytes).
 uint8_t* registered_device_ptr(const void* p, size_t bytes) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_reg.upper_bound(a);
-    if (it == g_reg.begin()) return nullptr;
+    auto it = g_spans.upper_bound(a);
+    if (it == g_spans.begin()) return nullptr;
     --it;
-    if (a + bytes > it->first + it->second.bytes) return nullptr;
-    return it->second.dev + (a - it->first);
+    if (a + bytes > it->second.hi) return nullptr;
+    bool live = false;
+    auto pb = g_pool.upper_bound(a);
+    if (pb != g_pool.begin()) {
+        --pb;
+        live = a + bytes <= pb->first + pb->second.bytes;
+    }
+    auto ur = g_user.upper_bound(a);
+    for (int k = 0; k < 8 && !live && ur != g_user.begin(); ++k) {
+        --ur;
+        live = a + bytes <= ur->first + ur->second.bytes;
+    }
+    return live ? it->second.dev + (a - it->first) : nullptr;
 }
 
 // Bind the calling thread to the CPUs local to `device` (its PCI function's
@@ -270,15 +362,37 @@ extern "C" {
 int rs_host_register(void* ptr, size_t bytes) {
     return abi_guard([&]() -> int {
         if (!ptr || !bytes) return RS_ERR_INVAL;
-        // mapped: kernels may address it directly (zero-copy host batches and calls)
-        Region region("hipHostRegister");
-        RS_TRY(hip_ok(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister"));
-        void* dev = nullptr;
-        if (hipHostGetDevicePointer(&dev, ptr, 0) == hipSuccess && dev) {
-            std::lock_guard<std::mutex> lk(g_reg_mu);
-            g_reg[reinterpret_cast<uintptr_t>(ptr)] = RegRange{bytes, static_cast<uint8_t*>(dev)};
-            g_reg_count.store(static_cast<int>(g_reg.size()));
+        const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), ps = page_bytes();
+        if (a + bytes < a) return RS_ERR_INVAL;
+        const uintptr_t lo = a & ~(ps - 1), hi = (a + bytes + ps - 1) & ~(ps - 1);
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        if (g_user.count(a)) return RS_ERR_INVAL;  // already registered at this address
+        std::vector<uintptr_t> held, created;
+        uintptr_t cur = lo;
+        int rc = RS_OK;
+        while (cur < hi && rc == RS_OK) {
+            auto it = g_spans.upper_bound(cur);  // the span covering cur, if any, precedes it
+            if (it != g_spans.begin() && std::prev(it)->second.hi > cur) {
+                Span& sp = std::prev(it)->second;
+                ++sp.refs;
+                held.push_back(std::prev(it)->first);
+                cur = sp.hi;
+                continue;
+            }
+            const uintptr_t end = it != g_spans.end() && it->first < hi ? it->first : hi;  // the gap up to the next span
+            rc = span_register(cur, end);
+            if (rc == RS_OK) {
+                held.push_back(cur);
+                created.push_back(cur);
+                cur = end;
+            }
         }
+        if (rc != RS_OK) {  // roll back: nothing used the new spans yet
+            for (uintptr_t d : spans_release(held)) (void)hipHostUnregister(reinterpret_cast<void*>(d));
+            return rc;
+        }
+        g_user.emplace(a, UserReg{bytes, std::move(held)});
+        g_reg_count.store(static_cast<int>(g_spans.size()));
         return RS_OK;
     });
 }
@@ -301,12 +415,82 @@ int rs_bind_thread_to_device(int device) {
 int rs_host_unregister(void* ptr) {
     return abi_guard([&]() -> int {
         if (!ptr) return RS_ERR_INVAL;
+        std::vector<uintptr_t> dead;
         {
             std::lock_guard<std::mutex> lk(g_reg_mu);
-            g_reg.erase(reinterpret_cast<uintptr_t>(ptr));
-            g_reg_count.store(static_cast<int>(g_reg.size()));
+            auto it = g_user.find(reinterpret_cast<uintptr_t>(ptr));
+            if (it == g_user.end()) return RS_ERR_INVAL;
+            dead = spans_release(it->second.spans);
+            g_user.erase(it);
         }
-        return hip_ok(hipHostUnregister(ptr), "hipHostUnregister");
+        if (dead.empty()) return RS_OK;  // every page still held by another registration or the pool
+        // No longer found by the lookup; whatever the caller queued over the
+        // range finishes before the pages leave the runtime.
+        drain_used_devices();
+        int rc = RS_OK;
+        for (uintptr_t lo : dead) {
+            const int r = hip_ok(hipHostUnregister(reinterpret_cast<void*>(lo)), "hipHostUnregister");
+            if (rc == RS_OK) rc = r;
+        }
+        return rc;
+    });
+}
+
+int rs_host_alloc(size_t bytes, void** out) {
+    return abi_guard([&]() -> int {
+        if (!out) return RS_ERR_INVAL;
+        *out = nullptr;
+        if (bytes == 0 || bytes > (size_t{1} << 40)) return RS_ERR_INVAL;
+        size_t cls = size_t{64} << 10;
+        while (cls < bytes) cls <<= 1;
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto f = g_pool_free.find(cls);
+        if (f != g_pool_free.end()) {
+            const uintptr_t b = f->second;
+            g_pool_free.erase(f);
+            g_pool[b].free = false;
+            g_pool_in_use += cls;
+            *out = reinterpret_cast<void*>(b);
+            return RS_OK;
+        }
+        void* m = mmap(nullptr, cls, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) return RS_ERR_NOMEM;
+        const uintptr_t b = reinterpret_cast<uintptr_t>(m);
+        const int rc = span_register(b, b + cls);  // the pool's own reference: never released
+        if (rc != RS_OK) {
+            munmap(m, cls);
+            return rc;
+        }
+        g_reg_count.store(static_cast<int>(g_spans.size()));
+        g_pool.emplace(b, PoolBlock{cls, false});
+        g_pool_mapped += cls;
+        g_pool_in_use += cls;
+        *out = m;
+        return RS_OK;
+    });
+}
+
+int rs_host_free(void* ptr) {
+    return abi_guard([&]() -> int {
+        if (!ptr) return RS_OK;
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_pool.find(reinterpret_cast<uintptr_t>(ptr));
+        if (it == g_pool.end() || it->second.free) return RS_ERR_INVAL;  // not a pool block, or freed twice
+        it->second.free = true;
+        g_pool_in_use -= it->second.bytes;
+        g_pool_free.emplace(it->second.bytes, it->first);
+        return RS_OK;
+    });
+}
+
+int rs_host_pool_stats(size_t* mapped, size_t* in_use, size_t* blocks, size_t* spans) {
+    return abi_guard([&]() -> int {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        if (mapped) *mapped = g_pool_mapped;
+        if (in_use) *in_use = g_pool_in_use;
+        if (blocks) *blocks = g_pool.size();
+        if (spans) *spans = g_spans.size();
+        return RS_OK;
     });
 }
 

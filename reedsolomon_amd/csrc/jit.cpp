@@ -35,7 +35,9 @@
 // server pays no compile for the matrices it has seen before.  Files are
 // written atomically (temporary file + rename) and checked on load (magic,
 // two independent key hashes, length, a checksum of the code, ELF magic);
-// anything else is ignored and recompiled.
+// anything else is ignored and recompiled.  The directory must be the
+// user's own and not group / world-writable, and so must each file (created
+// 0700 / 0600): otherwise the cache is neither read nor written.
 #include "jit.hpp"
 
 #include <hip/hiprtc.h>
@@ -344,16 +346,30 @@ std::string cache_dir() {
     return dir;
 }
 
+// The cache holds GPU code this process loads and runs, so it must be the
+// caller's alone: a directory or file owned by another user, or writable by
+// group / others, could carry code injected by another process (the FNV
+// checksum and key hashes catch corruption, not tampering).  Directories are
+// created 0700 and files 0600; anything else is not read and not written.
+bool private_to_us(const struct stat& st) {
+    return st.st_uid == geteuid() && (st.st_mode & (S_IWGRP | S_IWOTH)) == 0;
+}
+
+bool cache_dir_private(const std::string& d) {
+    struct stat st {};
+    return lstat(d.c_str(), &st) == 0 && S_ISDIR(st.st_mode) && private_to_us(st);
+}
+
 bool make_dirs(const std::string& d) {
     if (d.empty()) return false;
     std::string cur;
     for (size_t i = 0; i <= d.size(); ++i) {
         if (i == d.size() || d[i] == '/') {
-            if (!cur.empty() && mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+            if (!cur.empty() && mkdir(cur.c_str(), 0700) != 0 && errno != EEXIST) return false;
         }
         if (i < d.size()) cur += d[i];
     }
-    return true;
+    return cache_dir_private(d);
 }
 
 struct DiskKey {
@@ -376,10 +392,13 @@ struct FileHeader {
 std::vector<char> disk_load(const DiskKey& k) {
     std::vector<char> code;
     const std::string path = k.path();
-    const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (!cache_dir_private(cache_dir())) return code;
+    const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC | O_NOFOLLOW);
     if (fd < 0) return code;
+    struct stat st {};
     FileHeader h{};
-    bool ok = read(fd, &h, sizeof h) == static_cast<ssize_t>(sizeof h) &&
+    bool ok = fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && private_to_us(st) &&
+              read(fd, &h, sizeof h) == static_cast<ssize_t>(sizeof h) &&
               std::memcmp(h.magic, kDiskMagic, 8) == 0 && h.format == kDiskFormat && h.gen == kJitGenVersion &&
               h.h1 == k.h1 && h.h2 == k.h2 && h.key_len == k.text.size() && h.code_len > 4 &&
               h.code_len < (uint64_t{256} << 20);
@@ -405,7 +424,7 @@ void disk_store(const DiskKey& k, const std::vector<char>& code) {
     std::snprintf(tmp_suffix, sizeof tmp_suffix, ".tmp.%d.%llx", static_cast<int>(getpid()),
                   static_cast<unsigned long long>(mix64(reinterpret_cast<uintptr_t>(&code) ^ k.h1)));
     const std::string tmp = path + tmp_suffix;
-    const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+    const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC | O_NOFOLLOW, 0600);
     if (fd < 0) return;
     FileHeader h{};
     std::memcpy(h.magic, kDiskMagic, 8);

@@ -1066,8 +1066,8 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
         }
         // system-scope acquire, always: without it the first call on a fresh
         // coherent block read zeros (lines the runtime's clear left in L2).
-        // One wave's invalidate covers the workgroup: its waves share the
-        // CU's L1 and the XCD's L2, and they load only after the barrier below
+        // The polling wave's covers its own table loads; the other waves that
+        // load call data acquire after the barrier below
         if (works && poller) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t tab_id = static_cast<uint32_t>(w5 >> 32);
         if (works && tab_id != tab_have) {  // [col][kEngineMaxRows][5] dwords, every load in flight at once (one PCIe trip)
@@ -1085,6 +1085,15 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
             tab_have = tab_id;
         }
         __syncthreads();  // tables and addresses ready; s_raw read by every wave
+        // Every other wave that loads this call's data acquires too.  The
+        // polling wave's invalidate already covers its workgroup's caches on
+        // this build (no threadgroup-split mode: a workgroup's waves share the
+        // CU's L1 and the XCD's L2), but the memory model does not promise
+        // that, and a lone call (the latency case) loads on the first wave
+        // only, so only overlapping calls pay for it.
+        if (works && !poller &&
+            ((threadIdx.x >> 6) * nwg + local) * 64u < nstripes * units)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint64_t t_tab = __builtin_amdgcn_s_memrealtime();
         const EngineCall call{s_vaddr, stride, units, works ? nstripes * units : 0u, cols, accumulate, local, nwg};
         const bool split_rows = (w5 & 16) != 0 && rows <= static_cast<int>(blockDim.x >> 6);

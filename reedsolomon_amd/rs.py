@@ -627,5 +627,28 @@ def host_unregister(ptr: int) -> None:
     _check(lib().rs_host_unregister(ctypes.c_void_p(ptr)))
 
 
+def host_alloc(nbytes: int) -> np.ndarray:
+    """A uint8 array of `nbytes` over a library-owned page-locked block
+    (rs_host_alloc): host calls and host batches on it run zero-copy.  Give
+    it back with :func:`host_free` (the block stays registered for reuse)."""
+    p = ctypes.c_void_p()
+    _check(lib().rs_host_alloc(int(nbytes), ctypes.byref(p)))
+    buf = (ctypes.c_uint8 * int(nbytes)).from_address(int(p.value))
+    return np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
+
+
+def host_free(buf) -> None:
+    """Return a block from :func:`host_alloc` (the array, or its address)."""
+    ptr = buf if isinstance(buf, int) else buf.ctypes.data
+    _check(lib().rs_host_free(ctypes.c_void_p(int(ptr))))
+
+
+def host_pool_stats() -> dict:
+    """rs_host_pool_stats: pool bytes mapped / in use, pool blocks, registered page spans."""
+    v = [ctypes.c_size_t(0) for _ in range(4)]
+    _check(lib().rs_host_pool_stats(*[ctypes.byref(x) for x in v]))
+    return dict(zip(("mapped", "in_use", "blocks", "spans"), (int(x.value) for x in v)))
+
+
 def device_count() -> int:
     return int(lib().rs_device_count())

@@ -373,3 +373,22 @@ def test_jit_compile_check(rslib, orc):
     finally:
         L.rs_tune(b"jit_backend", 1)
 
+
+
+def test_host_memory_entry_points_without_device(rslib):
+    """rs_host_free / rs_host_unregister / rs_host_pool_stats argument checks
+    (no HIP call is made for these): freeing NULL is a no-op, foreign
+    pointers and addresses never registered are refused, the pool is empty."""
+    import ctypes
+
+    L = rslib.lib()
+    assert L.rs_host_free(None) == 0
+    junk = np.zeros(64, np.uint8)
+    inval = 13  # RS_ERR_INVAL
+    assert L.rs_host_free(ctypes.c_void_p(junk.ctypes.data)) == inval
+    assert L.rs_host_unregister(ctypes.c_void_p(junk.ctypes.data)) == inval
+    assert L.rs_host_unregister(None) == inval
+    out = ctypes.c_void_p()
+    assert L.rs_host_alloc(0, ctypes.byref(out)) == inval and not out.value
+    st = rslib.host_pool_stats()
+    assert st["in_use"] == 0 and set(st) == {"mapped", "in_use", "blocks", "spans"}

@@ -410,3 +410,89 @@ def test_engine_relaunch_under_concurrent_calls(rslib, orc, torch_dev, engine):
     assert not errors, errors[:5]
     calls, launches = r.host_engine_stats()
     assert calls > 0 and launches > 1, (calls, launches)
+
+
+def test_engine_drain_before_stop(rslib, orc, torch_dev, engine):
+    """Calls in flight when the instance is stopped for something other than a
+    same-shape relaunch complete on their own shape (advisor finding, round 3:
+    a workgroup that left at its life / idle limit before a call reached it,
+    followed by a table-registry recycle or a shape change, used to have its
+    done word raised past the call, which then returned with that
+    workgroup's units never written).  Six threads of host Encode / Update
+    calls with 100 us instance lives and a 20 us idle window, while one thread
+    forces registry recycles (a 4-entry registry and device products over
+    fresh matrices on the same handle) and another flips the engine's
+    workgroup count and waves per workgroup.  Every host result is checked
+    against the oracle and every device product against encode_numpy."""
+    torch = torch_dev
+    assert engine.rs_tune(b"host_engine_life_us", 100) == 0
+    assert engine.rs_tune(b"host_engine_idle_us", 20) == 0
+    L = engine
+    assert L.rs_tune(b"table_registry_max", 4) == 0
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    errors, stop = [], threading.Event()
+
+    def caller(tid):
+        rng = np.random.default_rng(900 + tid)
+        try:
+            for it in range(60):
+                data = [_rand(rng, size) for _ in range(d)]
+                exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, exp) == 0
+                v = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
+                r.Encode(v)
+                if tid % 2:
+                    row = int(rng.integers(0, d))
+                    new = _rand(rng, size)
+                    r.Update(v[row].copy(), new, row, v[d:])
+                    v[row][:] = new
+                    exp[row] = new.copy()
+                    assert orc.encode(d, p, exp) == 0
+                for j in range(d, d + p):
+                    if not np.array_equal(v[j], exp[j]):
+                        errors.append(("host", tid, it, j))
+                        return
+        except Exception as e:  # noqa: BLE001
+            errors.append(("host", tid, repr(e)))
+
+    def recycler():
+        rng = np.random.default_rng(990)
+        try:
+            src = torch.randint(0, 256, (2, 6, 4096), dtype=torch.uint8, device="cuda:0")
+            dst = torch.zeros((2, 3, 4096), dtype=torch.uint8, device="cuda:0")
+            hsrc = src.cpu().numpy()
+            while not stop.is_set():
+                mat = rng.integers(0, 256, (3, 6), dtype=np.uint8)
+                r.gf_matmul_batch(mat, src, None, dst, None)
+                torch.cuda.synchronize()
+                if not np.array_equal(dst.cpu().numpy(), orc.encode_numpy(mat, hsrc)):
+                    errors.append(("device product", mat.tolist()))
+                    return
+        except Exception as e:  # noqa: BLE001
+            errors.append(("recycler", repr(e)))
+
+    def shaper():
+        k = 0
+        while not stop.is_set():
+            L.rs_tune(b"host_engine_waves", (8, 4, 16, 8)[k % 4])
+            L.rs_tune(b"host_engine_group_waves", (8, 2, 4, 8)[k % 4])
+            k += 1
+            time.sleep(0.002)
+
+    callers = [threading.Thread(target=caller, args=(t,)) for t in range(6)]
+    aux = [threading.Thread(target=recycler), threading.Thread(target=shaper)]
+    try:
+        for t in aux + callers:
+            t.start()
+        for t in callers:
+            t.join(120)
+    finally:
+        stop.set()
+        for t in aux:
+            t.join(60)
+        L.rs_tune(b"table_registry_max", 1 << 14)
+    assert not any(t.is_alive() for t in callers + aux)
+    assert not errors, errors[:5]
+    calls, launches = r.host_engine_stats()
+    assert calls >= 6 * 60 and launches > 2, (calls, launches)

@@ -1,0 +1,134 @@
+"""Host memory handed to the library: rs_host_register / rs_host_unregister
+(page spans shared by reference, device drain before a span leaves the
+runtime) and the library-owned pool (rs_host_alloc / rs_host_free).
+
+Round 3's GPU suite faulted (hipErrorIllegalAddress at a later pageable
+`.cuda()` copy) after tests registered heap numpy memory, unregistered it and
+let it be freed; the reference's callers reuse their buffers freely
+(rs.go:101-111 retains nothing), so the supported API must allow exactly that
+sequence.  Every result is checked against the oracle (rs_oracle.c)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available()
+    torch.cuda.init()
+    return torch
+
+
+def _encode_ok(orc, r, d, p, v, rng):
+    size = v[0].size
+    for i in range(d):
+        v[i][:] = rng.integers(0, 256, size, dtype=np.uint8)
+    for j in range(d, d + p):
+        v[j][:] = 0xA5
+    r.Encode(v)
+    exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), np.stack([x.copy() for x in v[:d]])[None])[0]
+    return all(np.array_equal(v[d + j], exp[j]) for j in range(p))
+
+
+def test_register_free_reuse_sequence_in_child(rslib, orc):
+    """register -> host call -> unregister -> free -> reallocate -> pageable
+    copy -> host call, in the two patterns round 3's tests used (page-aligned
+    interior of a heap array; whole heap arrays sharing pages), then the
+    library-owned pool in the same loop.  Run in a child process
+    (tools/reg_reuse_probe.py), so a fault would end only that process."""
+    env = dict(os.environ, RSAMD_PROBE_ITERS="12")
+    out = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "reg_reuse_probe.py"), "lib",
+                          "unaligned", "pool"], env=env, capture_output=True, text=True, timeout=400)
+    print(out.stdout, out.stderr[-2000:])
+    assert out.returncode == 0, out.stdout + out.stderr[-2000:]
+    assert out.stdout.count(": exit 0") == 3, out.stdout
+
+
+def test_registrations_sharing_pages(rslib, orc, torch_dev):
+    """Two buffers that share a page registered one after the other: the
+    second takes a reference on the first's page span and registers only the
+    pages no span covers; unregistering the first leaves the second
+    zero-copy (its host calls run straight over it, never through the
+    coalesced staging path) and correct; the span leaves the runtime with the
+    last registration, after which the same vectors are staged."""
+    d, p, size = 10, 4, 4096
+    L = rslib.lib()
+    assert L.rs_tune(b"host_engine_direct", 0) == 0  # staged calls counted by host_call_stats
+    try:
+        r = rslib.New(d, p)
+        rng = np.random.default_rng(11)
+        spans0 = rslib.host_pool_stats()["spans"]
+        arena = np.zeros(2 * (d + p) * size + 3 * 4096, np.uint8)
+        off = (-arena.ctypes.data) % 4096 + 16  # a starts 16 bytes into a page
+        a = arena[off: off + (d + p) * size]  # ends 16 bytes into its last page
+        b = arena[off + a.nbytes: off + a.nbytes + 4080 + (d + p) * size]  # starts in that page
+        va = [a[i * size:(i + 1) * size] for i in range(d + p)]
+        vb = [b[4080 + i * size: 4080 + (i + 1) * size] for i in range(d + p)]  # b's vectors: its own pages
+        rslib.host_register(a.ctypes.data, a.nbytes)
+        rslib.host_register(b.ctypes.data, b.nbytes)
+        assert rslib.host_pool_stats()["spans"] - spans0 == 2  # a's pages, then b's pages a did not cover
+        with pytest.raises(rslib.ErrInvalidArgument):
+            rslib.host_register(a.ctypes.data, a.nbytes)  # same address twice
+
+        def staged():
+            return r.host_call_stats()[1]
+
+        s0 = staged()
+        assert _encode_ok(orc, r, d, p, va, rng) and _encode_ok(orc, r, d, p, vb, rng)
+        assert staged() == s0  # both zero-copy
+        rslib.host_unregister(a.ctypes.data)
+        assert rslib.host_pool_stats()["spans"] - spans0 == 2  # b still holds the shared page's span
+        assert _encode_ok(orc, r, d, p, vb, rng)
+        assert staged() == s0  # b still zero-copy
+        assert _encode_ok(orc, r, d, p, va, rng)
+        assert staged() == s0 + 1  # a staged now
+        rslib.host_unregister(b.ctypes.data)
+        assert rslib.host_pool_stats()["spans"] == spans0
+        with pytest.raises(rslib.ErrInvalidArgument):
+            rslib.host_unregister(b.ctypes.data)
+        assert _encode_ok(orc, r, d, p, vb, rng)
+        assert staged() == s0 + 2
+    finally:
+        L.rs_tune(b"host_engine_direct", 1)
+
+
+def test_pool_blocks_reused_and_zero_copy(rslib, orc, torch_dev):
+    """rs_host_alloc blocks: host calls on them run straight over them (the
+    engine's address mode), a freed block is handed out again without a new
+    mapping, double frees and foreign pointers are refused, and pageable
+    copies of fresh heap arrays in between stay correct."""
+    torch = torch_dev
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(12)
+    st0 = rslib.host_pool_stats()
+    for it in range(6):
+        buf = rslib.host_alloc((d + p) * size)
+        assert buf.ctypes.data % 4096 == 0
+        v = [buf[i * size:(i + 1) * size] for i in range(d + p)]
+        c0, _ = r.host_engine_stats()
+        assert _encode_ok(orc, r, d, p, v, rng), it
+        c1, _ = r.host_engine_stats()
+        assert c1 - c0 == 1, (it, c0, c1)
+        addr = buf.ctypes.data
+        del v
+        rslib.host_free(buf)
+        with pytest.raises(rslib.ErrInvalidArgument):
+            rslib.host_free(addr)
+        x = np.full(20 << 20, it, np.uint8)
+        t = torch.from_numpy(x).cuda()
+        torch.cuda.synchronize()
+        assert int(t[-1].item()) == it
+    st = rslib.host_pool_stats()
+    assert st["blocks"] - st0["blocks"] <= 1 and st["in_use"] == st0["in_use"], (st0, st)
+    with pytest.raises(rslib.ErrInvalidArgument):
+        rslib.host_free(np.zeros(16, np.uint8).ctypes.data)

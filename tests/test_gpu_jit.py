@@ -356,3 +356,17 @@ def test_jit_disk_cache_across_processes(rslib, tmp_path):
     files[0].write_bytes(bytes(raw))
     c = run(2)
     assert c["ok"] and c["cache"]["rejects"] == 1 and c["jit"]["compiled"] == 1 and c["cache"]["writes"] == 1, c
+    # the cache holds code the process runs: a directory or file others may
+    # write is neither read nor written (advisor finding, round 3)
+    os.chmod(tmp_path / "jit", 0o777)
+    d = run(1)
+    assert d["ok"] and d["cache"]["hits"] == 0 and d["cache"]["writes"] == 0, d
+    os.chmod(tmp_path / "jit", 0o700)
+    for f in (tmp_path / "jit").glob("*.co"):
+        os.chmod(f, 0o666)
+    e = run(1)
+    assert e["ok"] and e["cache"]["hits"] == 0, e
+    for f in (tmp_path / "jit").glob("*.co"):
+        os.chmod(f, 0o600)
+    g = run(1)
+    assert g["ok"] and g["cache"]["hits"] == 1, g
