@@ -408,6 +408,14 @@ RS_API int rs_jit_prepare(rs_t* rs, const uint8_t* mat, int rows, int cols, int 
  * For tests and warm-up. */
 RS_API int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms);
 
+/* The run-time kernel generator's two outputs agree: the machine code it
+ * encodes directly (the default backend) equals, byte for byte, comgr's
+ * assembly of the assembly text it prints for the same rows x cols matrix
+ * (bounds as rs_jit_asm_source).  RS_OK, RS_ERR_DEVICE (the first difference
+ * goes to stderr) or RS_ERR_INVAL.  *code_bytes (may be NULL) receives the
+ * kernel's size.  For tests; no device needed. */
+RS_API int rs_jit_encoder_check(const uint8_t* mat, int rows, int cols, int accumulate, size_t* code_bytes);
+
 /* The gfx950 assembly the run-time kernel generator emits for a rows x cols
  * matrix (row-major, 1 <= rows <= 128, 1 <= cols <= 256), overwrite
  * (accumulate 0) or XOR-into-outputs (1): copied NUL-terminated into
@@ -485,9 +493,11 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * workgroup meet at a barrier every n columns, 0 = never; default 0),
  * "jit_waves" (assembly kernels hold at most n waves per SIMD, 2..8, by
  * declaring more registers; 0 = as many as fit; default 2),
- * "jit_backend" (1 default: kernels emitted as gfx950 assembly and assembled
- * by comgr, tens of ms per matrix, up to 128 output rows x 256 columns | 0:
- * C++ compiled by hiprtc, seconds per matrix, up to 16 x 64), "jit_disk_cache" (1 default: compiled
+ * "jit_backend" (2 default: kernels generated as gfx950 machine code and
+ * copied into a code-object template, up to 128 output rows x 256 columns |
+ * 1: the same kernels as assembly text assembled by comgr, 12 ms - 1.7 s per
+ * matrix | 0: C++ compiled by hiprtc, seconds per matrix, up to 16 x 64),
+ * "jit_disk_cache" (1 default: compiled
  * code objects are kept in an on-disk cache shared by processes, see
  * rs_jit_cache_stats | 0: compile in every process),
  * "table_registry_max" (distinct coefficient matrices

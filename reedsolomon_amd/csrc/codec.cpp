@@ -550,7 +550,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_sync") g_jit_sync = value < 0 ? 0 : value > 64 ? 64 : value;
         else if (n == "jit_waves") g_jit_waves = value < 0 ? 0 : value > 8 ? 8 : value;
         else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;
-        else if (n == "jit_backend") g_jit_backend = value ? 1 : 0;
+        else if (n == "jit_backend") g_jit_backend = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
@@ -682,4 +682,8 @@ int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int accumulate
 
 int rs_jit_compile_check(const uint8_t* mat, int rows, int cols, int accumulate, double* ms) {
     return abi_guard([&]() -> int { return jit_compile_check(mat, rows, cols, accumulate != 0, ms); });
+}
+
+int rs_jit_encoder_check(const uint8_t* mat, int rows, int cols, int accumulate, size_t* code_bytes) {
+    return abi_guard([&]() -> int { return jit_encoder_check(mat, rows, cols, accumulate != 0, code_bytes); });
 }

@@ -86,9 +86,13 @@ int g_jit_waves = [] {
     return e ? std::atoi(e) : 2;
 }();
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
-int g_jit_backend = [] {  // rs_tune("jit_backend", 1 | 0): assembly (jit_asm.cpp) | hiprtc C++; env RSAMD_JIT_BACKEND
+// rs_tune("jit_backend", 2 | 1 | 0): machine code encoded directly into a
+// code-object template (jit_asm.cpp) | the same kernel as assembly text
+// assembled by comgr | hiprtc C++; env RSAMD_JIT_BACKEND
+int g_jit_backend = [] {
     const char* e = std::getenv("RSAMD_JIT_BACKEND");
-    return e ? (std::atoi(e) ? 1 : 0) : 1;
+    const int v = e ? std::atoi(e) : 2;
+    return v < 0 ? 0 : v > 2 ? 2 : v;
 }();
 int jit_max_rows() { return g_jit_backend ? kAsmMaxRows : kJitMaxRows; }
 int jit_max_cols() { return g_jit_backend ? kAsmMaxCols : kJitMaxCols; }
@@ -459,6 +463,19 @@ Compiled compile_asm(const std::string& src) {
     return out;
 }
 
+Compiled compile_binary_shape(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync,
+                              int waves) {
+    Compiled out;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint32_t> code;
+    int used = 0;
+    if (!asm_binary(mat, rows, cols, acc, nw, pf, sync, &code, &used, &out.log)) return out;
+    double lms = 0;
+    out.ok = asm_link_binary(code, nw, used, waves, &out.code, &out.log, &lms);
+    out.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return out;
+}
+
 Compiled compile(const std::string& src) {
     Compiled out;
     const auto t0 = std::chrono::steady_clock::now();
@@ -517,14 +534,23 @@ Compiled compile(const std::string& src) {
 
 struct Entry {
     enum State { kQueued, kCompiling, kReady, kLoaded, kFailed } state = kQueued;
-    bool is_asm = false;  // generated assembly (rs_bs_asm) or hiprtc C++ (rs_bs_jit_64 / _256)
-    int nw = 1;           // assembly kernels: waves per workgroup
-    std::string src;
+    bool is_asm = false;  // generated kernel (rs_bs_asm) or hiprtc C++ (rs_bs_jit_64 / _256)
+    int nw = 1;           // generated kernels: waves per workgroup
+    int backend = 1;
+    std::string src;      // backends 1 (assembly) and 0 (C++)
+    // backend 2 (machine code): the matrix and the generator's settings
+    std::vector<uint8_t> mat;
+    int rows = 0, cols = 0, pf = 3, sync = 0, waves = 2;
+    bool acc = false;
     DiskKey disk;  // on-disk cache key (text empty: the disk cache is off)
     std::vector<char> code;
     hipModule_t module = nullptr;
     hipFunction_t fn64 = nullptr, fn256 = nullptr;
 };
+
+Compiled compile_binary(const Entry& e) {
+    return compile_binary_shape(e.mat.data(), e.rows, e.cols, e.acc, e.nw, e.pf, e.sync, e.waves);
+}
 
 constexpr size_t kMaxEntries = 256;
 constexpr size_t kMaxSeen = 4096;  // matrices counted but not compiled yet (cleared when full)
@@ -549,7 +575,7 @@ struct Jit {
     std::atomic<uint64_t> launches{0};
 
     void run_one(const std::shared_ptr<Entry>& e) {  // caller does not hold mu
-        Compiled c = e->is_asm ? compile_asm(e->src) : compile(e->src);
+        Compiled c = e->backend == 2 ? compile_binary(*e) : e->is_asm ? compile_asm(e->src) : compile(e->src);
         // The compiler libraries hiprtc loads on its first compile register
         // their static destructors then, i.e. after jit_atexit: those ran
         // first at exit and a compile still in flight on the worker crashed
@@ -573,6 +599,8 @@ struct Jit {
         }
         e->src.clear();
         e->src.shrink_to_fit();
+        e->mat.clear();
+        e->mat.shrink_to_fit();
     }
 
     void work() {
@@ -636,12 +664,55 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
 
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
     if (!mat || rows < 1 || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
-    Compiled c = g_jit_backend
-                     ? compile_asm(asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync, g_jit_waves, nullptr))
-                     : compile(jit_source(mat, rows, cols, accumulate));
+    Compiled c =
+        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync,
+                                                  g_jit_waves)
+        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync,
+                                                    g_jit_waves, nullptr))
+                           : compile(jit_source(mat, rows, cols, accumulate));
     if (ms) *ms = c.ms;
     if (!c.ok) std::fprintf(stderr, "librsamd: jit compile check failed: %s\n", c.log.substr(0, 4000).c_str());
     return c.ok ? RS_OK : RS_ERR_DEVICE;
+}
+
+int jit_encoder_check(const uint8_t* mat, int rows, int cols, bool accumulate, size_t* code_bytes) {
+    if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
+    const int nw = asm_waves(rows);
+    std::vector<uint32_t> bin;
+    int used = 0;
+    std::string err;
+    if (!asm_binary(mat, rows, cols, accumulate, nw, g_jit_pf, g_jit_sync, &bin, &used, &err)) {
+        std::fprintf(stderr, "librsamd: encoder failed: %s\n", err.c_str());
+        return RS_ERR_DEVICE;
+    }
+    Compiled c = compile_asm(asm_source(mat, rows, cols, accumulate, nw, g_jit_pf, g_jit_sync, g_jit_waves, nullptr));
+    std::vector<char> text;
+    if (!c.ok || !asm_text_section(c.code, &text)) {
+        std::fprintf(stderr, "librsamd: encoder check: assembly failed: %s\n", c.log.substr(0, 2000).c_str());
+        return RS_ERR_DEVICE;
+    }
+    if (code_bytes) *code_bytes = bin.size() * 4;
+    const size_t n = bin.size() * 4;
+    if (text.size() < n) {
+        std::fprintf(stderr, "librsamd: encoder check: %zu bytes encoded, the assembler's .text has %zu\n", n,
+                     text.size());
+        return RS_ERR_DEVICE;
+    }
+    const char* b = reinterpret_cast<const char*>(bin.data());
+    for (size_t i = 0; i < n; i += 4)
+        if (std::memcmp(b + i, text.data() + i, 4) != 0) {
+            uint32_t x, y;
+            std::memcpy(&x, b + i, 4);
+            std::memcpy(&y, text.data() + i, 4);
+            std::fprintf(stderr, "librsamd: encoder check: byte %zu differs: encoder %08x, assembler %08x\n", i, x, y);
+            return RS_ERR_DEVICE;
+        }
+    for (size_t i = n; i < text.size(); ++i)  // (the assembler's .text may end with alignment padding)
+        if (text[i] != 0) {
+            std::fprintf(stderr, "librsamd: encoder check: the assembler's .text goes on past byte %zu\n", n);
+            return RS_ERR_DEVICE;
+        }
+    return RS_OK;
 }
 
 void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms) {
@@ -686,7 +757,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
         return std::string(b);
     }();
     DiskKey k;
-    k.text = arch + '\n' + fixed + (g_jit_backend ? " asm " : " hiprtc ") + '\n';
+    k.text = arch + '\n' + fixed + (g_jit_backend == 2 ? " bin " : g_jit_backend ? " asm " : " hiprtc ") + '\n';
     k.text += static_cast<char>(a.accumulate ? 1 : 0);
     k.text += static_cast<char>(a.rows);
     k.text += static_cast<char>(a.cols);
@@ -745,6 +816,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                     if (h) j.seen.erase(key);
                     e = std::make_shared<Entry>();
                     e->is_asm = backend != 0;
+                    e->backend = backend;
                     e->nw = asm_waves(a.rows);
                     e->code = std::move(code);
                     e->state = Entry::kReady;
@@ -768,9 +840,21 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
             }
             e = std::make_shared<Entry>();
             e->is_asm = backend != 0;
+            e->backend = backend;
             e->nw = asm_waves(a.rows);
-            e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->nw, g_jit_pf, g_jit_sync, g_jit_waves, nullptr)
-                               : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
+            if (backend == 2) {
+                e->mat.assign(a.host_mat, a.host_mat + static_cast<size_t>(a.rows) * a.cols);
+                e->rows = a.rows;
+                e->cols = a.cols;
+                e->acc = a.accumulate != 0;
+                e->pf = g_jit_pf;
+                e->sync = g_jit_sync;
+                e->waves = g_jit_waves;
+            } else {
+                e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->nw, g_jit_pf,
+                                                g_jit_sync, g_jit_waves, nullptr)
+                                   : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
+            }
             if (g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
             j.entries.emplace(key, e);
             if (mode == 2) {

@@ -39,9 +39,11 @@ extern int g_jit_waves;
 // been launched this many times, moving jit_min_bytes in total (default 2)
 extern int g_jit_min_launches;
 
-// rs_tune("jit_backend", 1 | 0): kernels generated as gfx950 assembly and
-// assembled by comgr (jit_asm.cpp; default: tens of ms per matrix, up to 128
-// rows x 256 columns) | C++ compiled by hiprtc (1-16 s, up to 16 x 64)
+// rs_tune("jit_backend", 2 | 1 | 0): kernels generated as gfx950 machine code
+// dropped into a code-object template (jit_asm.cpp; default) | the same
+// kernels as assembly assembled by comgr (12 ms - 1.7 s per matrix) | C++
+// compiled by hiprtc (1-16 s, up to 16 x 64); both generated forms go up to
+// 128 rows x 256 columns
 extern int g_jit_backend;
 int jit_max_rows();
 int jit_max_cols();
@@ -67,8 +69,12 @@ void jit_count_launch();
 // The kernel source for one matrix (rows x cols, row-major); exposed for the
 // CPU tests (rs_jit_compile_check).
 std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate);
-// Compile only (hiprtc, no device needed): RS_OK or RS_ERR_DEVICE.
+// Compile only (no device needed): RS_OK or RS_ERR_DEVICE.
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms);
+// The generator's machine code (backend 2) equals comgr's assembly of its
+// text (backend 1) byte for byte: RS_OK, or RS_ERR_DEVICE (first difference
+// on stderr).  No device needed.
+int jit_encoder_check(const uint8_t* mat, int rows, int cols, bool accumulate, size_t* code_bytes);
 // Compile (wait: on this thread, and load on the current device) or queue
 // the kernel for a matrix now, whatever its launch history (rs_jit_prepare).
 int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wait);

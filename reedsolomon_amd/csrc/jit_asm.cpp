@@ -1,20 +1,28 @@
-// jit_asm.cpp — run-time bit-sliced kernels emitted directly as gfx950
-// assembly and assembled by the code-object manager (comgr), instead of
-// C++ compiled by hiprtc.
+// jit_asm.cpp — run-time bit-sliced kernels generated for one matrix as
+// gfx950 machine code.
 //
 // Why: hiprtc runs the whole LLVM pipeline over a straight-line network of
-// thousands of XORs: 1.2-1.5 s for a 10 x 8 matrix (0.85 s of it fixed cost:
-// headers, device libraries) and 6-16 s for 16 x 32 .. 16 x 64,
-// too slow for erasure patterns seen a few times, and out of reach for
-// networks wider than 16 rows.  The network needs no optimiser: register
-// allocation is fixed by the layout below, and assembling is linear in its
-// size (tens of ms).
+// thousands of XORs: 1.2-1.5 s for a 10 x 8 matrix and 6-16 s for 16 x 32 ..
+// 16 x 64.  The network needs no optimiser: register
+// allocation is fixed by the layout below.  Round 3 printed it as assembly
+// and had comgr assemble and link it: 12 ms for 5 x 10, ~30 ms for 16 x 16,
+// 0.3-0.4 s for 28 x 100 / 64 x 64 and 1.5-1.7 s for 128 x 128 (llvm-mc over
+// hundreds of thousands of lines).  The generator now builds the kernel as a
+// list of instructions (Prog) that is either printed as assembly (asm_source:
+// the CPU emulator's input, and the comgr path kept for comparison) or
+// encoded straight into machine code (asm_binary) and dropped into a
+// code-object template (asm_link_binary): the template - kernel descriptor,
+// metadata, and a .text of the right size class filled with s_endpgm - is
+// assembled by comgr once per (waves per workgroup, VGPR budget, size class)
+// and reused for every matrix.  tests/test_jit_asm.py checks that the
+// encoder's bytes equal comgr's for generated kernels, instruction for
+// instruction.
 //
-// Kernel contract (AsmArgs, jit.hpp).  Grid x = 2 KiB chunks of each vector,
-// grid y = stripes of the launch; a workgroup is NW waves over the same
-// chunk.  Lane t of a wave owns 32 bytes of every vector: four 8-byte pieces
-// at 8t + 512k (k = 0..3) of the chunk, so each wave instruction moves 512
-// contiguous bytes (the perm-table kernels' dwordx2 pattern).  Wave w
+// Kernel contract (AsmArgs, jit_asm.hpp).  Grid x = 2 KiB chunks of each
+// vector, grid y = stripes of the launch; a workgroup is NW waves over the
+// same chunk.  Lane t of a wave owns 32 bytes of every vector: four 8-byte
+// pieces at 8t + 512k (k = 0..3) of the chunk, so each wave instruction moves
+// 512 contiguous bytes (the perm-table kernels' dwordx2 pattern).  Wave w
 // computes rows [w*RW, w*RW + RW) of the matrix (rows past the matrix are
 // not emitted); with NW > 1 the waves load the same input lines, the first
 // fetch going to HBM and the others hitting the CU's L1 / the XCD's L2.
@@ -34,12 +42,13 @@
 #include <amd_comgr/amd_comgr.h>
 
 #include <algorithm>
-
 #include <chrono>
 #include <cstdarg>
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace rsamd {
@@ -58,21 +67,309 @@ uint8_t gmul8(uint8_t a, uint8_t b) {  // GF(2^8), polynomial 0x11d
     return r;
 }
 
-class Asm {
-public:
+// ---------------------------------------------------------------- instructions
+//
+// Source operands use the hardware's 9-bit operand space: SGPR n = n, inline
+// integer k (0..64) = 128 + k, -1 = 193, a 32-bit literal = 255 (value in
+// `imm`), VGPR n = 256 + n.
+constexpr int kLit = 255;
+constexpr int V(int n) { return 256 + n; }
+constexpr int C(int k) { return 128 + k; }
+
+enum class K : uint8_t {
+    Label,
+    SLoad,      // a = sdst, b = dwords (1 | 2), c = sbase, imm = byte offset
+    SMovLit,    // a = sdst, imm (d = 1: printed zero-padded)
+    SOp1,       // sub: mov | getpc | setpc; a = sdst, b = ssrc
+    SOp2,       // sub: add | addc | lshl | lshl64 | mul | mulhi | and; a = sdst, b = src0, c = src1, imm
+    SCmp,       // sub: eq32 | eq64; a = src0, b = src1
+    SNop,       // a = wait states - 1
+    SWaitLgkm0,
+    SWaitVm,    // a = count
+    SBarrier,
+    SEndpgm,
+    SBranch,    // sub: scc0 | scc1; a = label
+    SAddPcrel,  // sub: lo (s_add_u32 with the literal label(a) - label(b)) | hi (s_addc_u32 with its upper half); c = sdst = src0
+    VOp2,       // sub: and | lshl | lshr | add | xor; a = vdst, b = src0, c = vsrc1 (VGPR number), imm
+    VMov,       // a = vdst, b = src0
+    VReadLane,  // a = sdst, b = VGPR number
+    VBfi,       // a = vdst, b = src0, c = src1, d = src2 (9-bit operands)
+    VXor3,      // v_bitop3_b32 ... bitop3:0x96; a = vdst, b, c, d = VGPR numbers
+    BufLoad2,   // a = vdata, b = vaddr, c = srsrc (first SGPR), d = offset, sub = nt
+    BufStore2,  // same
+};
+
+enum Sub : uint8_t {
+    kNone = 0,
+    kMov, kGetpc, kSetpc,
+    kAdd, kAddc, kLshl, kLshl64, kMul, kMulhi, kAnd,
+    kEq32, kEq64,
+    kScc0, kScc1,
+    kLo, kHi,
+    kVAnd, kVLshl, kVLshr, kVAdd, kVXor,
+};
+
+struct Ins {
+    K k;
+    uint8_t sub;
+    int16_t a, b, c, d;
+    uint32_t imm;
+};
+
+struct Prog {
+    std::vector<Ins> ins;
+    std::vector<std::string> label_names;
+    int new_label(const std::string& name) {
+        label_names.push_back(name);
+        return static_cast<int>(label_names.size()) - 1;
+    }
+    void put(K k, int sub, int a = 0, int b = 0, int c = 0, int d = 0, uint32_t imm = 0) {
+        ins.push_back(Ins{k, static_cast<uint8_t>(sub), static_cast<int16_t>(a), static_cast<int16_t>(b),
+                          static_cast<int16_t>(c), static_cast<int16_t>(d), imm});
+    }
+    void label(int l) { put(K::Label, kNone, l); }
+    void s_load(int sdst, int dwords, int sbase, uint32_t off) { put(K::SLoad, kNone, sdst, dwords, sbase, 0, off); }
+    void s_mov_lit(int sdst, uint32_t v, bool pad) { put(K::SMovLit, kNone, sdst, 0, 0, pad ? 1 : 0, v); }
+    void s_mov(int sdst, int ssrc) { put(K::SOp1, kMov, sdst, ssrc); }
+    void s_getpc(int sdst) { put(K::SOp1, kGetpc, sdst, 0); }
+    void s_setpc(int ssrc) { put(K::SOp1, kSetpc, 0, ssrc); }
+    void s_op2(Sub s, int sdst, int src0, int src1, uint32_t imm = 0) { put(K::SOp2, s, sdst, src0, src1, 0, imm); }
+    void s_cmp(Sub s, int src0, int src1) { put(K::SCmp, s, src0, src1); }
+    void s_nop(int n) { put(K::SNop, kNone, n); }
+    void wait_lgkm0() { put(K::SWaitLgkm0, kNone); }
+    void wait_vm(int n) { put(K::SWaitVm, kNone, n); }
+    void s_barrier() { put(K::SBarrier, kNone); }
+    void s_endpgm() { put(K::SEndpgm, kNone); }
+    void branch(Sub s, int label) { put(K::SBranch, s, label); }
+    void add_pcrel(Sub s, int sreg, int target, int pc) { put(K::SAddPcrel, s, target, pc, sreg); }
+    void v_op2(Sub s, int vdst, int src0, int vsrc1, uint32_t imm = 0) { put(K::VOp2, s, vdst, src0, vsrc1, 0, imm); }
+    void v_mov(int vdst, int src0) { put(K::VMov, kNone, vdst, src0); }
+    void v_readlane(int sdst, int vsrc) { put(K::VReadLane, kNone, sdst, vsrc); }
+    void v_bfi(int vdst, int src0, int src1, int src2) { put(K::VBfi, kNone, vdst, src0, src1, src2); }
+    void v_xor3(int vdst, int a, int b, int c) { put(K::VXor3, kNone, vdst, a, b, c); }
+    void buf_load2(int vdata, int vaddr, int srsrc, int off, bool nt) {
+        put(K::BufLoad2, nt ? 1 : 0, vdata, vaddr, srsrc, off);
+    }
+    void buf_store2(int vdata, int vaddr, int srsrc, int off) { put(K::BufStore2, 1, vdata, vaddr, srsrc, off); }
+};
+
+// ---------------------------------------------------------------- text
+
+std::string opnd(int x, uint32_t imm) {  // a 9-bit source operand as assembly text
+    char b[32];
+    if (x >= 256) std::snprintf(b, sizeof b, "v%d", x - 256);
+    else if (x == kLit) std::snprintf(b, sizeof b, "0x%x", imm);
+    else if (x >= 128 && x <= 192) std::snprintf(b, sizeof b, "%d", x - 128);
+    else if (x >= 193 && x <= 208) std::snprintf(b, sizeof b, "%d", 192 - x);
+    else std::snprintf(b, sizeof b, "s%d", x);
+    return b;
+}
+
+std::string print(const Prog& p) {
     std::string out;
-    void line(const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
-        char buf[256];
+    char b[256];
+    auto line = [&](const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
         va_list ap;
         va_start(ap, fmt);
-        std::vsnprintf(buf, sizeof buf, fmt, ap);
+        std::vsnprintf(b, sizeof b, fmt, ap);
         va_end(ap);
         out += '\t';
-        out += buf;
+        out += b;
         out += '\n';
+    };
+    for (const Ins& i : p.ins) {
+        switch (i.k) {
+            case K::Label: out += p.label_names[static_cast<size_t>(i.a)] + ":\n"; break;
+            case K::SLoad:
+                if (i.b == 1) line("s_load_dword s%d, s[%d:%d], 0x%x", i.a, i.c, i.c + 1, i.imm);
+                else line("s_load_dwordx2 s[%d:%d], s[%d:%d], 0x%x", i.a, i.a + 1, i.c, i.c + 1, i.imm);
+                break;
+            case K::SMovLit: line(i.d ? "s_mov_b32 s%d, 0x%08x" : "s_mov_b32 s%d, 0x%x", i.a, i.imm); break;
+            case K::SOp1:
+                if (i.sub == kMov) line("s_mov_b32 s%d, s%d", i.a, i.b);
+                else if (i.sub == kGetpc) line("s_getpc_b64 s[%d:%d]", i.a, i.a + 1);
+                else line("s_setpc_b64 s[%d:%d]", i.b, i.b + 1);
+                break;
+            case K::SOp2: {
+                static const char* const nm[] = {"s_add_u32", "s_addc_u32", "s_lshl_b32", "s_lshl_b64",
+                                                 "s_mul_i32", "s_mul_hi_u32", "s_and_b32"};
+                const char* n = nm[i.sub - kAdd];
+                if (i.sub == kLshl64)
+                    line("%s s[%d:%d], s[%d:%d], %s", n, i.a, i.a + 1, i.b, i.b + 1, opnd(i.c, i.imm).c_str());
+                else
+                    line("%s s%d, %s, %s", n, i.a, opnd(i.b, i.imm).c_str(), opnd(i.c, i.imm).c_str());
+                break;
+            }
+            case K::SCmp:
+                if (i.sub == kEq64) line("s_cmp_eq_u64 s[%d:%d], %s", i.a, i.a + 1, opnd(i.b, 0).c_str());
+                else line("s_cmp_eq_u32 %s, %s", opnd(i.a, 0).c_str(), opnd(i.b, 0).c_str());
+                break;
+            case K::SNop: line("s_nop %d", i.a); break;
+            case K::SWaitLgkm0: line("s_waitcnt lgkmcnt(0)"); break;
+            case K::SWaitVm: line("s_waitcnt vmcnt(%d)", i.a); break;
+            case K::SBarrier: line("s_barrier"); break;
+            case K::SEndpgm: line("s_endpgm"); break;
+            case K::SBranch:
+                line("%s %s", i.sub == kScc0 ? "s_cbranch_scc0" : "s_cbranch_scc1",
+                     p.label_names[static_cast<size_t>(i.a)].c_str());
+                break;
+            case K::SAddPcrel: {
+                const std::string& t = p.label_names[static_cast<size_t>(i.a)];
+                const std::string& pc = p.label_names[static_cast<size_t>(i.b)];
+                if (i.sub == kLo) line("s_add_u32 s%d, s%d, (%s-%s)&4294967295", i.c, i.c, t.c_str(), pc.c_str());
+                else line("s_addc_u32 s%d, s%d, (%s-%s)>>32", i.c, i.c, t.c_str(), pc.c_str());
+                break;
+            }
+            case K::VOp2: {
+                static const char* const nm[] = {"v_and_b32", "v_lshlrev_b32", "v_lshrrev_b32", "v_add_u32",
+                                                 "v_xor_b32"};
+                line("%s v%d, %s, v%d", nm[i.sub - kVAnd], i.a, opnd(i.b, i.imm).c_str(), i.c);
+                break;
+            }
+            case K::VMov: line("v_mov_b32 v%d, %s", i.a, opnd(i.b, 0).c_str()); break;
+            case K::VReadLane: line("v_readfirstlane_b32 s%d, v%d", i.a, i.b); break;
+            case K::VBfi:
+                line("v_bfi_b32 v%d, %s, %s, %s", i.a, opnd(i.b, 0).c_str(), opnd(i.c, 0).c_str(),
+                     opnd(i.d, 0).c_str());
+                break;
+            case K::VXor3: line("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", i.a, i.b, i.c, i.d); break;
+            case K::BufLoad2:
+            case K::BufStore2: {
+                const bool ld = i.k == K::BufLoad2;
+                char off[32] = "";
+                if (i.d) std::snprintf(off, sizeof off, " offset:%d", i.d);
+                line("%s v[%d:%d], v%d, s[%d:%d], 0 offen%s%s", ld ? "buffer_load_dwordx2" : "buffer_store_dwordx2",
+                     i.a, i.a + 1, i.b, i.c, i.c + 3, off, i.sub ? " nt" : "");
+                break;
+            }
+        }
     }
-    void label(const std::string& l) { out += l + ":\n"; }
-};
+    return out;
+}
+
+// ---------------------------------------------------------------- machine code (gfx950)
+//
+// Encodings as llvm-mc --mcpu=gfx950 --show-encoding emits them (GFX9
+// formats): SOP1/SOP2/SOPC/SOPP/SMEM/VOP1/VOP2/VOP3/MUBUF.  Size in bytes.
+int ins_size(const Ins& i) {
+    switch (i.k) {
+        case K::Label: return 0;
+        case K::SLoad: case K::VBfi: case K::VXor3: case K::BufLoad2: case K::BufStore2: return 8;
+        case K::SMovLit: return 8;
+        case K::SAddPcrel: return 8;
+        case K::SOp2: return (i.b == kLit || i.c == kLit) ? 8 : 4;
+        case K::VOp2: return i.b == kLit ? 8 : 4;
+        default: return 4;
+    }
+}
+
+bool encode(const Prog& p, std::vector<uint32_t>* out, std::string* err) {
+    std::vector<int64_t> at(p.label_names.size(), -1);
+    int64_t pc = 0;
+    for (const Ins& i : p.ins) {
+        if (i.k == K::Label) at[static_cast<size_t>(i.a)] = pc;
+        pc += ins_size(i);
+    }
+    out->clear();
+    out->reserve(static_cast<size_t>(pc / 4));
+    auto w = [&](uint32_t x) { out->push_back(x); };
+    auto bad = [&](const char* what) {
+        if (err) *err = what;
+        return false;
+    };
+    static const uint8_t sop2_op[] = {0x00, 0x04, 0x1c, 0x1d, 0x24, 0x2c, 0x0c};  // add addc lshl lshl64 mul mulhi and
+    static const uint8_t vop2_op[] = {0x13, 0x12, 0x10, 0x34, 0x15};              // and lshlrev lshrrev add_u32 xor
+    pc = 0;
+    for (const Ins& i : p.ins) {
+        const int64_t here = pc;
+        pc += ins_size(i);
+        switch (i.k) {
+            case K::Label: break;
+            case K::SLoad:  // SMEM: op 0 (dword) / 1 (dwordx2), imm offset
+                w(0xc0020000u | (i.b == 2 ? 1u << 18 : 0u) | (static_cast<uint32_t>(i.a) << 6) |
+                  (static_cast<uint32_t>(i.c) >> 1));
+                if (i.imm >= (1u << 20)) return bad("s_load offset");
+                w(i.imm);
+                break;
+            case K::SMovLit:  // SOP1 s_mov_b32 sdst, literal
+                w(0xbe800000u | (static_cast<uint32_t>(i.a) << 16) | 0xffu);
+                w(i.imm);
+                break;
+            case K::SOp1: {
+                const uint32_t op = i.sub == kMov ? 0x00 : i.sub == kGetpc ? 0x1c : 0x1d;
+                w(0xbe800000u | (static_cast<uint32_t>(i.a) << 16) | (op << 8) | static_cast<uint32_t>(i.b));
+                break;
+            }
+            case K::SOp2:
+                if (i.b > 255 || i.c > 255) return bad("SOP2 operand");
+                w(0x80000000u | (static_cast<uint32_t>(sop2_op[i.sub - kAdd]) << 23) |
+                  (static_cast<uint32_t>(i.a) << 16) | (static_cast<uint32_t>(i.c) << 8) | static_cast<uint32_t>(i.b));
+                if (i.b == kLit || i.c == kLit) w(i.imm);
+                break;
+            case K::SCmp:
+                w(0xbf000000u | ((i.sub == kEq64 ? 0x12u : 0x06u) << 16) | (static_cast<uint32_t>(i.b) << 8) |
+                  static_cast<uint32_t>(i.a));
+                break;
+            case K::SNop: w(0xbf800000u | static_cast<uint32_t>(i.a)); break;
+            case K::SWaitLgkm0: w(0xbf8cc07fu); break;  // vmcnt 63, expcnt 7, lgkmcnt 0
+            case K::SWaitVm: {  // vmcnt[3:0] bits 3:0, [5:4] bits 15:14; expcnt 7, lgkmcnt 15
+                const uint32_t n = static_cast<uint32_t>(i.a) & 63;
+                w(0xbf8c0000u | (n & 15) | ((n >> 4) << 14) | 0x70u | 0xf00u);
+                break;
+            }
+            case K::SBarrier: w(0xbf8a0000u); break;
+            case K::SEndpgm: w(0xbf810000u); break;
+            case K::SBranch: {
+                const int64_t t = at[static_cast<size_t>(i.a)];
+                if (t < 0) return bad("branch label");
+                const int64_t rel = (t - (here + 4)) / 4;
+                if (rel < -32768 || rel > 32767) return bad("branch range");
+                w(0xbf800000u | ((i.sub == kScc0 ? 0x04u : 0x05u) << 16) | (static_cast<uint32_t>(rel) & 0xffffu));
+                break;
+            }
+            case K::SAddPcrel: {
+                const int64_t t = at[static_cast<size_t>(i.a)], b = at[static_cast<size_t>(i.b)];
+                if (t < 0 || b < 0) return bad("pc-relative label");
+                const int64_t d = t - b;
+                const uint32_t s = static_cast<uint32_t>(i.c);
+                // s_add_u32 s, s, literal (low half) | s_addc_u32 s, s, literal (high half),
+                // as the assembler encodes the label expressions
+                w(0x80000000u | (i.sub == kLo ? 0u : 0x04u << 23) | (s << 16) | (0xffu << 8) | s);
+                w(static_cast<uint32_t>(i.sub == kLo ? static_cast<uint64_t>(d) : static_cast<uint64_t>(d) >> 32));
+                break;
+            }
+            case K::VOp2:
+                if (i.c > 255) return bad("VOP2 vsrc1");
+                w((static_cast<uint32_t>(vop2_op[i.sub - kVAnd]) << 25) | (static_cast<uint32_t>(i.a) << 17) |
+                  (static_cast<uint32_t>(i.c) << 9) | static_cast<uint32_t>(i.b));
+                if (i.b == kLit) w(i.imm);
+                break;
+            case K::VMov: w(0x7e000000u | (static_cast<uint32_t>(i.a) << 17) | (0x01u << 9) | static_cast<uint32_t>(i.b)); break;
+            case K::VReadLane:
+                w(0x7e000000u | (static_cast<uint32_t>(i.a) << 17) | (0x02u << 9) | (256u + static_cast<uint32_t>(i.b)));
+                break;
+            case K::VBfi:  // VOP3a op 0x1ca
+                w(0xd1ca0000u | static_cast<uint32_t>(i.a));
+                w(static_cast<uint32_t>(i.b) | (static_cast<uint32_t>(i.c) << 9) | (static_cast<uint32_t>(i.d) << 18));
+                break;
+            case K::VXor3:  // VOP3 op 0x234, truth table 0x96 spread over ABS / OMOD / NEG
+                w(0xd2340200u | static_cast<uint32_t>(i.a));
+                w(0xd0000000u | (256u + static_cast<uint32_t>(i.b)) | ((256u + static_cast<uint32_t>(i.c)) << 9) |
+                  ((256u + static_cast<uint32_t>(i.d)) << 18));
+                break;
+            case K::BufLoad2:
+            case K::BufStore2: {  // MUBUF op 0x15 / 0x1d, offen, nt = bit 17
+                if (i.d < 0 || i.d > 4095) return bad("buffer offset");
+                const uint32_t op = i.k == K::BufLoad2 ? 0x15u : 0x1du;
+                w(0xe0000000u | (op << 18) | (i.sub ? 1u << 17 : 0u) | (1u << 12) | static_cast<uint32_t>(i.d));
+                w(0x80000000u | ((static_cast<uint32_t>(i.c) >> 2) << 16) | (static_cast<uint32_t>(i.a) << 8) |
+                  static_cast<uint32_t>(i.b));
+                break;
+            }
+        }
+    }
+    return true;
+}
 
 // SGPRs
 constexpr int kSKarg = 0;      // s[0:1] kernarg segment pointer
@@ -100,12 +397,12 @@ struct Layout {
 
 // In-place 8x8 bit transpose of v[r[0]..r[7]] (bs_transpose8, kernels.hip):
 // swap(a, b, s, m): b = (m & (a >> s)) | (~m & b); a = ((m << s) & (b << s)) | (~(m << s) & a)
-void transpose8(Asm& A, const int (&r)[8]) {
+void transpose8(Prog& P, const int (&r)[8]) {
     auto swap = [&](int a, int b, int s, int mi) {
-        A.line("v_lshrrev_b32 v%d, %d, v%d", kVT0, s, a);
-        A.line("v_lshlrev_b32 v%d, %d, v%d", kVT1, s, b);
-        A.line("v_bfi_b32 v%d, s%d, v%d, v%d", b, kSMask + mi, kVT0, b);
-        A.line("v_bfi_b32 v%d, s%d, v%d, v%d", a, kSMask + mi + 1, kVT1, a);
+        P.v_op2(kVLshr, kVT0, C(s), a);
+        P.v_op2(kVLshl, kVT1, C(s), b);
+        P.v_bfi(b, kSMask + mi, V(kVT0), V(b));
+        P.v_bfi(a, kSMask + mi + 1, V(kVT1), V(a));
     };
     for (int i = 0; i < 4; ++i) swap(r[i], r[i + 4], 4, 0);
     swap(r[0], r[2], 2, 2);
@@ -115,10 +412,8 @@ void transpose8(Asm& A, const int (&r)[8]) {
     for (int i = 0; i < 8; i += 2) swap(r[i], r[i + 1], 1, 4);
 }
 
-}  // namespace
-
-std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int max_waves,
-                       int* vgprs_out) {
+// The kernel's instructions for one matrix (see the file header).
+Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int* vgprs_out) {
     const int rw = (rows + nw - 1) / nw;  // rows per wave
     Layout L;
     L.pf = pf < 1 ? 1 : pf > 4 ? 4 : pf;
@@ -141,62 +436,64 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
             }
         }
 
-    Asm A;
-    A.out += "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n";
-    A.out += "\t.globl\trs_bs_asm\n\t.p2align\t8\n\t.type\trs_bs_asm,@function\nrs_bs_asm:\n";
+    Prog P;
+    P.ins.reserve(static_cast<size_t>(cols) * (80 + 8 * rw) * static_cast<size_t>(nw) + 64);
+    const int l_stripe_done = P.new_label(".Lstripe_done");
+    const int l_idle = P.new_label(".Lidle");
+    std::vector<int> l_wave(static_cast<size_t>(nw), -1);
+    for (int w = 1; w < nw; ++w) l_wave[static_cast<size_t>(w)] = P.new_label(".Lwave" + std::to_string(w));
     // ---- prologue: stripe, lane offset, wave, masks, descriptor constants
-    A.line("s_load_dword s%d, s[%d:%d], 0x%x", kSDescIn + 2, kSKarg, kSKarg + 1,
-           static_cast<unsigned>(offsetof(AsmArgs, body)));
-    A.line("s_load_dwordx2 s[%d:%d], s[%d:%d], 0x%x", kSTmp, kSTmp + 1, kSKarg, kSKarg + 1,
-           static_cast<unsigned>(offsetof(AsmArgs, stripe_ids)));
-    A.line("s_load_dword s%d, s[%d:%d], 0x%x", kSTmp + 3, kSKarg, kSKarg + 1,
-           static_cast<unsigned>(offsetof(AsmArgs, stripe0)));
-    for (int i = 0; i < 6; ++i) A.line("s_mov_b32 s%d, 0x%08x", kSMask + i, kMasks[i]);
-    A.line("s_mov_b32 s%d, 0x20000", kSDescIn + 3);
-    A.line("s_mov_b32 s%d, 0x20000", kSDescOut + 3);
-    A.line("v_and_b32 v%d, 63, v%d", kVOff, kVTid);
-    A.line("v_lshlrev_b32 v%d, 3, v%d", kVOff, kVOff);
-    A.line("s_lshl_b32 s%d, s%d, 11", kSTmp + 2, kSWgX);
-    A.line("v_add_u32 v%d, s%d, v%d", kVOff, kSTmp + 2, kVOff);
+    P.s_load(kSDescIn + 2, 1, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, body)));
+    P.s_load(kSTmp, 2, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, stripe_ids)));
+    P.s_load(kSTmp + 3, 1, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, stripe0)));
+    for (int i = 0; i < 6; ++i) P.s_mov_lit(kSMask + i, kMasks[i], true);
+    P.s_mov_lit(kSDescIn + 3, 0x20000, false);
+    P.s_mov_lit(kSDescOut + 3, 0x20000, false);
+    P.v_op2(kVAnd, kVOff, C(63), kVTid);
+    P.v_op2(kVLshl, kVOff, C(3), kVOff);
+    P.s_op2(kLshl, kSTmp + 2, kSWgX, C(11));
+    P.v_op2(kVAdd, kVOff, kSTmp + 2, kVOff);
     // wave id = bits 6-9 of the work-item id (packed work-item ids: y / z sit
     // in bits 10-29; zero for these 1-D launches, masked anyway)
-    A.line("v_and_b32 v%d, 0x3c0, v%d", kVT0, kVTid);
-    A.line("v_lshrrev_b32 v%d, 6, v%d", kVT0, kVT0);
+    P.v_op2(kVAnd, kVT0, kLit, kVTid, 0x3c0);
+    P.v_op2(kVLshr, kVT0, C(6), kVT0);
     // a VALU write of a VGPR followed at once by v_readfirstlane of it reads
     // the OLD value (one wait state required; measured: the wave id came out
     // as 64, not 1, tools/asm_probe/wave_id.s)
-    A.line("s_nop 1");
-    A.line("v_readfirstlane_b32 s%d, v%d", kSWave, kVT0);
-    A.line("s_waitcnt lgkmcnt(0)");
-    A.line("s_mov_b32 s%d, s%d", kSDescOut + 2, kSDescIn + 2);
-    A.line("s_add_u32 s%d, s%d, s%d", kSStripe, kSWgY, kSTmp + 3);  // stripe0 + y
-    A.line("s_cmp_eq_u64 s[%d:%d], 0", kSTmp, kSTmp + 1);
-    A.line("s_cbranch_scc1 .Lstripe_done");
-    A.line("s_lshl_b32 s%d, s%d, 2", kSTmp + 2, kSStripe);
-    A.line("s_add_u32 s%d, s%d, s%d", kSTmp, kSTmp, kSTmp + 2);
-    A.line("s_addc_u32 s%d, s%d, 0", kSTmp + 1, kSTmp + 1);
-    A.line("s_load_dword s%d, s[%d:%d], 0x0", kSStripe, kSTmp, kSTmp + 1);
-    A.line("s_waitcnt lgkmcnt(0)");
-    A.label(".Lstripe_done");
-    A.line("s_nop 4");  // (v_readfirstlane -> SGPR read hazard margin)
+    P.s_nop(1);
+    P.v_readlane(kSWave, kVT0);
+    P.wait_lgkm0();
+    P.s_mov(kSDescOut + 2, kSDescIn + 2);
+    P.s_op2(kAdd, kSStripe, kSWgY, kSTmp + 3);  // stripe0 + y
+    P.s_cmp(kEq64, kSTmp, C(0));
+    P.branch(kScc1, l_stripe_done);
+    P.s_op2(kLshl, kSTmp + 2, kSStripe, C(2));
+    P.s_op2(kAdd, kSTmp, kSTmp, kSTmp + 2);
+    P.s_op2(kAddc, kSTmp + 1, kSTmp + 1, C(0));
+    P.s_load(kSStripe, 1, kSTmp, 0);
+    P.wait_lgkm0();
+    P.label(l_stripe_done);
+    P.s_nop(4);  // (v_readfirstlane -> SGPR read hazard margin)
     // wave w -> its rows' code (long jumps: a wave's straight-line code can
     // exceed the 16-bit branch range); waves without rows leave
     for (int w = 1; w < nw; ++w) {
-        const std::string tgt = w * rw < rows ? ".Lwave" + std::to_string(w) : std::string(".Lidle");
-        A.line("s_cmp_eq_u32 s%d, %d", kSWave, w);
-        A.line("s_cbranch_scc0 .Lnot%d", w);
-        A.line("s_getpc_b64 s[%d:%d]", kSTmp, kSTmp + 1);
-        A.label(".Lpc" + std::to_string(w));
-        A.line("s_add_u32 s%d, s%d, (%s-.Lpc%d)&4294967295", kSTmp, kSTmp, tgt.c_str(), w);
-        A.line("s_addc_u32 s%d, s%d, (%s-.Lpc%d)>>32", kSTmp + 1, kSTmp + 1, tgt.c_str(), w);
-        A.line("s_setpc_b64 s[%d:%d]", kSTmp, kSTmp + 1);
-        A.label(".Lnot" + std::to_string(w));
+        const int tgt = w * rw < rows ? l_wave[static_cast<size_t>(w)] : l_idle;
+        const int l_not = P.new_label(".Lnot" + std::to_string(w));
+        const int l_pc = P.new_label(".Lpc" + std::to_string(w));
+        P.s_cmp(kEq32, kSWave, C(w));
+        P.branch(kScc0, l_not);
+        P.s_getpc(kSTmp);
+        P.label(l_pc);
+        P.add_pcrel(kLo, kSTmp, tgt, l_pc);
+        P.add_pcrel(kHi, kSTmp + 1, tgt, l_pc);
+        P.s_setpc(kSTmp);
+        P.label(l_not);
     }
 
     for (int w = 0; w < nw; ++w) {
         const int r0 = w * rw, nr = std::min(rw, rows - r0);
         if (nr <= 0) break;
-        if (w) A.label(".Lwave" + std::to_string(w));
+        if (w) P.label(l_wave[static_cast<size_t>(w)]);
         // per-wave VMEM queue: ids of issued ops, in order (vmcnt bookkeeping)
         std::vector<int> vq;
         int next_id = 0;
@@ -208,7 +505,7 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
                 if (x == id) found = true;
             }
             if (!found) return;
-            A.line("s_waitcnt vmcnt(%d)", after > 63 ? 63 : after);
+            P.wait_vm(after > 63 ? 63 : after);
             // everything issued up to and including `id` is done
             std::vector<int> rest;
             bool keep = false;
@@ -221,21 +518,19 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
         // scalar staging of vector v's (ptr, stride16) into stage slot `st`
         auto stage = [&](int v, int st) {
             const int s = kSStage + 4 * st;
-            A.line("s_load_dwordx2 s[%d:%d], s[%d:%d], 0x%x", s, s + 1, kSKarg, kSKarg + 1,
-                   static_cast<unsigned>(offsetof(AsmArgs, ptr) + 8 * v));
-            A.line("s_load_dword s%d, s[%d:%d], 0x%x", s + 2, kSKarg, kSKarg + 1,
-                   static_cast<unsigned>(offsetof(AsmArgs, stride16) + 4 * v));
+            P.s_load(s, 2, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, ptr) + 8 * v));
+            P.s_load(s + 2, 1, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, stride16) + 4 * v));
         };
         // descriptor base = ptr + stripe * stride16 * 16, from stage slot `st`
         auto desc = [&](int st, int d) {
             const int s = kSStage + 4 * st;
-            A.line("s_waitcnt lgkmcnt(0)");
-            A.line("s_mul_i32 s%d, s%d, s%d", kSTmp, kSStripe, s + 2);
-            A.line("s_mul_hi_u32 s%d, s%d, s%d", kSTmp + 1, kSStripe, s + 2);
-            A.line("s_lshl_b64 s[%d:%d], s[%d:%d], 4", kSTmp, kSTmp + 1, kSTmp, kSTmp + 1);
-            A.line("s_add_u32 s%d, s%d, s%d", d, s, kSTmp);
-            A.line("s_addc_u32 s%d, s%d, s%d", d + 1, s + 1, kSTmp + 1);
-            A.line("s_and_b32 s%d, s%d, 0xffff", d + 1, d + 1);
+            P.wait_lgkm0();
+            P.s_op2(kMul, kSTmp, kSStripe, s + 2);
+            P.s_op2(kMulhi, kSTmp + 1, kSStripe, s + 2);
+            P.s_op2(kLshl64, kSTmp, kSTmp, C(4));
+            P.s_op2(kAdd, d, s, kSTmp);
+            P.s_op2(kAddc, d + 1, s + 1, kSTmp + 1);
+            P.s_op2(kAnd, d + 1, d + 1, kLit, 0xffff);
         };
         auto slot_reg = [&](int c, int j) { return kVSlots + 8 * (c % L.pf) + j; };
         std::vector<int> col_id(static_cast<size_t>(cols), -1);  // last VMEM op of each column's loads
@@ -243,16 +538,12 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
         // workgroup read the same lines, so those loads keep them cached for
         // the other waves (measured with nt: 64+64 Encode fetched 1.45x its
         // input bytes from HBM, 128+128 2.8x; profiles/r03/pmc_traffic_*.json)
-        const char* in_aux = nw > 1 ? "" : " nt";
+        const bool in_nt = nw == 1;
         auto issue_col = [&](int c) {  // stage(c) was issued into slot c & 1
             desc(c & 1, kSDescIn);
             if (c + 1 < cols) stage(c + 1, (c + 1) & 1);
             for (int k = 0; k < 4; ++k) {
-                const int v = slot_reg(c, 2 * k);
-                if (k) A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen offset:%d%s", v, v + 1, kVOff,
-                              kSDescIn, kSDescIn + 3, 512 * k, in_aux);
-                else A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen%s", v, v + 1, kVOff, kSDescIn,
-                            kSDescIn + 3, in_aux);
+                P.buf_load2(slot_reg(c, 2 * k), kVOff, kSDescIn, 512 * k, in_nt);
                 vq.push_back(next_id);
                 col_id[static_cast<size_t>(c)] = next_id++;
             }
@@ -265,14 +556,14 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
             vmem_wait_for(col_id[static_cast<size_t>(c)]);
             int pr[8];
             for (int j = 0; j < 8; ++j) pr[j] = slot_reg(c, j);
-            transpose8(A, pr);
+            transpose8(P, pr);
             // subsets of each half used by this column's rows
-            std::string name[2][16];
+            int reg[2][16];
             for (int half = 0; half < 2; ++half) {
                 bool have[16] = {}, used[16] = {}, need[16] = {};
                 for (int b = 0; b < 4; ++b) {
                     have[1 << b] = true;
-                    name[half][1 << b] = "v" + std::to_string(pr[4 * half + b]);
+                    reg[half][1 << b] = pr[4 * half + b];
                 }
                 for (int r = r0; r < r0 + nr; ++r)
                     for (int i = 0; i < 8; ++i)
@@ -286,33 +577,33 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
                         if (!need[m] || __builtin_popcount(m) != pc) continue;
                         const int low = m & -m, rest = m ^ low;
                         const int dst = sub_reg(half, m);
-                        A.line("v_xor_b32 v%d, %s, %s", dst, name[half][rest].c_str(), name[half][low].c_str());
-                        name[half][m] = "v" + std::to_string(dst);
+                        P.v_op2(kVXor, dst, V(reg[half][rest]), reg[half][low]);
+                        reg[half][m] = dst;
                         have[m] = true;
                     }
             }
             for (int r = r0; r < r0 + nr; ++r)
                 for (int i = 0; i < 8; ++i) {
                     const int m = mask[(static_cast<size_t>(c) * rows + r) * 8 + i];
-                    const std::string* t[2];
+                    int t[2];
                     int nt = 0;
-                    if (m & 15) t[nt++] = &name[0][m & 15];
-                    if (m >> 4) t[nt++] = &name[1][m >> 4];
+                    if (m & 15) t[nt++] = reg[0][m & 15];
+                    if (m >> 4) t[nt++] = reg[1][m >> 4];
                     const int a = acc_reg(r - r0, i);
                     if (c == 0) {
-                        if (nt == 0) A.line("v_mov_b32 v%d, 0", a);
-                        else if (nt == 1) A.line("v_mov_b32 v%d, %s", a, t[0]->c_str());
-                        else A.line("v_xor_b32 v%d, %s, %s", a, t[0]->c_str(), t[1]->c_str());
+                        if (nt == 0) P.v_mov(a, C(0));
+                        else if (nt == 1) P.v_mov(a, V(t[0]));
+                        else P.v_op2(kVXor, a, V(t[0]), t[1]);
                     } else if (nt == 2) {
-                        A.line("v_bitop3_b32 v%d, v%d, %s, %s bitop3:0x96", a, a, t[0]->c_str(), t[1]->c_str());
+                        P.v_xor3(a, a, t[0], t[1]);
                     } else if (nt == 1) {
-                        A.line("v_xor_b32 v%d, v%d, %s", a, a, t[0]->c_str());
+                        P.v_op2(kVXor, a, V(a), t[0]);
                     }
                 }
             if (c + L.pf < cols) issue_col(c + L.pf);  // the slot is free again
             // keep the waves within `sync` columns of each other, so the lines
             // the first wave fetched are still cached when the others load them
-            if (nw > 1 && sync > 0 && (c + 1) % sync == 0 && c + 1 < cols) A.line("s_barrier");
+            if (nw > 1 && sync > 0 && (c + 1) % sync == 0 && c + 1 < cols) P.s_barrier();
         }
         // ---- outputs: transpose back, (accumulate: XOR the old bytes), store
         int ostage = 0;
@@ -321,11 +612,7 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
         auto old_reg = [&](int r, int j) { return kVSlots + 8 * (r % 2) + j; };  // pf >= 1: 8 regs; 2 rows need 16
         auto issue_old = [&](int r) {  // descriptor of row r is in kSDescOut
             for (int k = 0; k < 4; ++k) {
-                const int v = old_reg(r, 2 * k);
-                if (k) A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen offset:%d", v, v + 1, kVOff,
-                              kSDescOut, kSDescOut + 3, 512 * k);
-                else A.line("buffer_load_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen", v, v + 1, kVOff, kSDescOut,
-                            kSDescOut + 3);
+                P.buf_load2(old_reg(r, 2 * k), kVOff, kSDescOut, 512 * k, false);
                 vq.push_back(next_id);
                 old_id[static_cast<size_t>(r)] = next_id++;
             }
@@ -340,30 +627,36 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
             for (int j = 0; j < 8; ++j) pr[j] = acc_reg(r, j);
             if (acc) {
                 issue_old(r);
-                transpose8(A, pr);
+                transpose8(P, pr);
                 vmem_wait_for(old_id[static_cast<size_t>(r)]);
-                for (int j = 0; j < 8; ++j) A.line("v_xor_b32 v%d, v%d, v%d", pr[j], pr[j], old_reg(r, j));
+                for (int j = 0; j < 8; ++j) P.v_op2(kVXor, pr[j], V(pr[j]), old_reg(r, j));
             } else {
-                transpose8(A, pr);
+                transpose8(P, pr);
             }
             for (int k = 0; k < 4; ++k) {
-                if (k) A.line("buffer_store_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen offset:%d nt", pr[2 * k],
-                              pr[2 * k + 1], kVOff, kSDescOut, kSDescOut + 3, 512 * k);
-                else A.line("buffer_store_dwordx2 v[%d:%d], v%d, s[%d:%d], 0 offen nt", pr[0], pr[1], kVOff,
-                            kSDescOut, kSDescOut + 3);
+                P.buf_store2(pr[2 * k], kVOff, kSDescOut, 512 * k);
                 vq.push_back(next_id++);
             }
         }
-        A.line("s_endpgm");
+        P.s_endpgm();
     }
-    A.label(".Lidle");
-    A.line("s_endpgm");
-    A.out += ".Lfunc_end0:\n\t.size\trs_bs_asm, .Lfunc_end0-rs_bs_asm\n";
-    // ---- kernel descriptor and metadata (code object v6)
-    int accum = (L.vgprs + 3) / 4 * 4;
-    // occupancy cap: 512 VGPRs per SIMD lane, allocated in granules of 8
+    P.label(l_idle);
+    P.s_endpgm();
+    return P;
+}
+
+// VGPRs the kernel declares: what it uses, or more for the occupancy cap
+// (512 VGPRs per SIMD lane, allocated in granules of 8).
+int declared_vgprs(int used, int max_waves) {
+    int accum = (used + 3) / 4 * 4;
     if (max_waves > 1 && max_waves <= 8) accum = std::max(accum, std::min(256, 512 / max_waves / 8 * 8));
+    return accum;
+}
+
+// Kernel descriptor and metadata (code object v6) of a kernel named rs_bs_asm.
+std::string descriptor(int nw, int accum) {
     char kd[2048];
+    std::string s;
     std::snprintf(kd, sizeof kd,
                   "\t.rodata\n\t.p2align\t6\n\t.amdhsa_kernel rs_bs_asm\n"
                   "\t\t.amdhsa_group_segment_fixed_size 0\n\t\t.amdhsa_private_segment_fixed_size 0\n"
@@ -375,7 +668,7 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
                   "\t\t.amdhsa_reserve_vcc 0\n\t\t.amdhsa_ieee_mode 1\n\t\t.amdhsa_dx10_clamp 1\n"
                   "\t.end_amdhsa_kernel\n",
                   sizeof(AsmArgs), accum, kSgprs, accum);
-    A.out += kd;
+    s += kd;
     std::snprintf(kd, sizeof kd,
                   "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: 0\n    .args:\n"
                   "      - .offset: 0\n        .size: %zu\n        .value_kind: by_value\n"
@@ -387,8 +680,128 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw,
                   "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n"
                   "\t.end_amdgpu_metadata\n",
                   sizeof(AsmArgs), sizeof(AsmArgs), 64 * nw, kSgprs + 6, accum);
-    A.out += kd;
-    return A.out;
+    s += kd;
+    return s;
+}
+
+const char* const kHeader =
+    "\t.amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n\t.amdhsa_code_object_version 6\n\t.text\n"
+    "\t.globl\trs_bs_asm\n\t.p2align\t8\n\t.type\trs_bs_asm,@function\nrs_bs_asm:\n";
+const char* const kTrailer = ".Lfunc_end0:\n\t.size\trs_bs_asm, .Lfunc_end0-rs_bs_asm\n";
+
+// ---------------------------------------------------------------- ELF
+
+struct Elf64Ehdr {
+    unsigned char ident[16];
+    uint16_t type, machine;
+    uint32_t version;
+    uint64_t entry, phoff, shoff;
+    uint32_t flags;
+    uint16_t ehsize, phentsize, phnum, shentsize, shnum, shstrndx;
+};
+struct Elf64Shdr {
+    uint32_t name, type;
+    uint64_t flags, addr, offset, size;
+    uint32_t link, info;
+    uint64_t addralign, entsize;
+};
+
+// File offset and size of the section named `want` in an ELF64 image.
+bool elf_section(const std::vector<char>& elf, const char* want, size_t* off, size_t* size) {
+    if (elf.size() < sizeof(Elf64Ehdr) || std::memcmp(elf.data(), "\x7f" "ELF", 4) != 0 || elf[4] != 2) return false;
+    Elf64Ehdr eh;
+    std::memcpy(&eh, elf.data(), sizeof eh);
+    if (eh.shentsize != sizeof(Elf64Shdr) || eh.shstrndx >= eh.shnum ||
+        eh.shoff + static_cast<uint64_t>(eh.shnum) * sizeof(Elf64Shdr) > elf.size())
+        return false;
+    auto sh = [&](int i) {
+        Elf64Shdr s;
+        std::memcpy(&s, elf.data() + eh.shoff + static_cast<size_t>(i) * sizeof(Elf64Shdr), sizeof s);
+        return s;
+    };
+    const Elf64Shdr strs = sh(eh.shstrndx);
+    for (int i = 0; i < eh.shnum; ++i) {
+        const Elf64Shdr s = sh(i);
+        if (strs.offset + s.name + std::strlen(want) + 1 > elf.size()) continue;
+        if (std::strcmp(elf.data() + strs.offset + s.name, want) == 0) {
+            if (s.offset + s.size > elf.size()) return false;
+            *off = s.offset;
+            *size = s.size;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Code-object templates: the kernel descriptor and metadata for (waves per
+// workgroup, declared VGPRs) and a .text of `bytes` filled with s_endpgm,
+// assembled by comgr once per process and shape.
+struct Template {
+    std::vector<char> elf;
+    size_t text_off = 0, text_size = 0;
+};
+std::mutex g_tmpl_mu;
+std::map<std::tuple<int, int, size_t>, Template>& templates() {
+    static auto* m = new std::map<std::tuple<int, int, size_t>, Template>;
+    return *m;
+}
+
+}  // namespace
+
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int max_waves,
+                       int* vgprs_out) {
+    int used = 0;
+    const Prog P = generate(mat, rows, cols, acc, nw, pf, sync, &used);
+    if (vgprs_out) *vgprs_out = used;
+    return kHeader + print(P) + kTrailer + descriptor(nw, declared_vgprs(used, max_waves));
+}
+
+bool asm_binary(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, std::vector<uint32_t>* code,
+                int* vgprs_out, std::string* err) {
+    int used = 0;
+    const Prog P = generate(mat, rows, cols, acc, nw, pf, sync, &used);
+    if (vgprs_out) *vgprs_out = used;
+    return encode(P, code, err);
+}
+
+bool asm_text_section(const std::vector<char>& elf, std::vector<char>* text) {
+    size_t off = 0, size = 0;
+    if (!elf_section(elf, ".text", &off, &size)) return false;
+    text->assign(elf.begin() + static_cast<long>(off), elf.begin() + static_cast<long>(off + size));
+    return true;
+}
+
+bool asm_link_binary(const std::vector<uint32_t>& code, int nw, int vgprs_used, int max_waves, std::vector<char>* elf,
+                     std::string* log, double* ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t need = code.size() * 4;
+    size_t cls = size_t{16} << 10;
+    while (cls < need) cls <<= 1;
+    const int accum = declared_vgprs(vgprs_used, max_waves);
+    const Template* t = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_tmpl_mu);
+        auto key = std::make_tuple(nw, accum, cls);
+        auto it = templates().find(key);
+        if (it == templates().end()) {
+            std::string src = kHeader;
+            src += "\t.fill " + std::to_string(cls / 4) + ", 4, 0xbf810000\n";  // s_endpgm
+            src += kTrailer + descriptor(nw, accum);
+            Template nt;
+            double ams = 0;
+            if (!asm_assemble(src, &nt.elf, log, &ams) || !elf_section(nt.elf, ".text", &nt.text_off, &nt.text_size) ||
+                nt.text_size < cls) {
+                if (log && log->empty()) *log = "code-object template: no .text of the expected size";
+                return false;
+            }
+            it = templates().emplace(key, std::move(nt)).first;
+        }
+        t = &it->second;  // (entries are never erased)
+    }
+    *elf = t->elf;
+    std::memcpy(elf->data() + t->text_off, code.data(), need);
+    if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return true;
 }
 
 // Assemble and link through comgr: relocatable, then executable code object.
@@ -409,7 +822,7 @@ bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* 
     ok = ok && amd_comgr_action_info_set_logging(info, true) == AMD_COMGR_STATUS_SUCCESS;
     auto collect_log = [&](amd_comgr_data_set_t set) {
         size_t n = 0;
-        if (amd_comgr_action_data_count(set, AMD_COMGR_DATA_KIND_LOG, &n) != AMD_COMGR_STATUS_SUCCESS) return;
+        if (!log || amd_comgr_action_data_count(set, AMD_COMGR_DATA_KIND_LOG, &n) != AMD_COMGR_STATUS_SUCCESS) return;
         for (size_t i = 0; i < n; ++i) {
             amd_comgr_data_t lg;
             if (amd_comgr_action_data_get_data(set, AMD_COMGR_DATA_KIND_LOG, i, &lg) != AMD_COMGR_STATUS_SUCCESS)

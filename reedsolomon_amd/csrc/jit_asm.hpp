@@ -4,6 +4,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "kernels.hpp"
@@ -41,5 +42,18 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, 
                        int max_waves, int* vgprs);
 // Assemble + link (comgr) into a code object; false with the log on failure.
 bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* log, double* ms);
+// The same kernel as asm_source, encoded directly as gfx950 machine code (no
+// assembler): the bytes of its .text.  false (with *err) if an operand does
+// not fit its encoding.
+bool asm_binary(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int sync,
+                std::vector<uint32_t>* code, int* vgprs_used, std::string* err);
+// A code object for machine code from asm_binary: a template (kernel
+// descriptor and metadata for nw waves per workgroup and the declared VGPRs,
+// .text of the next size class) assembled once per process and shape, with
+// the code copied into its .text.
+bool asm_link_binary(const std::vector<uint32_t>& code, int nw, int vgprs_used, int max_waves, std::vector<char>* elf,
+                     std::string* log, double* ms);
+// The .text section of a code object (tests: encoder vs assembler).
+bool asm_text_section(const std::vector<char>& elf, std::vector<char>* text);
 
 }  // namespace rsamd

@@ -615,6 +615,16 @@ def jit_compile_check(mat, accumulate: bool = False) -> float:
     return ms.value
 
 
+def jit_encoder_check(mat, accumulate: bool = False) -> int:
+    """The run-time kernel's directly encoded machine code equals comgr's
+    assembly of its text (rs_jit_encoder_check); returns the code size in
+    bytes, raises ErrDevice on a difference."""
+    m = np.ascontiguousarray(mat, dtype=np.uint8)
+    n = ctypes.c_size_t(0)
+    _check(lib().rs_jit_encoder_check(m.ctypes.data, m.shape[0], m.shape[1], int(bool(accumulate)), ctypes.byref(n)))
+    return int(n.value)
+
+
 def gf_mul(a: int, b: int) -> int:
     return int(lib().rs_gf_mul(a, b))
 

@@ -341,9 +341,10 @@ def test_multi_pattern_mask_validation_wide(rslib):
 
 
 def test_jit_compile_check(rslib, orc):
-    """The run-time bit-sliced kernel generators produce code that assembles
-    (jit_asm.cpp, comgr; the default backend) or compiles (jit.cpp, hiprtc)
-    for gfx950 with no device: a Reconst-of-8 matrix of 10+8 (overwrite) and
+    """The run-time bit-sliced kernel generators produce code objects for
+    gfx950 with no device - machine code in a template (jit_asm.cpp, the
+    default backend), assembly through comgr, or C++ through hiprtc (jit.cpp):
+    a Reconst-of-8 matrix of 10+8 (overwrite) and
     a 16-column 5-row XOR-accumulate product, plus a 64 x 64 product for the
     assembly backend; shapes outside each backend's bounds are refused
     (assembly: 1-128 rows, 1-256 columns; hiprtc: 5-16 rows, 1-64 columns;
@@ -358,7 +359,8 @@ def test_jit_compile_check(rslib, orc):
     m = r.reconst_matrix(survived, list(range(8))).reshape(8, 10)  # rows of the inverse for data 0..7
     rng = np.random.default_rng(3)
     try:
-        for backend, bad, extra in ((1, [(129, 10), (8, 257)], [(64, 64)]), (0, [(17, 10), (8, 65)], [])):
+        for backend, bad, extra in ((2, [(129, 10), (8, 257)], [(64, 64), (128, 128)]),
+                                    (1, [(129, 10), (8, 257)], [(64, 64)]), (0, [(17, 10), (8, 65)], [])):
             assert L.rs_tune(b"jit_backend", backend) == 0
             assert rslib.jit_compile_check(m) > 0
             assert rslib.jit_compile_check(rng.integers(0, 256, (5, 16), dtype=np.uint8), accumulate=True) > 0
@@ -371,7 +373,7 @@ def test_jit_compile_check(rslib, orc):
                 with pytest.raises(ErrInvalidArgument):  # rs_jit_prepare checks the shape before any device work
                     r.jit_prepare(np.ones(shape, np.uint8))
     finally:
-        L.rs_tune(b"jit_backend", 1)
+        L.rs_tune(b"jit_backend", 2)
 
 
 

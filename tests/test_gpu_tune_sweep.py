@@ -65,7 +65,7 @@ SWEEP = {
     "jit_sync": [1, 4, 0],
     "jit_waves": [0, 4, 2],
     "jit_disk_cache": [0, 1],
-    "jit_backend": [0, 1],
+    "jit_backend": [0, 1, 2],
     "table_registry_max": [1, 1 << 14],
 }
 

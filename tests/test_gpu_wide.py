@@ -195,7 +195,7 @@ def test_wide_matches_row_groups(rslib, torch_dev, no_jit):
 @pytest.fixture
 def asm_jit(rslib):
     L = rslib.lib()
-    assert L.rs_tune(b"jit", 2) == 0 and L.rs_tune(b"jit_backend", 1) == 0
+    assert L.rs_tune(b"jit", 2) == 0 and L.rs_tune(b"jit_backend", 2) == 0
     yield L
     L.rs_tune(b"jit", 1)
 

@@ -95,3 +95,25 @@ def test_asm_kernel_occupancy_cap(rslib, waves, vgprs):
         assert declared < 128  # 5 rows x 8 planes + slots + subsets
     else:
         assert declared == vgprs
+
+
+@pytest.mark.parametrize("rows,cols,acc,pf,sync", [(5, 10, 0, 3, 0), (8, 10, 1, 3, 0), (3, 7, 0, 1, 0),
+                                                   (16, 16, 0, 4, 0), (12, 5, 1, 2, 0), (33, 3, 1, 3, 0),
+                                                   (17, 5, 0, 3, 1), (40, 9, 0, 3, 4), (9, 1, 0, 3, 0),
+                                                   (64, 64, 0, 3, 0), (56, 200, 1, 3, 0), (128, 128, 0, 3, 0),
+                                                   (128, 256, 1, 2, 0)])
+def test_machine_code_equals_assembler(rslib, rows, cols, acc, pf, sync):
+    """The default backend encodes the kernel straight into gfx950 machine
+    code (no assembler at run time); those bytes equal comgr's assembly of the
+    generator's text for the same matrix and settings, instruction for
+    instruction (rs_jit_encoder_check), so the emulator runs above and the GPU
+    tests of the assembly path cover the machine code too."""
+    L = rslib.lib()
+    mat = np.random.default_rng(rows * 31 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
+    assert L.rs_tune(b"jit_pf", pf) == 0 and L.rs_tune(b"jit_sync", sync) == 0
+    try:
+        n = rslib.jit_encoder_check(mat, bool(acc))
+    finally:
+        L.rs_tune(b"jit_pf", 3)
+        L.rs_tune(b"jit_sync", 0)
+    assert n > 0 and n % 4 == 0
