@@ -366,7 +366,52 @@ def prewarm(step, stream, min_launches: int, max_launches: int, window: int = 20
             if time.perf_counter() - t0 > max_seconds:
                 break
     last_mean = sum(durs[-window:]) / min(window, len(durs)) if durs else None
-    return n, (time.perf_counter() - t0) * 1e3, last_mean, converged
+    return n, (time.perf_counter() - t0) * 1e3, last_mean, converged, durs
+
+
+def spread(ms) -> dict | None:
+    """min / median / p90 / max / mean of launch times (ms), so a box whose
+    clocks never settle can be told from a slower kernel."""
+    if not ms:
+        return None
+    x = sorted(ms)
+    n = len(x)
+
+    def q(f):
+        return x[min(n - 1, int(round(f * (n - 1))))]
+
+    return {"n": n, "min_ms": round(x[0], 4), "median_ms": round(q(0.5), 4), "p90_ms": round(q(0.9), 4),
+            "max_ms": round(x[-1], 4), "mean_ms": round(sum(x) / n, 4)}
+
+
+def prewarm_summary(n, ms, last_mean, converged, durs, min_launches) -> dict:
+    """The line's `prewarm` object: what the pre-warm ran and the spread of
+    its last 100 launch times."""
+    return {"launches": n, "ms": round(ms, 1), "converged": converged,
+            "last20_mean_ms": round(last_mean, 4) if last_mean else None,
+            "last100": spread(durs[-100:]),
+            "rule": f"untimed launches (>= {min_launches}) until 20 consecutive agree within 3 % "
+                    "and their mean within 0.5 % of the 20 before; the counted warm-up is queued "
+                    "behind them with no idle gap; last100 = spread of the last 100 pre-warm launches "
+                    "(HIP events per launch)"}
+
+
+def launch_spread(step, stream, n: int):
+    """Per-launch times of n launches queued right behind the timed region
+    (GPU warm, no idle gap), each bracketed by HIP events on the launch
+    stream: the spread of the steady state the timed window averages (events
+    inside the timed window itself would add gaps between its kernels)."""
+    import torch
+
+    evs = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step(0)
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in evs]
 
 
 def cold_launches(step, stream, nbytes: int, max_over, idle_s: float = 0.1, n: int = 50):
@@ -425,14 +470,24 @@ def rehearse_cpu(args, world: int, rank: int) -> dict | None:
     def step(_i):
         np.bitwise_xor.reduce(buf[:, :10], axis=1)
 
-    for _ in range(args.warmup):
-        step(0)
+    def host_times(n):  # (the pre-warm's and the spread pass's per-launch times, on the host clock)
+        out = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            step(0)
+            out.append((time.perf_counter() - t0) * 1e3)
+        return out
+
+    pw = host_times(max(args.warmup, 3))
     el = timed_region(step, args.steps, barrier, lambda: None, max_over)
+    after = spread(host_times(max(args.steps, 20)))
     out = None
     if rank == 0:
         out = {"metric": "REHEARSAL (no GPU, no kernel)", "value": None, "n_gpus": world, "ranks_seen": ranks_seen,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
-               "data": "rehearsal: numpy XOR stand-in, not a measurement"}
+               "data": "rehearsal: numpy XOR stand-in, not a measurement",
+               "prewarm": prewarm_summary(len(pw), sum(pw), sum(pw[-20:]) / len(pw[-20:]), True, pw, 0),
+               "timed_spread": after}
         print(json.dumps(out), flush=True)
     if pg is not None:
         pg.barrier()
@@ -557,7 +612,7 @@ def main(argv=None):
 
     # Pre-warm until launch times settle, then the counted warm-up and the
     # timed region follow back to back (no idle gap, no per-launch events).
-    pw_n, pw_ms, pw_mean, pw_ok = prewarm(step, stream, args.prewarm_min, args.prewarm_max)
+    pw_n, pw_ms, pw_mean, pw_ok, pw_durs = prewarm(step, stream, args.prewarm_min, args.prewarm_max)
     for _ in range(args.warmup):
         step(0)
     torch.cuda.synchronize(dev)
@@ -578,6 +633,7 @@ def main(argv=None):
 
     bytes_per_step_rank = S * (k + m) * vec
     value = throughput(bytes_per_step_rank, n_gpus, args.steps, elapsed)
+    after = spread(launch_spread(step, stream, max(args.steps, 20)))
     cold = cold_launches(step, stream, bytes_per_step_rank, max_over) if args.cold else None
 
     e2e = None
@@ -625,11 +681,10 @@ def main(argv=None):
                 "kernel_ms_mean": round(kern_mean_s * 1e3, 4),
                 "kernel_timing": "HIP event pair on the launch stream around the K timed launches / K",
             },
-            "prewarm": {"launches": pw_n, "ms": round(pw_ms, 1), "converged": pw_ok,
-                        "last20_mean_ms": round(pw_mean, 4) if pw_mean else None,
-                        "rule": f"untimed launches (>= {args.prewarm_min}) until 20 consecutive agree within 3 % "
-                                "and their mean within 0.5 % of the 20 before; the counted warm-up is queued "
-                                "behind them with no idle gap"},
+            "prewarm": prewarm_summary(pw_n, pw_ms, pw_mean, pw_ok, pw_durs, args.prewarm_min),
+            "timed_spread": dict(after or {}, rule="rank 0: per-launch HIP-event times of max(K, 20) launches "
+                                 "queued right behind the timed region (same steady state; the timed window "
+                                 "itself has one event pair, no per-launch events)"),
         }
         result["cold"] = cold
         result["end_to_end"] = e2e

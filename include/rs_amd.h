@@ -493,6 +493,11 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * workgroup meet at a barrier every n columns, 0 = never; default 0),
  * "jit_waves" (assembly kernels hold at most n waves per SIMD, 2..8, by
  * declaring more registers; 0 = as many as fit; default 2),
+ * "jit_layout" (generated kernels of more than 16 rows: 0 default = the
+ * rows over the waves of a workgroup, all on the same 2 KiB chunk | 1 = row
+ * groups of up to 16 rows over workgroups whose waves take consecutive
+ * chunks with the same code, the row groups of a chunk on one XCD),
+ * "jit_group_waves" (layout 1: waves per workgroup, 1..8; default 4),
  * "jit_backend" (2 default: kernels generated as gfx950 machine code and
  * copied into a code-object template, up to 128 output rows x 256 columns |
  * 1: the same kernels as assembly text assembled by comgr, 12 ms - 1.7 s per

@@ -59,6 +59,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -85,6 +86,16 @@ int g_jit_waves = [] {
     const char* e = std::getenv("RSAMD_JIT_WAVES");
     return e ? std::atoi(e) : 2;
 }();
+// rs_tune("jit_layout", 0 | 1) / ("jit_group_waves", 1..8): how generated
+// kernels of more than 16 rows split their work (AsmShape, jit_asm.hpp):
+// rows over the waves of a workgroup (0) or row groups over workgroups whose
+// waves take consecutive chunks with the same code (1, group_waves waves)
+int g_jit_layout = [] {
+    const char* e = std::getenv("RSAMD_JIT_LAYOUT");
+    return e ? (std::atoi(e) == 1 ? 1 : 0) : 0;
+}();
+int g_jit_group_waves = 4;
+AsmShape jit_shape(int rows) { return asm_shape(rows, g_jit_layout, g_jit_group_waves); }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // rs_tune("jit_backend", 2 | 1 | 0): machine code encoded directly into a
 // code-object template (jit_asm.cpp) | the same kernel as assembly text
@@ -463,15 +474,15 @@ Compiled compile_asm(const std::string& src) {
     return out;
 }
 
-Compiled compile_binary_shape(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync,
-                              int waves) {
+Compiled compile_binary_shape(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& sh, int pf,
+                              int sync, int waves) {
     Compiled out;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint32_t> code;
     int used = 0;
-    if (!asm_binary(mat, rows, cols, acc, nw, pf, sync, &code, &used, &out.log)) return out;
+    if (!asm_binary(mat, rows, cols, acc, sh, pf, sync, &code, &used, &out.log)) return out;
     double lms = 0;
-    out.ok = asm_link_binary(code, nw, used, waves, &out.code, &out.log, &lms);
+    out.ok = asm_link_binary(code, sh.nw, used, waves, &out.code, &out.log, &lms);
     out.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return out;
 }
@@ -536,12 +547,15 @@ struct Entry {
     enum State { kQueued, kCompiling, kReady, kLoaded, kFailed } state = kQueued;
     bool is_asm = false;  // generated kernel (rs_bs_asm) or hiprtc C++ (rs_bs_jit_64 / _256)
     int nw = 1;           // generated kernels: waves per workgroup
+    AsmShape shape;       // ... and how they split the work
     int backend = 1;
     std::string src;      // backends 1 (assembly) and 0 (C++)
     // backend 2 (machine code): the matrix and the generator's settings
     std::vector<uint8_t> mat;
     int rows = 0, cols = 0, pf = 3, sync = 0, waves = 2;
     bool acc = false;
+    int dev = 0;
+    uint64_t last_use = 0;  // (eviction: least recently looked up first)
     DiskKey disk;  // on-disk cache key (text empty: the disk cache is off)
     std::vector<char> code;
     hipModule_t module = nullptr;
@@ -549,14 +563,35 @@ struct Entry {
 };
 
 Compiled compile_binary(const Entry& e) {
-    return compile_binary_shape(e.mat.data(), e.rows, e.cols, e.acc, e.nw, e.pf, e.sync, e.waves);
+    return compile_binary_shape(e.mat.data(), e.rows, e.cols, e.acc, e.shape, e.pf, e.sync, e.waves);
 }
 
-constexpr size_t kMaxEntries = 256;
+constexpr size_t kMaxEntries = 256;  // compiled matrices per process; the older half is evicted beyond
+
+// Backend 2 in the default mode compiles a matrix on the launching thread
+// once the time its launches are estimated to have lost on the table kernels
+// exceeds the estimated time to generate and load its kernel, so a one-off
+// pattern large enough to pay for its kernel gets it on its FIRST launch, and
+// a small one only once it recurs.  First sight to loaded, measured on MI355X
+// (tools/jit_compile_probe.py, profiles/r04/jit_compile_probe.log): 0.17-0.26
+// ms up to 16 x 20, 0.64 ms at 28 x 100, 0.76-0.94 ms at 64 x 64, 2.2 ms at
+// 56 x 200, 2.6-3.0 ms at 128 x 128.
+double est_compile_us(int rows, int cols) { return 150.0 + 0.15 * rows * cols; }
+// Microseconds per byte moved that a product with `rows` outputs loses on the
+// table kernels: those run 5-8 rows at ~5 TB/s (VALU-bound) and more rows on
+// the single-pass wide kernel at ~3.4 TB/s for 16 rows, falling about as
+// 1 / rows beyond; compiled kernels run ~6 TB/s up to 32 rows, 2.4 at 64 and
+// 1.3 at 128.
+double lost_us_per_byte(int rows) {
+    const double fb = rows <= 8 ? 5.0 : std::min(5.0, 3.4 * 16.0 / rows);  // TB/s = 1e6 bytes per us
+    const double jt = rows <= 32 ? 6.0 : 6.0 * 32.0 / rows;
+    return std::max(0.0, 1.0 / fb - 1.0 / jt) * 1e-6;
+}
 constexpr size_t kMaxSeen = 4096;  // matrices counted but not compiled yet (cleared when full)
 
 struct Seen {
     uint64_t launches = 0, bytes = 0;
+    double lost_us = 0;  // backend 2: time its launches are estimated to have lost on the table kernels
     bool disk_checked = false;  // no code object on disk for it at first sight
 };
 
@@ -570,7 +605,7 @@ struct Jit {
     std::deque<std::shared_ptr<Entry>> queue;
     std::thread worker;
     bool stop = false;
-    uint64_t compiled = 0, failed = 0;
+    uint64_t compiled = 0, failed = 0, evictions = 0;
     double compile_ms = 0;
     std::atomic<uint64_t> launches{0};
 
@@ -618,7 +653,13 @@ struct Jit {
     }
 
     pid_t owner = 0;  // the process that started the worker
+    uint64_t use_clock = 0;
+    std::atomic<bool> evict_wanted{false};
 };
+
+// Launches hold this shared from the lookup of a compiled kernel until it is
+// enqueued; eviction holds it exclusively, drains the devices and unloads.
+std::shared_mutex g_evict_mu;
 
 // Never destroyed (a std::thread destructor on a joinable thread aborts, and a
 // forked child inherits the object but not the thread); the process that
@@ -665,9 +706,9 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
     if (!mat || rows < 1 || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
     Compiled c =
-        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync,
+        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, jit_shape(rows), g_jit_pf, g_jit_sync,
                                                   g_jit_waves)
-        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync,
+        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, jit_shape(rows), g_jit_pf, g_jit_sync,
                                                     g_jit_waves, nullptr))
                            : compile(jit_source(mat, rows, cols, accumulate));
     if (ms) *ms = c.ms;
@@ -677,15 +718,15 @@ int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, d
 
 int jit_encoder_check(const uint8_t* mat, int rows, int cols, bool accumulate, size_t* code_bytes) {
     if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
-    const int nw = asm_waves(rows);
+    const AsmShape sh = jit_shape(rows);
     std::vector<uint32_t> bin;
     int used = 0;
     std::string err;
-    if (!asm_binary(mat, rows, cols, accumulate, nw, g_jit_pf, g_jit_sync, &bin, &used, &err)) {
+    if (!asm_binary(mat, rows, cols, accumulate, sh, g_jit_pf, g_jit_sync, &bin, &used, &err)) {
         std::fprintf(stderr, "librsamd: encoder failed: %s\n", err.c_str());
         return RS_ERR_DEVICE;
     }
-    Compiled c = compile_asm(asm_source(mat, rows, cols, accumulate, nw, g_jit_pf, g_jit_sync, g_jit_waves, nullptr));
+    Compiled c = compile_asm(asm_source(mat, rows, cols, accumulate, sh, g_jit_pf, g_jit_sync, g_jit_waves, nullptr));
     std::vector<char> text;
     if (!c.ok || !asm_text_section(c.code, &text)) {
         std::fprintf(stderr, "librsamd: encoder check: assembly failed: %s\n", c.log.substr(0, 2000).c_str());
@@ -764,6 +805,8 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_pf);
     k.text += static_cast<char>(g_jit_backend ? g_jit_sync : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_waves : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_layout : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_group_waves : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -794,11 +837,16 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(g_jit_pf);
     key += static_cast<char>(backend ? g_jit_sync : 0);
     key += static_cast<char>(backend ? g_jit_waves : 0);
+    key += static_cast<char>(backend ? g_jit_layout : 0);
+    key += static_cast<char>(backend ? g_jit_group_waves : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);
         if (it == j.entries.end()) {
-            if (j.entries.size() >= kMaxEntries) return {};
+            if (j.entries.size() >= kMaxEntries) {  // full: evict the older half before a later launch
+                j.evict_wanted.store(true, std::memory_order_release);
+                return {};
+            }
             // a code object on disk (another process, an earlier run): load it
             // now whatever the launch history; checked once per matrix
             DiskKey dk;
@@ -807,7 +855,9 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                 if (j.seen.size() >= kMaxSeen) j.seen.clear();
                 h = &j.seen[key];
             }
-            if (g_jit_disk_cache && !cache_dir().empty() && !(h && h->disk_checked)) {
+            // (backend 2 builds a kernel about as fast as it would read the
+            // file: no disk cache, so a storm of one-off patterns writes nothing)
+            if (backend != 2 && g_jit_disk_cache && !cache_dir().empty() && !(h && h->disk_checked)) {
                 dk = disk_key(arch, a);
                 std::vector<char> code = disk_load(dk);
                 if (h) h->disk_checked = true;
@@ -817,7 +867,8 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                     e = std::make_shared<Entry>();
                     e->is_asm = backend != 0;
                     e->backend = backend;
-                    e->nw = asm_waves(a.rows);
+                    e->shape = jit_shape(a.rows);
+                    e->nw = e->shape.nw;
                     e->code = std::move(code);
                     e->state = Entry::kReady;
                     e->disk = std::move(dk);
@@ -829,19 +880,25 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
         }
         if (it == j.entries.end()) {
             if (mode == 1) {
-                // compile only a matrix that recurs: a one-off erasure pattern
-                // would cost a compile (seconds of host time) and never pay it back
                 Seen& h = j.seen[key];
                 ++h.launches;
                 h.bytes += launch_bytes;
-                if (h.launches < static_cast<uint64_t>(g_jit_min_launches) || h.bytes < g_jit_min_bytes)
+                if (backend == 2) {
+                    // compile once it pays for itself (est_compile_us above)
+                    h.lost_us += static_cast<double>(launch_bytes) * lost_us_per_byte(a.rows);
+                    if (h.lost_us < est_compile_us(a.rows, a.cols)) return {};
+                } else if (h.launches < static_cast<uint64_t>(g_jit_min_launches) || h.bytes < g_jit_min_bytes) {
+                    // compile only a matrix that recurs: a one-off erasure pattern
+                    // would cost a compile (seconds of host time) and never pay it back
                     return {};
+                }
                 j.seen.erase(key);
             }
             e = std::make_shared<Entry>();
             e->is_asm = backend != 0;
             e->backend = backend;
-            e->nw = asm_waves(a.rows);
+            e->shape = jit_shape(a.rows);
+            e->nw = e->shape.nw;
             if (backend == 2) {
                 e->mat.assign(a.host_mat, a.host_mat + static_cast<size_t>(a.rows) * a.cols);
                 e->rows = a.rows;
@@ -851,13 +908,14 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                 e->sync = g_jit_sync;
                 e->waves = g_jit_waves;
             } else {
-                e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->nw, g_jit_pf,
+                e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->shape, g_jit_pf,
                                                 g_jit_sync, g_jit_waves, nullptr)
                                    : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             }
-            if (g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
+            if (backend != 2 && g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
+            e->dev = dev;
             j.entries.emplace(key, e);
-            if (mode == 2) {
+            if (mode == 2 || (mode == 1 && backend == 2)) {
                 e->state = Entry::kCompiling;
                 lk.unlock();
                 j.run_one(e);  // on this thread
@@ -882,10 +940,14 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
         } else {
             e = it->second;
         }
+        e->dev = dev;
+        e->last_use = ++j.use_clock;
         auto result = [&]() -> JitKernel {
             JitKernel k;
             k.is_asm = e->is_asm;
             k.nw = e->nw;
+            k.layout = e->shape.layout;
+            k.groups = e->shape.groups;
             k.fn = e->is_asm ? e->fn64 : (bs == 256 ? e->fn256 : e->fn64);
             return k;
         };
@@ -915,13 +977,51 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     }
 }
 
+// The older half of the compiled kernels leaves: with every launch that
+// looked one up enqueued (exclusive g_evict_mu) and the devices drained, none
+// of their code can still be in use.
+static void jit_evict() {
+    std::unique_lock<std::shared_mutex> ex(g_evict_mu);
+    Jit& j = jit();
+    std::lock_guard<std::mutex> lk(j.mu);
+    if (!j.evict_wanted.load(std::memory_order_acquire)) return;
+    std::vector<std::pair<uint64_t, std::string>> loaded;
+    for (auto& kv : j.entries)
+        if (kv.second->state == Entry::kLoaded || kv.second->state == Entry::kFailed ||
+            kv.second->state == Entry::kReady)
+            loaded.emplace_back(kv.second->last_use, kv.first);
+    std::sort(loaded.begin(), loaded.end());
+    loaded.resize(std::max<size_t>(loaded.size() / 2, std::min<size_t>(loaded.size(), 1)));
+    std::set<int> devs;
+    for (auto& x : loaded) devs.insert(j.entries[x.second]->dev);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int dv : devs) {
+        (void)hipSetDevice(dv);
+        (void)hipDeviceSynchronize();
+    }
+    (void)hipSetDevice(cur);
+    for (auto& x : loaded) {
+        auto it = j.entries.find(x.second);
+        if (it->second->module) (void)hipModuleUnload(it->second->module);
+        j.entries.erase(it);
+    }
+    ++j.evictions;
+    j.evict_wanted.store(false, std::memory_order_release);
+}
+
+std::shared_lock<std::shared_mutex> jit_launch_guard() {
+    if (jit().evict_wanted.load(std::memory_order_acquire)) jit_evict();
+    return std::shared_lock<std::shared_mutex>(g_evict_mu);
+}
+
 JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
     return lookup(a, bs, launch_bytes, g_jit_mode);
 }
 
 int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out) {
     if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
-    *out = asm_source(mat, rows, cols, accumulate, asm_waves(rows), g_jit_pf, g_jit_sync, g_jit_waves, nullptr);
+    *out = asm_source(mat, rows, cols, accumulate, jit_shape(rows), g_jit_pf, g_jit_sync, g_jit_waves, nullptr);
     return RS_OK;
 }
 
@@ -933,7 +1033,11 @@ int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wa
     a.rows = rows;
     a.cols = cols;
     a.accumulate = accumulate ? 1 : 0;
-    const JitKernel k = lookup(a, 64, ~uint64_t{0}, wait ? 2 : 3);
+    JitKernel k = lookup(a, 64, ~uint64_t{0}, wait ? 2 : 3);
+    if (!k.fn && jit().evict_wanted.load(std::memory_order_acquire)) {  // full: make room, then once more
+        jit_evict();
+        k = lookup(a, 64, ~uint64_t{0}, wait ? 2 : 3);
+    }
     return (k.fn || !wait) ? RS_OK : RS_ERR_DEVICE;
 }
 

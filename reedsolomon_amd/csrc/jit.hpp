@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <shared_mutex>
 #include <string>
 
 #include "kernels.hpp"
@@ -28,11 +29,15 @@ extern int g_jit_min_rows;         // rs_tune("jit_min_rows"): launches with few
 // and launch the perm-table kernels until the code is ready (default) /
 // compile on the launching thread (tests, benchmarks).
 extern int g_jit_mode;
-// rs_tune("jit_min_bytes"): a matrix whose launches moved fewer bytes in
-// total starts no compile (a compile costs 1.5-4.5 s of host time; a launch
-// of 64 MiB ~10 us of GPU time).
+// rs_tune("jit_min_bytes"): backends 0 / 1 (hiprtc, comgr: seconds / tens of
+// ms per matrix): a matrix whose launches moved fewer bytes in total starts no
+// compile.  Backend 2 (machine code, 0.2-3 ms) compiles a matrix on the
+// launching thread once its launches' estimated loss on the table kernels
+// exceeds its estimated compile time (jit.cpp, est_compile_us).
 extern uint64_t g_jit_min_bytes;
 extern int g_jit_pf;
+extern int g_jit_layout;        // rs_tune("jit_layout")
+extern int g_jit_group_waves;   // rs_tune("jit_group_waves")
 extern int g_jit_sync;
 extern int g_jit_waves;
 // rs_tune("jit_min_launches"): background mode compiles a matrix once it has
@@ -55,12 +60,17 @@ struct JitKernel {
     hipFunction_t fn = nullptr;
     bool is_asm = false;
     int nw = 1;
+    int layout = 0, groups = 1;  // generated kernels: AsmShape (jit_asm.hpp)
 };
 // The compiled kernel for this launch's matrix (a.host_mat, a.rows, a.cols,
 // a.accumulate) on the current device (hiprtc kernels: `bs`-lane
 // workgroups, 64 or 256), or fn == nullptr (JIT off, shape not covered, not
 // compiled yet, or failed).
 JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes);
+// Held from jit_kernel_for until its kernel is enqueued: compiled kernels are
+// only evicted (the older half, once 256 are loaded; devices drained first)
+// while no launch holds it.
+std::shared_lock<std::shared_mutex> jit_launch_guard();
 // The assembly source the generator emits for a matrix (tests: the CPU
 // emulator in tests/asm_emu.py runs it against the oracle).
 int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out);

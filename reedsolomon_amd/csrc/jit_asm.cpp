@@ -102,8 +102,8 @@ enum class K : uint8_t {
 enum Sub : uint8_t {
     kNone = 0,
     kMov, kGetpc, kSetpc,
-    kAdd, kAddc, kLshl, kLshl64, kMul, kMulhi, kAnd,
-    kEq32, kEq64,
+    kAdd, kAddc, kLshl, kLshl64, kMul, kMulhi, kAnd, kLshr, kSub, kOr,
+    kEq32, kEq64, kGe32,
     kScc0, kScc1,
     kLo, kHi,
     kVAnd, kVLshl, kVLshr, kVAdd, kVXor,
@@ -191,8 +191,8 @@ std::string print(const Prog& p) {
                 else line("s_setpc_b64 s[%d:%d]", i.b, i.b + 1);
                 break;
             case K::SOp2: {
-                static const char* const nm[] = {"s_add_u32", "s_addc_u32", "s_lshl_b32", "s_lshl_b64",
-                                                 "s_mul_i32", "s_mul_hi_u32", "s_and_b32"};
+                static const char* const nm[] = {"s_add_u32", "s_addc_u32", "s_lshl_b32", "s_lshl_b64", "s_mul_i32",
+                                                 "s_mul_hi_u32", "s_and_b32", "s_lshr_b32", "s_sub_u32", "s_or_b32"};
                 const char* n = nm[i.sub - kAdd];
                 if (i.sub == kLshl64)
                     line("%s s[%d:%d], s[%d:%d], %s", n, i.a, i.a + 1, i.b, i.b + 1, opnd(i.c, i.imm).c_str());
@@ -202,7 +202,8 @@ std::string print(const Prog& p) {
             }
             case K::SCmp:
                 if (i.sub == kEq64) line("s_cmp_eq_u64 s[%d:%d], %s", i.a, i.a + 1, opnd(i.b, 0).c_str());
-                else line("s_cmp_eq_u32 %s, %s", opnd(i.a, 0).c_str(), opnd(i.b, 0).c_str());
+                else line("%s %s, %s", i.sub == kGe32 ? "s_cmp_ge_u32" : "s_cmp_eq_u32", opnd(i.a, 0).c_str(),
+                          opnd(i.b, 0).c_str());
                 break;
             case K::SNop: line("s_nop %d", i.a); break;
             case K::SWaitLgkm0: line("s_waitcnt lgkmcnt(0)"); break;
@@ -277,7 +278,8 @@ bool encode(const Prog& p, std::vector<uint32_t>* out, std::string* err) {
         if (err) *err = what;
         return false;
     };
-    static const uint8_t sop2_op[] = {0x00, 0x04, 0x1c, 0x1d, 0x24, 0x2c, 0x0c};  // add addc lshl lshl64 mul mulhi and
+    // add addc lshl lshl64 mul mulhi and lshr sub or
+    static const uint8_t sop2_op[] = {0x00, 0x04, 0x1c, 0x1d, 0x24, 0x2c, 0x0c, 0x1e, 0x01, 0x0e};
     static const uint8_t vop2_op[] = {0x13, 0x12, 0x10, 0x34, 0x15};              // and lshlrev lshrrev add_u32 xor
     pc = 0;
     for (const Ins& i : p.ins) {
@@ -307,8 +309,8 @@ bool encode(const Prog& p, std::vector<uint32_t>* out, std::string* err) {
                 if (i.b == kLit || i.c == kLit) w(i.imm);
                 break;
             case K::SCmp:
-                w(0xbf000000u | ((i.sub == kEq64 ? 0x12u : 0x06u) << 16) | (static_cast<uint32_t>(i.b) << 8) |
-                  static_cast<uint32_t>(i.a));
+                w(0xbf000000u | ((i.sub == kEq64 ? 0x12u : i.sub == kGe32 ? 0x09u : 0x06u) << 16) |
+                  (static_cast<uint32_t>(i.b) << 8) | static_cast<uint32_t>(i.a));
                 break;
             case K::SNop: w(0xbf800000u | static_cast<uint32_t>(i.a)); break;
             case K::SWaitLgkm0: w(0xbf8cc07fu); break;  // vmcnt 63, expcnt 7, lgkmcnt 0
@@ -377,6 +379,7 @@ constexpr int kSWgX = 2;       // workgroup id x: chunk
 constexpr int kSWgY = 3;       // workgroup id y: launch stripe
 constexpr int kSStripe = 4;    // stripe index (through stripe_ids)
 constexpr int kSWave = 5;      // wave index in the workgroup
+constexpr int kSGrp = 6;       // layout 1: s6 row group, s7 chunk group
 constexpr int kSTmp = 8;       // s[8:11] scratch
 constexpr int kSDescIn = 12;   // s[12:15] input buffer descriptor
 constexpr int kSDescOut = 16;  // s[16:19] output buffer descriptor
@@ -412,9 +415,14 @@ void transpose8(Prog& P, const int (&r)[8]) {
     for (int i = 0; i < 8; i += 2) swap(r[i], r[i + 1], 1, 4);
 }
 
-// The kernel's instructions for one matrix (see the file header).
-Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int* vgprs_out) {
-    const int rw = (rows + nw - 1) / nw;  // rows per wave
+// The kernel's instructions for one matrix (see the file header and
+// AsmShape, jit_asm.hpp).
+Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& sh, int pf, int sync,
+              int* vgprs_out) {
+    const bool by_group = sh.layout == 1;
+    const int nw = sh.nw;
+    const int rw = sh.rw;  // rows per code path (per wave in layout 0, per workgroup in layout 1)
+    const int npaths = (rows + rw - 1) / rw;
     Layout L;
     L.pf = pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
@@ -437,11 +445,12 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, 
         }
 
     Prog P;
-    P.ins.reserve(static_cast<size_t>(cols) * (80 + 8 * rw) * static_cast<size_t>(nw) + 64);
+    P.ins.reserve(static_cast<size_t>(cols) * (80 + 8 * rw) * static_cast<size_t>(npaths) + 96);
     const int l_stripe_done = P.new_label(".Lstripe_done");
     const int l_idle = P.new_label(".Lidle");
-    std::vector<int> l_wave(static_cast<size_t>(nw), -1);
-    for (int w = 1; w < nw; ++w) l_wave[static_cast<size_t>(w)] = P.new_label(".Lwave" + std::to_string(w));
+    std::vector<int> l_path(static_cast<size_t>(npaths), -1);
+    for (int w = 1; w < npaths; ++w)
+        l_path[static_cast<size_t>(w)] = P.new_label((by_group ? ".Lgroup" : ".Lwave") + std::to_string(w));
     // ---- prologue: stripe, lane offset, wave, masks, descriptor constants
     P.s_load(kSDescIn + 2, 1, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, body)));
     P.s_load(kSTmp, 2, kSKarg, static_cast<uint32_t>(offsetof(AsmArgs, stripe_ids)));
@@ -451,8 +460,10 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, 
     P.s_mov_lit(kSDescOut + 3, 0x20000, false);
     P.v_op2(kVAnd, kVOff, C(63), kVTid);
     P.v_op2(kVLshl, kVOff, C(3), kVOff);
-    P.s_op2(kLshl, kSTmp + 2, kSWgX, C(11));
-    P.v_op2(kVAdd, kVOff, kSTmp + 2, kVOff);
+    if (!by_group) {
+        P.s_op2(kLshl, kSTmp + 2, kSWgX, C(11));
+        P.v_op2(kVAdd, kVOff, kSTmp + 2, kVOff);
+    }
     // wave id = bits 6-9 of the work-item id (packed work-item ids: y / z sit
     // in bits 10-29; zero for these 1-D launches, masked anyway)
     P.v_op2(kVAnd, kVT0, kLit, kVTid, 0x3c0);
@@ -474,13 +485,57 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, 
     P.wait_lgkm0();
     P.label(l_stripe_done);
     P.s_nop(4);  // (v_readfirstlane -> SGPR read hazard margin)
-    // wave w -> its rows' code (long jumps: a wave's straight-line code can
-    // exceed the 16-bit branch range); waves without rows leave
-    for (int w = 1; w < nw; ++w) {
-        const int tgt = w * rw < rows ? l_wave[static_cast<size_t>(w)] : l_idle;
+    if (by_group) {
+        // Layout 1: workgroup x -> (chunk group cg, row group g) with the row
+        // groups of one chunk group on one XCD, back to back in its dispatch
+        // order (the hardware hands workgroup x to XCD x % 8):
+        //   x = ((cg / 8) * G + g) * 8 + cg % 8
+        // so the G workgroups reading the same input lines share that XCD's
+        // L2.  Wave w of the workgroup takes chunk cg * NW + w.
+        const int G = npaths;
+        P.s_op2(kAnd, kSGrp + 1, kSWgX, C(7));       // cg % 8
+        P.s_op2(kLshr, kSTmp, kSWgX, C(3));          // q = x / 8
+        if (G > 1 && (G & (G - 1)) == 0) {
+            int lg = 0;
+            while ((1 << lg) < G) ++lg;
+            P.s_op2(kAnd, kSGrp, kSTmp, C(G - 1));      // g = q % G
+            P.s_op2(kLshr, kSTmp, kSTmp, C(lg));         // q / G
+        } else if (G > 1) {
+            // cg / 8 = q / G: multiply by ceil(2^32 / G) (exact for q < 2^29 / G)
+            const uint32_t magic = static_cast<uint32_t>(((uint64_t{1} << 32) + G - 1) / G);
+            P.s_op2(kMulhi, kSTmp + 1, kSTmp, kLit, magic);
+            P.s_op2(kMul, kSTmp + 2, kSTmp + 1, C(G));
+            P.s_op2(kSub, kSGrp, kSTmp, kSTmp + 2);    // g = q - (q / G) * G
+            P.s_mov(kSTmp, kSTmp + 1);
+        }  // (G == 1: a single path, no dispatch on g)
+        P.s_op2(kLshl, kSTmp, kSTmp, C(3));
+        P.s_op2(kOr, kSGrp + 1, kSGrp + 1, kSTmp);   // cg
+        // chunk groups past the vector body: nothing to do
+        int lg_nw = 0;
+        while ((1 << lg_nw) < nw) ++lg_nw;
+        P.s_op2(kAdd, kSTmp, kSDescIn + 2, kLit, static_cast<uint32_t>((2048u << lg_nw) - 1));
+        P.s_op2(kLshr, kSTmp, kSTmp, C(11 + lg_nw));
+        const int l_go = P.new_label(".Lgo");
+        P.s_cmp(kGe32, kSGrp + 1, kSTmp);
+        P.branch(kScc0, l_go);  // (.Lidle lies past all the code: out of branch range)
+        P.s_endpgm();
+        P.label(l_go);
+        // lane offset = ((cg * NW + wave) << 11) + 8 * lane
+        P.s_op2(kLshl, kSTmp, kSGrp + 1, C(lg_nw));
+        P.s_op2(kAdd, kSTmp, kSTmp, kSWave);
+        P.s_op2(kLshl, kSTmp, kSTmp, C(11));
+        P.v_op2(kVAdd, kVOff, kSTmp, kVOff);
+    }
+    // path p (layout 0: wave p; layout 1: row group p) -> its rows' code
+    // (long jumps: a path's straight-line code can exceed the 16-bit branch
+    // range); waves without rows leave
+    const int sel = by_group ? kSGrp : kSWave;
+    const int nsel = by_group ? npaths : nw;
+    for (int w = 1; w < nsel; ++w) {
+        const int tgt = w < npaths ? l_path[static_cast<size_t>(w)] : l_idle;
         const int l_not = P.new_label(".Lnot" + std::to_string(w));
         const int l_pc = P.new_label(".Lpc" + std::to_string(w));
-        P.s_cmp(kEq32, kSWave, C(w));
+        P.s_cmp(kEq32, sel, C(w));
         P.branch(kScc0, l_not);
         P.s_getpc(kSTmp);
         P.label(l_pc);
@@ -490,10 +545,10 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, 
         P.label(l_not);
     }
 
-    for (int w = 0; w < nw; ++w) {
+    for (int w = 0; w < npaths; ++w) {
         const int r0 = w * rw, nr = std::min(rw, rows - r0);
         if (nr <= 0) break;
-        if (w) P.label(l_wave[static_cast<size_t>(w)]);
+        if (w) P.label(l_path[static_cast<size_t>(w)]);
         // per-wave VMEM queue: ids of issued ops, in order (vmcnt bookkeeping)
         std::vector<int> vq;
         int next_id = 0;
@@ -534,11 +589,13 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, 
         };
         auto slot_reg = [&](int c, int j) { return kVSlots + 8 * (c % L.pf) + j; };
         std::vector<int> col_id(static_cast<size_t>(cols), -1);  // last VMEM op of each column's loads
-        // a lone wave streams its inputs (nt); the waves of a multi-wave
-        // workgroup read the same lines, so those loads keep them cached for
-        // the other waves (measured with nt: 64+64 Encode fetched 1.45x its
-        // input bytes from HBM, 128+128 2.8x; profiles/r03/pmc_traffic_*.json)
-        const bool in_nt = nw == 1;
+        // an input line read by one wave only is streamed (nt); lines other
+        // waves read too (layout 0 with several waves: the same chunk;
+        // layout 1 with several row groups: the other groups' workgroups on
+        // the same XCD) stay cached for them (measured with nt: 64+64 Encode
+        // fetched 1.45x its input bytes from HBM, 128+128 2.8x;
+        // profiles/r03/pmc_traffic_*.json)
+        const bool in_nt = npaths == 1;
         auto issue_col = [&](int c) {  // stage(c) was issued into slot c & 1
             desc(c & 1, kSDescIn);
             if (c + 1 < cols) stage(c + 1, (c + 1) & 1);
@@ -602,7 +659,9 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, 
                 }
             if (c + L.pf < cols) issue_col(c + L.pf);  // the slot is free again
             // keep the waves within `sync` columns of each other, so the lines
-            // the first wave fetched are still cached when the others load them
+            // the first wave fetched are still cached when the others load
+            // them (layout 0; in layout 1 every wave of a workgroup runs the
+            // same path, so the barriers match there too)
             if (nw > 1 && sync > 0 && (c + 1) % sync == 0 && c + 1 < cols) P.s_barrier();
         }
         // ---- outputs: transpose back, (accumulate: XOR the old bytes), store
@@ -748,18 +807,18 @@ std::map<std::tuple<int, int, size_t>, Template>& templates() {
 
 }  // namespace
 
-std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, int max_waves,
-                       int* vgprs_out) {
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& sh, int pf, int sync,
+                       int max_waves, int* vgprs_out) {
     int used = 0;
-    const Prog P = generate(mat, rows, cols, acc, nw, pf, sync, &used);
+    const Prog P = generate(mat, rows, cols, acc, sh, pf, sync, &used);
     if (vgprs_out) *vgprs_out = used;
-    return kHeader + print(P) + kTrailer + descriptor(nw, declared_vgprs(used, max_waves));
+    return kHeader + print(P) + kTrailer + descriptor(sh.nw, declared_vgprs(used, max_waves));
 }
 
-bool asm_binary(const uint8_t* mat, int rows, int cols, bool acc, int nw, int pf, int sync, std::vector<uint32_t>* code,
-                int* vgprs_out, std::string* err) {
+bool asm_binary(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& sh, int pf, int sync,
+                std::vector<uint32_t>* code, int* vgprs_out, std::string* err) {
     int used = 0;
-    const Prog P = generate(mat, rows, cols, acc, nw, pf, sync, &used);
+    const Prog P = generate(mat, rows, cols, acc, sh, pf, sync, &used);
     if (vgprs_out) *vgprs_out = used;
     return encode(P, code, err);
 }

@@ -29,23 +29,47 @@ static_assert(offsetof(AsmArgs, ptr) == 16 && offsetof(AsmArgs, stride16) == 16 
 constexpr int kAsmMaxRows = 128, kAsmMaxCols = 256;  // (up to 8 waves of 16 rows)
 constexpr int kAsmChunk = 2048;                      // bytes of each vector per workgroup
 
-// Waves per workgroup for a rows-row matrix (16 rows per wave at most).
-inline int asm_waves(int rows) { return rows <= 16 ? 1 : (rows + 15) / 16; }
+// How a generated kernel splits the work (every row of a code path keeps 8
+// bit-plane accumulators in VGPRs, so a path holds 16 rows at most):
+//   layout 0: a workgroup is nw waves over the same 2 KiB chunk of every
+//     vector, wave w computing rows [w * rw, w * rw + rw) - the waves of a CU
+//     run different code;
+//   layout 1: a workgroup is nw waves over nw consecutive 2 KiB chunks, all
+//     computing one row group [g * rw, g * rw + rw) with the same code; the G
+//     row groups of a chunk group are G workgroups placed on one XCD back to
+//     back (grid x = ceil(chunk groups / 8) * 8 * G), sharing its L2.
+struct AsmShape {
+    int layout = 0;
+    int nw = 1;   // waves per workgroup
+    int rw = 1;   // rows per code path
+    int groups = 1;  // layout 1: row groups G (= code paths)
+};
+inline AsmShape asm_shape(int rows, int layout, int group_waves) {
+    AsmShape s;
+    const int paths = rows <= 16 ? 1 : (rows + 15) / 16;
+    s.layout = layout == 1 ? 1 : 0;
+    s.rw = (rows + paths - 1) / paths;
+    s.nw = s.layout ? (group_waves < 1 ? 1 : group_waves > 8 ? 8 : group_waves) : paths;
+    s.groups = s.layout ? paths : 1;
+    return s;
+}
+// Waves per workgroup of layout 0 (16 rows per wave at most).
+inline int asm_waves(int rows) { return asm_shape(rows, 0, 1).nw; }
 
 // The assembly source of the kernel for a rows x cols matrix (row-major),
-// accumulate (XOR into the outputs) or overwrite, nw waves per workgroup,
+// accumulate (XOR into the outputs) or overwrite, split as `shape` says,
 // pf columns of loads in flight.  *vgprs receives the VGPRs per lane.
 // sync > 0: the waves of a multi-wave workgroup meet at s_barrier every
 // `sync` columns; max_waves > 1: the kernel declares enough VGPRs that at
 // most that many waves share a SIMD (0: as many as its registers allow).
-std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int sync,
-                       int max_waves, int* vgprs);
+std::string asm_source(const uint8_t* mat, int rows, int cols, bool accumulate, const AsmShape& shape, int pf,
+                       int sync, int max_waves, int* vgprs);
 // Assemble + link (comgr) into a code object; false with the log on failure.
 bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* log, double* ms);
 // The same kernel as asm_source, encoded directly as gfx950 machine code (no
 // assembler): the bytes of its .text.  false (with *err) if an operand does
 // not fit its encoding.
-bool asm_binary(const uint8_t* mat, int rows, int cols, bool accumulate, int nw, int pf, int sync,
+bool asm_binary(const uint8_t* mat, int rows, int cols, bool accumulate, const AsmShape& shape, int pf, int sync,
                 std::vector<uint32_t>* code, int* vgprs_used, std::string* err);
 // A code object for machine code from asm_binary: a template (kernel
 // descriptor and metadata for nw waves per workgroup and the declared VGPRs,

@@ -1513,6 +1513,7 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
         // ab_jit_ao.log, ab_jit_pf.log), else the build-time kernels' per-layout rule
         const int jbs = (bs_block_for(a) == 256 || (tuning().bs_block == 0 && a.cols >= 24)) ? 256 : 64;
         const uint64_t bytes = a.body * static_cast<uint64_t>(a.nstripes) * static_cast<uint64_t>(a.rows + a.cols);
+        const auto hold = jit_launch_guard();  // (the kernel stays loaded until it is enqueued)
         const JitKernel k = jit_kernel_for(a, jbs, bytes);
         if (k.fn && k.is_asm) {
             // assembly kernel: grid (2 KiB chunks, stripes), nw waves per
@@ -1529,7 +1530,12 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
                 x.stride16[v] = static_cast<uint32_t>(ss >> 4);
             }
             if (ok) {
-                const unsigned gx = static_cast<unsigned>((a.body + kAsmChunk - 1) / kAsmChunk);
+                // layout 0: one workgroup per 2 KiB chunk; layout 1: chunk
+                // groups of nw chunks, G row groups each, in blocks of 8
+                // chunk groups (the kernel maps x back, jit_asm.cpp)
+                const uint64_t chunks = (a.body + kAsmChunk - 1) / kAsmChunk;
+                const uint64_t cgs = (chunks + k.nw - 1) / k.nw;
+                const unsigned gx = static_cast<unsigned>(k.layout == 1 ? (cgs + 7) / 8 * 8 * k.groups : chunks);
                 for (int y0 = 0; y0 < a.nstripes; y0 += 65535) {
                     x.stripe0 = static_cast<uint32_t>(y0);
                     const unsigned gy = static_cast<unsigned>(a.nstripes - y0 < 65535 ? a.nstripes - y0 : 65535);

@@ -151,7 +151,7 @@ class Wave:
             if op == "s_nop" or op == "s_barrier":  # waves run one after another here
                 continue
             if ops and op not in ("s_cbranch_scc1", "s_cbranch_scc0", "s_branch", "s_cmp_eq_u64", "s_cmp_eq_u32",
-                                  "s_setpc_b64", "buffer_store_dwordx2"):
+                                  "s_cmp_ge_u32", "s_setpc_b64", "buffer_store_dwordx2"):
                 self._use(ops[0], write=True)  # the destination
             if op == "s_load_dword" or op == "s_load_dwordx2":
                 d, base, off = ops[0], ops[1], int(ops[2], 0)
@@ -165,7 +165,8 @@ class Wave:
             if op == "s_mov_b32":
                 self.s[_regs(ops[0])[1]] = self.sval(ops[1]) & M32
                 continue
-            if op in ("s_add_u32", "s_addc_u32", "s_mul_i32", "s_mul_hi_u32", "s_and_b32", "s_lshl_b32"):
+            if op in ("s_add_u32", "s_addc_u32", "s_mul_i32", "s_mul_hi_u32", "s_and_b32", "s_lshl_b32", "s_lshr_b32",
+                      "s_sub_u32", "s_or_b32"):
                 d = _regs(ops[0])[1]
                 a = self.sval(ops[1]) & M32
                 b = self._imm_expr(ops[2], labels, pc) if op in ("s_add_u32", "s_addc_u32") else self.sval(ops[2]) & M32
@@ -183,6 +184,14 @@ class Wave:
                 elif op == "s_and_b32":
                     self.s[d] = a & b
                     self.scc = int(self.s[d] != 0)
+                elif op == "s_or_b32":
+                    self.s[d] = a | b
+                    self.scc = int(self.s[d] != 0)
+                elif op == "s_sub_u32":
+                    self.s[d], self.scc = (a - b) & M32, int(b > a)
+                elif op == "s_lshr_b32":
+                    self.s[d] = a >> (b & 31)
+                    self.scc = int(self.s[d] != 0)
                 else:
                     self.s[d] = (a << (b & 31)) & M32
                     self.scc = int(self.s[d] != 0)
@@ -197,6 +206,9 @@ class Wave:
                 continue
             if op == "s_cmp_eq_u32":
                 self.scc = int((self.sval(ops[0]) & M32) == (self.sval(ops[1]) & M32))
+                continue
+            if op == "s_cmp_ge_u32":
+                self.scc = int((self.sval(ops[0]) & M32) >= (self.sval(ops[1]) & M32))
                 continue
             if op == "s_cbranch_scc1":
                 if self.scc:

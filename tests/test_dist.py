@@ -120,6 +120,25 @@ def test_bench_under_torchrun_like_the_driver():
     assert r.returncode == 0, r.stderr[-3000:]
     line = _last_json(r.stdout)
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2, line
+    # the line carries the launch-time spread of the pre-warm's last 100
+    # launches and of a pass right behind the timed region (verdict round 3:
+    # tell a box that never settles from a slower kernel)
+    for obj in (line["prewarm"]["last100"], line["timed_spread"]):
+        assert {"n", "min_ms", "median_ms", "p90_ms", "max_ms", "mean_ms"} <= set(obj), obj
+        assert obj["min_ms"] <= obj["median_ms"] <= obj["p90_ms"] <= obj["max_ms"], obj
+
+
+def test_bench_spread_summary():
+    """bench.spread: order statistics of launch times."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    s = bench.spread([float(x) for x in range(1, 101)])
+    assert s["n"] == 100 and s["min_ms"] == 1 and s["max_ms"] == 100 and s["median_ms"] in (50, 51)
+    assert s["p90_ms"] in (90, 91) and s["mean_ms"] == 50.5
+    assert bench.spread([]) is None
+    pw = bench.prewarm_summary(300, 170.0, 0.57, False, [0.6] * 150 + [0.57] * 150, 250)
+    assert pw["last100"]["n"] == 100 and pw["converged"] is False
 
 
 @pytest.mark.timeout(120)

@@ -182,13 +182,14 @@ def test_jit_encode_without_build_time_network(rslib, orc, torch_dev, jit_sync, 
 
 
 def test_jit_background_compile(rslib, orc, torch_dev):
-    """Default mode: the first launch of a new matrix only counts it, the
-    second runs the perm-table kernels and queues a compile (jit_min_launches
-    2); once the compile is done the next launch runs the compiled kernel; all
-    give the same bytes."""
+    """Default mode on the assembly backend (comgr, tens of ms per matrix):
+    the first launch of a new matrix only counts it, the second runs the
+    perm-table kernels and queues a compile (jit_min_launches 2); once the
+    compile is done the next launch runs the compiled kernel; all give the
+    same bytes."""
     torch = torch_dev
     L = rslib.lib()
-    assert L.rs_tune(b"jit", 1) == 0
+    assert L.rs_tune(b"jit", 1) == 0 and L.rs_tune(b"jit_backend", 1) == 0
     L.rs_tune(b"jit_min_bytes", 0)
     try:
         rng = np.random.default_rng(4242)
@@ -219,18 +220,19 @@ def test_jit_background_compile(rslib, orc, torch_dev):
         assert rslib.jit_stats()["launches"] == st0["launches"] + 1
     finally:
         L.rs_tune(b"jit_min_bytes", 8 << 20)
+        L.rs_tune(b"jit_backend", 2)
 
 
 def test_jit_concurrent_threads_background(rslib, orc, torch_dev):
-    """Default (background) mode under concurrency: 4 threads, each with its
-    own handle, stream and matrix, launch repeatedly while their compiles are
-    queued, run and loaded; every launch's bytes equal the oracle's, whichever
-    kernel ran it."""
+    """Background mode (assembly backend) under concurrency: 4 threads, each
+    with its own handle, stream and matrix, launch repeatedly while their
+    compiles are queued, run and loaded; every launch's bytes equal the
+    oracle's, whichever kernel ran it."""
     import threading
 
     torch = torch_dev
     L = rslib.lib()
-    assert L.rs_tune(b"jit", 1) == 0
+    assert L.rs_tune(b"jit", 1) == 0 and L.rs_tune(b"jit_backend", 1) == 0
     L.rs_tune(b"jit_min_bytes", 0)
     errors = []
     try:
@@ -277,6 +279,49 @@ def test_jit_concurrent_threads_background(rslib, orc, torch_dev):
         assert st["launches"] > st0["launches"], (st0, st)
     finally:
         L.rs_tune(b"jit_min_bytes", 8 << 20)
+        L.rs_tune(b"jit_backend", 2)
+
+
+def test_jit_machine_code_first_sight_policy(rslib, orc, torch_dev):
+    """Default mode on the default (machine-code) backend: a launch whose
+    estimated loss on the table kernels exceeds the estimated time to build
+    its kernel compiles at FIRST sight, on the launching thread, and runs it
+    (a one-off erasure pattern of a wide code); a small launch of a fresh
+    matrix runs on the table kernels until its launches have lost that much,
+    then compiles.  Bytes equal the oracle's (small) or the no-compile run
+    (large)."""
+    torch = torch_dev
+    L = rslib.lib()
+    assert L.rs_tune(b"jit", 1) == 0 and L.rs_tune(b"jit_backend", 2) == 0
+    rng = np.random.default_rng(777)
+    r = rslib.New(10, 4)
+    # large: 96 rows x 16 columns, 4 stripes of 1 MiB vectors (470 MB moved:
+    # ~590 us estimated loss on the wide table kernel, ~380 us to build)
+    rows, cols, S, n = 96, 16, 4, 1 << 20
+    mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
+    src = torch.randint(0, 256, (S, cols, n), dtype=torch.uint8, device="cuda")
+    ref = torch.zeros((S, rows, n), dtype=torch.uint8, device="cuda")
+    assert L.rs_tune(b"jit", 0) == 0
+    r.gf_matmul_batch(mat, src, None, ref, None)  # the table kernels' bytes
+    assert L.rs_tune(b"jit", 1) == 0
+    st0 = rslib.jit_stats()
+    dst = torch.zeros_like(ref)
+    r.gf_matmul_batch(mat, src, None, dst, None)
+    torch.cuda.synchronize()
+    st1 = rslib.jit_stats()
+    assert st1["compiled"] == st0["compiled"] + 1 and st1["launches"] == st0["launches"] + 1, (st0, st1)
+    assert torch.equal(dst, ref)
+    # small: 7 x 11 over 2 x 32 KiB: ~1.2 MB per launch, a few ns lost each
+    mat = rng.integers(0, 256, (7, 11), dtype=np.uint8)
+    src = torch.from_numpy(rng.integers(0, 256, (2, 11, 32768), dtype=np.uint8)).cuda()
+    exp = orc.encode_numpy(mat, src.cpu().numpy())
+    dst = torch.zeros((2, 7, 32768), dtype=torch.uint8, device="cuda")
+    for k in range(3):
+        r.gf_matmul_batch(mat, src, None, dst, None)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst.cpu().numpy(), exp)
+    st2 = rslib.jit_stats()
+    assert st2["compiled"] == st1["compiled"] and st2["launches"] == st1["launches"], (st1, st2)
 
 
 def test_jit_prepare_then_first_launch_runs_compiled(rslib, orc, torch_dev):
@@ -334,7 +379,10 @@ def test_jit_disk_cache_across_processes(rslib, tmp_path):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RSAMD_JIT_CACHE_DIR=str(tmp_path / "jit"), RSAMD_JIT_DISK_CACHE="1")
+    # (the disk cache serves the comgr / hiprtc backends; the machine-code
+    # backend builds a kernel about as fast as it would read the file)
+    env = dict(os.environ, RSAMD_JIT_CACHE_DIR=str(tmp_path / "jit"), RSAMD_JIT_DISK_CACHE="1",
+               RSAMD_JIT_BACKEND="1")
     script = "ROOT = %r\n" % root + _DISK_SCRIPT
 
     def run(mode):

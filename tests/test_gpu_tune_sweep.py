@@ -66,6 +66,8 @@ SWEEP = {
     "jit_waves": [0, 4, 2],
     "jit_disk_cache": [0, 1],
     "jit_backend": [0, 1, 2],
+    "jit_layout": [1, 0],
+    "jit_group_waves": [2, 8, 4],
     "table_registry_max": [1, 1 << 14],
 }
 

@@ -45,7 +45,24 @@ def test_asm_kernel_with_barriers(rslib, orc, rows, cols, sync):
     assert src.count("s_barrier") == nw * ((cols - 1) // sync)
 
 
-def _check_kernel(rslib, orc, rows, cols, acc):
+@pytest.mark.parametrize("rows,cols,acc,gw", [(33, 3, 1, 2), (17, 5, 0, 1), (40, 9, 0, 4), (9, 1, 0, 2),
+                                            (20, 4, 0, 8), (16, 16, 1, 4), (64, 5, 0, 2)])
+def test_asm_kernel_row_group_layout(rslib, orc, rows, cols, acc, gw):
+    """rs_tune("jit_layout", 1): row groups over workgroups (grid x = chunk
+    groups of gw chunks x row groups, laid out 8 chunk groups at a time so
+    the row groups of one chunk group share an XCD), every wave of a
+    workgroup on its own chunk with the same code; padded workgroups past the
+    body leave at once."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_layout", 1) == 0 and L.rs_tune(b"jit_group_waves", gw) == 0
+    try:
+        _check_kernel(rslib, orc, rows, cols, acc, layout=1, gw=gw)
+    finally:
+        L.rs_tune(b"jit_layout", 0)
+        L.rs_tune(b"jit_group_waves", 4)
+
+
+def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4):
     rng = np.random.default_rng(rows * 1000 + cols * 10 + acc)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
     src = rslib.jit_asm_source(mat, bool(acc))
@@ -64,9 +81,14 @@ def _check_kernel(rslib, orc, rows, cols, acc):
     ids = mem.alloc(4 * S)
     mem.view(ids, 4 * S).view(np.uint32)[:] = np.arange(S)[::-1]
     from reedsolomon_amd.rs import lib  # noqa: F401  (library loaded by the fixture)
-    nw = 1 if rows <= 16 else (rows + 15) // 16
+    paths = 1 if rows <= 16 else (rows + 15) // 16
+    if layout == 1:  # the library's launch rule (kernels.hip): ceil(chunk groups / 8) * 8 * row groups
+        nw, cgs = gw, (body // 2048 + gw - 1) // gw
+        grid = ((cgs + 7) // 8 * 8 * paths, S)
+    else:
+        nw, grid = paths, (body // 2048, S)
     emu = Emu(mem)
-    emu.launch(src, _karg(body, 0, ids, ptrs, [stride // 16] * nvec), (body // 2048, S), nw)
+    emu.launch(src, _karg(body, 0, ids, ptrs, [stride // 16] * nvec), grid, nw)
     got = mem.view(region, S * stride).reshape(S, nvec, vlen)
     exp = orc.encode_numpy(mat, host[:, :cols, :body])
     if acc:
@@ -97,12 +119,14 @@ def test_asm_kernel_occupancy_cap(rslib, waves, vgprs):
         assert declared == vgprs
 
 
-@pytest.mark.parametrize("rows,cols,acc,pf,sync", [(5, 10, 0, 3, 0), (8, 10, 1, 3, 0), (3, 7, 0, 1, 0),
-                                                   (16, 16, 0, 4, 0), (12, 5, 1, 2, 0), (33, 3, 1, 3, 0),
-                                                   (17, 5, 0, 3, 1), (40, 9, 0, 3, 4), (9, 1, 0, 3, 0),
-                                                   (64, 64, 0, 3, 0), (56, 200, 1, 3, 0), (128, 128, 0, 3, 0),
-                                                   (128, 256, 1, 2, 0)])
-def test_machine_code_equals_assembler(rslib, rows, cols, acc, pf, sync):
+@pytest.mark.parametrize("rows,cols,acc,pf,sync,layout", [(5, 10, 0, 3, 0, 0), (8, 10, 1, 3, 0, 0), (3, 7, 0, 1, 0, 0),
+                                                          (16, 16, 0, 4, 0, 0), (12, 5, 1, 2, 0, 0), (33, 3, 1, 3, 0, 0),
+                                                          (17, 5, 0, 3, 1, 0), (40, 9, 0, 3, 4, 0), (9, 1, 0, 3, 0, 0),
+                                                          (64, 64, 0, 3, 0, 0), (56, 200, 1, 3, 0, 0),
+                                                          (128, 128, 0, 3, 0, 0), (128, 256, 1, 2, 0, 0),
+                                                          (33, 3, 1, 3, 0, 1), (128, 128, 0, 3, 0, 1),
+                                                          (56, 200, 1, 3, 2, 1), (16, 16, 0, 3, 0, 1)])
+def test_machine_code_equals_assembler(rslib, rows, cols, acc, pf, sync, layout):
     """The default backend encodes the kernel straight into gfx950 machine
     code (no assembler at run time); those bytes equal comgr's assembly of the
     generator's text for the same matrix and settings, instruction for
@@ -111,9 +135,11 @@ def test_machine_code_equals_assembler(rslib, rows, cols, acc, pf, sync):
     L = rslib.lib()
     mat = np.random.default_rng(rows * 31 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
     assert L.rs_tune(b"jit_pf", pf) == 0 and L.rs_tune(b"jit_sync", sync) == 0
+    assert L.rs_tune(b"jit_layout", layout) == 0
     try:
         n = rslib.jit_encoder_check(mat, bool(acc))
     finally:
         L.rs_tune(b"jit_pf", 3)
         L.rs_tune(b"jit_sync", 0)
+        L.rs_tune(b"jit_layout", 0)
     assert n > 0 and n % 4 == 0

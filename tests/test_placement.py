@@ -5,7 +5,8 @@ ranks; gather_reconst moves survivors to owners with all_to_all, decodes
 (here with the oracle standing in for the HIP decode — tests may use it),
 and writes the rebuilt shards back home.  Every rank's shards must equal the
 originals afterwards.  The GPU test runs the same exchange with the HIP
-decode: two ranks sharing cuda:0 over gloo."""
+decode: two ranks sharing cuda:0 over gloo, every rebuilt shard checked
+against the oracle's Reconst."""
 import os
 import socket
 import subprocess
@@ -120,12 +121,40 @@ def test_placement_validation():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-def test_gather_reconst_hip_two_ranks():
-    """tools/placement_demo.py: two ranks on cuda:0 (gloo), HIP decode."""
+def test_gather_reconst_hip_two_ranks(tmp_path, orc):
+    """tools/placement_demo.py: two ranks on cuda:0 (gloo), HIP decode.
+    Every rebuilt shard equals the CPU oracle's Reconst of the same stripe
+    (lost shards garbled, survivors intact: rs.go:221-380), not only the
+    HIP-encoded original, and the transfer plan's survivors of each stripe
+    are the first d by index, as the oracle's checkReconst picks them
+    (rs.go:264-335).  (The nccl / xGMI leg needs two GPUs: unmeasured here.)"""
     env = dict(os.environ, RSAMD_BENCH_DEVICE="0")
+    d, p = 10, 4
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(ROOT, "tools", "placement_demo.py"), "--backend", "gloo"],
+                        os.path.join(ROOT, "tools", "placement_demo.py"), "--backend", "gloo", "--stripes", "24",
+                        "--vec", "8192", "--dump", str(tmp_path)],
                        capture_output=True, text=True, timeout=280, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("placement_demo ok") == 2
+    total = 0
+    for rank in range(2):
+        z = np.load(tmp_path / f"rank{rank}.npz")
+        full, masks = z["full"], z["masks"]
+        for s, surv, lostm in zip(z["plan_stripes"], z["plan_surv"], z["plan_lost"]):
+            lost = [v for v in range(d + p) if int(lostm) >> v & 1]
+            assert int(masks[s]) == int(lostm)
+            rc, vs, nr, _dn = orc.check_reconst(d, p, [], lost)
+            assert rc == 0 and list(surv) == vs[:d] and sorted(nr) == lost, (s, list(surv), vs, nr)
+        expect = {}
+        for (s, v), got in zip(z["keys"], z["vals"]):
+            if s not in expect:
+                vects = [full[s, i].copy() for i in range(d + p)]
+                lost = [i for i in range(d + p) if int(masks[s]) >> i & 1]
+                for i in lost:
+                    vects[i][:] = 0xEE
+                assert orc.reconst(d, p, vects, [], lost) == 0
+                expect[s] = vects
+            assert np.array_equal(got, expect[s][v]), (rank, s, v)
+            total += 1
+    assert total > 0

@@ -12,7 +12,7 @@ stream; end-to-end numbers time host wall clock around the pinned pipeline.
     python tools/ops_bench.py                    # every section
     python tools/ops_bench.py --only wide,api    # some sections
 
-Sections: encode, shapes, split, rec8, rec4, multi, upd, wide, host, api.
+Sections: encode, shapes, split, rec8, rec4, multi, upd, wide, first, host, api.
 """
 import json
 import os
@@ -49,7 +49,7 @@ def rec(name, nbytes, t, **kw):
     print(f"{name:44s} {nbytes / t / GiB:10.2f} GiB/s  {t * 1e6:10.2f} us/call", flush=True)
 
 
-SECTIONS = ["encode", "shapes", "split", "rec8", "rec4", "multi", "upd", "wide", "host", "api"]
+SECTIONS = ["encode", "shapes", "split", "rec8", "rec4", "multi", "upd", "wide", "first", "host", "api"]
 
 
 def want(name):
@@ -92,6 +92,55 @@ def wide(g):
     L.rs_tune(b"wide_single_pass", 1)
 
 
+def first_sight(g):
+    """A rebuild storm: every launch a different erasure pattern, seen once
+    (its decode matrix new to the process), launched back to back with the
+    library's default policy (jit=1: the machine-code backend builds a
+    pattern's kernel on the launching thread when the launch is large enough
+    to pay for it, jit.cpp est_compile_us) - timed on the host clock from the
+    first launch to the last one's completion, so every compile is inside the
+    window; against the same launches with one pattern already compiled
+    (jit=2, repeated) and with no run-time kernels at all (jit=0).  The
+    stripes are rebuilt in place from intact survivors, so they must come
+    out unchanged: checked after every run."""
+    import numpy as np
+
+    L = rs.lib()
+    rng = np.random.default_rng(11)
+    for k, m, vec, nlost in ((16, 16, 1 << 20, 16), (100, 28, 256 << 10, 20), (100, 28, 256 << 10, 28)):
+        S = max(1, (3584 << 20) // ((k + m) * vec))
+        r = rs.New(k, m)
+        data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)
+        par = torch.empty((S, m, vec), dtype=torch.uint8, device="cuda")
+        r.encode_batch_split(data, par)
+        ref_d, ref_p = data.clone(), par.clone()
+        nbytes = S * (k + nlost) * vec
+        n = 20
+        pats = [sorted(int(x) for x in rng.choice(k + m, nlost, replace=False)) for _ in range(n)]
+        L.rs_tune(b"jit", 2)
+        t = dev_time(lambda: r.reconst_batch_split(data, par, [], pats[0]), iters=10, warm=3)
+        rec(f"reconst {k}+{m} {vec >> 10}KiB lost={nlost} x{S}, one pattern compiled (jit=2)", nbytes, t)
+        for jit, label in ((0, "no run-time kernels (jit=0)"), (1, "default policy (jit=1)")):
+            L.rs_tune(b"jit", jit)
+            fresh = [sorted(int(x) for x in rng.choice(k + m, nlost, replace=False)) for _ in range(n)]
+            r.reconst_batch_split(data, par, [], fresh[0])  # (clocks up; this pattern is not timed again)
+            st0 = rs.jit_stats()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for pt in fresh[1:]:
+                r.reconst_batch_split(data, par, [], pt)
+            torch.cuda.synchronize()
+            t = (time.perf_counter() - t0) / (n - 1)
+            st = rs.jit_stats()
+            rec(f"reconst {k}+{m} {vec >> 10}KiB lost={nlost} x{S}, {n - 1} new patterns, {label}", nbytes, t,
+                compiled=st["compiled"] - st0["compiled"], compiled_launches=st["launches"] - st0["launches"],
+                compile_ms=round(st["compile_ms"] - st0["compile_ms"], 2))
+            assert torch.equal(data, ref_d) and torch.equal(par, ref_p), "first-sight reconst changed the stripes"
+        del data, par, ref_d, ref_p
+        torch.cuda.empty_cache()
+    L.rs_tune(b"jit", 2)
+
+
 def main():
     g = torch.Generator(device="cuda").manual_seed(42)
     # run-time bit-sliced kernels (5-8 output rows) compile on first use here,
@@ -100,6 +149,8 @@ def main():
     rs.lib().rs_tune(b"jit", 2)
     if want("wide"):
         wide(g)
+    if want("first"):
+        first_sight(g)
     if want("encode"):
         # ---- encode, device-resident
         for k, m, vec, S in ((10, 4, 1 << 20, 256), (12, 4, 1 << 20, 256), (10, 4, 8 << 10, 32768), (10, 4, 8 << 10, 1)):

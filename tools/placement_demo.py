@@ -11,7 +11,10 @@ survivors -> owner over all_to_all (RCCL/xGMI with nccl), one multi-pattern
 HIP decode per owner, rebuilt shards -> home.  Each rank checks its shards
 against the originals and prints "placement_demo ok" with the exchange time.
 RSAMD_BENCH_DEVICE pins every rank to one device (rehearsal on a 1-GPU box,
-with --backend gloo)."""
+with --backend gloo).  --dump DIR writes each rank's stripes, masks, rebuilt
+shards and the transfer plan to DIR/rank<r>.npz, so tests/test_placement.py
+can check every rebuilt shard against the CPU oracle's Reconst of the same
+stripe and the plan's survivors against the oracle's checkReconst."""
 import argparse
 import os
 import sys
@@ -26,13 +29,14 @@ def main():
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--stripes", type=int, default=64)
     ap.add_argument("--vec", type=int, default=65536)
+    ap.add_argument("--dump", default="", help="directory for rank<r>.npz (stripes, masks, rebuilt shards, plan)")
     args = ap.parse_args()
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import reedsolomon_amd as rs
-    from reedsolomon_amd.placement import Placement, gather_reconst
+    from reedsolomon_amd.placement import Placement, _plan, gather_reconst
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev_idx = int(os.environ.get("RSAMD_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -73,6 +77,17 @@ def main():
     ok = torch.equal(local, orig) and all(torch.equal(t, full[s, v]) for (s, v), t in rebuilt.items())
     if not ok:
         raise SystemExit(f"rank {rank}: rebuilt shards differ")
+    if args.dump:
+        keys = sorted(rebuilt)
+        plan = _plan(pl, masks)
+        ps = sorted(plan)
+        np.savez(os.path.join(args.dump, f"rank{rank}.npz"), full=full.cpu().numpy(), masks=masks,
+                 keys=np.array(keys, np.int64).reshape(-1, 2),
+                 vals=(torch.stack([rebuilt[x] for x in keys]).cpu().numpy() if keys
+                       else np.zeros((0, vec), np.uint8)),
+                 plan_stripes=np.array(ps, np.int64),
+                 plan_surv=np.array([plan[x][0] for x in ps], np.int64).reshape(len(ps), d),
+                 plan_lost=np.array([sum(1 << v for v in plan[x][1]) for x in ps], np.uint64))
     print(f"placement_demo ok rank={rank} world={world} rebuilt={len(rebuilt)} time_ms={el * 1e3:.2f}", flush=True)
     dist.barrier()
     dist.destroy_process_group()

@@ -19,7 +19,7 @@ for d in sorted(glob.glob(os.path.join(out, "p*"))):
     if not files:
         continue
     rows = [r for r in csv.DictReader(open(files[0]))
-            if any(k in r["Kernel_Name"] for k in ("gf_matmul", "gf_bitslice", "rs_bs_jit"))]
+            if any(k in r["Kernel_Name"] for k in ("gf_matmul", "gf_bitslice", "rs_bs_jit", "rs_bs_asm"))]
     if not rows:
         continue
     dom = statistics.mode(r["Kernel_Name"] for r in rows)
@@ -37,6 +37,9 @@ for d in sorted(glob.glob(os.path.join(out, "p*"))):
         "share_wait_inst_any": mean.get("SQ_WAIT_INST_ANY", 0) / wc,
         "share_active_inst_any": mean.get("SQ_ACTIVE_INST_ANY", 0) / wc,
         "share_active_valu": mean.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+        "ifetch_per_wave": mean.get("SQ_IFETCH", 0) / max(mean.get("SQ_WAVES", 1), 1),
+        "icache_miss_rate": mean.get("SQC_ICACHE_MISSES", 0) / max(mean.get("SQC_ICACHE_REQ", 0), 1),
+        "icache_hit_rate": mean.get("SQC_ICACHE_HITS", 0) / max(mean.get("SQC_ICACHE_REQ", 0), 1),
     }
     setting = open(os.path.join(d, "setting.txt")).read().strip() if os.path.exists(os.path.join(d, "setting.txt")) else ""
     res[os.path.basename(d)] = {"setting": setting, "kernel": dom, "launches": len(next(iter(per.values()))),
