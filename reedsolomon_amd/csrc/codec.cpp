@@ -124,17 +124,31 @@ int dev_fail(hipError_t e, const char* where) {
 // by the same tables as the 4-row kernels' LDS image [rup(cols, 4)][20]
 // (zero rows and columns as padding), which those kernels stage with a plain
 // copy.  Uploaded once per distinct matrix and reused by every later launch.
-// Caller holds tab_mu until its launch is enqueued: a full registry is
-// recycled after a device sync, so no table may be handed out and launched
-// across a recycle.
-int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t** out, int* rows_pad_out) {
+// The upload is asynchronous on the launching stream (pinned staging slots):
+// a synchronous copy from pageable memory waited for every kernel already
+// queued, which put a full GPU drain in front of every new erasure pattern
+// (a rebuild storm of one-off patterns: profiles/r04/).  A later launch on
+// another stream waits for the upload's event.  Caller holds tab_mu until its
+// launch is enqueued: a full registry is recycled after a device sync, so no
+// table may be handed out and launched across a recycle.
+int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t stream, const uint32_t** out,
+               int* rows_pad_out) {
     const int rows_pad = static_cast<int>(rup(rows, 8));
     std::string key(reinterpret_cast<const char*>(&rows), sizeof rows);
     key.append(reinterpret_cast<const char*>(&cols), sizeof cols);
     key.append(reinterpret_cast<const char*>(mat), static_cast<size_t>(rows) * cols);
     auto it = rs->tables.find(key);
     if (it != rs->tables.end()) {
-        *out = it->second;
+        rs_t::TableEntry& te = it->second;
+        if (te.ready) {
+            if (hipEventQuery(te.ready) == hipSuccess) {
+                (void)hipEventDestroy(te.ready);
+                te.ready = nullptr;
+            } else if (stream != te.stream) {
+                RS_TRY(hip_ok(hipStreamWaitEvent(stream, te.ready, 0), "table upload wait"));
+            }
+        }
+        *out = te.dev;
         *rows_pad_out = rows_pad;
         return RS_OK;
     }
@@ -145,7 +159,10 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
         RS_TRY(engine_drain(rs));  // calls in flight complete first (a stopped instance would strand them)
         engine_stop(rs);
         RS_TRY(hip_ok(hipDeviceSynchronize(), "table registry drain"));
-        for (auto& kv : rs->tables) (void)hipFree(kv.second);
+        for (auto& kv : rs->tables) {
+            (void)hipFree(kv.second.dev);
+            if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
+        }
         rs->tables.clear();
     }
     const size_t main_dw = static_cast<size_t>(cols) * rows_pad * 5;
@@ -155,7 +172,27 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
     // takes from VGPRs first, as two 64-bit pairs); an odd last column's
     // partner has zero tables
     const size_t wide_dw = rows > 8 ? static_cast<size_t>((cols + 1) / 2) * rows_pad * 12 : 0;
-    std::vector<uint32_t> host(main_dw + img_dw + wide_dw, 0);
+    const size_t bytes = (main_dw + img_dw + wide_dw) * 4;
+    rs_t::TabStage& st = rs->tab_stage[rs->tab_stage_next];
+    rs->tab_stage_next = (rs->tab_stage_next + 1) % rs_t::kTabStages;
+    if (st.pending) {  // the copy enqueued from this slot kTabStages uploads ago
+        RS_TRY(hip_ok(hipEventSynchronize(st.done), "table staging slot"));
+        st.pending = false;
+    }
+    if (!st.done) RS_TRY(hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "table staging event"));
+    if (st.cap < bytes) {
+        if (st.host) (void)hipHostFree(st.host);
+        st.host = nullptr;
+        st.cap = 0;
+        const size_t cap = rup(bytes, size_t{64} << 10);
+        if (hipHostMalloc(reinterpret_cast<void**>(&st.host), cap, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return RS_ERR_NOMEM;
+        }
+        st.cap = cap;
+    }
+    uint32_t* host = reinterpret_cast<uint32_t*>(st.host);
+    std::memset(host, 0, bytes);
     for (int c = 0; c < cols; ++c)
         for (int r = 0; r < rows; ++r) {
             uint32_t t[5];
@@ -173,13 +210,25 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t*
             }
         }
     uint32_t* dptr = nullptr;
-    if (hipMalloc(&dptr, host.size() * 4) != hipSuccess) return RS_ERR_NOMEM;
-    const hipError_t e = hipMemcpy(dptr, host.data(), host.size() * 4, hipMemcpyHostToDevice);
+    if (hipMalloc(&dptr, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return RS_ERR_NOMEM;
+    }
+    rs_t::TableEntry te;
+    te.dev = dptr;
+    te.stream = stream;
+    hipError_t e = hipMemcpyAsync(dptr, host, bytes, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipEventRecord(st.done, stream);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&te.ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(te.ready, stream);
     if (e != hipSuccess) {
+        (void)hipStreamSynchronize(stream);
+        if (te.ready) (void)hipEventDestroy(te.ready);
         (void)hipFree(dptr);
         return dev_fail(e, "table upload");
     }
-    rs->tables.emplace(std::move(key), dptr);
+    st.pending = true;
+    rs->tables.emplace(std::move(key), te);
     *out = dptr;
     *rows_pad_out = rows_pad;
     return RS_OK;
@@ -196,7 +245,7 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     MatmulArgs a;
     std::memset(&a, 0, sizeof a);
     std::lock_guard<std::mutex> lk(rs->tab_mu);  // table lookup through launch (get_tables)
-    int rc = get_tables(rs, mat, rows, cols, &a.tables, &a.rows_pad);
+    int rc = get_tables(rs, mat, rows, cols, stream, &a.tables, &a.rows_pad);
     if (rc) return rc;
     a.img4 = rows <= 4 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
     a.wide = rows > 8 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;

@@ -98,7 +98,24 @@ struct rs_codec {
     bool device_ready = false;
 
     std::mutex tab_mu;  // coefficient-table registry: matrix bytes -> device perm tables
-    std::map<std::string, uint32_t*> tables;
+    struct TableEntry {
+        uint32_t* dev = nullptr;
+        hipEvent_t ready = nullptr;      // its upload's completion (nullptr once seen complete)
+        hipStream_t stream = nullptr;    // ... enqueued on this stream
+    };
+    std::map<std::string, TableEntry> tables;
+    // Pinned staging of table uploads (async on the launching stream, so a new
+    // matrix does not wait for the kernels already queued): a slot is reused
+    // once the copy enqueued from it kRing uploads earlier has finished.
+    struct TabStage {
+        uint8_t* host = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+        bool pending = false;
+    };
+    static constexpr int kTabStages = 4;
+    TabStage tab_stage[kTabStages];
+    int tab_stage_next = 0;
 
     std::mutex stage_mu;  // staging for the host-memory entry points
     uint8_t* stage = nullptr;
@@ -273,7 +290,14 @@ inline void rs_codec::release_device() {
         step("device sync");
         (void)hipDeviceSynchronize();
         step("frees");
-        for (auto& kv : tables) (void)hipFree(kv.second);
+        for (auto& kv : tables) {
+            (void)hipFree(kv.second.dev);
+            if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
+        }
+        for (TabStage& t : tab_stage) {
+            if (t.host) (void)hipHostFree(t.host);
+            if (t.done) (void)hipEventDestroy(t.done);
+        }
         for (UploadSlot& u : up) {
             if (u.host) (void)hipHostFree(u.host);
             if (u.dev) (void)hipFree(u.dev);
@@ -314,7 +338,8 @@ uint64_t cache_key(const int* survived, int ns);                    // rs.go:414
 
 // ---------------------------------------------------------------- device product (codec.cpp)
 int ensure_device(rs_t* rs);
-int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint32_t** out, int* rows_pad_out);
+int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t stream, const uint32_t** out,
+               int* rows_pad_out);
 int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs,
               const uint8_t* in_sid, uint8_t* const* out_ptrs, const uint8_t* out_sid, const int64_t ss[4],
               int nstripes, uint64_t len, bool accumulate, hipStream_t stream, const int32_t* stripe_ids = nullptr);

@@ -605,7 +605,8 @@ struct Jit {
     std::deque<std::shared_ptr<Entry>> queue;
     std::thread worker;
     bool stop = false;
-    uint64_t compiled = 0, failed = 0, evictions = 0;
+    uint64_t compiled = 0, failed = 0, evictions = 0, loads = 0;
+    double load_ms = 0;  // in hipModuleLoadData (diagnostics: env RSAMD_JIT_TRACE prints these at exit)
     double compile_ms = 0;
     std::atomic<uint64_t> launches{0};
 
@@ -668,6 +669,19 @@ std::shared_mutex g_evict_mu;
 Jit& jit() {
     static Jit* j = new Jit;
     return *j;
+}
+
+void jit_trace_report() {
+    Jit& j = jit();
+    std::fprintf(stderr, "{\"jit_trace\": {\"compiled\": %llu, \"compile_ms\": %.3f, \"loads\": %llu, "
+                 "\"load_ms\": %.3f, \"evictions\": %llu}}\n",
+                 static_cast<unsigned long long>(j.compiled), j.compile_ms, static_cast<unsigned long long>(j.loads),
+                 j.load_ms, static_cast<unsigned long long>(j.evictions));
+}
+
+void jit_trace_register() {
+    static const bool on = std::getenv("RSAMD_JIT_TRACE") != nullptr && std::atexit(jit_trace_report) == 0;
+    (void)on;
 }
 
 void jit_atexit() {
@@ -956,7 +970,12 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
         // load the code object on this device (launching thread, under mu)
         hipModule_t m = nullptr;
         hipFunction_t f64 = nullptr, f256 = nullptr;
-        const bool ok = hipModuleLoadData(&m, e->code.data()) == hipSuccess &&
+        const auto tl = std::chrono::steady_clock::now();
+        const bool loaded = hipModuleLoadData(&m, e->code.data()) == hipSuccess;
+        ++j.loads;
+        j.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count();
+        jit_trace_register();
+        const bool ok = loaded &&
                         (e->is_asm ? hipModuleGetFunction(&f64, m, "rs_bs_asm") == hipSuccess
                                    : hipModuleGetFunction(&f64, m, "rs_bs_jit_64") == hipSuccess &&
                                          hipModuleGetFunction(&f256, m, "rs_bs_jit_256") == hipSuccess);

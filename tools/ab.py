@@ -10,7 +10,7 @@ jit: 2 (default here: run-time bit-sliced kernels compiled before timing) | 0 (p
 op: enc (Encode, default) | rec1 / rec2 / rec4 / rec5 / rec6 / rec8 (Reconst of
 1 / 2 / 4 / 5 / 6 / 8 lost data vectors, split layout; rec8p: 4 data + 4
 parity, needs AB_M >= 8) | multi16 (rs_reconst_batch_multi, 16 patterns) |
-upd (Update of one row) | rep3 (Replace of 3 rows), both on the interleaved
+upd (Update of one row) | repN (Replace of N rows, e.g. rep1, rep3), both on the interleaved
 [S][d+p][len] buffer.
 """
 import os
@@ -91,8 +91,10 @@ def main():
             return (lambda: r.reconst_batch_split(data, par, [], lost)), S * (K + len(lost)) * VEC
         if op == "upd":  # Update row 3 of every stripe: reads old, new, 4 parity; writes 4 parity
             return (lambda: r.update_batch(data[:, 0], data[:, 1], 3, buf)), S * (2 + 2 * M) * VEC
-        if op == "rep3":  # Replace rows 1, 4, 7: reads 3 data + 4 parity, writes 4 parity
-            return (lambda: r.replace_batch(data[:, :3], [1, 4, 7], buf)), S * (3 + 2 * M) * VEC
+        if op.startswith("rep"):  # Replace of n rows (1, 4, 7, ...): reads n data + m parity, writes m parity
+            rn = int(op[3:])
+            rows = [1 + 3 * i for i in range(rn)]
+            return (lambda: r.replace_batch(data[:, :rn], rows, buf)), S * (rn + 2 * M) * VEC
         if op == "multi16s":
             return (lambda: r.reconst_batch_multi(data, par, masks_sorted)), (S * K + nrec16) * VEC
         if op == "multi16":

@@ -308,6 +308,77 @@ extern "C" int probe_buf_g(int kind, void* a, void* b, uint64_t vec, int nstripe
     return hipGetLastError();
 }
 
+// The k+m encode pattern at several geometries (round 4, 16+4 vs 10+4):
+// kind 0 = 128 lanes x 8 B, 1 = 256 x 16 B, 2 = 256 x 8 B; data vector i of
+// stripe s at a + s*dss + i*vec, output j at b + s*pss + j*vec (split layout:
+// b a separate region; interleaved: b = a + k*vec, dss = pss = (k+m)*vec).
+extern "C" int probe_km_g(int kind, int k, int m, void* a, void* b, uint64_t vec, uint64_t dss, uint64_t pss,
+                          int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+#define KMG(K, M, BS, BPL) do { const uint64_t cps = vec / (BS * BPL); \
+    hipLaunchKernelGGL((kb_pattern_g<K, M, BS, BPL>), dim3(cps * nstripes), dim3(BS), 0, st, (const uint8_t*)a, \
+                       (uint8_t*)b, vec, dss, pss, cps); } while (0)
+#define KMK(K, M) if (k == K && m == M) { switch (kind) { case 0: KMG(K, M, 128, 8); break; \
+    case 1: KMG(K, M, 256, 16); break; case 2: KMG(K, M, 256, 8); break; default: return -1; } \
+    return hipGetLastError(); }
+    KMK(10, 4) KMK(16, 4) KMK(12, 4) KMK(20, 4)
+#undef KMK
+#undef KMG
+    return -1;
+}
+
+// Update / Replace access pattern: K input vectors read, M output vectors read
+// and written back in place (XOR for the math), BS lanes x BPL bytes per
+// vector per workgroup; stripes interleaved [S][d+p][vec] with inputs at
+// base + s*sstride + in_off + i*vec and outputs at base + s*sstride + out_off + j*vec.
+template <int K, int M, int BS, int BPL>
+__global__ __launch_bounds__(BS) void kb_rmw(uint8_t* base, uint64_t vec, uint64_t sstride, uint64_t in_off,
+                                             uint64_t out_off, uint64_t cps) {
+    const uint64_t s = blockIdx.x / cps, cb = blockIdx.x % cps;
+    const uint32_t off = (uint32_t)(cb * (BS * BPL) + threadIdx.x * BPL);
+    uint8_t* st = base + s * sstride;
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    if constexpr (BPL == 16) {
+        u32x4 x[K], y[M];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(st + in_off + i * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+        for (int j = 0; j < M; ++j) y[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(st + out_off + j * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) y[j] ^= x[i];
+            __builtin_amdgcn_raw_buffer_store_b128(y[j], rsrc(st + out_off + j * vec, (uint32_t)vec), off, 0, 2);
+        }
+    } else {
+        u32x2 x[K], y[M];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b64(rsrc(st + in_off + i * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+        for (int j = 0; j < M; ++j) y[j] = __builtin_amdgcn_raw_buffer_load_b64(rsrc(st + out_off + j * vec, (uint32_t)vec), off, 0, 2);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) y[j] ^= x[i];
+            __builtin_amdgcn_raw_buffer_store_b64(y[j], rsrc(st + out_off + j * vec, (uint32_t)vec), off, 0, 2);
+        }
+    }
+}
+
+// kind: 0 = 128 lanes x 8 B, 1 = 256 x 16 B; k = 1 (Replace rn=1) or 2 (Update: old, new), m = 4
+extern "C" int probe_rmw(int kind, int k, void* base, uint64_t vec, uint64_t sstride, uint64_t in_off, uint64_t out_off,
+                         int nstripes, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+#define RMW(K, BS, BPL) do { const uint64_t cps = vec / (BS * BPL); \
+    hipLaunchKernelGGL((kb_rmw<K, 4, BS, BPL>), dim3(cps * nstripes), dim3(BS), 0, st, (uint8_t*)base, vec, sstride, \
+                       in_off, out_off, cps); } while (0)
+    if (k == 1) { if (kind == 0) RMW(1, 128, 8); else RMW(1, 256, 16); }
+    else if (k == 2) { if (kind == 0) RMW(2, 128, 8); else RMW(2, 256, 16); }
+    else return -1;
+#undef RMW
+    return hipGetLastError();
+}
+
 // Counter calibration (MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are
 // calibrated only for 16-B-per-lane streams): one pass over `bytes` with each
 // access width, buffer nt like the codec kernels.  Distinct kernel names so

@@ -223,6 +223,37 @@ def pattern_probes(L, a, n, vp, sp, timeit):
                                                   ctypes.c_uint64((k + m) * vec), S, k, m, sp),
                        S * (k + m) * vec, iters=20)
         return
+    if os.environ.get("PROBE_KMG", "0") == "1":
+        # round 4: the 16+4 / 12+4 / 20+4 encode patterns against 10+4, split and interleaved,
+        # at the library's two geometries (128 x 8 B, 256 x 16 B) and 256 x 8 B; and the
+        # Replace rn=1 / Update read-modify-write pattern at 8 KiB (10+4 stripes)
+        import torch
+        L.probe_km_g.restype = ctypes.c_int
+        L.probe_rmw.restype = ctypes.c_int
+        vec = 1 << 20
+        b = torch.empty(256 * 4 * vec, dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            for k, m in ((10, 4), (12, 4), (16, 4), (20, 4)):
+                S = min(256, int(n // ((k + m) * vec)))
+                for kind, gname in ((0, "128x8B"), (1, "256x16B"), (2, "256x8B")):
+                    timeit(f"{k}+{m} split {gname}",
+                           lambda: L.probe_km_g(kind, k, m, vp(a), vp(b), ctypes.c_uint64(vec),
+                                                ctypes.c_uint64(k * vec), ctypes.c_uint64(m * vec), S, sp),
+                           S * (k + m) * vec, iters=20)
+                    timeit(f"{k}+{m} interleaved {gname}",
+                           lambda: L.probe_km_g(kind, k, m, vp(a), ctypes.c_void_p(a.data_ptr() + k * vec),
+                                                ctypes.c_uint64(vec), ctypes.c_uint64((k + m) * vec),
+                                                ctypes.c_uint64((k + m) * vec), S, sp),
+                           S * (k + m) * vec, iters=20)
+            v8, S8 = 8192, 32768
+            assert S8 * 14 * v8 <= n
+            for k, name in ((1, "Replace rn=1"), (2, "Update")):
+                for kind, gname in ((0, "128x8B"), (1, "256x16B")):
+                    timeit(f"{name} 10+4 8KiB read-modify-write {gname}",
+                           lambda: L.probe_rmw(kind, k, vp(a), ctypes.c_uint64(v8), ctypes.c_uint64(14 * v8),
+                                               ctypes.c_uint64(0), ctypes.c_uint64(10 * v8), S8, sp),
+                           S8 * (k + 8) * v8, iters=20)
+        return
     if os.environ.get("PROBE_KM", "0") == "1":
         vec = 1 << 20
         for k, m in ((1, 1), (2, 2), (4, 4), (7, 7), (10, 10), (4, 0), (10, 0), (14, 0), (10, 2), (10, 4), (12, 4), (6, 3)):
