@@ -95,7 +95,10 @@ int g_jit_layout = [] {
     return e ? (std::atoi(e) == 1 ? 1 : 0) : 0;
 }();
 int g_jit_group_waves = 4;
-AsmShape jit_shape(int rows) { return asm_shape(rows, g_jit_layout, g_jit_group_waves); }
+// rs_tune("jit_path_rows", 1..16): rows per code path of generated kernels of
+// more than 16 rows (each row holds 8 VGPR accumulators)
+int g_jit_path_rows = 16;
+AsmShape jit_shape(int rows) { return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows); }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // rs_tune("jit_backend", 2 | 1 | 0): machine code encoded directly into a
 // code-object template (jit_asm.cpp) | the same kernel as assembly text
@@ -821,6 +824,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_backend ? g_jit_waves : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_layout : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_group_waves : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_path_rows : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -853,6 +857,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(backend ? g_jit_waves : 0);
     key += static_cast<char>(backend ? g_jit_layout : 0);
     key += static_cast<char>(backend ? g_jit_group_waves : 0);
+    key += static_cast<char>(backend ? g_jit_path_rows : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);

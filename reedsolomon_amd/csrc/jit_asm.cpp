@@ -426,8 +426,8 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     Layout L;
     L.pf = pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
-    L.sub = L.slots_end;        // 2 x 15 subset registers (index by half * 15 + m - 1; singles unused)
-    L.acc = L.sub + 30;
+    L.sub = L.slots_end;        // 2 x 11 subset registers: the XORs of 2-4 planes of each half
+    L.acc = L.sub + 22;
     L.vgprs = L.acc + 8 * rw;
     if (vgprs_out) *vgprs_out = L.vgprs;
 
@@ -607,7 +607,12 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         };
         stage(0, 0);
         for (int c = 0; c < L.pf && c < cols; ++c) issue_col(c);
-        auto sub_reg = [&](int half, int m) { return L.sub + half * 15 + m - 1; };
+        // subset m of a half (2-4 of its planes) -> one of 11 registers (the
+        // single planes stay where the transpose left them)
+        auto sub_reg = [&](int half, int m) {
+            static const int8_t kIdx[16] = {-1, -1, -1, 0, -1, 1, 2, 3, -1, 4, 5, 6, 7, 8, 9, 10};
+            return L.sub + half * 11 + kIdx[m];
+        };
         auto acc_reg = [&](int r, int i) { return L.acc + 8 * r + i; };
         for (int c = 0; c < cols; ++c) {
             vmem_wait_for(col_id[static_cast<size_t>(c)]);

@@ -44,9 +44,10 @@ struct AsmShape {
     int rw = 1;   // rows per code path
     int groups = 1;  // layout 1: row groups G (= code paths)
 };
-inline AsmShape asm_shape(int rows, int layout, int group_waves) {
+inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16) {
     AsmShape s;
-    const int paths = rows <= 16 ? 1 : (rows + 15) / 16;
+    const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
+    const int paths = rows <= 16 ? 1 : (rows + pr - 1) / pr;
     s.layout = layout == 1 ? 1 : 0;
     s.rw = (rows + paths - 1) / paths;
     s.nw = s.layout ? (group_waves < 1 ? 1 : group_waves > 8 ? 8 : group_waves) : paths;
@@ -55,6 +56,8 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves) {
 }
 // Waves per workgroup of layout 0 (16 rows per wave at most).
 inline int asm_waves(int rows) { return asm_shape(rows, 0, 1).nw; }
+// (path_rows: products of more than 16 rows run in code paths of at most
+// this many rows - fewer rows, fewer VGPRs, more waves per SIMD)
 
 // The assembly source of the kernel for a rows x cols matrix (row-major),
 // accumulate (XOR into the outputs) or overwrite, split as `shape` says,

@@ -68,6 +68,7 @@ SWEEP = {
     "jit_backend": [0, 1, 2],
     "jit_layout": [1, 0],
     "jit_group_waves": [2, 8, 4],
+    "jit_path_rows": [5, 11, 16],
     "table_registry_max": [1, 1 << 14],
 }
 

@@ -62,7 +62,7 @@ def test_asm_kernel_row_group_layout(rslib, orc, rows, cols, acc, gw):
         L.rs_tune(b"jit_group_waves", 4)
 
 
-def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4):
+def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4, paths=None):
     rng = np.random.default_rng(rows * 1000 + cols * 10 + acc)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
     src = rslib.jit_asm_source(mat, bool(acc))
@@ -81,7 +81,8 @@ def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4):
     ids = mem.alloc(4 * S)
     mem.view(ids, 4 * S).view(np.uint32)[:] = np.arange(S)[::-1]
     from reedsolomon_amd.rs import lib  # noqa: F401  (library loaded by the fixture)
-    paths = 1 if rows <= 16 else (rows + 15) // 16
+    if paths is None:
+        paths = 1 if rows <= 16 else (rows + 15) // 16
     if layout == 1:  # the library's launch rule (kernels.hip): ceil(chunk groups / 8) * 8 * row groups
         nw, cgs = gw, (body // 2048 + gw - 1) // gw
         grid = ((cgs + 7) // 8 * 8 * paths, S)
@@ -143,3 +144,17 @@ def test_machine_code_equals_assembler(rslib, rows, cols, acc, pf, sync, layout)
         L.rs_tune(b"jit_sync", 0)
         L.rs_tune(b"jit_layout", 0)
     assert n > 0 and n % 4 == 0
+
+
+@pytest.mark.parametrize("rows,cols,acc,path_rows,layout", [(40, 9, 0, 11, 0), (33, 5, 1, 8, 1), (20, 3, 0, 7, 0)])
+def test_asm_kernel_path_rows(rslib, orc, rows, cols, acc, path_rows, layout):
+    """rs_tune("jit_path_rows", n): products of more than 16 rows in code
+    paths of n rows (fewer VGPRs per wave), either layout, against the oracle."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_path_rows", path_rows) == 0 and L.rs_tune(b"jit_layout", layout) == 0
+    try:
+        paths = (rows + path_rows - 1) // path_rows
+        _check_kernel(rslib, orc, rows, cols, acc, layout=layout, gw=4, paths=paths)
+    finally:
+        L.rs_tune(b"jit_path_rows", 16)
+        L.rs_tune(b"jit_layout", 0)

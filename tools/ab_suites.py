@@ -53,6 +53,17 @@ SUITES = {
                 ["jit_layout=0", "jit_layout=1,jit_group_waves=2", "jit_layout=1,jit_group_waves=4",
                  "jit_layout=1,jit_group_waves=8"])
                for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
+    # round 4: occupancy of the wide generated kernels (VALU-latency bound at 2 waves per SIMD:
+    # profiles/r04/pmc_icache): the 2-wave cap off, fewer columns of loads in flight, fewer rows per path
+    "wide_occupancy": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
+                        ["jit_waves=2", "jit_waves=0", "jit_waves=0,jit_pf=1", "jit_waves=0,jit_path_rows=13,jit_pf=2",
+                         "jit_waves=0,jit_path_rows=11,jit_pf=1", "jit_waves=0,jit_path_rows=10,jit_pf=2",
+                         "jit_waves=0,jit_path_rows=8"])
+                       for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
+    # round 4: 3-4 rows over more than 4 runtime columns, 16-byte units on 256 lanes (default since
+    # round 1) vs 8-byte units on 128 lanes (var=201, experiments build), split and interleaved
+    "wide34_r4": shapes([(16, 4), (20, 4), (8, 4), (6, 3), (9, 3), (16, 3)],
+                        ["", "var=201", "layout=inter", "var=201,layout=inter"], AB_ROUNDS="8"),
     # round 4: the weakest 4-row shapes (16+4 Encode, Replace of 1 row, Update at 8 KiB) at the
     # library's lane widths; their XOR-only access-pattern ceilings: hbm_probe.py PROBE_KMG=1
     "gap16_4": [(dict(AB_K="16", AB_M="4"), ["", "layout=inter", "lane_bytes=16", "lane_bytes=16,layout=inter",
