@@ -389,8 +389,14 @@ constexpr int kSgprs = 34;
 // VGPRs
 constexpr int kVTid = 0;       // work-item id
 constexpr int kVOff = 1;       // lane's byte offset in the vectors (chunk * 2048 + 8 * lane)
-constexpr int kVT0 = 2, kVT1 = 3;  // transpose temporaries
-constexpr int kVSlots = 4;     // pf slots of 8 (64-bit aligned pairs)
+// Transpose temporaries: the work-item id's register once the prologue has
+// used it, and the last subset register (subsets are dead while columns and
+// outputs are transposed, and no load ever targets it: the old outputs of
+// accumulate mode go to slot registers 0-15 of the subset region at most).
+// Two VGPRs fewer than dedicated temporaries: 16-row paths with two columns
+// of loads in flight fit 168 VGPRs, i.e. 3 waves per SIMD without the cap.
+constexpr int kVT0 = 0;
+constexpr int kVSlots = 2;     // pf slots of 8 (64-bit aligned pairs)
 
 const uint32_t kMasks[6] = {0x0F0F0F0Fu, 0xF0F0F0F0u, 0x33333333u, 0xCCCCCCCCu, 0x55555555u, 0xAAAAAAAAu};
 
@@ -400,12 +406,12 @@ struct Layout {
 
 // In-place 8x8 bit transpose of v[r[0]..r[7]] (bs_transpose8, kernels.hip):
 // swap(a, b, s, m): b = (m & (a >> s)) | (~m & b); a = ((m << s) & (b << s)) | (~(m << s) & a)
-void transpose8(Prog& P, const int (&r)[8]) {
+void transpose8(Prog& P, const int (&r)[8], int t1) {
     auto swap = [&](int a, int b, int s, int mi) {
         P.v_op2(kVLshr, kVT0, C(s), a);
-        P.v_op2(kVLshl, kVT1, C(s), b);
+        P.v_op2(kVLshl, t1, C(s), b);
         P.v_bfi(b, kSMask + mi, V(kVT0), V(b));
-        P.v_bfi(a, kSMask + mi + 1, V(kVT1), V(a));
+        P.v_bfi(a, kSMask + mi + 1, V(t1), V(a));
     };
     for (int i = 0; i < 4; ++i) swap(r[i], r[i + 4], 4, 0);
     swap(r[0], r[2], 2, 2);
@@ -428,6 +434,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     L.slots_end = kVSlots + 8 * L.pf;
     L.sub = L.slots_end;        // 2 x 11 subset registers: the XORs of 2-4 planes of each half
     L.acc = L.sub + 22;
+    const int kVT1 = L.sub + 21;  // (see kVT0)
     L.vgprs = L.acc + 8 * rw;
     if (vgprs_out) *vgprs_out = L.vgprs;
 
@@ -618,7 +625,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
             vmem_wait_for(col_id[static_cast<size_t>(c)]);
             int pr[8];
             for (int j = 0; j < 8; ++j) pr[j] = slot_reg(c, j);
-            transpose8(P, pr);
+            transpose8(P, pr, kVT1);
             // subsets of each half used by this column's rows
             int reg[2][16];
             for (int half = 0; half < 2; ++half) {
@@ -691,11 +698,11 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
             for (int j = 0; j < 8; ++j) pr[j] = acc_reg(r, j);
             if (acc) {
                 issue_old(r);
-                transpose8(P, pr);
+                transpose8(P, pr, kVT1);
                 vmem_wait_for(old_id[static_cast<size_t>(r)]);
                 for (int j = 0; j < 8; ++j) P.v_op2(kVXor, pr[j], V(pr[j]), old_reg(r, j));
             } else {
-                transpose8(P, pr);
+                transpose8(P, pr, kVT1);
             }
             for (int k = 0; k < 4; ++k) {
                 P.buf_store2(pr[2 * k], kVOff, kSDescOut, 512 * k);
