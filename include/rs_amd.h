@@ -500,6 +500,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "jit_group_waves" (layout 1: waves per workgroup, 1..8; default 4),
  * "jit_path_rows" (generated kernels of more than 16 rows: rows per code
  * path, 1..16, each row 8 VGPR accumulators; default 16),
+ * "jit_wide_pf", "jit_wide_waves" (jit_pf and jit_waves of the generated
+ * kernels of more than 16 rows; defaults 2 and 3: their 16-row paths fit 168
+ * VGPRs, so 3 waves share a SIMD; jit_pf / jit_waves apply to 1-16 rows),
  * "jit_backend" (2 default: kernels generated as gfx950 machine code and
  * copied into a code-object template, up to 128 output rows x 256 columns |
  * 1: the same kernels as assembly text assembled by comgr, 12 ms - 1.7 s per

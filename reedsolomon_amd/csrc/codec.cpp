@@ -601,6 +601,8 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_layout") g_jit_layout = value == 1 ? 1 : 0;
         else if (n == "jit_group_waves") g_jit_group_waves = value < 1 ? 1 : value > 8 ? 8 : value;
         else if (n == "jit_path_rows") g_jit_path_rows = value < 1 ? 1 : value > 16 ? 16 : value;
+        else if (n == "jit_wide_pf") g_jit_wide_pf = value < 1 ? 1 : value > 4 ? 4 : value;
+        else if (n == "jit_wide_waves") g_jit_wide_waves = value < 0 ? 0 : value > 8 ? 8 : value;
         else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;
         else if (n == "jit_backend") g_jit_backend = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);

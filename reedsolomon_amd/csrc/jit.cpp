@@ -100,6 +100,15 @@ int g_jit_group_waves = 4;
 int g_jit_path_rows = 16;
 AsmShape jit_shape(int rows) { return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows); }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
+// Generated kernels of more than 16 rows (several code paths): two columns of
+// loads in flight and at most 3 waves per SIMD (their 16-row paths fit 168
+// VGPRs then): 32+32 Encode +4 %, 64+64 +7 %, 128+128 +5 % over the
+// single-path settings, which lose 2.5 % on 16+16 (profiles/r04/ab_wide_waves3.log);
+// rs_tune("jit_wide_pf") / ("jit_wide_waves")
+int g_jit_wide_pf = 2;
+int g_jit_wide_waves = 3;
+int jit_pf_for(int rows) { return rows > 16 ? g_jit_wide_pf : g_jit_pf; }
+int jit_waves_for(int rows) { return rows > 16 ? g_jit_wide_waves : g_jit_waves; }
 // rs_tune("jit_backend", 2 | 1 | 0): machine code encoded directly into a
 // code-object template (jit_asm.cpp) | the same kernel as assembly text
 // assembled by comgr | hiprtc C++; env RSAMD_JIT_BACKEND
@@ -723,10 +732,10 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
     if (!mat || rows < 1 || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
     Compiled c =
-        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, jit_shape(rows), g_jit_pf, g_jit_sync,
-                                                  g_jit_waves)
-        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, jit_shape(rows), g_jit_pf, g_jit_sync,
-                                                    g_jit_waves, nullptr))
+        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, jit_shape(rows), jit_pf_for(rows),
+                                                  g_jit_sync, jit_waves_for(rows))
+        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, jit_shape(rows), jit_pf_for(rows),
+                                                    g_jit_sync, jit_waves_for(rows), nullptr))
                            : compile(jit_source(mat, rows, cols, accumulate));
     if (ms) *ms = c.ms;
     if (!c.ok) std::fprintf(stderr, "librsamd: jit compile check failed: %s\n", c.log.substr(0, 4000).c_str());
@@ -739,11 +748,12 @@ int jit_encoder_check(const uint8_t* mat, int rows, int cols, bool accumulate, s
     std::vector<uint32_t> bin;
     int used = 0;
     std::string err;
-    if (!asm_binary(mat, rows, cols, accumulate, sh, g_jit_pf, g_jit_sync, &bin, &used, &err)) {
+    if (!asm_binary(mat, rows, cols, accumulate, sh, jit_pf_for(rows), g_jit_sync, &bin, &used, &err)) {
         std::fprintf(stderr, "librsamd: encoder failed: %s\n", err.c_str());
         return RS_ERR_DEVICE;
     }
-    Compiled c = compile_asm(asm_source(mat, rows, cols, accumulate, sh, g_jit_pf, g_jit_sync, g_jit_waves, nullptr));
+    Compiled c = compile_asm(
+        asm_source(mat, rows, cols, accumulate, sh, jit_pf_for(rows), g_jit_sync, jit_waves_for(rows), nullptr));
     std::vector<char> text;
     if (!c.ok || !asm_text_section(c.code, &text)) {
         std::fprintf(stderr, "librsamd: encoder check: assembly failed: %s\n", c.log.substr(0, 2000).c_str());
@@ -819,9 +829,9 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(a.accumulate ? 1 : 0);
     k.text += static_cast<char>(a.rows);
     k.text += static_cast<char>(a.cols);
-    k.text += static_cast<char>(g_jit_pf);
+    k.text += static_cast<char>(g_jit_backend ? jit_pf_for(a.rows) : g_jit_pf);
     k.text += static_cast<char>(g_jit_backend ? g_jit_sync : 0);
-    k.text += static_cast<char>(g_jit_backend ? g_jit_waves : 0);
+    k.text += static_cast<char>(g_jit_backend ? jit_waves_for(a.rows) : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_layout : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_group_waves : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_path_rows : 0);
@@ -852,9 +862,9 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(a.rows >> 8);
     key += static_cast<char>(a.cols);
     key += static_cast<char>(a.cols >> 8);
-    key += static_cast<char>(g_jit_pf);
+    key += static_cast<char>(backend ? jit_pf_for(a.rows) : g_jit_pf);
     key += static_cast<char>(backend ? g_jit_sync : 0);
-    key += static_cast<char>(backend ? g_jit_waves : 0);
+    key += static_cast<char>(backend ? jit_waves_for(a.rows) : 0);
     key += static_cast<char>(backend ? g_jit_layout : 0);
     key += static_cast<char>(backend ? g_jit_group_waves : 0);
     key += static_cast<char>(backend ? g_jit_path_rows : 0);
@@ -923,12 +933,12 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                 e->rows = a.rows;
                 e->cols = a.cols;
                 e->acc = a.accumulate != 0;
-                e->pf = g_jit_pf;
+                e->pf = jit_pf_for(a.rows);
                 e->sync = g_jit_sync;
-                e->waves = g_jit_waves;
+                e->waves = jit_waves_for(a.rows);
             } else {
-                e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->shape, g_jit_pf,
-                                                g_jit_sync, g_jit_waves, nullptr)
+                e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->shape,
+                                                jit_pf_for(a.rows), g_jit_sync, jit_waves_for(a.rows), nullptr)
                                    : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             }
             if (backend != 2 && g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
@@ -1045,7 +1055,8 @@ JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
 
 int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out) {
     if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
-    *out = asm_source(mat, rows, cols, accumulate, jit_shape(rows), g_jit_pf, g_jit_sync, g_jit_waves, nullptr);
+    *out = asm_source(mat, rows, cols, accumulate, jit_shape(rows), jit_pf_for(rows), g_jit_sync, jit_waves_for(rows),
+                      nullptr);
     return RS_OK;
 }
 

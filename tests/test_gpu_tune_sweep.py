@@ -69,6 +69,8 @@ SWEEP = {
     "jit_layout": [1, 0],
     "jit_group_waves": [2, 8, 4],
     "jit_path_rows": [5, 11, 16],
+    "jit_wide_pf": [1, 3, 2],
+    "jit_wide_waves": [0, 2, 3],
     "table_registry_max": [1, 1 << 14],
 }
 

@@ -58,14 +58,23 @@ SUITES = {
     "wide_occupancy": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
                         ["jit_waves=2", "jit_waves=0", "jit_waves=0,jit_pf=1", "jit_waves=0,jit_path_rows=13,jit_pf=2",
                          "jit_waves=0,jit_path_rows=11,jit_pf=1", "jit_waves=0,jit_path_rows=10,jit_pf=2",
-                         "jit_waves=0,jit_path_rows=8"])
+                         "jit_waves=0,jit_path_rows=8"])  # (before jit_wide_*: jit_pf / jit_waves applied to every row count)
                        for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
     # round 4: 16-row paths in 168 VGPRs at two columns of loads in flight (3 waves per SIMD
     # without the cap) against the capped default
     "wide_waves3": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
                      ["jit_waves=2", "jit_waves=0,jit_pf=2", "jit_waves=3,jit_pf=2", "jit_waves=0"])
                     for k, m, s in ((16, 16, 112), (32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))] +
-                   [(dict(AB_K="16", AB_M="16", AB_S="112"), ["op=rec16,jit_waves=2", "op=rec16,jit_waves=0,jit_pf=2"])],
+                   [(dict(AB_K="16", AB_M="16", AB_S="112"), ["op=rec24,jit_waves=2", "op=rec24,jit_waves=0,jit_pf=2"])],
+    # round 4: the 3-wave setting with the row-group layout
+    "wide_combo": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
+                    ["jit_wide_waves=2,jit_wide_pf=3", "", "jit_layout=1,jit_group_waves=2",
+                     "jit_layout=1,jit_group_waves=4", "jit_layout=1,jit_group_waves=3"])
+                   for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))] +
+                  [(dict(AB_K="32", AB_M="32", AB_S="56"),
+                    ["op=rec24,jit_wide_waves=2,jit_wide_pf=3", "op=rec24", "op=rec24,jit_layout=1,jit_group_waves=2",
+                     "layout=inter,op=rec24,jit_wide_waves=2,jit_wide_pf=3", "layout=inter,op=rec24",
+                     "layout=inter,op=rec24,jit_layout=1,jit_group_waves=2"])],
     # round 4: 3-4 rows over more than 4 runtime columns, 16-byte units on 256 lanes (default since
     # round 1) vs 8-byte units on 128 lanes (var=201, experiments build), split and interleaved
     "wide34_r4": shapes([(16, 4), (20, 4), (8, 4), (6, 3), (9, 3), (16, 3)],
