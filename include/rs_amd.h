@@ -497,7 +497,8 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * rows over the waves of a workgroup, all on the same 2 KiB chunk | 1 = row
  * groups of up to 16 rows over workgroups whose waves take consecutive
  * chunks with the same code, the row groups of a chunk on one XCD),
- * "jit_group_waves" (layout 1: waves per workgroup, 1..8; default 4),
+ * "jit_group_waves" (layout 1: waves per workgroup, 1, 2, 4 or 8 - other
+ * values round down; default 4),
  * "jit_path_rows" (generated kernels of more than 16 rows: rows per code
  * path, 1..16, each row 8 VGPR accumulators; default 16),
  * "jit_wide_pf", "jit_wide_waves" (jit_pf and jit_waves of the generated

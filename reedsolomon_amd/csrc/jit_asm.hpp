@@ -50,7 +50,8 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     const int paths = rows <= 16 ? 1 : (rows + pr - 1) / pr;
     s.layout = layout == 1 ? 1 : 0;
     s.rw = (rows + paths - 1) / paths;
-    s.nw = s.layout ? (group_waves < 1 ? 1 : group_waves > 8 ? 8 : group_waves) : paths;
+    // (layout 1: a power of two, the kernel maps chunks with shifts)
+    s.nw = s.layout ? (group_waves >= 8 ? 8 : group_waves >= 4 ? 4 : group_waves >= 2 ? 2 : 1) : paths;
     s.groups = s.layout ? paths : 1;
     return s;
 }

@@ -69,7 +69,7 @@ SUITES = {
     # round 4: the 3-wave setting with the row-group layout
     "wide_combo": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
                     ["jit_wide_waves=2,jit_wide_pf=3", "", "jit_layout=1,jit_group_waves=2",
-                     "jit_layout=1,jit_group_waves=4", "jit_layout=1,jit_group_waves=3"])
+                     "jit_layout=1,jit_group_waves=4"])
                    for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))] +
                   [(dict(AB_K="32", AB_M="32", AB_S="56"),
                     ["op=rec24,jit_wide_waves=2,jit_wide_pf=3", "op=rec24", "op=rec24,jit_layout=1,jit_group_waves=2",
