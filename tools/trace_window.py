@@ -27,11 +27,15 @@ def main():
     main_rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in main_rows]
     K, W = line["steps"], line["warmup"]
-    C = (line.get("cold") or {}).get("launches", 0)  # launches after the timed region (same grid)
-    end = len(dur) - C
+    # launches of the same grid after the timed region: the spread pass queued
+    # right behind it (round 4: `timed_spread`), then the `cold` launches
+    Sp = (line.get("timed_spread") or {}).get("n", 0) or 0
+    C = (line.get("cold") or {}).get("launches", 0)
+    end = len(dur) - C - Sp
     timed = dur[end - K:end]
     pre = dur[:end - (K + W)]
-    cold = dur[end:]
+    spread_pass = dur[end:end + Sp]
+    cold = dur[end + Sp:]
     alg = line["roofline"]["algorithmic_bytes_per_launch"]
     mean_t = statistics.mean(timed)
     out = {
@@ -44,6 +48,9 @@ def main():
         "warmup_mean_ms": round(statistics.mean(dur[end - (K + W):end - K]), 4) if W else None,
         "cold": {"launches": len(cold), "mean_ms": round(statistics.mean(cold), 4) if cold else None,
                  "line_mean_ms": (line.get("cold") or {}).get("mean_ms")},
+        "spread_pass": {"launches": len(spread_pass),
+                        "mean_ms": round(statistics.mean(spread_pass), 4) if spread_pass else None,
+                        "line_median_ms": (line.get("timed_spread") or {}).get("median_ms")},
         "prewarm": {"launches": len(pre), "first_10_ms": [round(x, 3) for x in pre[:10]],
                     "max_ms": round(max(pre), 4) if pre else None,
                     "last_20_mean_ms": round(statistics.mean(pre[-20:]), 4) if len(pre) >= 20 else None},
@@ -64,7 +71,7 @@ def main():
             w.writerow(["Phase", "Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs", "StdDev",
                         "AlgorithmicBytesPerCall", "FracOf8TBps"])
             for phase, xs in (("timed", timed), ("warmup", dur[end - (K + W):end - K]), ("prewarm", pre),
-                              ("cold", cold)):
+                              ("spread_pass", spread_pass), ("cold", cold)):
                 if not xs:
                     continue
                 ns = [x * 1e6 for x in xs]
