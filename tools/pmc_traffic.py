@@ -5,6 +5,7 @@
     python tools/pmc_traffic.py run enc:64+64                  # the workload (5 launches)
     python tools/pmc_traffic.py run rec:16+16:16 --jit 0        # Reconst of 16 lost
     python tools/pmc_traffic.py run inrec:10+8:8                # the same in place (interleaved layout)
+    python tools/pmc_traffic.py run enc:128+128@jit_layout=1,jit_group_waves=4   # rs_tune knobs first
     python tools/pmc_traffic.py summarize <tag> <dir_FETCH> <dir_WRITE> <calib_FETCH> <calib_WRITE>
 
 `run` encodes (or rebuilds) ~3.5 GiB of 1 MiB-vector stripes on the split
@@ -31,11 +32,15 @@ def run(spec, jit):
 
     import reedsolomon_amd as rs
 
+    spec, _, knobs = spec.partition("@")
     op, shape, *rest = spec.split(":")
     k, m = (int(x) for x in shape.split("+"))
     vec = 1 << 20
     S = max(1, (3584 << 20) // ((k + m) * vec))
     assert rs.lib().rs_tune(b"jit", jit) == 0
+    for kv in filter(None, knobs.split(",")):
+        name, val = kv.split("=")
+        assert rs.lib().rs_tune(name.encode(), int(val)) == 0, kv
     r = rs.New(k, m)
     g = torch.Generator(device="cuda").manual_seed(7)
     data = torch.randint(0, 256, (S, k, vec), dtype=torch.uint8, device="cuda", generator=g)

@@ -16,7 +16,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
       python3 "$REPO/tools/fetch_calib.py" > "$OUT/calib_$C.log" 2>&1 || { echo "calib $C failed"; exit 1; }
 done
 for SPEC in "$@"; do
-  tag="${SPEC//[:+]/_}"
+  tag="${SPEC//[:+@=,]/_}"
   for C in FETCH_SIZE WRITE_SIZE; do
     echo "== $SPEC $C"
     timeout -s KILL 90 rocprofv3 --pmc $C -d "$OUT/${tag}_$C" -o pmc --output-format csv -- \
@@ -26,4 +26,4 @@ for SPEC in "$@"; do
   python3 "$REPO/tools/pmc_traffic.py" summarize "$SPEC" "$OUT/${tag}_FETCH_SIZE" "$OUT/${tag}_WRITE_SIZE" \
       "$OUT/calib_FETCH_SIZE" "$OUT/calib_WRITE_SIZE" "$alg" | tee "$OUT/traffic_$tag.json"
 done
-bash "$REPO/tools/pmc_icache.sh" "$@"
+[ "${PMC_WIDE_SQ:-1}" = 0 ] || bash "$REPO/tools/pmc_icache.sh" "$@"
