@@ -2,7 +2,13 @@
 """Concurrency stress on one GPU: T threads for S seconds, random operations
 on shared and private handles, every result checked against the CPU oracle.
 
-    python tools/gpu_stress.py [threads=8] [seconds=90]
+    python tools/gpu_stress.py [threads=8] [seconds=90] [jit=policy|all]
+
+jit=policy keeps the library's default compile policy (machine-code
+networks once a matrix's launches would pay for one); jit=all compiles
+every matrix on the launching thread at its first launch (rs_tune jit 2),
+which with the random erasure sets below passes the 256-matrix cap and
+exercises eviction under concurrent launches.
 
 Mix per iteration (one of):
   host  - Go-API calls on pageable numpy vectors (Encode / Reconst / Update /
@@ -31,16 +37,17 @@ import torch  # noqa: E402
 import reedsolomon_amd as rs  # noqa: E402
 from oracle import oracle as orc  # noqa: E402  (checker only)
 
-SHAPES = [(10, 4), (12, 4), (10, 8), (6, 3), (20, 8), (16, 8), (8, 6)]
+SHAPES = [(10, 4), (12, 4), (10, 8), (6, 3), (20, 8), (16, 8), (8, 6), (16, 16), (32, 24)]
 
 
 def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     SECS = float(sys.argv[2]) if len(sys.argv) > 2 else 90.0
+    MODE = sys.argv[3] if len(sys.argv) > 3 else "policy"
     orc.build()
     assert torch.cuda.is_available()
-    rs.lib().rs_tune(b"jit_min_bytes", 0)
-    rs.lib().rs_tune(b"jit_min_launches", 1)  # compile every matrix on first sight: hammer the compile path
+    if MODE == "all":  # compile every matrix on first sight: hammer the compile and eviction paths
+        assert rs.lib().rs_tune(b"jit", 2) == 0
     shared = {s: rs.New(*s) for s in SHAPES}
     lock = threading.Lock()
     stats = {"host": 0, "dev": 0, "multi": 0, "errors": []}
@@ -164,7 +171,7 @@ def main():
                   f"{len(stats['errors'])} errors", flush=True)
     for t in th:
         t.join()
-    out = {"threads": T, "seconds": SECS, "host": stats["host"], "dev": stats["dev"], "multi": stats["multi"],
+    out = {"threads": T, "seconds": SECS, "jit_mode": MODE, "host": stats["host"], "dev": stats["dev"], "multi": stats["multi"],
            "errors": stats["errors"][:20], "jit": rs.jit_stats()}
     print(json.dumps(out), flush=True)
     sys.exit(1 if stats["errors"] else 0)
