@@ -470,8 +470,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
  * when the L1D is unknown; 0 default = the re-encode definition everywhere;
  * see DESIGN.md §4 "Reference defect"),
- * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit), "host_chunk" (bytes;
- * host-memory call staging), "host_coalesce_max" (bytes per vector up to which
+ * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit, the default since
+ * round 4: every synchronous host call takes the chunked zero-copy pipeline),
+ * "host_chunk" (bytes; host-memory call staging), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),
  * "host_coalesce_linger_us" (a ready shared batch waits this long for more
  * callers before it launches; default 0), "host_coalesce_running" (shared

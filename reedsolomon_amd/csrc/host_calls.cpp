@@ -25,9 +25,13 @@ namespace detail {
 size_t g_pinned_max = 256 * 1024;
 // Host calls on vectors up to this size take the chunked zero-copy pipeline
 // (host_matmul: the kernel reads and writes the pinned mirror over PCIe, no
-// DMA set-up either way); larger ones the runtime's pageable copies, which
-// measured 7 % faster at 4 MiB (profiles/r01/host_latency.log).
-size_t g_zc_max = 2 * 1024 * 1024;
+// DMA set-up either way); larger ones the staged path (device staging slots,
+// DMA through the pinned bounce buffer).  Round 1 measured the runtime's
+// pageable copies 7 % faster than the pipeline at 4 MiB and set 2 MiB here;
+// since the bounce buffer replaced those copies (round 3) the staged path is
+// the slower one at every size (4 MiB Encode 2,267-2,448 vs 1,592-1,939 us,
+// profiles/r04/host_zc_threshold.log), so there is no limit by default.
+size_t g_zc_max = SIZE_MAX;
 
 bool use_pinned(rs_t* rs, int slots, size_t pitch) {
     if (pitch > g_pinned_max) return false;

@@ -988,7 +988,7 @@ def test_host_calls_staging_paths(rslib, orc, torch_dev, mode):
             for j in range(p):
                 assert np.array_equal(par[j], ora[j]), (size, j)
     finally:
-        for k, v in {"host_chunk": 128 << 10, "host_zc_max": 2 << 20, "host_pinned_max": 256 << 10}.items():
+        for k, v in {"host_chunk": 128 << 10, "host_zc_max": -1, "host_pinned_max": 256 << 10}.items():
             L.rs_tune(k.encode(), v)
 
 

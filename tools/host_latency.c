@@ -10,6 +10,9 @@
  *   calls then run zero-copy over the caller's memory)
  *   HL_ENGINE=0/1: the resident host-call engine off / on (default on);
  *   HL_ENGINE_WAVES=n: its workgroups
+ *   HL_ZC_MAX / HL_PINNED_MAX / HL_CHUNK=bytes: rs_tune host_zc_max /
+ *   host_pinned_max / host_chunk (as the positional arguments);
+ *   HL_SIZES=a,b,...: these vector sizes instead of 4 KiB..4 MiB;
  *   HL_VEC=bytes: only this vector size; HL_OPS=mask: only these ops (bit 0
  *   Encode, 1 Reconst lost=1, 2 Reconst lost=4, 3 Update, 4 Replace)
  *   HL_VRAM=0/1: engine call slots and input staging in host-writable device
@@ -87,14 +90,25 @@ static void report(const char* op, size_t vec, double bytes, int reps) {
 }
 
 int main(int argc, char** argv) {
-    static const size_t sizes[] = {4096, 8192, 65536, 262144, 1048576, 4194304};
+    size_t sizes[16] = {4096, 8192, 65536, 262144, 1048576, 4194304};
+    size_t nsizes = 6;
     rs_t* rs = NULL;
     size_t si;
+    if (getenv("HL_SIZES")) {
+        char buf[256], *tok;
+        strncpy(buf, getenv("HL_SIZES"), sizeof buf - 1);
+        buf[sizeof buf - 1] = 0;
+        nsizes = 0;
+        for (tok = strtok(buf, ","); tok && nsizes < 16; tok = strtok(NULL, ",")) sizes[nsizes++] = (size_t)atol(tok);
+    }
     if (argc >= 3) {
         rs_tune("host_zc_max", atoi(argv[1]));
         rs_tune("host_pinned_max", atoi(argv[2]));
     }
     if (argc >= 4) rs_tune("host_chunk", atoi(argv[3]));
+    if (getenv("HL_ZC_MAX")) rs_tune("host_zc_max", atoi(getenv("HL_ZC_MAX")));
+    if (getenv("HL_PINNED_MAX")) rs_tune("host_pinned_max", atoi(getenv("HL_PINNED_MAX")));
+    if (getenv("HL_CHUNK")) rs_tune("host_chunk", atoi(getenv("HL_CHUNK")));
     if (getenv("HL_ENGINE")) rs_tune("host_engine", atoi(getenv("HL_ENGINE")));
     if (getenv("HL_ENGINE_MAX")) rs_tune("host_engine_max_bytes", atoi(getenv("HL_ENGINE_MAX")));  /* resident host-call engine on / off */
     if (getenv("HL_ENGINE_WAVES")) rs_tune("host_engine_waves", atoi(getenv("HL_ENGINE_WAVES")));
@@ -112,7 +126,7 @@ int main(int argc, char** argv) {
     if (rs_gen_matrix(rs, gen) != RS_OK) return 11;
     const long only_vec = getenv("HL_VEC") ? atol(getenv("HL_VEC")) : 0;
     const int ops = getenv("HL_OPS") ? atoi(getenv("HL_OPS")) : 31;
-    for (si = 0; si < sizeof sizes / sizeof sizes[0]; ++si) {
+    for (si = 0; si < nsizes; ++si) {
         const size_t vec = sizes[si];
         if (only_vec && (size_t)only_vec != vec) continue;
         const int reps = vec >= 4194304 ? REPS / 8 : (vec >= 262144 ? REPS / 4 : REPS);

@@ -303,9 +303,9 @@ def main():
         k, m = 10, 4
         r = rs.New(k, m)
         # (label, host_pinned_max, host_zc_max, host_engine); the library's
-        # defaults are 256 KiB / 2 MiB / engine on
-        modes = (("default: host-call engine up to 1 MiB", 256 << 10, 2 << 20, 1),
-                 ("engine off: chunked zero-copy pipeline", 256 << 10, 2 << 20, 0),
+        # defaults are 256 KiB / no limit / engine on
+        modes = (("default: host-call engine up to 1 MiB", 256 << 10, -1, 1),
+                 ("engine off: chunked zero-copy pipeline", 256 << 10, -1, 0),
                  ("engine off, staged: pinned mirror + DMA <= 4MiB", 4 << 20, 0, 0),
                  ("engine off, staged: pageable per-vector copies", 0, 0, 0))
         for label, pinned_max, zc_max, engine in modes:
@@ -337,7 +337,7 @@ def main():
                         assert all(np.array_equal(a, b) for a, b in zip(w, full))
                         rec(f"Reconst() host API 10+4 8KiB lost={len(lost)} ({label})", (k + len(lost)) * vec, t)
         L.rs_tune(b"host_pinned_max", 256 << 10)
-        L.rs_tune(b"host_zc_max", 2 << 20)
+        L.rs_tune(b"host_zc_max", -1)
         L.rs_tune(b"host_engine", 1)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     tag = "_".join(sys.argv[sys.argv.index("--only") + 1].split(",")) if "--only" in sys.argv else "all"
