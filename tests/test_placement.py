@@ -119,26 +119,24 @@ def test_placement_validation():
     assert plan == {0: ([2, 3, 4, 5], [0, 1]), 2: ([0, 1, 2, 3], [5])}  # first d survivors (rs.go)
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(300)
-def test_gather_reconst_hip_two_ranks(tmp_path, orc):
-    """tools/placement_demo.py: two ranks on cuda:0 (gloo), HIP decode.
-    Every rebuilt shard equals the CPU oracle's Reconst of the same stripe
-    (lost shards garbled, survivors intact: rs.go:221-380), not only the
-    HIP-encoded original, and the transfer plan's survivors of each stripe
-    are the first d by index, as the oracle's checkReconst picks them
-    (rs.go:264-335).  (The nccl / xGMI leg needs two GPUs: unmeasured here.)"""
+def _run_demo(tmp_path, nproc, backend, stripes):
     env = dict(os.environ, RSAMD_BENCH_DEVICE="0")
-    d, p = 10, 4
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(ROOT, "tools", "placement_demo.py"), "--backend", "gloo", "--stripes", "24",
-                        "--vec", "8192", "--dump", str(tmp_path)],
+                        os.path.join(ROOT, "tools", "placement_demo.py"), "--backend", backend, "--stripes",
+                        str(stripes), "--vec", "8192", "--dump", str(tmp_path)],
                        capture_output=True, text=True, timeout=280, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert r.stdout.count("placement_demo ok") == 2
+    assert r.stdout.count("placement_demo ok") == nproc
+
+
+def _check_dumps(tmp_path, nproc, orc, d=10, p=4):
+    """Every rebuilt shard equals the CPU oracle's Reconst of the same stripe
+    (lost shards garbled, survivors intact: rs.go:221-380), and the transfer
+    plan's survivors of each stripe are the first d by index, as the oracle's
+    checkReconst picks them (rs.go:264-335)."""
     total = 0
-    for rank in range(2):
+    for rank in range(nproc):
         z = np.load(tmp_path / f"rank{rank}.npz")
         full, masks = z["full"], z["masks"]
         for s, surv, lostm in zip(z["plan_stripes"], z["plan_surv"], z["plan_lost"]):
@@ -158,3 +156,23 @@ def test_gather_reconst_hip_two_ranks(tmp_path, orc):
             assert np.array_equal(got, expect[s][v]), (rank, s, v)
             total += 1
     assert total > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gather_reconst_hip_two_ranks(tmp_path, orc):
+    """tools/placement_demo.py: two ranks on cuda:0 (gloo), HIP decode, every
+    rebuilt shard and the plan checked against the oracle (_check_dumps).
+    (The nccl / xGMI leg between two GPUs needs a second GPU: unmeasured here.)"""
+    _run_demo(tmp_path, 2, "gloo", 24)
+    _check_dumps(tmp_path, 2, orc)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gather_reconst_nccl_one_rank(tmp_path, orc):
+    """The nccl (RCCL) code path of gather_reconst on the GPU: one rank, so
+    both all_to_all_single calls run through RCCL on device tensors (one GPU
+    cannot host two RCCL ranks); rebuilt shards and plan against the oracle."""
+    _run_demo(tmp_path, 1, "nccl", 16)
+    _check_dumps(tmp_path, 1, orc)
