@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# Same-box A/B of one synchronous 10+4 @ 8 KiB host call between the
+# Same-box A/B of one synchronous 10+4 host call (AB_SIZES, default 8 KiB;
+# AB_OPS host_latency's op mask) between the
 # current library and another build of it (default tools/_build/r03lib:
 # the round-3 tree built from its commit), alternating A B A B so box drift
 # hits both.  Every call's result is checked by tools/host_latency.c.
@@ -15,8 +16,8 @@ gcc -O2 -std=c99 -pthread -Iinclude tools/host_latency.c -L"$OTHER" -lrsamd \
 {
   for i in 1 2; do
     for v in host_latency host_latency_other; do
-      echo "# $v pageable ($i)"; timeout -k 10 120 env HL_VEC=8192 tools/_build/$v | grep '^{"op"'
-      echo "# $v registered ($i)"; timeout -k 10 120 env HL_VEC=8192 HL_REGISTER=1 tools/_build/$v | grep '^{"op"'
+      echo "# $v pageable ($i)"; timeout -k 10 120 env HL_SIZES="${AB_SIZES:-8192}" HL_OPS="${AB_OPS:-31}" tools/_build/$v | grep '^{"op"'
+      echo "# $v registered ($i)"; timeout -k 10 120 env HL_SIZES="${AB_SIZES:-8192}" HL_OPS="${AB_OPS:-31}" HL_REGISTER=1 tools/_build/$v | grep '^{"op"'
     done
   done
 } > gpurun_out/engine_ab.log 2>&1

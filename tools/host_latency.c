@@ -9,9 +9,12 @@
  *   HL_REGISTER=1: page-aligned vectors registered with rs_host_register (the
  *   calls then run zero-copy over the caller's memory)
  *   HL_ENGINE=0/1: the resident host-call engine off / on (default on);
+ *   HL_ENGINE_IDLE / HL_ENGINE_LIFE=us: its idle exit and lifetime;
  *   HL_ENGINE_WAVES=n: its workgroups
  *   HL_ZC_MAX / HL_PINNED_MAX / HL_CHUNK=bytes: rs_tune host_zc_max /
  *   host_pinned_max / host_chunk (as the positional arguments);
+ *   HL_GAP_US=us: idle time between calls (outside the timed region), so the
+ *   engine's idle exit is exercised as a sporadic caller would;
  *   HL_SIZES=a,b,...: these vector sizes instead of 4 KiB..4 MiB;
  *   HL_VEC=bytes: only this vector size; HL_OPS=mask: only these ops (bit 0
  *   Encode, 1 Reconst lost=1, 2 Reconst lost=4, 3 Update, 4 Replace)
@@ -48,6 +51,15 @@ static int cmp(const void* a, const void* b) {
 }
 
 static double t[REPS];
+static double g_gap_us;
+
+static void gap(void) {  /* idle the caller between calls (HL_GAP_US) */
+    if (g_gap_us > 0) {
+        const double end = now_us() + g_gap_us;
+        while (now_us() < end) {
+        }
+    }
+}
 static uint8_t gexp[512], glog[256], gen[P * D];
 static long checked;
 
@@ -117,6 +129,8 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE_POLL_GAP")) rs_tune("host_engine_poll_gap", atoi(getenv("HL_ENGINE_POLL_GAP")));
     if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
     if (getenv("HL_VRAM")) rs_tune("host_engine_vram", atoi(getenv("HL_VRAM")));
+    if (getenv("HL_ENGINE_IDLE")) rs_tune("host_engine_idle_us", atoi(getenv("HL_ENGINE_IDLE")));
+    if (getenv("HL_ENGINE_LIFE")) rs_tune("host_engine_life_us", atoi(getenv("HL_ENGINE_LIFE")));
     if (getenv("HL_SPLIT_ROWS")) rs_tune("host_engine_split_rows", atoi(getenv("HL_SPLIT_ROWS")));
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
@@ -125,6 +139,7 @@ int main(int argc, char** argv) {
     gf_init();
     if (rs_gen_matrix(rs, gen) != RS_OK) return 11;
     const long only_vec = getenv("HL_VEC") ? atol(getenv("HL_VEC")) : 0;
+    g_gap_us = getenv("HL_GAP_US") ? atof(getenv("HL_GAP_US")) : 0;
     const int ops = getenv("HL_OPS") ? atoi(getenv("HL_OPS")) : 31;
     for (si = 0; si < nsizes; ++si) {
         const size_t vec = sizes[si];
@@ -150,6 +165,7 @@ int main(int argc, char** argv) {
             for (k = 0; k < reps; ++k) {
                 double a;
                 for (i = D; i < N; ++i) memset(v[i], 0x5a, vec);
+                gap();
                 a = now_us();
                 if (rs_encode(rs, v, lens, N) != RS_OK) return 2;
                 t[k] = now_us() - a;
@@ -163,6 +179,7 @@ int main(int argc, char** argv) {
             for (k = 0; k < reps; ++k) {
                 double a;
                 memset(v[0], 0x77, vec);
+                gap();
                 a = now_us();
                 if (rs_reconst(rs, v, lens, N, NULL, 0, need, 1) != RS_OK) return 3;
                 t[k] = now_us() - a;
@@ -176,6 +193,7 @@ int main(int argc, char** argv) {
             for (k = 0; k < reps; ++k) {
                 double a;
                 for (i = 0; i < 4; ++i) memset(v[need[i]], 0x77, vec);
+                gap();
                 a = now_us();
                 if (rs_reconst(rs, v, lens, N, NULL, 0, need, 4) != RS_OK) return 4;
                 t[k] = now_us() - a;
@@ -191,6 +209,7 @@ int main(int argc, char** argv) {
             for (k = 0; k < reps; ++k) {
                 double a;
                 uint8_t* nw = (k & 1) ? saved[2] : saved[3];
+                gap();
                 a = now_us();
                 if (rs_update(rs, v[2], vec, nw, vec, 2, v + D, lens + D, P) != RS_OK) return 5;
                 t[k] = now_us() - a;
@@ -209,6 +228,7 @@ int main(int argc, char** argv) {
                 size_t b;
                 int j;
                 for (j = 0; j < P; ++j) memcpy(saved[D + j], v[D + j], vec);
+                gap();
                 a = now_us();
                 if (rs_replace(rs, (const uint8_t* const*)v, lens, 1, rows, 1, v + D, lens + D, P) != RS_OK)
                     return 6;
