@@ -458,7 +458,7 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "host_engine_yield_us" (a caller waiting longer than this on its engine
  * call yields its core between polls; 0 default = always spin),
  * "host_engine_idle_us" (the engine leaves after this long without a call,
- * default 200), "host_engine_life_us" (and once it has run this long, even
+ * default 2000; a call that finds it gone pays a relaunch), "host_engine_life_us" (and once it has run this long, even
  * while calls keep coming: a device-wide synchronisation waits at most about
  * this long for it; default 4000), "host_engine_max_bytes" (larger batches
  * launch; default 1 MiB), "host_engine_vram" (1: the engine's call slots and

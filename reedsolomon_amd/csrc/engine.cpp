@@ -51,7 +51,14 @@ int g_engine = [] {                     // rs_tune("host_engine", 0 | 1); env RS
 }();
 int g_engine_waves = 8;                 // rs_tune("host_engine_waves", 1..64): workgroups (one polling wave each)
 int g_engine_group_waves = 8;           // rs_tune("host_engine_group_waves", 1..8): waves per workgroup
-int g_engine_idle_us = 200;             // rs_tune("host_engine_idle_us")
+// Idle exit (rs_tune("host_engine_idle_us")).  A call that finds the engine
+// gone pays a relaunch (10+4 @ 8 KiB: ~39 us instead of ~11), so the engine
+// stays through the gaps of a steadily calling thread: at 200 us a caller
+// that checked each result between calls relaunched it on every 16-64 KiB
+// call (registered 16 / 32 / 64 KiB Encode 35 / 41 / 49 us against 10.7 /
+// 15.3 / 23.0 us at 2 ms; profiles/r04/engine_idle.log).  Device-wide
+// synchronisations wait at most host_engine_life_us anyway.
+int g_engine_idle_us = 2000;
 // Longest life of one instance (rs_tune("host_engine_life_us")): a relaunch
 // costs a stream sync and a launch (~20-30 us of stalled calls), so 4 ms
 // keeps that under 1 % of a busy engine's time.

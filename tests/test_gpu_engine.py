@@ -29,7 +29,7 @@ def engine(rslib):
     L.rs_tune(b"host_engine", 1)
     L.rs_tune(b"host_engine_waves", 8)
     L.rs_tune(b"host_engine_group_waves", 8)
-    L.rs_tune(b"host_engine_idle_us", 200)
+    L.rs_tune(b"host_engine_idle_us", 2000)
     L.rs_tune(b"host_engine_life_us", 4000)
     L.rs_tune(b"host_engine_max_bytes", 1 << 20)
     L.rs_tune(b"host_engine_wg_units", 0)
@@ -120,7 +120,7 @@ def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
         assert all(np.array_equal(v[j], exp[j]) for j in range(d, d + p)), k
     calls2, launches2 = r.host_engine_stats()
     assert calls2 == 56 and launches2 == launches + 1, (calls2, launches2)
-    assert engine.rs_tune(b"host_engine_idle_us", 200) == 0
+    assert engine.rs_tune(b"host_engine_idle_us", 2000) == 0
 
 
 def test_engine_waves_changed_on_live_handle(rslib, orc, torch_dev, engine):

@@ -40,7 +40,7 @@ SWEEP = {
     "host_engine_wg_units": [1, 0],
     "host_engine_poll_gap": [100, 0],
     "host_engine_yield_us": [1, 0],
-    "host_engine_idle_us": [20, 200],
+    "host_engine_idle_us": [20, 2000],
     "host_engine_life_us": [100, 4000],
     "host_engine_vram": [0, 1],
     "host_engine_split_rows": [1, 0],
