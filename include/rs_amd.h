@@ -502,6 +502,10 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * values round down; default 4),
  * "jit_path_rows" (generated kernels of more than 16 rows: rows per code
  * path, 1..16, each row 8 VGPR accumulators; default 16),
+ * "jit_share" (generated kernels of several waves, layout 0: 1 = each column
+ * is loaded and bit-transposed by one wave and shared with the others
+ * through LDS, one barrier per nw columns, the default | 0: every wave
+ * loads and transposes every column),
  * "jit_wide_pf", "jit_wide_waves" (jit_pf and jit_waves of the generated
  * kernels of more than 16 rows; defaults 2 and 3: their 16-row paths fit 168
  * VGPRs, so 3 waves share a SIMD; jit_pf / jit_waves apply to 1-16 rows),

@@ -98,7 +98,14 @@ int g_jit_group_waves = 4;
 // rs_tune("jit_path_rows", 1..16): rows per code path of generated kernels of
 // more than 16 rows (each row holds 8 VGPR accumulators)
 int g_jit_path_rows = 16;
-AsmShape jit_shape(int rows) { return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows); }
+// rs_tune("jit_share", 0 | 1): generated kernels of several waves (layout 0)
+// share each column's load and transpose through LDS (AsmShape::share):
+// 32+32 / 64+64 / 128+128 / 200+56 Encode 4.79 / 2.94 / 1.56 / 2.11 ->
+// 5.33 / 3.68 / 2.02 / 2.85 TB/s (profiles/r04/ab_share.log)
+int g_jit_share = 1;
+AsmShape jit_shape(int rows) {
+    return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share);
+}
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // Generated kernels of more than 16 rows (several code paths): two columns of
 // loads in flight and at most 3 waves per SIMD (their 16-row paths fit 168
@@ -494,7 +501,7 @@ Compiled compile_binary_shape(const uint8_t* mat, int rows, int cols, bool acc, 
     int used = 0;
     if (!asm_binary(mat, rows, cols, acc, sh, pf, sync, &code, &used, &out.log)) return out;
     double lms = 0;
-    out.ok = asm_link_binary(code, sh.nw, used, waves, &out.code, &out.log, &lms);
+    out.ok = asm_link_binary(code, sh, used, waves, &out.code, &out.log, &lms);
     out.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return out;
 }
@@ -835,6 +842,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_backend ? g_jit_layout : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_group_waves : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_path_rows : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_share : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -868,6 +876,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(backend ? g_jit_layout : 0);
     key += static_cast<char>(backend ? g_jit_group_waves : 0);
     key += static_cast<char>(backend ? g_jit_path_rows : 0);
+    key += static_cast<char>(backend ? g_jit_share : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);

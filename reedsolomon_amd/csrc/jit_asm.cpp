@@ -97,6 +97,8 @@ enum class K : uint8_t {
     VXor3,      // v_bitop3_b32 ... bitop3:0x96; a = vdst, b, c, d = VGPR numbers
     BufLoad2,   // a = vdata, b = vaddr, c = srsrc (first SGPR), d = offset, sub = nt
     BufStore2,  // same
+    DsWrite4,   // ds_write_b128: a = vaddr, b = first data VGPR, imm = offset
+    DsRead4,    // ds_read_b128: a = first vdst, b = vaddr, imm = offset
 };
 
 enum Sub : uint8_t {
@@ -151,6 +153,8 @@ struct Prog {
         put(K::BufLoad2, nt ? 1 : 0, vdata, vaddr, srsrc, off);
     }
     void buf_store2(int vdata, int vaddr, int srsrc, int off) { put(K::BufStore2, 1, vdata, vaddr, srsrc, off); }
+    void ds_write4(int vaddr, int vdata, uint32_t off) { put(K::DsWrite4, kNone, vaddr, vdata, 0, 0, off); }
+    void ds_read4(int vdst, int vaddr, uint32_t off) { put(K::DsRead4, kNone, vdst, vaddr, 0, 0, off); }
 };
 
 // ---------------------------------------------------------------- text
@@ -243,6 +247,12 @@ std::string print(const Prog& p) {
                      i.a, i.a + 1, i.b, i.c, i.c + 3, off, i.sub ? " nt" : "");
                 break;
             }
+            case K::DsWrite4:
+                line("ds_write_b128 v%d, v[%d:%d] offset:%u", i.a, i.b, i.b + 3, i.imm);
+                break;
+            case K::DsRead4:
+                line("ds_read_b128 v[%d:%d], v%d offset:%u", i.a, i.a + 3, i.b, i.imm);
+                break;
         }
     }
     return out;
@@ -256,6 +266,7 @@ int ins_size(const Ins& i) {
     switch (i.k) {
         case K::Label: return 0;
         case K::SLoad: case K::VBfi: case K::VXor3: case K::BufLoad2: case K::BufStore2: return 8;
+        case K::DsWrite4: case K::DsRead4: return 8;
         case K::SMovLit: return 8;
         case K::SAddPcrel: return 8;
         case K::SOp2: return (i.b == kLit || i.c == kLit) ? 8 : 4;
@@ -368,6 +379,16 @@ bool encode(const Prog& p, std::vector<uint32_t>* out, std::string* err) {
                   static_cast<uint32_t>(i.b));
                 break;
             }
+            case K::DsWrite4:  // DS op 0xdf: offset 15:0, op 24:17; addr, data0 << 8
+                if (i.imm > 0xffffu) return bad("ds offset");
+                w(0xd8000000u | (0xdfu << 17) | i.imm);
+                w(static_cast<uint32_t>(i.a) | (static_cast<uint32_t>(i.b) << 8));
+                break;
+            case K::DsRead4:  // DS op 0xff; addr, vdst << 24
+                if (i.imm > 0xffffu) return bad("ds offset");
+                w(0xd8000000u | (0xffu << 17) | i.imm);
+                w(static_cast<uint32_t>(i.b) | (static_cast<uint32_t>(i.a) << 24));
+                break;
         }
     }
     return true;
@@ -429,10 +450,14 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     const int nw = sh.nw;
     const int rw = sh.rw;  // rows per code path (per wave in layout 0, per workgroup in layout 1)
     const int npaths = (rows + rw - 1) / rw;
+    const bool share = sh.share && !by_group && npaths > 1;
     Layout L;
-    L.pf = pf < 1 ? 1 : pf > 4 ? 4 : pf;
+    // (share: one column of loads in flight per wave, i.e. nw columns of the
+    // workgroup; the planes read back from LDS get registers of their own)
+    L.pf = share ? 1 : pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
-    L.sub = L.slots_end;        // 2 x 11 subset registers: the XORs of 2-4 planes of each half
+    const int kVPlanes = L.slots_end;
+    L.sub = L.slots_end + (share ? 8 : 0);  // 2 x 11 subset registers: the XORs of 2-4 planes of each half
     L.acc = L.sub + 22;
     const int kVT1 = L.sub + 21;  // (see kVT0)
     L.vgprs = L.acc + 8 * rw;
@@ -602,18 +627,24 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         // the same XCD) stay cached for them (measured with nt: 64+64 Encode
         // fetched 1.45x its input bytes from HBM, 128+128 2.8x;
         // profiles/r03/pmc_traffic_*.json)
-        const bool in_nt = npaths == 1;
-        auto issue_col = [&](int c) {  // stage(c) was issued into slot c & 1
-            desc(c & 1, kSDescIn);
-            if (c + 1 < cols) stage(c + 1, (c + 1) & 1);
+        const bool in_nt = npaths == 1 || share;
+        // the columns this wave loads, in order: all of them, or (share) its
+        // own column of each step, w, w + nw, ...
+        const int c_first = share ? w : 0, c_step = share ? npaths : 1;
+        auto issue_col = [&](int c) {  // stage(c) was issued into slot (c / c_step) & 1
+            const int k_ = c / c_step;
+            desc(k_ & 1, kSDescIn);
+            if (c + c_step < cols) stage(c + c_step, (k_ + 1) & 1);
             for (int k = 0; k < 4; ++k) {
-                P.buf_load2(slot_reg(c, 2 * k), kVOff, kSDescIn, 512 * k, in_nt);
+                P.buf_load2(slot_reg(k_, 2 * k), kVOff, kSDescIn, 512 * k, in_nt);
                 vq.push_back(next_id);
                 col_id[static_cast<size_t>(c)] = next_id++;
             }
         };
-        stage(0, 0);
-        for (int c = 0; c < L.pf && c < cols; ++c) issue_col(c);
+        if (c_first < cols) {
+            stage(c_first, 0);
+            for (int k_ = 0; k_ < L.pf && c_first + k_ * c_step < cols; ++k_) issue_col(c_first + k_ * c_step);
+        }
         // subset m of a half (2-4 of its planes) -> one of 11 registers (the
         // single planes stay where the transpose left them)
         auto sub_reg = [&](int half, int m) {
@@ -621,12 +652,9 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
             return L.sub + half * 11 + kIdx[m];
         };
         auto acc_reg = [&](int r, int i) { return L.acc + 8 * r + i; };
-        for (int c = 0; c < cols; ++c) {
-            vmem_wait_for(col_id[static_cast<size_t>(c)]);
-            int pr[8];
-            for (int j = 0; j < 8; ++j) pr[j] = slot_reg(c, j);
-            transpose8(P, pr, kVT1);
-            // subsets of each half used by this column's rows
+        // column c's planes in pr[]: its subsets of each half that this
+        // path's rows use, then one xor3 per output plane and row
+        auto combine = [&](int c, const int (&pr)[8]) {
             int reg[2][16];
             for (int half = 0; half < 2; ++half) {
                 bool have[16] = {}, used[16] = {}, need[16] = {};
@@ -669,12 +697,59 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                         P.v_op2(kVXor, a, V(a), t[0]);
                     }
                 }
-            if (c + L.pf < cols) issue_col(c + L.pf);  // the slot is free again
-            // keep the waves within `sync` columns of each other, so the lines
-            // the first wave fetched are still cached when the others load
-            // them (layout 0; in layout 1 every wave of a workgroup runs the
-            // same path, so the barriers match there too)
-            if (nw > 1 && sync > 0 && (c + 1) % sync == 0 && c + 1 < cols) P.s_barrier();
+        };
+        if (!share) {
+            for (int c = 0; c < cols; ++c) {
+                vmem_wait_for(col_id[static_cast<size_t>(c)]);
+                int pr[8];
+                for (int j = 0; j < 8; ++j) pr[j] = slot_reg(c, j);
+                transpose8(P, pr, kVT1);
+                combine(c, pr);
+                if (c + L.pf < cols) issue_col(c + L.pf);  // the slot is free again
+                // keep the waves within `sync` columns of each other, so the lines
+                // the first wave fetched are still cached when the others load
+                // them (layout 0; in layout 1 every wave of a workgroup runs the
+                // same path, so the barriers match there too)
+                if (nw > 1 && sync > 0 && (c + 1) % sync == 0 && c + 1 < cols) P.s_barrier();
+            }
+        } else {
+            // Step s: this wave transposes its column s * nw + w into LDS
+            // buffer s & 1 (lane t's 8 planes as two 16-byte pieces, 1 KiB
+            // apart), loads its next column, and after the barrier combines the
+            // step's nw columns from LDS into its rows.  One barrier per step
+            // also frees buffer s & 1 for step s + 2: every wave has combined
+            // step s before it passes the barrier of step s + 1.
+            const int steps = (cols + npaths - 1) / npaths;
+            for (int st = 0; st < steps; ++st) {
+                const int c = st * npaths + w;
+                const uint32_t buf = static_cast<uint32_t>(st & 1) * static_cast<uint32_t>(npaths) * 2048u;
+                if (c < cols) {
+                    vmem_wait_for(col_id[static_cast<size_t>(c)]);
+                    int pr[8];
+                    for (int j = 0; j < 8; ++j) pr[j] = slot_reg(0, j);
+                    transpose8(P, pr, kVT1);
+                }
+                // LDS address of lane t: 16 t (kVT0 is free between transposes)
+                P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
+                P.v_op2(kVLshl, kVT0, C(1), kVT0);
+                if (c < cols) {
+                    const uint32_t off = buf + static_cast<uint32_t>(w) * 2048u;
+                    P.ds_write4(kVT0, slot_reg(0, 0), off);
+                    P.ds_write4(kVT0, slot_reg(0, 4), off + 1024u);
+                    P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
+                    if (c + npaths < cols) issue_col(c + npaths);
+                }
+                P.s_barrier();
+                for (int j = 0; j < npaths && st * npaths + j < cols; ++j) {
+                    const uint32_t off = buf + static_cast<uint32_t>(j) * 2048u;
+                    P.ds_read4(kVPlanes, kVT0, off);
+                    P.ds_read4(kVPlanes + 4, kVT0, off + 1024u);
+                    P.wait_lgkm0();
+                    int pr[8];
+                    for (int q = 0; q < 8; ++q) pr[q] = kVPlanes + q;
+                    combine(st * npaths + j, pr);
+                }
+            }
         }
         // ---- outputs: transpose back, (accumulate: XOR the old bytes), store
         int ostage = 0;
@@ -725,12 +800,12 @@ int declared_vgprs(int used, int max_waves) {
 }
 
 // Kernel descriptor and metadata (code object v6) of a kernel named rs_bs_asm.
-std::string descriptor(int nw, int accum) {
+std::string descriptor(int nw, int accum, int lds) {
     char kd[2048];
     std::string s;
     std::snprintf(kd, sizeof kd,
                   "\t.rodata\n\t.p2align\t6\n\t.amdhsa_kernel rs_bs_asm\n"
-                  "\t\t.amdhsa_group_segment_fixed_size 0\n\t\t.amdhsa_private_segment_fixed_size 0\n"
+                  "\t\t.amdhsa_group_segment_fixed_size %d\n\t\t.amdhsa_private_segment_fixed_size 0\n"
                   "\t\t.amdhsa_kernarg_size %zu\n\t\t.amdhsa_user_sgpr_count 2\n"
                   "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1\n"
                   "\t\t.amdhsa_system_sgpr_workgroup_id_x 1\n\t\t.amdhsa_system_sgpr_workgroup_id_y 1\n"
@@ -738,19 +813,19 @@ std::string descriptor(int nw, int accum) {
                   "\t\t.amdhsa_next_free_vgpr %d\n\t\t.amdhsa_next_free_sgpr %d\n\t\t.amdhsa_accum_offset %d\n"
                   "\t\t.amdhsa_reserve_vcc 0\n\t\t.amdhsa_ieee_mode 1\n\t\t.amdhsa_dx10_clamp 1\n"
                   "\t.end_amdhsa_kernel\n",
-                  sizeof(AsmArgs), accum, kSgprs, accum);
+                  lds, sizeof(AsmArgs), accum, kSgprs, accum);
     s += kd;
     std::snprintf(kd, sizeof kd,
                   "\t.amdgpu_metadata\n---\namdhsa.kernels:\n  - .agpr_count: 0\n    .args:\n"
                   "      - .offset: 0\n        .size: %zu\n        .value_kind: by_value\n"
-                  "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n"
+                  "    .group_segment_fixed_size: %d\n    .kernarg_segment_align: 8\n"
                   "    .kernarg_segment_size: %zu\n    .max_flat_workgroup_size: %d\n    .name: rs_bs_asm\n"
                   "    .private_segment_fixed_size: 0\n    .sgpr_count: %d\n    .sgpr_spill_count: 0\n"
                   "    .symbol: rs_bs_asm.kd\n    .uniform_work_group_size: 1\n    .vgpr_count: %d\n"
                   "    .vgpr_spill_count: 0\n    .wavefront_size: 64\n"
                   "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n"
                   "\t.end_amdgpu_metadata\n",
-                  sizeof(AsmArgs), sizeof(AsmArgs), 64 * nw, kSgprs + 6, accum);
+                  sizeof(AsmArgs), lds, sizeof(AsmArgs), 64 * nw, kSgprs + 6, accum);
     s += kd;
     return s;
 }
@@ -805,15 +880,15 @@ bool elf_section(const std::vector<char>& elf, const char* want, size_t* off, si
 }
 
 // Code-object templates: the kernel descriptor and metadata for (waves per
-// workgroup, declared VGPRs) and a .text of `bytes` filled with s_endpgm,
+// workgroup, declared VGPRs, LDS bytes) and a .text of `bytes` filled with s_endpgm,
 // assembled by comgr once per process and shape.
 struct Template {
     std::vector<char> elf;
     size_t text_off = 0, text_size = 0;
 };
 std::mutex g_tmpl_mu;
-std::map<std::tuple<int, int, size_t>, Template>& templates() {
-    static auto* m = new std::map<std::tuple<int, int, size_t>, Template>;
+std::map<std::tuple<int, int, size_t, int>, Template>& templates() {
+    static auto* m = new std::map<std::tuple<int, int, size_t, int>, Template>;
     return *m;
 }
 
@@ -824,7 +899,7 @@ std::string asm_source(const uint8_t* mat, int rows, int cols, bool acc, const A
     int used = 0;
     const Prog P = generate(mat, rows, cols, acc, sh, pf, sync, &used);
     if (vgprs_out) *vgprs_out = used;
-    return kHeader + print(P) + kTrailer + descriptor(sh.nw, declared_vgprs(used, max_waves));
+    return kHeader + print(P) + kTrailer + descriptor(sh.nw, declared_vgprs(used, max_waves), asm_lds_bytes(sh));
 }
 
 bool asm_binary(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& sh, int pf, int sync,
@@ -842,8 +917,8 @@ bool asm_text_section(const std::vector<char>& elf, std::vector<char>* text) {
     return true;
 }
 
-bool asm_link_binary(const std::vector<uint32_t>& code, int nw, int vgprs_used, int max_waves, std::vector<char>* elf,
-                     std::string* log, double* ms) {
+bool asm_link_binary(const std::vector<uint32_t>& code, const AsmShape& sh, int vgprs_used, int max_waves,
+                     std::vector<char>* elf, std::string* log, double* ms) {
     const auto t0 = std::chrono::steady_clock::now();
     const size_t need = code.size() * 4;
     size_t cls = size_t{16} << 10;
@@ -852,12 +927,13 @@ bool asm_link_binary(const std::vector<uint32_t>& code, int nw, int vgprs_used, 
     const Template* t = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_tmpl_mu);
-        auto key = std::make_tuple(nw, accum, cls);
+        const int lds = asm_lds_bytes(sh);
+        auto key = std::make_tuple(sh.nw, accum, cls, lds);
         auto it = templates().find(key);
         if (it == templates().end()) {
             std::string src = kHeader;
             src += "\t.fill " + std::to_string(cls / 4) + ", 4, 0xbf810000\n";  // s_endpgm
-            src += kTrailer + descriptor(nw, accum);
+            src += kTrailer + descriptor(sh.nw, accum, lds);
             Template nt;
             double ams = 0;
             if (!asm_assemble(src, &nt.elf, log, &ams) || !elf_section(nt.elf, ".text", &nt.text_off, &nt.text_size) ||

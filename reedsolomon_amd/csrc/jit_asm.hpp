@@ -38,13 +38,19 @@ constexpr int kAsmChunk = 2048;                      // bytes of each vector per
 //     computing one row group [g * rw, g * rw + rw) with the same code; the G
 //     row groups of a chunk group are G workgroups placed on one XCD back to
 //     back (grid x = ceil(chunk groups / 8) * 8 * G), sharing its L2.
+//   share (layout 0 with several waves): the waves share the column work
+//     through LDS instead of each loading and transposing every column:
+//     in step s wave w loads and transposes column s * nw + w and writes its
+//     bit-planes to LDS; after a barrier every wave combines the nw columns
+//     of the step into its own rows (two LDS buffers, 2 x nw x 2 KiB).
 struct AsmShape {
     int layout = 0;
     int nw = 1;   // waves per workgroup
     int rw = 1;   // rows per code path
     int groups = 1;  // layout 1: row groups G (= code paths)
+    int share = 0;   // layout 0, nw > 1: columns shared through LDS
 };
-inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16) {
+inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0) {
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
     const int paths = rows <= 16 ? 1 : (rows + pr - 1) / pr;
@@ -53,8 +59,11 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     // (layout 1: a power of two, the kernel maps chunks with shifts)
     s.nw = s.layout ? (group_waves >= 8 ? 8 : group_waves >= 4 ? 4 : group_waves >= 2 ? 2 : 1) : paths;
     s.groups = s.layout ? paths : 1;
+    s.share = (share && !s.layout && paths > 1) ? 1 : 0;
     return s;
 }
+// LDS bytes per workgroup of a generated kernel.
+inline int asm_lds_bytes(const AsmShape& s) { return s.share ? 2 * s.nw * 2048 : 0; }
 // Waves per workgroup of layout 0 (16 rows per wave at most).
 inline int asm_waves(int rows) { return asm_shape(rows, 0, 1).nw; }
 // (path_rows: products of more than 16 rows run in code paths of at most
@@ -76,11 +85,11 @@ bool asm_assemble(const std::string& src, std::vector<char>* code, std::string* 
 bool asm_binary(const uint8_t* mat, int rows, int cols, bool accumulate, const AsmShape& shape, int pf, int sync,
                 std::vector<uint32_t>* code, int* vgprs_used, std::string* err);
 // A code object for machine code from asm_binary: a template (kernel
-// descriptor and metadata for nw waves per workgroup and the declared VGPRs,
+// descriptor and metadata for the shape's waves per workgroup and LDS, the declared VGPRs,
 // .text of the next size class) assembled once per process and shape, with
 // the code copied into its .text.
-bool asm_link_binary(const std::vector<uint32_t>& code, int nw, int vgprs_used, int max_waves, std::vector<char>* elf,
-                     std::string* log, double* ms);
+bool asm_link_binary(const std::vector<uint32_t>& code, const AsmShape& shape, int vgprs_used, int max_waves,
+                     std::vector<char>* elf, std::string* log, double* ms);
 // The .text section of a code object (tests: encoder vs assembler).
 bool asm_text_section(const std::vector<char>& elf, std::vector<char>* text);
 

@@ -17,6 +17,15 @@ has not been waited for raises `WaitcntError` — the hardware would have
 used stale data.  So does `v_readfirstlane` of a VGPR the instruction just
 before it wrote: the hardware needs one wait state there and otherwise reads
 the old value (measured on MI355X, tools/asm_probe/wave_id.s).
+
+Workgroups with LDS (the shared-column kernels): ds_write_b128 /
+ds_read_b128 on a per-workgroup LDS of the size the kernel descriptor
+declares (bounds and 16-byte alignment checked); reads land at
+`lgkmcnt(0)` like scalar loads.  The waves of a workgroup run in rounds
+from one s_barrier to the next, in alternating order, and a wave that reads
+LDS bytes another wave wrote in the same round, or writes bytes another
+wave read or wrote in it, raises `LdsRaceError`: without the barrier
+between them the hardware's result would depend on timing.
 """
 from __future__ import annotations
 
@@ -82,9 +91,45 @@ class WaitcntError(AssertionError):
     pass
 
 
+class LdsRaceError(AssertionError):
+    pass
+
+
+class Lds:
+    """A workgroup's LDS plus, per barrier round, who wrote / read each byte."""
+
+    def __init__(self, size: int, nw: int):
+        self.buf = np.zeros(max(size, 16), np.uint8)
+        self.size = size
+        self.writer = np.full(self.buf.size, -1, np.int16)
+        self.readers = np.zeros((nw, self.buf.size), bool)
+
+    def new_round(self):
+        self.writer[:] = -1
+        self.readers[:] = False
+
+    def _span(self, wave, addr, write):
+        if addr % 16 or addr < 0 or addr + 16 > self.size:
+            raise AssertionError(f"wave {wave}: LDS access at {addr} out of bounds / unaligned (size {self.size})")
+        sl = slice(addr, addr + 16)
+        w = self.writer[sl]
+        if np.any((w >= 0) & (w != wave)):
+            raise LdsRaceError(f"wave {wave}: LDS bytes {addr}.. written by wave {int(w.max())} in this round")
+        if write:
+            others = np.delete(self.readers[:, sl], wave, axis=0)
+            if others.any():
+                raise LdsRaceError(f"wave {wave}: LDS bytes {addr}.. read by another wave in this round")
+            self.writer[sl] = wave
+        else:
+            self.readers[wave, sl] = True
+        return sl
+
+
 class Wave:
-    def __init__(self, emu, karg_addr, wg, tid0):
+    def __init__(self, emu, karg_addr, wg, tid0, lds=None):
         self.emu = emu
+        self.lds = lds
+        self.wid = tid0 // 64
         self.s = [0] * 128
         self.v = np.zeros((256, 64), np.uint64)
         self.s[0], self.s[1] = karg_addr & M32, karg_addr >> 32
@@ -95,14 +140,18 @@ class Wave:
         self.scc = 0
         self.vm = []        # outstanding vector memory ops, issue order: set of load-destination VGPRs
         self.lgkm = set()   # SGPRs of outstanding scalar loads
+        self.lgkm_v = set()  # VGPRs of outstanding LDS reads, and the data VGPRs of LDS writes
         self.pc = 0
         self.prev_vdst = None  # VGPR the previous instruction wrote (VALU), for the readlane hazard
+        self.lds_data = set()  # (subset of lgkm_v) LDS-write data VGPRs: may be read, not written
 
     # wait-count checks
     def _chk(self, kind, idx, n, write=False):
         for i in range(idx, idx + n):
             if kind == "v" and any(i in d for d in self.vm):
                 raise WaitcntError(f"pc {self.pc}: v{i} {'written' if write else 'read'} before its load was waited for")
+            if kind == "v" and i in self.lgkm_v and (write or i not in self.lds_data):
+                raise WaitcntError(f"pc {self.pc}: v{i} {'written' if write else 'read'} before lgkmcnt(0) (LDS)")
             if kind == "s" and i in self.lgkm:
                 raise WaitcntError(f"pc {self.pc}: s{i} {'written' if write else 'read'} before its load was waited for")
 
@@ -129,6 +178,7 @@ class Wave:
         return np.full(64, self.sval(tok) & M32, np.uint64)
 
     def run(self, prog, labels):
+        """A generator: yields at every s_barrier, returns at s_endpgm."""
         pc = 0
         emu = self.emu
         while True:
@@ -147,11 +197,48 @@ class Wave:
                             self.vm.pop(0)
                     elif n == 0:
                         self.lgkm.clear()
+                        self.lgkm_v.clear()
+                        self.lds_data.clear()
                 continue
-            if op == "s_nop" or op == "s_barrier":  # waves run one after another here
+            if op == "s_barrier":
+                yield "barrier"
+                continue
+            if op == "s_nop":
+                continue
+            if op in ("ds_write_b128", "ds_read_b128"):
+                assert self.lds is not None, "LDS access in a kernel without LDS"
+                mods = rest.split()
+                off = 0
+                for m_ in mods:
+                    if m_.startswith("offset:"):
+                        off = int(m_.split(":")[1])
+                if op == "ds_write_b128":
+                    ar, dr = _regs(ops[0]), _regs(ops[1].split()[0])
+                    self._chk("v", ar[1], 1)
+                    self._chk("v", dr[1], 4)
+                    addr = self.v[ar[1]].astype(np.int64) + off
+                    for lane in range(64):
+                        sl = self.lds._span(self.wid, int(addr[lane]), True)
+                        self.lds.buf[sl] = np.array([self.v[dr[1] + q, lane] for q in range(4)],
+                                                    np.uint32).view(np.uint8)
+                    for q in range(4):
+                        self.lgkm_v.add(dr[1] + q)
+                        self.lds_data.add(dr[1] + q)
+                else:
+                    dr, ar = _regs(ops[0]), _regs(ops[1].split()[0])
+                    self._chk("v", ar[1], 1)
+                    self._chk("v", dr[1], 4, write=True)
+                    addr = self.v[ar[1]].astype(np.int64) + off
+                    for lane in range(64):
+                        sl = self.lds._span(self.wid, int(addr[lane]), False)
+                        w = self.lds.buf[sl].view(np.uint32)
+                        for q in range(4):
+                            self.v[dr[1] + q, lane] = int(w[q])
+                    for q in range(4):
+                        self.lgkm_v.add(dr[1] + q)
                 continue
             if ops and op not in ("s_cbranch_scc1", "s_cbranch_scc0", "s_branch", "s_cmp_eq_u64", "s_cmp_eq_u32",
-                                  "s_cmp_ge_u32", "s_setpc_b64", "buffer_store_dwordx2"):
+                                  "s_cmp_ge_u32", "s_setpc_b64", "buffer_store_dwordx2", "ds_write_b128"):
                 self._use(ops[0], write=True)  # the destination
             if op == "s_load_dword" or op == "s_load_dwordx2":
                 d, base, off = ops[0], ops[1], int(ops[2], 0)
@@ -322,8 +409,26 @@ class Emu:
 
     def launch(self, src: str, karg: bytes, grid, nw: int):
         prog, labels = _parse(src)
+        m = re.search(r"\.amdhsa_group_segment_fixed_size\s+(\d+)", src)
+        lds_size = int(m.group(1)) if m else 0
         self.karg = (0x7F0000000000, karg)
         for y in range(grid[1]):
             for x in range(grid[0]):
-                for w in range(nw):
-                    Wave(self, self.karg[0], (x, y), 64 * w).run(prog, labels)
+                lds = Lds(lds_size, nw) if lds_size else None
+                live = [Wave(self, self.karg[0], (x, y), 64 * w, lds).run(prog, labels) for w in range(nw)]
+                rnd = 0
+                while live:
+                    if lds is not None:
+                        lds.new_round()
+                    order = live if rnd % 2 == 0 else live[::-1]
+                    still = []
+                    for g in order:
+                        try:
+                            next(g)
+                            still.append(g)
+                        except StopIteration:
+                            pass
+                    if still and len(still) != len(live):
+                        raise AssertionError("a wave ended while others wait at a barrier")
+                    live = [g for g in live if g in still]
+                    rnd += 1

@@ -71,6 +71,7 @@ SWEEP = {
     "jit_path_rows": [5, 11, 16],
     "jit_wide_pf": [1, 3, 2],
     "jit_wide_waves": [0, 2, 3],
+    "jit_share": [0, 1],
     "table_registry_max": [1, 1 << 14],
 }
 

@@ -201,11 +201,11 @@ def asm_jit(rslib):
 
 
 @pytest.mark.parametrize("rows,cols", [(9, 10), (16, 64), (17, 5), (24, 33), (56, 200), (64, 64), (100, 100),
-                                       (128, 128), (128, 1)])
+                                       (128, 128), (128, 1), (40, 1), (33, 7), (128, 9)])
 def test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols):
     """The assembly-generated bit-sliced kernels (jit_asm.cpp) for 9-128
     output rows: 1-8 waves per workgroup, each wave up to 16 rows, all over
-    the same input lines; overwrite and XOR-accumulate, aligned and ragged
+    the same chunk (columns shared through LDS, the default); overwrite and XOR-accumulate, aligned and ragged
     sizes, against the oracle.  The compiled kernel really runs (launch
     counter)."""
     torch = torch_dev
@@ -252,3 +252,16 @@ def test_wide_asm_jit_reconst(rslib, orc, torch_dev, asm_jit, d, p, lost):
     r.reconst_batch_split(data, par, [], lost)
     torch.cuda.synchronize()
     assert np.array_equal(data.cpu().numpy(), host[:, :d]) and np.array_equal(par.cpu().numpy(), host[:, d:])
+
+
+@pytest.mark.parametrize("rows,cols", [(17, 5), (24, 33), (56, 200), (64, 64), (128, 128), (40, 1), (33, 7)])
+def test_wide_asm_jit_unshared_columns(rslib, orc, torch_dev, asm_jit, rows, cols):
+    """rs_tune("jit_share", 0): every wave of a multi-wave kernel loads and
+    transposes every column itself (the default shares them through LDS, and
+    the tests above run that); overwrite and accumulate, aligned and ragged
+    sizes, against the oracle."""
+    assert asm_jit.rs_tune(b"jit_share", 0) == 0
+    try:
+        test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
+    finally:
+        asm_jit.rs_tune(b"jit_share", 1)

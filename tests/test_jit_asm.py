@@ -36,11 +36,12 @@ def test_asm_kernel_with_barriers(rslib, orc, rows, cols, sync):
     """rs_tune("jit_sync", n): the waves of a multi-wave kernel meet at
     s_barrier every n columns; the same number of barriers in every wave."""
     L = rslib.lib()
-    assert L.rs_tune(b"jit_sync", sync) == 0
+    assert L.rs_tune(b"jit_sync", sync) == 0 and L.rs_tune(b"jit_share", 0) == 0  # (shared columns: own barriers)
     try:
         src = _check_kernel(rslib, orc, rows, cols, 0)
     finally:
         L.rs_tune(b"jit_sync", 0)
+        L.rs_tune(b"jit_share", 1)
     nw = (rows + 15) // 16
     assert src.count("s_barrier") == nw * ((cols - 1) // sync)
 
@@ -62,12 +63,15 @@ def test_asm_kernel_row_group_layout(rslib, orc, rows, cols, acc, gw):
         L.rs_tune(b"jit_group_waves", 4)
 
 
-def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4, paths=None):
+def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4, paths=None, edit=None):
     rng = np.random.default_rng(rows * 1000 + cols * 10 + acc)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
     src = rslib.jit_asm_source(mat, bool(acc))
+    if edit:
+        src = edit(src)
     assert "rs_bs_asm" in src and "s_endpgm" in src
-    rslib.jit_compile_check(mat, bool(acc))  # assembles and links with comgr (the library's own path)
+    if not edit:
+        rslib.jit_compile_check(mat, bool(acc))  # assembles and links with comgr (the library's own path)
     S, body, vlen = 3, 4096, 4096 + 32      # two 2 KiB chunks per vector, bytes past the body untouched
     nvec = cols + rows
     mem = Memory(S * nvec * vlen + 65536)
@@ -158,3 +162,57 @@ def test_asm_kernel_path_rows(rslib, orc, rows, cols, acc, path_rows, layout):
     finally:
         L.rs_tune(b"jit_path_rows", 16)
         L.rs_tune(b"jit_layout", 0)
+
+
+@pytest.mark.parametrize("rows,cols,acc,share", [(33, 7, 0, 1), (40, 9, 1, 1), (17, 5, 0, 1), (64, 5, 1, 1),
+                                                (20, 1, 0, 1), (48, 12, 0, 1), (33, 7, 0, 0), (40, 9, 1, 0)])
+def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share):
+    """rs_tune("jit_share", 1, the default): the waves of a multi-path workgroup share the
+    column work through LDS (step s: wave w loads and transposes column
+    s * nw + w into LDS buffer s & 1, barrier, every wave combines the step's
+    columns).  Against the oracle, with the emulator's LDS race check (waves
+    run between barriers in alternating order; a read of bytes another wave
+    wrote in the same round fails); ragged last steps and waves without a
+    column included.  share=0: every wave loads and transposes every column,
+    no LDS, no barrier."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_share", share) == 0
+    try:
+        src = _check_kernel(rslib, orc, rows, cols, acc)
+    finally:
+        L.rs_tune(b"jit_share", 1)
+    nw = (rows + 15) // 16
+    steps = (cols + nw - 1) // nw
+    assert src.count("s_barrier") == (nw * steps if share else 0)
+    assert src.count("ds_write_b128") == (2 * cols if share else 0)
+    assert f".amdhsa_group_segment_fixed_size {2 * nw * 2048 if share else 0}" in src
+
+
+@pytest.mark.parametrize("rows,cols,acc,share", [(64, 64, 0, 1), (56, 200, 1, 1), (128, 128, 0, 1), (33, 3, 1, 1),
+                                                (17, 5, 0, 1), (64, 64, 0, 0), (128, 256, 1, 0)])
+def test_machine_code_equals_assembler_shared(rslib, rows, cols, acc, share):
+    """The shared-column kernels' machine code (ds_write_b128 / ds_read_b128,
+    barriers), and the unshared ones', equal comgr's assembly of their text."""
+    L = rslib.lib()
+    mat = np.random.default_rng(rows * 37 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
+    assert L.rs_tune(b"jit_share", share) == 0
+    try:
+        n = rslib.jit_encoder_check(mat, bool(acc))
+    finally:
+        L.rs_tune(b"jit_share", 1)
+    assert n > 0 and n % 4 == 0
+
+
+def test_emulator_catches_a_missing_barrier(rslib, orc):
+    """The race check is live: the shared-column kernel with its barriers
+    removed fails in the emulator (a wave reads LDS bytes another wave wrote
+    in the same round)."""
+    from asm_emu import LdsRaceError
+
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_share", 1) == 0
+    try:
+        with pytest.raises(LdsRaceError):
+            _check_kernel(rslib, orc, 33, 7, 0, edit=lambda s: s.replace("\ts_barrier\n", ""))
+    finally:
+        L.rs_tune(b"jit_share", 1)

@@ -75,6 +75,12 @@ SUITES = {
                     ["op=rec24,jit_wide_waves=2,jit_wide_pf=3", "op=rec24", "op=rec24,jit_layout=1,jit_group_waves=2",
                      "layout=inter,op=rec24,jit_wide_waves=2,jit_wide_pf=3", "layout=inter,op=rec24",
                      "layout=inter,op=rec24,jit_layout=1,jit_group_waves=2"])],
+    # round 4: the waves of a multi-path workgroup share each column's load and transpose
+    # through LDS (jit_share=1) against every wave loading and transposing every column
+    "share": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
+               ["", "jit_share=1", "jit_share=1,jit_wide_waves=2", "jit_share=1,jit_wide_waves=0"])
+              for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))] +
+             [(dict(AB_K="32", AB_M="32", AB_S="56"), ["op=rec24", "op=rec24,jit_share=1"])],
     # round 4: 3-4 rows over more than 4 runtime columns, 16-byte units on 256 lanes (default since
     # round 1) vs 8-byte units on 128 lanes (var=201, experiments build), split and interleaved
     "wide34_r4": shapes([(16, 4), (20, 4), (8, 4), (6, 3), (9, 3), (16, 3)],
