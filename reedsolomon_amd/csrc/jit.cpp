@@ -103,8 +103,12 @@ int g_jit_path_rows = 16;
 // 32+32 / 64+64 / 128+128 / 200+56 Encode 4.79 / 2.94 / 1.56 / 2.11 ->
 // 5.33 / 3.68 / 2.02 / 2.85 TB/s (profiles/r04/ab_share.log)
 int g_jit_share = 1;
+// rs_tune("jit_share_deep", -1 | 0 | 1): shared-column kernels with two steps
+// of loads in flight and the next column's planes read from LDS ahead
+// (-1: for 8-wave workgroups only)
+int g_jit_share_deep = -1;
 AsmShape jit_shape(int rows) {
-    return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share);
+    return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep);
 }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // Generated kernels of more than 16 rows (several code paths): two columns of
@@ -843,6 +847,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_backend ? g_jit_group_waves : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_path_rows : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_share_deep : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -877,6 +882,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(backend ? g_jit_group_waves : 0);
     key += static_cast<char>(backend ? g_jit_path_rows : 0);
     key += static_cast<char>(backend ? g_jit_share : 0);
+    key += static_cast<char>(backend ? g_jit_share_deep : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);

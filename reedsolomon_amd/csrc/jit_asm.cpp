@@ -84,7 +84,7 @@ enum class K : uint8_t {
     SOp2,       // sub: add | addc | lshl | lshl64 | mul | mulhi | and; a = sdst, b = src0, c = src1, imm
     SCmp,       // sub: eq32 | eq64; a = src0, b = src1
     SNop,       // a = wait states - 1
-    SWaitLgkm0,
+    SWaitLgkm0, // a = count (lgkmcnt(a))
     SWaitVm,    // a = count
     SBarrier,
     SEndpgm,
@@ -138,7 +138,8 @@ struct Prog {
     void s_op2(Sub s, int sdst, int src0, int src1, uint32_t imm = 0) { put(K::SOp2, s, sdst, src0, src1, 0, imm); }
     void s_cmp(Sub s, int src0, int src1) { put(K::SCmp, s, src0, src1); }
     void s_nop(int n) { put(K::SNop, kNone, n); }
-    void wait_lgkm0() { put(K::SWaitLgkm0, kNone); }
+    void wait_lgkm0() { put(K::SWaitLgkm0, kNone, 0); }
+    void wait_lgkm(int n) { put(K::SWaitLgkm0, kNone, n); }
     void wait_vm(int n) { put(K::SWaitVm, kNone, n); }
     void s_barrier() { put(K::SBarrier, kNone); }
     void s_endpgm() { put(K::SEndpgm, kNone); }
@@ -210,7 +211,7 @@ std::string print(const Prog& p) {
                           opnd(i.b, 0).c_str());
                 break;
             case K::SNop: line("s_nop %d", i.a); break;
-            case K::SWaitLgkm0: line("s_waitcnt lgkmcnt(0)"); break;
+            case K::SWaitLgkm0: line("s_waitcnt lgkmcnt(%d)", i.a); break;
             case K::SWaitVm: line("s_waitcnt vmcnt(%d)", i.a); break;
             case K::SBarrier: line("s_barrier"); break;
             case K::SEndpgm: line("s_endpgm"); break;
@@ -324,7 +325,9 @@ bool encode(const Prog& p, std::vector<uint32_t>* out, std::string* err) {
                   (static_cast<uint32_t>(i.b) << 8) | static_cast<uint32_t>(i.a));
                 break;
             case K::SNop: w(0xbf800000u | static_cast<uint32_t>(i.a)); break;
-            case K::SWaitLgkm0: w(0xbf8cc07fu); break;  // vmcnt 63, expcnt 7, lgkmcnt 0
+            case K::SWaitLgkm0:  // vmcnt 63, expcnt 7, lgkmcnt bits 11:8
+                w(0xbf8cc07fu | ((static_cast<uint32_t>(i.a) & 15u) << 8));
+                break;
             case K::SWaitVm: {  // vmcnt[3:0] bits 3:0, [5:4] bits 15:14; expcnt 7, lgkmcnt 15
                 const uint32_t n = static_cast<uint32_t>(i.a) & 63;
                 w(0xbf8c0000u | (n & 15) | ((n >> 4) << 14) | 0x70u | 0xf00u);
@@ -451,13 +454,15 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     const int rw = sh.rw;  // rows per code path (per wave in layout 0, per workgroup in layout 1)
     const int npaths = (rows + rw - 1) / rw;
     const bool share = sh.share && !by_group && npaths > 1;
+    const bool deep = share && sh.deep;
     Layout L;
     // (share: one column of loads in flight per wave, i.e. nw columns of the
-    // workgroup; the planes read back from LDS get registers of their own)
-    L.pf = share ? 1 : pf < 1 ? 1 : pf > 4 ? 4 : pf;
+    // workgroup - two with deep; the planes read back from LDS get registers
+    // of their own, two sets with deep)
+    L.pf = share ? (deep ? 2 : 1) : pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
     const int kVPlanes = L.slots_end;
-    L.sub = L.slots_end + (share ? 8 : 0);  // 2 x 11 subset registers: the XORs of 2-4 planes of each half
+    L.sub = L.slots_end + (share ? (deep ? 16 : 8) : 0);  // 2 x 11 subset registers: the XORs of 2-4 planes of each half
     L.acc = L.sub + 22;
     const int kVT1 = L.sub + 21;  // (see kVT0)
     L.vgprs = L.acc + 8 * rw;
@@ -726,7 +731,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                 if (c < cols) {
                     vmem_wait_for(col_id[static_cast<size_t>(c)]);
                     int pr[8];
-                    for (int j = 0; j < 8; ++j) pr[j] = slot_reg(0, j);
+                    for (int j = 0; j < 8; ++j) pr[j] = slot_reg(st, j);
                     transpose8(P, pr, kVT1);
                 }
                 // LDS address of lane t: 16 t (kVT0 is free between transposes)
@@ -734,20 +739,36 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                 P.v_op2(kVLshl, kVT0, C(1), kVT0);
                 if (c < cols) {
                     const uint32_t off = buf + static_cast<uint32_t>(w) * 2048u;
-                    P.ds_write4(kVT0, slot_reg(0, 0), off);
-                    P.ds_write4(kVT0, slot_reg(0, 4), off + 1024u);
+                    P.ds_write4(kVT0, slot_reg(st, 0), off);
+                    P.ds_write4(kVT0, slot_reg(st, 4), off + 1024u);
                     P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
-                    if (c + npaths < cols) issue_col(c + npaths);
+                    if (c + L.pf * npaths < cols) {
+                        issue_col(c + L.pf * npaths);
+                        // (its scalar loads back before the LDS reads below, so
+                        // lgkmcnt counts LDS reads only, in order)
+                        if (deep) P.wait_lgkm0();
+                    }
                 }
                 P.s_barrier();
-                for (int j = 0; j < npaths && st * npaths + j < cols; ++j) {
+                const int ncol = std::min(npaths, cols - st * npaths);
+                auto read = [&](int j) {
                     const uint32_t off = buf + static_cast<uint32_t>(j) * 2048u;
-                    P.ds_read4(kVPlanes, kVT0, off);
-                    P.ds_read4(kVPlanes + 4, kVT0, off + 1024u);
-                    P.wait_lgkm0();
+                    const int d = kVPlanes + (deep ? 8 * (j & 1) : 0);
+                    P.ds_read4(d, kVT0, off);
+                    P.ds_read4(d + 4, kVT0, off + 1024u);
+                };
+                read(0);
+                for (int j = 0; j < ncol; ++j) {
+                    if (deep && j + 1 < ncol) {
+                        read(j + 1);  // the next column's planes arrive while this one combines
+                        P.wait_lgkm(2);
+                    } else {
+                        P.wait_lgkm0();
+                    }
                     int pr[8];
-                    for (int q = 0; q < 8; ++q) pr[q] = kVPlanes + q;
+                    for (int q = 0; q < 8; ++q) pr[q] = kVPlanes + (deep ? 8 * (j & 1) : 0) + q;
                     combine(st * npaths + j, pr);
+                    if (!deep && j + 1 < ncol) read(j + 1);
                 }
             }
         }

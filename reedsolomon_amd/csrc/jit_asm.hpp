@@ -49,8 +49,12 @@ struct AsmShape {
     int rw = 1;   // rows per code path
     int groups = 1;  // layout 1: row groups G (= code paths)
     int share = 0;   // layout 0, nw > 1: columns shared through LDS
+    int deep = 0;    // share: two steps of loads in flight and the next column's planes read ahead
 };
-inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0) {
+// deep: -1 = when the workgroup has 8 waves (one workgroup per CU whatever
+// the registers: the extra 24 VGPRs cost no occupancy), 0 / 1 = off / on.
+inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0,
+                          int deep = -1) {
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
     const int paths = rows <= 16 ? 1 : (rows + pr - 1) / pr;
@@ -60,6 +64,7 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     s.nw = s.layout ? (group_waves >= 8 ? 8 : group_waves >= 4 ? 4 : group_waves >= 2 ? 2 : 1) : paths;
     s.groups = s.layout ? paths : 1;
     s.share = (share && !s.layout && paths > 1) ? 1 : 0;
+    s.deep = s.share && (deep < 0 ? s.nw >= 8 : deep > 0) ? 1 : 0;
     return s;
 }
 // LDS bytes per workgroup of a generated kernel.

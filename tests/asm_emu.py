@@ -140,18 +140,20 @@ class Wave:
         self.scc = 0
         self.vm = []        # outstanding vector memory ops, issue order: set of load-destination VGPRs
         self.lgkm = set()   # SGPRs of outstanding scalar loads
-        self.lgkm_v = set()  # VGPRs of outstanding LDS reads, and the data VGPRs of LDS writes
+        self.lds_q = []     # outstanding LDS ops in issue order: (VGPRs, is_write); they complete in order
         self.pc = 0
         self.prev_vdst = None  # VGPR the previous instruction wrote (VALU), for the readlane hazard
-        self.lds_data = set()  # (subset of lgkm_v) LDS-write data VGPRs: may be read, not written
+
 
     # wait-count checks
     def _chk(self, kind, idx, n, write=False):
         for i in range(idx, idx + n):
             if kind == "v" and any(i in d for d in self.vm):
                 raise WaitcntError(f"pc {self.pc}: v{i} {'written' if write else 'read'} before its load was waited for")
-            if kind == "v" and i in self.lgkm_v and (write or i not in self.lds_data):
-                raise WaitcntError(f"pc {self.pc}: v{i} {'written' if write else 'read'} before lgkmcnt(0) (LDS)")
+            # an LDS read's destination may be neither read nor written before it
+            # lands; an LDS write's data registers may be read but not overwritten
+            if kind == "v" and any(i in regs and (write or not wr) for regs, wr in self.lds_q):
+                raise WaitcntError(f"pc {self.pc}: v{i} {'written' if write else 'read'} before its LDS op completed")
             if kind == "s" and i in self.lgkm:
                 raise WaitcntError(f"pc {self.pc}: s{i} {'written' if write else 'read'} before its load was waited for")
 
@@ -197,8 +199,14 @@ class Wave:
                             self.vm.pop(0)
                     elif n == 0:
                         self.lgkm.clear()
-                        self.lgkm_v.clear()
-                        self.lds_data.clear()
+                        self.lds_q.clear()
+                    else:
+                        # scalar loads return out of order: a nonzero count is
+                        # only meaningful with none outstanding
+                        if self.lgkm:
+                            raise WaitcntError(f"pc {self.pc}: lgkmcnt({n}) with scalar loads outstanding")
+                        while len(self.lds_q) > n:
+                            self.lds_q.pop(0)
                 continue
             if op == "s_barrier":
                 yield "barrier"
@@ -221,9 +229,7 @@ class Wave:
                         sl = self.lds._span(self.wid, int(addr[lane]), True)
                         self.lds.buf[sl] = np.array([self.v[dr[1] + q, lane] for q in range(4)],
                                                     np.uint32).view(np.uint8)
-                    for q in range(4):
-                        self.lgkm_v.add(dr[1] + q)
-                        self.lds_data.add(dr[1] + q)
+                    self.lds_q.append(({dr[1] + q for q in range(4)}, True))
                 else:
                     dr, ar = _regs(ops[0]), _regs(ops[1].split()[0])
                     self._chk("v", ar[1], 1)
@@ -234,8 +240,7 @@ class Wave:
                         w = self.lds.buf[sl].view(np.uint32)
                         for q in range(4):
                             self.v[dr[1] + q, lane] = int(w[q])
-                    for q in range(4):
-                        self.lgkm_v.add(dr[1] + q)
+                    self.lds_q.append(({dr[1] + q for q in range(4)}, False))
                 continue
             if ops and op not in ("s_cbranch_scc1", "s_cbranch_scc0", "s_branch", "s_cmp_eq_u64", "s_cmp_eq_u32",
                                   "s_cmp_ge_u32", "s_setpc_b64", "buffer_store_dwordx2", "ds_write_b128"):

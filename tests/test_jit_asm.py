@@ -164,9 +164,12 @@ def test_asm_kernel_path_rows(rslib, orc, rows, cols, acc, path_rows, layout):
         L.rs_tune(b"jit_layout", 0)
 
 
-@pytest.mark.parametrize("rows,cols,acc,share", [(33, 7, 0, 1), (40, 9, 1, 1), (17, 5, 0, 1), (64, 5, 1, 1),
-                                                (20, 1, 0, 1), (48, 12, 0, 1), (33, 7, 0, 0), (40, 9, 1, 0)])
-def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share):
+@pytest.mark.parametrize("rows,cols,acc,share,deep", [(33, 7, 0, 1, -1), (40, 9, 1, 1, -1), (17, 5, 0, 1, -1),
+                                                     (64, 5, 1, 1, -1), (20, 1, 0, 1, -1), (48, 12, 0, 1, -1),
+                                                     (33, 7, 0, 0, -1), (40, 9, 1, 0, -1), (33, 7, 1, 1, 1),
+                                                     (64, 13, 0, 1, 1), (17, 2, 0, 1, 1), (128, 9, 1, 1, -1),
+                                                     (128, 17, 0, 1, 0)])
+def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share, deep):
     """rs_tune("jit_share", 1, the default): the waves of a multi-path workgroup share the
     column work through LDS (step s: wave w loads and transposes column
     s * nw + w into LDS buffer s & 1, barrier, every wave combines the step's
@@ -174,13 +177,18 @@ def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share):
     run between barriers in alternating order; a read of bytes another wave
     wrote in the same round fails); ragged last steps and waves without a
     column included.  share=0: every wave loads and transposes every column,
-    no LDS, no barrier."""
+    no LDS, no barrier.  deep (rs_tune("jit_share_deep"); -1 = 8-wave
+    workgroups only): two steps of loads in flight and the next column's
+    planes read from LDS while the current one combines (lgkmcnt(2))."""
     L = rslib.lib()
-    assert L.rs_tune(b"jit_share", share) == 0
+    assert L.rs_tune(b"jit_share", share) == 0 and L.rs_tune(b"jit_share_deep", deep) == 0
     try:
         src = _check_kernel(rslib, orc, rows, cols, acc)
     finally:
         L.rs_tune(b"jit_share", 1)
+        L.rs_tune(b"jit_share_deep", -1)
+    is_deep = share and (deep == 1 or (deep == -1 and rows > 112))
+    assert ("lgkmcnt(2)" in src) == bool(is_deep and cols > 1)
     nw = (rows + 15) // 16
     steps = (cols + nw - 1) // nw
     assert src.count("s_barrier") == (nw * steps if share else 0)
@@ -189,17 +197,21 @@ def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share):
 
 
 @pytest.mark.parametrize("rows,cols,acc,share", [(64, 64, 0, 1), (56, 200, 1, 1), (128, 128, 0, 1), (33, 3, 1, 1),
-                                                (17, 5, 0, 1), (64, 64, 0, 0), (128, 256, 1, 0)])
+                                                (17, 5, 0, 1), (64, 64, 0, 0), (128, 256, 1, 0), (64, 64, 1, 2),
+                                                (24, 7, 0, 2)])
 def test_machine_code_equals_assembler_shared(rslib, rows, cols, acc, share):
     """The shared-column kernels' machine code (ds_write_b128 / ds_read_b128,
-    barriers), and the unshared ones', equal comgr's assembly of their text."""
+    barriers), and the unshared ones', equal comgr's assembly of their text
+    (share=2: the deep variant, lgkmcnt(2) included)."""
     L = rslib.lib()
     mat = np.random.default_rng(rows * 37 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
-    assert L.rs_tune(b"jit_share", share) == 0
+    assert L.rs_tune(b"jit_share", min(share, 1)) == 0
+    assert L.rs_tune(b"jit_share_deep", 1 if share == 2 else -1) == 0
     try:
         n = rslib.jit_encoder_check(mat, bool(acc))
     finally:
         L.rs_tune(b"jit_share", 1)
+        L.rs_tune(b"jit_share_deep", -1)
     assert n > 0 and n % 4 == 0
 
 

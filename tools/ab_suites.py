@@ -81,6 +81,10 @@ SUITES = {
                ["", "jit_share=1", "jit_share=1,jit_wide_waves=2", "jit_share=1,jit_wide_waves=0"])
               for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))] +
              [(dict(AB_K="32", AB_M="32", AB_S="56"), ["op=rec24", "op=rec24,jit_share=1"])],
+    # round 4: shared columns with two steps of loads in flight and LDS reads one column ahead
+    "share_deep": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
+                    ["jit_share_deep=0", "jit_share_deep=1", "jit_share_deep=1,jit_wide_waves=0"])
+                   for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
     # round 4: 3-4 rows over more than 4 runtime columns, 16-byte units on 256 lanes (default since
     # round 1) vs 8-byte units on 128 lanes (var=201, experiments build), split and interleaved
     "wide34_r4": shapes([(16, 4), (20, 4), (8, 4), (6, 3), (9, 3), (16, 3)],
