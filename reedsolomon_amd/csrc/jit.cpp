@@ -57,6 +57,7 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <cmath>
 #include <mutex>
 #include <set>
 #include <shared_mutex>
@@ -603,11 +604,11 @@ double est_compile_us(int rows, int cols) { return 150.0 + 0.15 * rows * cols; }
 // Microseconds per byte moved that a product with `rows` outputs loses on the
 // table kernels: those run 5-8 rows at ~5 TB/s (VALU-bound) and more rows on
 // the single-pass wide kernel at ~3.4 TB/s for 16 rows, falling about as
-// 1 / rows beyond; compiled kernels run ~6 TB/s up to 32 rows, 2.4 at 64 and
-// 1.3 at 128.
+// 1 / rows beyond; compiled kernels run ~6 TB/s up to 32 rows, 3.7 at 64 and
+// 2.0 at 128 (shared columns): about 6 x (32 / rows)^0.8.
 double lost_us_per_byte(int rows) {
     const double fb = rows <= 8 ? 5.0 : std::min(5.0, 3.4 * 16.0 / rows);  // TB/s = 1e6 bytes per us
-    const double jt = rows <= 32 ? 6.0 : 6.0 * 32.0 / rows;
+    const double jt = rows <= 32 ? 6.0 : 6.0 * std::pow(32.0 / rows, 0.8);
     return std::max(0.0, 1.0 / fb - 1.0 / jt) * 1e-6;
 }
 constexpr size_t kMaxSeen = 4096;  // matrices counted but not compiled yet (cleared when full)
