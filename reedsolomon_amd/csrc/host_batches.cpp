@@ -415,14 +415,14 @@ int rs_bind_thread_to_device(int device) {
 int rs_host_unregister(void* ptr) {
     return abi_guard([&]() -> int {
         if (!ptr) return RS_ERR_INVAL;
-        std::vector<uintptr_t> dead;
-        {
-            std::lock_guard<std::mutex> lk(g_reg_mu);
-            auto it = g_user.find(reinterpret_cast<uintptr_t>(ptr));
-            if (it == g_user.end()) return RS_ERR_INVAL;
-            dead = spans_release(it->second.spans);
-            g_user.erase(it);
-        }
+        // (the lock is held until the runtime has let go of the dead spans: a
+        // registration of the same pages from another thread in between would
+        // find no span and ask the runtime to register pages it still holds)
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_user.find(reinterpret_cast<uintptr_t>(ptr));
+        if (it == g_user.end()) return RS_ERR_INVAL;
+        const std::vector<uintptr_t> dead = spans_release(it->second.spans);
+        g_user.erase(it);
         if (dead.empty()) return RS_OK;  // every page still held by another registration or the pool
         // No longer found by the lookup; whatever the caller queued over the
         // range finishes before the pages leave the runtime.

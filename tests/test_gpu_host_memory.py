@@ -132,3 +132,38 @@ def test_pool_blocks_reused_and_zero_copy(rslib, orc, torch_dev):
     assert st["blocks"] - st0["blocks"] <= 1 and st["in_use"] == st0["in_use"], (st0, st)
     with pytest.raises(rslib.ErrInvalidArgument):
         rslib.host_free(np.zeros(16, np.uint8).ctypes.data)
+
+
+def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
+    """Two threads register and unregister buffers that share pages (one
+    mapping, the threads' ranges overlapping by half a page) 200 times each:
+    no call fails.  An unregister holds the registry until the runtime has
+    dropped its dead spans, so the other thread never asks the runtime to
+    register pages it still holds."""
+    import mmap
+    import threading
+
+    import reedsolomon_amd as rs
+
+    page = mmap.PAGESIZE
+    m = mmap.mmap(-1, 8 * page)
+    base = np.frombuffer(m, dtype=np.uint8)
+    views = [base[page // 2: 3 * page + page // 2], base[3 * page: 6 * page]]  # share the page at 3 * page
+    errs = []
+
+    def worker(v):
+        try:
+            for _ in range(200):
+                rs.host_register(v.ctypes.data, v.nbytes)
+                rs.host_unregister(v.ctypes.data)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(v,)) for v in views]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    del views, base
+    m.close()
+    assert not errs, errs[:3]
