@@ -106,8 +106,9 @@ int g_jit_path_rows = 16;
 int g_jit_share = 1;
 // rs_tune("jit_share_deep", -1 | 0 | 1): shared-column kernels with two steps
 // of loads in flight and the next column's planes read from LDS ahead
-// (-1: for 8-wave workgroups only)
-int g_jit_share_deep = -1;
+// (-1: for 8-wave workgroups only).  Default off: within 1 % on 128+128 and
+// 1-9 % slower elsewhere (fewer waves per SIMD; profiles/r04/ab_share_deep.log)
+int g_jit_share_deep = 0;
 AsmShape jit_shape(int rows) {
     return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep);
 }

@@ -72,7 +72,7 @@ SWEEP = {
     "jit_wide_pf": [1, 3, 2],
     "jit_wide_waves": [0, 2, 3],
     "jit_share": [0, 1],
-    "jit_share_deep": [0, 1, -1],
+    "jit_share_deep": [1, -1, 0],
     "table_registry_max": [1, 1 << 14],
 }
 

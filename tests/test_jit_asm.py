@@ -186,7 +186,7 @@ def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share, deep):
         src = _check_kernel(rslib, orc, rows, cols, acc)
     finally:
         L.rs_tune(b"jit_share", 1)
-        L.rs_tune(b"jit_share_deep", -1)
+        L.rs_tune(b"jit_share_deep", 0)
     is_deep = share and (deep == 1 or (deep == -1 and rows > 112))
     assert ("lgkmcnt(2)" in src) == bool(is_deep and cols > 1)
     nw = (rows + 15) // 16
@@ -206,12 +206,12 @@ def test_machine_code_equals_assembler_shared(rslib, rows, cols, acc, share):
     L = rslib.lib()
     mat = np.random.default_rng(rows * 37 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
     assert L.rs_tune(b"jit_share", min(share, 1)) == 0
-    assert L.rs_tune(b"jit_share_deep", 1 if share == 2 else -1) == 0
+    assert L.rs_tune(b"jit_share_deep", 1 if share == 2 else 0) == 0
     try:
         n = rslib.jit_encoder_check(mat, bool(acc))
     finally:
         L.rs_tune(b"jit_share", 1)
-        L.rs_tune(b"jit_share_deep", -1)
+        L.rs_tune(b"jit_share_deep", 0)
     assert n > 0 and n % 4 == 0
 
 
