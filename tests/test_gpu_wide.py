@@ -265,3 +265,15 @@ def test_wide_asm_jit_unshared_columns(rslib, orc, torch_dev, asm_jit, rows, col
         test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
     finally:
         asm_jit.rs_tune(b"jit_share", 1)
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 64), (128, 17), (33, 7)])
+def test_wide_asm_jit_shared_deep(rslib, orc, torch_dev, asm_jit, rows, cols):
+    """rs_tune("jit_share_deep", 1): shared columns with two steps of loads in
+    flight and the next column's planes read from LDS ahead (lgkmcnt(2)),
+    against the oracle."""
+    assert asm_jit.rs_tune(b"jit_share_deep", 1) == 0
+    try:
+        test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
+    finally:
+        asm_jit.rs_tune(b"jit_share_deep", 0)
