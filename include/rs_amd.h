@@ -508,6 +508,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * loads and transposes every column), "jit_share_deep" (shared columns with
  * two steps of loads in flight and the next column's planes read ahead, 24
  * more VGPRs: 0 default | 1 | -1 = for 8-wave workgroups only),
+ * "jit_split_cols" (n > 0: products of 9-16 rows over at least n columns run
+ * as two 8-row paths sharing the columns; 0 default: one path; measured
+ * within -4..+4 %),
  * "jit_wide_pf", "jit_wide_waves" (jit_pf and jit_waves of the generated
  * kernels of more than 16 rows; defaults 2 and 3: their 16-row paths fit 168
  * VGPRs, so 3 waves share a SIMD; jit_pf / jit_waves apply to 1-16 rows),

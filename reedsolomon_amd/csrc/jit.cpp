@@ -109,8 +109,15 @@ int g_jit_share = 1;
 // (-1: for 8-wave workgroups only).  Default off: within 1 % on 128+128 and
 // 1-9 % slower elsewhere (fewer waves per SIMD; profiles/r04/ab_share_deep.log)
 int g_jit_share_deep = 0;
-AsmShape jit_shape(int rows) {
-    return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep);
+// rs_tune("jit_split_cols", n): products of 9-16 rows over at least n columns
+// run as two 8-row paths of one workgroup, sharing the columns (0: never)
+int g_jit_split_cols = 0;
+static bool jit_split_small(int rows, int cols) {
+    return g_jit_split_cols > 0 && rows > 8 && rows <= 16 && cols >= g_jit_split_cols;
+}
+AsmShape jit_shape(int rows, int cols) {
+    return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep,
+                     jit_split_small(rows, cols) ? 1 : 0);
 }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // Generated kernels of more than 16 rows (several code paths): two columns of
@@ -120,8 +127,10 @@ int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight
 // rs_tune("jit_wide_pf") / ("jit_wide_waves")
 int g_jit_wide_pf = 2;
 int g_jit_wide_waves = 3;
-int jit_pf_for(int rows) { return rows > 16 ? g_jit_wide_pf : g_jit_pf; }
-int jit_waves_for(int rows) { return rows > 16 ? g_jit_wide_waves : g_jit_waves; }
+int jit_pf_for(int rows, int cols) { return rows > 16 || jit_split_small(rows, cols) ? g_jit_wide_pf : g_jit_pf; }
+int jit_waves_for(int rows, int cols) {
+    return rows > 16 || jit_split_small(rows, cols) ? g_jit_wide_waves : g_jit_waves;
+}
 // rs_tune("jit_backend", 2 | 1 | 0): machine code encoded directly into a
 // code-object template (jit_asm.cpp) | the same kernel as assembly text
 // assembled by comgr | hiprtc C++; env RSAMD_JIT_BACKEND
@@ -745,10 +754,10 @@ std::string jit_source(const uint8_t* mat, int rows, int cols, bool accumulate) 
 int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, double* ms) {
     if (!mat || rows < 1 || rows > jit_max_rows() || cols < 1 || cols > jit_max_cols()) return RS_ERR_INVAL;
     Compiled c =
-        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, jit_shape(rows), jit_pf_for(rows),
-                                                  g_jit_sync, jit_waves_for(rows))
-        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, jit_shape(rows), jit_pf_for(rows),
-                                                    g_jit_sync, jit_waves_for(rows), nullptr))
+        g_jit_backend == 2 ? compile_binary_shape(mat, rows, cols, accumulate, jit_shape(rows, cols), jit_pf_for(rows, cols),
+                                                  g_jit_sync, jit_waves_for(rows, cols))
+        : g_jit_backend    ? compile_asm(asm_source(mat, rows, cols, accumulate, jit_shape(rows, cols), jit_pf_for(rows, cols),
+                                                    g_jit_sync, jit_waves_for(rows, cols), nullptr))
                            : compile(jit_source(mat, rows, cols, accumulate));
     if (ms) *ms = c.ms;
     if (!c.ok) std::fprintf(stderr, "librsamd: jit compile check failed: %s\n", c.log.substr(0, 4000).c_str());
@@ -757,16 +766,16 @@ int jit_compile_check(const uint8_t* mat, int rows, int cols, bool accumulate, d
 
 int jit_encoder_check(const uint8_t* mat, int rows, int cols, bool accumulate, size_t* code_bytes) {
     if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
-    const AsmShape sh = jit_shape(rows);
+    const AsmShape sh = jit_shape(rows, cols);
     std::vector<uint32_t> bin;
     int used = 0;
     std::string err;
-    if (!asm_binary(mat, rows, cols, accumulate, sh, jit_pf_for(rows), g_jit_sync, &bin, &used, &err)) {
+    if (!asm_binary(mat, rows, cols, accumulate, sh, jit_pf_for(rows, cols), g_jit_sync, &bin, &used, &err)) {
         std::fprintf(stderr, "librsamd: encoder failed: %s\n", err.c_str());
         return RS_ERR_DEVICE;
     }
     Compiled c = compile_asm(
-        asm_source(mat, rows, cols, accumulate, sh, jit_pf_for(rows), g_jit_sync, jit_waves_for(rows), nullptr));
+        asm_source(mat, rows, cols, accumulate, sh, jit_pf_for(rows, cols), g_jit_sync, jit_waves_for(rows, cols), nullptr));
     std::vector<char> text;
     if (!c.ok || !asm_text_section(c.code, &text)) {
         std::fprintf(stderr, "librsamd: encoder check: assembly failed: %s\n", c.log.substr(0, 2000).c_str());
@@ -842,14 +851,15 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(a.accumulate ? 1 : 0);
     k.text += static_cast<char>(a.rows);
     k.text += static_cast<char>(a.cols);
-    k.text += static_cast<char>(g_jit_backend ? jit_pf_for(a.rows) : g_jit_pf);
+    k.text += static_cast<char>(g_jit_backend ? jit_pf_for(a.rows, a.cols) : g_jit_pf);
     k.text += static_cast<char>(g_jit_backend ? g_jit_sync : 0);
-    k.text += static_cast<char>(g_jit_backend ? jit_waves_for(a.rows) : 0);
+    k.text += static_cast<char>(g_jit_backend ? jit_waves_for(a.rows, a.cols) : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_layout : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_group_waves : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_path_rows : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share_deep : 0);
+    k.text += static_cast<char>(g_jit_backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -877,14 +887,15 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(a.rows >> 8);
     key += static_cast<char>(a.cols);
     key += static_cast<char>(a.cols >> 8);
-    key += static_cast<char>(backend ? jit_pf_for(a.rows) : g_jit_pf);
+    key += static_cast<char>(backend ? jit_pf_for(a.rows, a.cols) : g_jit_pf);
     key += static_cast<char>(backend ? g_jit_sync : 0);
-    key += static_cast<char>(backend ? jit_waves_for(a.rows) : 0);
+    key += static_cast<char>(backend ? jit_waves_for(a.rows, a.cols) : 0);
     key += static_cast<char>(backend ? g_jit_layout : 0);
     key += static_cast<char>(backend ? g_jit_group_waves : 0);
     key += static_cast<char>(backend ? g_jit_path_rows : 0);
     key += static_cast<char>(backend ? g_jit_share : 0);
     key += static_cast<char>(backend ? g_jit_share_deep : 0);
+    key += static_cast<char>(backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);
@@ -913,7 +924,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                     e = std::make_shared<Entry>();
                     e->is_asm = backend != 0;
                     e->backend = backend;
-                    e->shape = jit_shape(a.rows);
+                    e->shape = jit_shape(a.rows, a.cols);
                     e->nw = e->shape.nw;
                     e->code = std::move(code);
                     e->state = Entry::kReady;
@@ -943,19 +954,19 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
             e = std::make_shared<Entry>();
             e->is_asm = backend != 0;
             e->backend = backend;
-            e->shape = jit_shape(a.rows);
+            e->shape = jit_shape(a.rows, a.cols);
             e->nw = e->shape.nw;
             if (backend == 2) {
                 e->mat.assign(a.host_mat, a.host_mat + static_cast<size_t>(a.rows) * a.cols);
                 e->rows = a.rows;
                 e->cols = a.cols;
                 e->acc = a.accumulate != 0;
-                e->pf = jit_pf_for(a.rows);
+                e->pf = jit_pf_for(a.rows, a.cols);
                 e->sync = g_jit_sync;
-                e->waves = jit_waves_for(a.rows);
+                e->waves = jit_waves_for(a.rows, a.cols);
             } else {
                 e->src = e->is_asm ? asm_source(a.host_mat, a.rows, a.cols, a.accumulate != 0, e->shape,
-                                                jit_pf_for(a.rows), g_jit_sync, jit_waves_for(a.rows), nullptr)
+                                                jit_pf_for(a.rows, a.cols), g_jit_sync, jit_waves_for(a.rows, a.cols), nullptr)
                                    : jit_source(a.host_mat, a.rows, a.cols, a.accumulate != 0);
             }
             if (backend != 2 && g_jit_disk_cache && !cache_dir().empty()) e->disk = disk_key(arch, a);
@@ -1072,7 +1083,7 @@ JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {
 
 int jit_asm_source_text(const uint8_t* mat, int rows, int cols, bool accumulate, std::string* out) {
     if (!mat || rows < 1 || rows > kAsmMaxRows || cols < 1 || cols > kAsmMaxCols) return RS_ERR_INVAL;
-    *out = asm_source(mat, rows, cols, accumulate, jit_shape(rows), jit_pf_for(rows), g_jit_sync, jit_waves_for(rows),
+    *out = asm_source(mat, rows, cols, accumulate, jit_shape(rows, cols), jit_pf_for(rows, cols), g_jit_sync, jit_waves_for(rows, cols),
                       nullptr);
     return RS_OK;
 }

@@ -53,11 +53,13 @@ struct AsmShape {
 };
 // deep: -1 = when the workgroup has 8 waves (one workgroup per CU whatever
 // the registers: the extra 24 VGPRs cost no occupancy), 0 / 1 = off / on.
+// split_small: a product of 9-16 rows runs as two paths of at most 8 rows
+// (half the accumulator registers per wave) instead of one.
 inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0,
-                          int deep = -1) {
+                          int deep = -1, int split_small = 0) {
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
-    const int paths = rows <= 16 ? 1 : (rows + pr - 1) / pr;
+    const int paths = rows <= 16 ? (split_small && rows > 8 ? 2 : 1) : (rows + pr - 1) / pr;
     s.layout = layout == 1 ? 1 : 0;
     s.rw = (rows + paths - 1) / paths;
     // (layout 1: a power of two, the kernel maps chunks with shifts)

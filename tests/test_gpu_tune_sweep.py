@@ -73,6 +73,7 @@ SWEEP = {
     "jit_wide_waves": [0, 2, 3],
     "jit_share": [0, 1],
     "jit_share_deep": [1, -1, 0],
+    "jit_split_cols": [4, 0],
     "table_registry_max": [1, 1 << 14],
 }
 

@@ -228,3 +228,17 @@ def test_emulator_catches_a_missing_barrier(rslib, orc):
             _check_kernel(rslib, orc, 33, 7, 0, edit=lambda s: s.replace("\ts_barrier\n", ""))
     finally:
         L.rs_tune(b"jit_share", 1)
+
+
+@pytest.mark.parametrize("rows,cols,acc", [(16, 20, 0), (12, 9, 1), (9, 17, 0)])
+def test_asm_kernel_split_small(rslib, orc, rows, cols, acc):
+    """rs_tune("jit_split_cols", n): products of 9-16 rows over at least n
+    columns run as two paths of at most 8 rows in one workgroup, sharing the
+    columns through LDS, against the oracle."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_split_cols", 8) == 0
+    try:
+        src = _check_kernel(rslib, orc, rows, cols, acc, paths=2)
+    finally:
+        L.rs_tune(b"jit_split_cols", 0)
+    assert "ds_write_b128" in src and ".amdhsa_group_segment_fixed_size 8192" in src

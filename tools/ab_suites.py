@@ -85,6 +85,13 @@ SUITES = {
     "share_deep": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
                     ["jit_share_deep=0", "jit_share_deep=1", "jit_share_deep=1,jit_wide_waves=0"])
                    for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
+    # round 4: 9-16 rows over many columns as two 8-row paths sharing the columns (jit_split_cols)
+    "split_small": [(dict(AB_K=str(k), AB_M=str(m), AB_VEC=str(v), **({"AB_S": str(s_)} if s_ else {})),
+                     [f"{op}", f"{op},jit_split_cols=16", f"{op},jit_split_cols=16,jit_wide_waves=0",
+                      f"{op},jit_split_cols=16,jit_wide_waves=4,jit_wide_pf=1"])
+                    for k, m, v, s_, op in ((48, 16, 262144, 224, "op=rec16"), (100, 16, 262144, 112, "op=rec16"),
+                                            (200, 16, 1 << 20, 16, "op=enc"), (16, 16, 1 << 20, 112, "op=enc"),
+                                            (32, 12, 1 << 20, 72, "op=enc"))],
     # round 4: 3-4 rows over more than 4 runtime columns, 16-byte units on 256 lanes (default since
     # round 1) vs 8-byte units on 128 lanes (var=201, experiments build), split and interleaved
     "wide34_r4": shapes([(16, 4), (20, 4), (8, 4), (6, 3), (9, 3), (16, 3)],
