@@ -123,11 +123,24 @@ def _host_array(buf, writable: bool) -> np.ndarray:
     return a
 
 
+_addr_of = ctypes.addressof
+_char_from = ctypes.c_char.from_buffer
+
+
+def _data_ptr(a: np.ndarray) -> int:
+    # a ctypes view of a writable buffer gives its address ~2.5x faster than
+    # __array_interface__ (which builds a dict per call); read-only arrays
+    # (and empty ones) take the interface
+    try:
+        return _addr_of(_char_from(a))
+    except (TypeError, ValueError):
+        return a.__array_interface__["data"][0]
+
+
 def _host_vecs(bufs: Sequence, writable: bool):
     arrs = [_host_array(b, writable) for b in bufs]
     n = len(arrs)
-    # one address read per vector (data_as() per vector costs ~2x more)
-    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.__array_interface__["data"][0] for a in arrs])
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[_data_ptr(a) for a in arrs])
     lens = (ctypes.c_size_t * max(n, 1))(*[a.size for a in arrs])
     return arrs, ctypes.cast(ptrs, c_u8pp), lens, n
 
