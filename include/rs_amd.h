@@ -508,6 +508,8 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * loads and transposes every column), "jit_share_deep" (shared columns with
  * two steps of loads in flight and the next column's planes read ahead, 24
  * more VGPRs: 0 default | 1 | -1 = for 8-wave workgroups only),
+ * "jit_share_cols" (shared columns: columns each wave loads per step, one
+ * barrier per nw x n columns: 1 default | 2 | -1 = 2 for 8-wave workgroups),
  * "jit_split_cols" (n > 0: products of 9-16 rows over at least n columns run
  * as two 8-row paths sharing the columns; 0 default: one path; measured
  * within -4..+4 %),

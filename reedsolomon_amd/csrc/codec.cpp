@@ -605,6 +605,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_share") g_jit_share = value ? 1 : 0;
         else if (n == "jit_share_deep") g_jit_share_deep = value < 0 ? -1 : value ? 1 : 0;
         else if (n == "jit_split_cols") g_jit_split_cols = value < 0 ? 0 : value;
+        else if (n == "jit_share_cols") g_jit_share_cols = value < 0 ? -1 : value > 2 ? 2 : value < 1 ? 1 : value;
         else if (n == "jit_wide_pf") g_jit_wide_pf = value < 1 ? 1 : value > 4 ? 4 : value;
         else if (n == "jit_wide_waves") g_jit_wide_waves = value < 0 ? 0 : value > 8 ? 8 : value;
         else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;

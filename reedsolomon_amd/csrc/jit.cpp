@@ -115,9 +115,13 @@ int g_jit_split_cols = 0;
 static bool jit_split_small(int rows, int cols) {
     return g_jit_split_cols > 0 && rows > 8 && rows <= 16 && cols >= g_jit_split_cols;
 }
+// rs_tune("jit_share_cols", 1 | 2 | -1): columns each wave of a shared-column
+// kernel loads per step, i.e. one barrier per nw x n columns (-1: 2 for 8-wave
+// workgroups, whose occupancy the 8 extra VGPRs do not change)
+int g_jit_share_cols = 1;
 AsmShape jit_shape(int rows, int cols) {
     return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep,
-                     jit_split_small(rows, cols) ? 1 : 0);
+                     jit_split_small(rows, cols) ? 1 : 0, g_jit_share_cols);
 }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // Generated kernels of more than 16 rows (several code paths): two columns of
@@ -860,6 +864,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_backend ? g_jit_share : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share_deep : 0);
     k.text += static_cast<char>(g_jit_backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_share_cols : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -896,6 +901,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(backend ? g_jit_share : 0);
     key += static_cast<char>(backend ? g_jit_share_deep : 0);
     key += static_cast<char>(backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
+    key += static_cast<char>(backend ? g_jit_share_cols : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);

@@ -454,12 +454,13 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     const int rw = sh.rw;  // rows per code path (per wave in layout 0, per workgroup in layout 1)
     const int npaths = (rows + rw - 1) / rw;
     const bool share = sh.share && !by_group && npaths > 1;
-    const bool deep = share && sh.deep;
+    const int K = share && sh.kcols > 1 ? sh.kcols : 1;  // own columns per wave and step
+    const bool deep = share && sh.deep && K == 1;
     Layout L;
     // (share: one column of loads in flight per wave, i.e. nw columns of the
     // workgroup - two with deep; the planes read back from LDS get registers
     // of their own, two sets with deep)
-    L.pf = share ? (deep ? 2 : 1) : pf < 1 ? 1 : pf > 4 ? 4 : pf;
+    L.pf = share ? (deep ? 2 : K) : pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
     const int kVPlanes = L.slots_end;
     L.sub = L.slots_end + (share ? (deep ? 16 : 8) : 0);  // 2 x 11 subset registers: the XORs of 2-4 planes of each half
@@ -723,24 +724,26 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
             // apart), loads its next column, and after the barrier combines the
             // step's nw columns from LDS into its rows.  One barrier per step
             // also frees buffer s & 1 for step s + 2: every wave has combined
-            // step s before it passes the barrier of step s + 1.
-            const int steps = (cols + npaths - 1) / npaths;
+            // step s before it passes the barrier of step s + 1.  With K > 1
+            // (AsmShape::kcols) a step is K columns per wave (half the barriers),
+            // column s * nw * K + q * nw + w being the wave's q-th of the step.
+            const int per = npaths * K;
+            const int steps = (cols + per - 1) / per;
             for (int st = 0; st < steps; ++st) {
-                const int c = st * npaths + w;
-                const uint32_t buf = static_cast<uint32_t>(st & 1) * static_cast<uint32_t>(npaths) * 2048u;
-                if (c < cols) {
+                const uint32_t buf = static_cast<uint32_t>(st & 1) * static_cast<uint32_t>(per) * 2048u;
+                for (int q = 0; q < K; ++q) {
+                    const int c = st * per + q * npaths + w, k_ = st * K + q;
+                    if (c >= cols) break;
                     vmem_wait_for(col_id[static_cast<size_t>(c)]);
                     int pr[8];
-                    for (int j = 0; j < 8; ++j) pr[j] = slot_reg(st, j);
+                    for (int j = 0; j < 8; ++j) pr[j] = slot_reg(k_, j);
                     transpose8(P, pr, kVT1);
-                }
-                // LDS address of lane t: 16 t (kVT0 is free between transposes)
-                P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
-                P.v_op2(kVLshl, kVT0, C(1), kVT0);
-                if (c < cols) {
-                    const uint32_t off = buf + static_cast<uint32_t>(w) * 2048u;
-                    P.ds_write4(kVT0, slot_reg(st, 0), off);
-                    P.ds_write4(kVT0, slot_reg(st, 4), off + 1024u);
+                    // LDS address of lane t: 16 t (kVT0 is free between transposes)
+                    P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
+                    P.v_op2(kVLshl, kVT0, C(1), kVT0);
+                    const uint32_t off = buf + static_cast<uint32_t>(q * npaths + w) * 2048u;
+                    P.ds_write4(kVT0, slot_reg(k_, 0), off);
+                    P.ds_write4(kVT0, slot_reg(k_, 4), off + 1024u);
                     P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
                     if (c + L.pf * npaths < cols) {
                         issue_col(c + L.pf * npaths);
@@ -749,8 +752,12 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                         if (deep) P.wait_lgkm0();
                     }
                 }
+                if (st * per + w >= cols) {  // no column of this wave in the step: the address still
+                    P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
+                    P.v_op2(kVLshl, kVT0, C(1), kVT0);
+                }
                 P.s_barrier();
-                const int ncol = std::min(npaths, cols - st * npaths);
+                const int ncol = std::min(per, cols - st * per);
                 auto read = [&](int j) {
                     const uint32_t off = buf + static_cast<uint32_t>(j) * 2048u;
                     const int d = kVPlanes + (deep ? 8 * (j & 1) : 0);
@@ -767,7 +774,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                     }
                     int pr[8];
                     for (int q = 0; q < 8; ++q) pr[q] = kVPlanes + (deep ? 8 * (j & 1) : 0) + q;
-                    combine(st * npaths + j, pr);
+                    combine(st * per + j, pr);
                     if (!deep && j + 1 < ncol) read(j + 1);
                 }
             }

@@ -50,13 +50,14 @@ struct AsmShape {
     int groups = 1;  // layout 1: row groups G (= code paths)
     int share = 0;   // layout 0, nw > 1: columns shared through LDS
     int deep = 0;    // share: two steps of loads in flight and the next column's planes read ahead
+    int kcols = 1;   // share: columns each wave loads per step (one barrier per nw * kcols columns)
 };
 // deep: -1 = when the workgroup has 8 waves (one workgroup per CU whatever
 // the registers: the extra 24 VGPRs cost no occupancy), 0 / 1 = off / on.
 // split_small: a product of 9-16 rows runs as two paths of at most 8 rows
 // (half the accumulator registers per wave) instead of one.
 inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0,
-                          int deep = -1, int split_small = 0) {
+                          int deep = -1, int split_small = 0, int kcols = 1) {
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
     const int paths = rows <= 16 ? (split_small && rows > 8 ? 2 : 1) : (rows + pr - 1) / pr;
@@ -67,10 +68,12 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     s.groups = s.layout ? paths : 1;
     s.share = (share && !s.layout && paths > 1) ? 1 : 0;
     s.deep = s.share && (deep < 0 ? s.nw >= 8 : deep > 0) ? 1 : 0;
+    s.kcols = s.share ? (kcols < 0 ? (s.nw >= 8 ? 2 : 1) : kcols < 1 ? 1 : kcols > 2 ? 2 : kcols) : 1;
+    if (s.kcols > 1) s.deep = 0;
     return s;
 }
 // LDS bytes per workgroup of a generated kernel.
-inline int asm_lds_bytes(const AsmShape& s) { return s.share ? 2 * s.nw * 2048 : 0; }
+inline int asm_lds_bytes(const AsmShape& s) { return s.share ? 2 * s.nw * s.kcols * 2048 : 0; }
 // Waves per workgroup of layout 0 (16 rows per wave at most).
 inline int asm_waves(int rows) { return asm_shape(rows, 0, 1).nw; }
 // (path_rows: products of more than 16 rows run in code paths of at most

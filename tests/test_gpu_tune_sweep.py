@@ -74,6 +74,7 @@ SWEEP = {
     "jit_share": [0, 1],
     "jit_share_deep": [1, -1, 0],
     "jit_split_cols": [4, 0],
+    "jit_share_cols": [2, -1, 1],
     "table_registry_max": [1, 1 << 14],
 }
 

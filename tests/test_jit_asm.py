@@ -164,12 +164,13 @@ def test_asm_kernel_path_rows(rslib, orc, rows, cols, acc, path_rows, layout):
         L.rs_tune(b"jit_layout", 0)
 
 
-@pytest.mark.parametrize("rows,cols,acc,share,deep", [(33, 7, 0, 1, -1), (40, 9, 1, 1, -1), (17, 5, 0, 1, -1),
-                                                     (64, 5, 1, 1, -1), (20, 1, 0, 1, -1), (48, 12, 0, 1, -1),
-                                                     (33, 7, 0, 0, -1), (40, 9, 1, 0, -1), (33, 7, 1, 1, 1),
-                                                     (64, 13, 0, 1, 1), (17, 2, 0, 1, 1), (128, 9, 1, 1, -1),
-                                                     (128, 17, 0, 1, 0)])
-def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share, deep):
+@pytest.mark.parametrize("rows,cols,acc,share,deep,kc", [(33, 7, 0, 1, -1, 1), (40, 9, 1, 1, -1, 1), (17, 5, 0, 1, -1, 1),
+                                                        (64, 5, 1, 1, -1, 1), (20, 1, 0, 1, -1, 1), (48, 12, 0, 1, -1, 1),
+                                                        (33, 7, 0, 0, -1, 1), (40, 9, 1, 0, -1, 1), (33, 7, 1, 1, 1, 1),
+                                                        (64, 13, 0, 1, 1, 1), (17, 2, 0, 1, 1, 1), (128, 9, 1, 1, -1, 1),
+                                                        (128, 17, 0, 1, 0, 1), (33, 7, 0, 1, 0, 2), (40, 13, 1, 1, 0, 2),
+                                                        (17, 3, 0, 1, 0, 2), (128, 19, 0, 1, 0, 2), (64, 1, 1, 1, 0, 2)])
+def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share, deep, kc):
     """rs_tune("jit_share", 1, the default): the waves of a multi-path workgroup share the
     column work through LDS (step s: wave w loads and transposes column
     s * nw + w into LDS buffer s & 1, barrier, every wave combines the step's
@@ -182,18 +183,20 @@ def test_asm_kernel_shared_columns(rslib, orc, rows, cols, acc, share, deep):
     planes read from LDS while the current one combines (lgkmcnt(2))."""
     L = rslib.lib()
     assert L.rs_tune(b"jit_share", share) == 0 and L.rs_tune(b"jit_share_deep", deep) == 0
+    assert L.rs_tune(b"jit_share_cols", kc) == 0
     try:
         src = _check_kernel(rslib, orc, rows, cols, acc)
     finally:
         L.rs_tune(b"jit_share", 1)
         L.rs_tune(b"jit_share_deep", 0)
-    is_deep = share and (deep == 1 or (deep == -1 and rows > 112))
+        L.rs_tune(b"jit_share_cols", 1)
+    is_deep = share and kc == 1 and (deep == 1 or (deep == -1 and rows > 112))
     assert ("lgkmcnt(2)" in src) == bool(is_deep and cols > 1)
     nw = (rows + 15) // 16
-    steps = (cols + nw - 1) // nw
+    steps = (cols + nw * kc - 1) // (nw * kc)
     assert src.count("s_barrier") == (nw * steps if share else 0)
     assert src.count("ds_write_b128") == (2 * cols if share else 0)
-    assert f".amdhsa_group_segment_fixed_size {2 * nw * 2048 if share else 0}" in src
+    assert f".amdhsa_group_segment_fixed_size {2 * nw * kc * 2048 if share else 0}" in src
 
 
 @pytest.mark.parametrize("rows,cols,acc,share", [(64, 64, 0, 1), (56, 200, 1, 1), (128, 128, 0, 1), (33, 3, 1, 1),

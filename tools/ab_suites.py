@@ -91,6 +91,10 @@ SUITES = {
                      ["", "jit_path_rows=13", "jit_path_rows=13,jit_share_deep=1", "jit_path_rows=11,jit_share_deep=1",
                       "jit_path_rows=11"])
                     for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
+    # round 4: shared columns, two columns per wave and step (half the barriers, 8 more VGPRs)
+    "share_cols": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
+                    ["", "jit_share_cols=2", "jit_share_cols=2,jit_wide_waves=0"])
+                   for k, m, s in ((32, 32, 56), (64, 64, 28), (128, 128, 14), (200, 56, 14))],
     # round 4: 9-16 rows over many columns as two 8-row paths sharing the columns (jit_split_cols)
     "split_small": [(dict(AB_K=str(k), AB_M=str(m), AB_VEC=str(v), **({"AB_S": str(s_)} if s_ else {})),
                      [f"{op}", f"{op},jit_split_cols=16", f"{op},jit_split_cols=16,jit_wide_waves=0",
