@@ -994,12 +994,17 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
         if (poller) {
             const uint64_t* lines = reinterpret_cast<const uint64_t*>(slot);
             uint64_t w = 0, seq = 0;
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             auto issue = [&]() -> uint64_t { return lane < kPollWords ? sys_load64(&lines[lane]) : 0; };
-            // the call number if the read shows call last + 1 complete, else 0
-            auto probe = [&](uint64_t x) -> uint64_t {
+            // does the call whose header word 5 is w5 name this workgroup?
+            auto concerns = [&](uint64_t w5) {
+                const uint32_t g0 = static_cast<uint32_t>(w5 >> 8) & 0xff, ng = static_cast<uint32_t>(w5 >> 16) & 0xff;
+                return (blockIdx.x + gridDim.x - g0) % gridDim.x < ng;
+            };
+            // the call number if the read shows call `want` complete, else 0
+            auto probe_at = [&](uint64_t x, uint64_t want) -> uint64_t {
                 const uint64_t s0 = lane_u64(x, 0), s1 = lane_u64(x, 7);
-                if (s0 != s1 || s0 != last + 1) return 0;
+                if (s0 != s1 || s0 != want) return 0;
                 // address mode: the lines holding this call's addresses carry its tag
                 const uint64_t w4 = lane_u64(x, 4), w5 = lane_u64(x, 5);
                 const int nv = static_cast<int>((w4 >> 32) & 0xffff) + static_cast<int>(w4 >> 48);
@@ -1009,6 +1014,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
                         tagged = tagged && lane_u64(x, 8 * l + 7) == s0;
                 return tagged ? s0 : 0;
             };
+            auto probe = [&](uint64_t x) -> uint64_t { return probe_at(x, last + 1); };
             // stop word, or no call for idle_ticks: seq stays 0 and every wave leaves
             auto leave = [&](uint64_t x, uint32_t n) {
                 if (lane_u64(x, 6) >= epoch) return true;
@@ -1017,10 +1023,38 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
                 return now - t0 > idle_ticks || now - t_birth > life_ticks;
             };
             if (poll_gap == 0) {  // one read per round trip
+                // With the slot's lines the same round trip brings the headers
+                // of the next kEngineSlots - 1 slots: rung calls that name other
+                // workgroups are passed without another read (each used to cost
+                // this workgroup a PCIe round trip, which bounded concurrent
+                // callers' throughput), and the done word records them.
+                uint64_t cur = last + 1;
                 for (uint32_t n = 1;; ++n) {
-                    w = issue();
-                    if ((seq = probe(w)) != 0 || leave(w, n)) break;
-                    __builtin_amdgcn_s_sleep(2);
+                    const uint64_t* ln = reinterpret_cast<const uint64_t*>(&slots[cur % kEngineSlots]);
+                    const uint64_t* nh = reinterpret_cast<const uint64_t*>(&slots[(cur + 1 + lane / 8) % kEngineSlots]);
+                    w = lane < kPollWords ? sys_load64(&ln[lane]) : 0;
+                    const uint64_t hn = lane < 8 * (kEngineSlots - 1) ? sys_load64(&nh[lane % 8]) : 0;
+                    if ((seq = probe_at(w, cur)) == 0) {
+                        if (leave(w, n)) break;
+                        __builtin_amdgcn_s_sleep(2);
+                        continue;
+                    }
+                    if (concerns(lane_u64(w, 5))) break;  // call cur is this workgroup's: w holds its lines
+                    uint64_t passed = cur;
+#pragma unroll
+                    for (int k = 0; k < kEngineSlots - 1; ++k) {
+                        const uint64_t s0 = lane_u64(hn, 8 * k), s1 = lane_u64(hn, 8 * k + 7);
+                        if (s0 != s1 || s0 != passed + 1 || lane_u64(hn, 8 * k + 6) >= epoch ||
+                            concerns(lane_u64(hn, 8 * k + 5)))
+                            break;
+                        ++passed;
+                    }
+                    if (lane == 0)
+                        __hip_atomic_store(&ring->done[blockIdx.x], passed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    cur = passed + 1;
+                    seq = 0;
+                    n = 0;  // (progress: the idle window starts again)
+                    t0 = __builtin_amdgcn_s_memrealtime();
                 }
             } else {  // two reads in flight, poll_gap ticks apart; the older is checked first
                 uint64_t wa = issue();
@@ -1047,6 +1081,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
         __syncthreads();
         const uint64_t seq = s_raw[0];
         if (seq == 0) return;  // uniform over the workgroup (doorbell values start at 1)
+        slot = &slots[seq % kEngineSlots];  // (the poller may have passed calls that name other workgroups)
         const uint64_t base = s_raw[1], stride = s_raw[2];
         const uint64_t w3 = s_raw[3], w4 = s_raw[4], w5 = s_raw[5];
         const uint32_t pitch = static_cast<uint32_t>(w3), units = static_cast<uint32_t>(w3 >> 32);
