@@ -869,6 +869,8 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {  // every lane hol
 }
 
 constexpr int kEngineColBatch = 16;  // column loads in flight per lane (one PCIe round trip per batch)
+// slot headers read ahead by each poll (8 words each: one 64-lane load)
+constexpr int kEngineLook = kEngineSlots - 1 < 7 ? kEngineSlots - 1 : 7;
 
 struct EngineCall {
     const uint64_t* vaddr;  // LDS: device address of vector i of stripe 0
@@ -1024,7 +1026,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
             };
             if (poll_gap == 0) {  // one read per round trip
                 // With the slot's lines the same round trip brings the headers
-                // of the next kEngineSlots - 1 slots: rung calls that name other
+                // of the next kEngineLook slots: rung calls that name other
                 // workgroups are passed without another read (each used to cost
                 // this workgroup a PCIe round trip, which bounded concurrent
                 // callers' throughput), and the done word records them.
@@ -1033,7 +1035,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
                     const uint64_t* ln = reinterpret_cast<const uint64_t*>(&slots[cur % kEngineSlots]);
                     const uint64_t* nh = reinterpret_cast<const uint64_t*>(&slots[(cur + 1 + lane / 8) % kEngineSlots]);
                     w = lane < kPollWords ? sys_load64(&ln[lane]) : 0;
-                    const uint64_t hn = lane < 8 * (kEngineSlots - 1) ? sys_load64(&nh[lane % 8]) : 0;
+                    const uint64_t hn = lane < 8 * kEngineLook ? sys_load64(&nh[lane % 8]) : 0;
                     if ((seq = probe_at(w, cur)) == 0) {
                         if (leave(w, n)) break;
                         __builtin_amdgcn_s_sleep(2);
@@ -1042,7 +1044,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
                     if (concerns(lane_u64(w, 5))) break;  // call cur is this workgroup's: w holds its lines
                     uint64_t passed = cur;
 #pragma unroll
-                    for (int k = 0; k < kEngineSlots - 1; ++k) {
+                    for (int k = 0; k < kEngineLook; ++k) {
                         const uint64_t s0 = lane_u64(hn, 8 * k), s1 = lane_u64(hn, 8 * k + 7);
                         if (s0 != s1 || s0 != passed + 1 || lane_u64(hn, 8 * k + 6) >= epoch ||
                             concerns(lane_u64(hn, 8 * k + 5)))
