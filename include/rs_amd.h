@@ -450,8 +450,10 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * 0 default = adaptive: a lone call spreads over the first wave of every
  * workgroup, calls that overlap others take one unit per lane of one
  * workgroup, so calls in flight run on different workgroups),
- * "host_engine_split_rows" (0 default: a lone call's output rows are all
- * computed by the first wave of each workgroup | 1: by separate waves, each
+ * "host_engine_split_rows" (2 default: a lone call of >= 3 rows and >= 4
+ * columns small enough for one 64-lane group per workgroup has its rows
+ * computed by separate waves from inputs loaded once into LDS | 0: every
+ * row by the first wave of each workgroup | 1: by separate waves, each
  * reading every input again; measured 2x slower over host memory),
  * "host_engine_poll_gap" (0 default: the engine reads the doorbell once per
  * PCIe round trip | n: two reads in flight, n x 10 ns apart),

@@ -90,11 +90,13 @@ size_t g_engine_max_bytes = 1u << 20;  // rs_tune("host_engine_max_bytes")
 // workgroup); rs_tune("host_engine_wg_units")
 int g_engine_wg_units = 0;
 // A lone call's output rows computed by separate waves of each workgroup
-// (1) or all by its first wave (0, default); rs_tune("host_engine_split_rows").
-// Measured slower: each wave reads every input over PCIe again (host memory is
-// not cached), 10+4 @ 8 KiB Encode 10.8 -> 20.5 us, Reconst of 4 10.9 -> 20.4
+// (1: each wave reads every input; 2: the waves load the inputs once into
+// LDS, default, for calls of >= 3 rows and >= 4 columns that one 64-unit group
+// per workgroup covers) or all by its first wave (0); rs_tune("host_engine_split_rows").
+// 1 measured slower: each wave reads every input over PCIe again (host memory
+// is not cached), 10+4 @ 8 KiB Encode 10.8 -> 20.5 us, Reconst of 4 10.9 -> 20.4
 // (profiles/r03/host_latency_split_rows.log)
-int g_engine_split_rows = 0;
+int g_engine_split_rows = 2;
 // Waiters spin this long, then yield the core between polls; rs_tune("host_engine_yield_us"), 0 = never
 // (default): 8-64 threads on the box measured the same either way and a lone
 // caller ~1 us slower with it (profiles/r02/engine_yield.log)
@@ -576,9 +578,17 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     h->cols = static_cast<uint16_t>(cols);
     // a lone call with all its units on the workgroups' first waves also
     // spreads its rows over their waves (host_engine_split_rows)
-    const bool split = g_engine_split_rows && lone && per_wg == 64 && rows > 1 && rows <= rs->eng_group_waves;
+    // (mode 2, the inputs read once into LDS: only where one group of 64 units
+    // per workgroup covers the call and there are enough rows and columns to
+    // share - 10+4 @ 8 KiB Encode 11.1 -> 10.5 us pageable, 9.7 -> 8.8
+    // registered; 64 KiB calls and 1-2-column Update / Replace were slower,
+    // profiles/r04/engine_shared_rows.log)
+    const bool split = g_engine_split_rows && lone && per_wg == 64 && rows > 1 && rows <= rs->eng_group_waves &&
+                       (g_engine_split_rows != 2 ||
+                        (rows >= 3 && cols >= 4 && total <= uint64_t{64} * static_cast<uint64_t>(inst_waves)));
     h->flags = (wk.accumulate ? 1u : 0u) | (wk.coherent ? 2u : 0u) | (g_engine_trace ? 4u : 0u) | (wk.addr ? 8u : 0u) |
-               (split ? 16u : 0u) | (static_cast<uint32_t>(wg0) << 8) | (static_cast<uint32_t>(nwg) << 16);
+               (split ? (g_engine_split_rows == 2 ? 32u : 16u) : 0u) | (static_cast<uint32_t>(wg0) << 8) |
+               (static_cast<uint32_t>(nwg) << 16);
     h->tab_id = rs->eng_tab_id;
     // (write-combined device-memory slots and staging blocks: sfence makes
     // every store before it visible first, tables, addresses and inputs

@@ -969,6 +969,57 @@ __device__ __forceinline__ void engine_units_row(const EngineCall& e, const uint
     }
 }
 
+// A lone call's rows over the waves of each workgroup with the inputs read
+// once (host_engine_split_rows 2): wave w loads columns w, w + nw, ... of the
+// workgroup's 64 units into LDS (the loads of all waves in flight together),
+// and after a barrier wave r < rows combines every column from LDS into row r.
+// The row-per-wave variant above read every input over PCIe once per wave.
+constexpr int kEngineShareCols = 8;  // columns per wave (nw >= 4 for 32 columns)
+__device__ __forceinline__ void engine_units_shared(const EngineCall& e, const uint32_t* tab, int rows,
+                                                    u32x4 (*sh)[64]) {
+    typedef __attribute__((address_space(1))) u32x4 gq;
+    const int wave = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
+    const int nw = static_cast<int>(blockDim.x >> 6);
+    for (uint32_t u0 = e.local * 64u; u0 < e.total; u0 += e.nwg * 64u) {  // (uniform over the workgroup)
+        const uint32_t u = u0 + static_cast<uint32_t>(lane);
+        const bool valid = u < e.total;
+        const uint32_t si = valid ? u / e.units : 0, k = valid ? u - si * e.units : 0;
+        const uint64_t sb = static_cast<uint64_t>(si) * e.stride + static_cast<uint64_t>(k) * 16;
+        u32x4 x[kEngineShareCols];
+#pragma unroll
+        for (int j = 0; j < kEngineShareCols; ++j) {
+            const int c = wave + j * nw;
+            if (c < e.cols)
+                x[j] = valid ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(e.vaddr[c] + sb)) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < kEngineShareCols; ++j) {
+            const int c = wave + j * nw;
+            if (c < e.cols) sh[c][lane] = x[j];
+        }
+        __syncthreads();
+        if (wave < rows) {
+            u32x4 acc = e.accumulate && valid
+                            ? __builtin_nontemporal_load(reinterpret_cast<const gq*>(e.vaddr[e.cols + wave] + sb))
+                            : u32x4{0, 0, 0, 0};
+            for (int c = 0; c < e.cols; ++c) {
+                const u32x4 v = sh[c][lane];
+                uint32_t t[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) t[i] = tab[(c * kEngineMaxRows + wave) * 5 + i];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t g0, g1, g2;
+                    split_groups(v[q], g0, g1, g2);
+                    acc[q] ^= gf_mul_packed(g0, g1, g2, t);
+                }
+            }
+            if (valid) __builtin_nontemporal_store(acc, reinterpret_cast<gq*>(e.vaddr[e.cols + wave] + sb));
+        }
+        __syncthreads();  // (the next group's loads overwrite sh)
+    }
+}
+
 __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineSlot* vslots, uint64_t start,
                                                  uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks,
                                                  uint32_t poll_gap) {
@@ -979,6 +1030,7 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
     __shared__ __attribute__((aligned(16))) uint32_t tab[kEngineMaxCols * kEngineMaxRows * 5];
     __shared__ uint64_t s_raw[kPollWords];  // the lines wave 0 saw (s_raw[0] = 0: leave)
     __shared__ uint64_t s_vaddr[kEngineMaxCols + kEngineMaxRows];
+    __shared__ u32x4 s_in[kEngineMaxCols][64];  // host_engine_split_rows 2: a group's inputs
     const int lane = threadIdx.x & 63;
     const bool poller = threadIdx.x < 64;  // wave 0 polls and signals; the others wait at the barrier
     // a relaunch resumes after the last call this workgroup completed
@@ -1128,13 +1180,18 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
         // CU's L1 and the XCD's L2), but the memory model does not promise
         // that, and a lone call (the latency case) loads on the first wave
         // only, so only overlapping calls pay for it.
+        const int nwaves = static_cast<int>(blockDim.x >> 6), my_wave = static_cast<int>(threadIdx.x >> 6);
+        const bool split_rows = (w5 & 16) != 0 && rows <= nwaves;
+        const bool shared_rows = (w5 & 32) != 0 && rows <= nwaves && nwaves * kEngineShareCols >= cols;
         if (works && !poller &&
-            ((threadIdx.x >> 6) * nwg + local) * 64u < nstripes * units)
+            ((shared_rows && my_wave < cols) || (split_rows && my_wave < rows) ||
+             ((threadIdx.x >> 6) * nwg + local) * 64u < nstripes * units))
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint64_t t_tab = __builtin_amdgcn_s_memrealtime();
         const EngineCall call{s_vaddr, stride, units, works ? nstripes * units : 0u, cols, accumulate, local, nwg};
-        const bool split_rows = (w5 & 16) != 0 && rows <= static_cast<int>(blockDim.x >> 6);
-        if (works && split_rows) {
+        if (works && shared_rows) {
+            engine_units_shared(call, tab, rows, s_in);
+        } else if (works && split_rows) {
             const int wave = static_cast<int>(threadIdx.x >> 6);
             if (wave < rows) engine_units_row(call, tab, wave);
         } else if (works) switch (rows) {
