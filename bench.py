@@ -73,6 +73,10 @@ def parse_args(argv=None):
     ap.add_argument("--prewarm-max", type=int, default=2000, help="pre-warm: at most this many launches")
     ap.add_argument("--cold", type=int, default=1,
                     help="after the timed region: 50 launches after a 100 ms idle (`cold` in the line)")
+    ap.add_argument("--group", type=int, default=0,
+                    help="one process drives N device-resident codecs through a device group "
+                         "(rs_group_codec; the topology of a Go storage server), instead of one rank per GPU; "
+                         "members share RSAMD_BENCH_DEVICE when it is set (rehearsal on fewer GPUs)")
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="TEST ONLY: rehearse the launcher / rank / timing protocol on CPU (gloo, no GPU, "
                          "no kernel); the line it prints is not a measurement")
@@ -277,17 +281,21 @@ def end_to_end(codec, data, parity, k, m, vec, S, reps, n_gpus, barrier, max_ove
                     "hipMemcpyAsync on 3 streams, 4 stripes per step; all GPUs at once; wall clock, max over ranks"}
 
 
-def load_traffic(config: str):
+def load_traffic(config: str, algorithmic_bytes: int):
     """(HBM bytes per launch, source) from the committed rocprofv3 PMC summary
     (profiles/traffic.json: FETCH_SIZE / WRITE_SIZE passes of this same
-    launch, corrected per MI355X_MICROARCH.md), or (None, None).  The counters
-    are not collected inside this run: `traffic_source` names the file."""
+    launch, corrected per MI355X_MICROARCH.md), or (None, None) when there is
+    none for this launch (another stripe count measures another launch).  The
+    counters are not collected inside this run: `traffic_source` names the file."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         ent = json.load(open(path)).get(config, {})
         b = ent.get("hbm_bytes_per_launch")
-        return b, (f"profiles/traffic.json <- {ent.get('source')}" if b else None)
-    except (OSError, ValueError):
+        alg = ent.get("algorithmic_bytes_per_launch")
+        if not b or (alg is not None and alg != algorithmic_bytes) or not (0.5 < b / algorithmic_bytes < 2.0):
+            return None, None
+        return b, f"profiles/traffic.json <- {ent.get('source')}"
+    except (OSError, ValueError, ZeroDivisionError):
         return None, None
 
 
@@ -508,6 +516,155 @@ def count_ranks(pg, device) -> int:
     return int(t.item())
 
 
+# ---------------------------------------------------------------- one process, N devices
+
+def group_devices(n: int, visible: int, pinned: int | None) -> list:
+    """Device ordinals of a --group N run: 0..N-1, or N members sharing
+    `pinned` (RSAMD_BENCH_DEVICE) to rehearse the topology on fewer GPUs."""
+    if n < 1:
+        raise SystemExit("bench: --group needs N >= 1")
+    if pinned is not None:
+        return [pinned] * n
+    if visible < n:
+        raise SystemExit(f"bench: --group {n} but only {visible} visible GPUs (set RSAMD_BENCH_DEVICE to rehearse)")
+    return list(range(n))
+
+
+def group_main(args) -> dict:
+    """`--group N`: ONE process drives N device-resident codecs (rs_group_new,
+    rs_group_codec), the way a Go storage server holding several GPUs would
+    (contiguous stripe slices, tables replicated, aggregate =
+    total bytes / wall time).  Each member owns S stripes in its device's HBM
+    (weak scaling, as with one rank per GPU) and its own stream; a step
+    launches every member's encode back to back from this one host thread
+    (launches are asynchronous), and the step ends when every device is done.
+    Every member's stripes are self-checked (encode -> erase -> reconst)."""
+    import torch
+
+    import reedsolomon_amd as rs
+
+    k, m, vec, S = CONFIGS[args.config]
+    if args.stripes:
+        S = args.stripes
+    pin = os.environ.get("RSAMD_BENCH_DEVICE")
+    devs = group_devices(args.group, torch.cuda.device_count(), int(pin) if pin is not None else None)
+    g = rs.NewGroup(k, m, devs)
+    members = []
+    for i, (dv, codec) in enumerate(zip(devs, g.members)):
+        dev = torch.device("cuda", dv)
+        gen = torch.Generator(device=dev).manual_seed(0x5EED + i)
+        data = torch.empty((S, k, vec), dtype=torch.uint8, device=dev)
+        parity = torch.empty((S, m, vec), dtype=torch.uint8, device=dev)
+        for s0 in range(0, S, 32):
+            data[s0:s0 + 32].random_(0, 256, generator=gen)
+        parity.fill_(0xA5)
+        members.append((codec, dev, torch.cuda.Stream(dev), data, parity))
+    distinct = sorted(set(devs))
+
+    def sync():
+        for dv in distinct:
+            torch.cuda.synchronize(dv)
+
+    def step(_i):
+        for codec, _dev, st, data, parity in members:
+            codec.encode_batch_split(data, parity, stream=st)
+
+    sync()
+    step(0)
+    if args.verify:
+        for i, (codec, _dev, st, data, parity) in enumerate(members):
+            sl = slice(S // 2, S // 2 + 1)
+            ref_d, ref_p = data[sl].clone(), parity[sl].clone()
+            data[sl, 1] = 0
+            parity[sl, m - 1] = 0
+            codec.reconst_batch_split(data[sl], parity[sl], [], [1, k + m - 1], stream=st)
+            st.synchronize()
+            if not (torch.equal(data[sl], ref_d) and torch.equal(parity[sl], ref_p)):
+                raise SystemExit(f"group member {i} (cuda:{devs[i]}): encode/reconst round trip failed")
+
+    # pre-warm: every member's device to its steady state (the same launch count
+    # as one rank's pre-warm minimum), then the counted warm-up behind it
+    for _ in range(max(args.prewarm_min, 1)):
+        step(0)
+    for _ in range(args.warmup):
+        step(0)
+    sync()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in members]
+
+    def timed_step(i):
+        for (codec, _dev, st, data, parity), (e0, e1) in zip(members, evs):
+            if i == 0:
+                e0.record(st)
+            codec.encode_batch_split(data, parity, stream=st)
+            if i == args.steps - 1:
+                e1.record(st)
+
+    elapsed = timed_region(timed_step, args.steps, lambda: None, sync, lambda x: x)
+    per_member_ms = [e0.elapsed_time(e1) / args.steps for e0, e1 in evs]
+    bytes_per_member = S * (k + m) * vec
+    value = throughput(bytes_per_member, len(members), args.steps, elapsed)
+    shared = len(distinct) < len(devs)
+    kern = max(per_member_ms)
+    e2e = None
+    if args.e2e_stripes > 0:
+        e2e = group_end_to_end(g, members, k, m, vec, min(args.e2e_stripes, S), args.e2e_reps)
+    out = {
+        "metric": metric_name(k, m, vec) + " [one process, device group]",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": len(distinct), "group_members": len(devs),
+        "devices": devs, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (uniform random bytes, seeded per member; parity pre-filled 0xA5)",
+        "config": {"workload": f"RS encode {k}+{m}, {vec} B vectors, {S} stripes per member, device-resident",
+                   "k": k, "m": m, "vector_bytes": vec, "stripes_per_member": S,
+                   "topology": "one process, rs_group_new over the listed devices, one stream per member, "
+                               "all launches from one host thread; no collective"},
+        "rehearsal": shared,
+        "per_member_kernel_ms": [round(x, 4) for x in per_member_ms],
+        "roofline": {"bound": "hbm", "achieved": round(bytes_per_member / (kern / 1e3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(bytes_per_member / (kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "kernel_timing": "slowest member: HIP event pair on its stream around the K timed launches / K"
+                                      + ("; members SHARE a device, so each launch competes for one HBM"
+                                         if shared else "")},
+        "end_to_end": e2e,
+        "build": rs.build_info(),
+    }
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def group_end_to_end(g, members, k, m, vec, E, reps) -> dict:
+    """Host-resident leg of --group: one pinned host batch of E stripes per
+    member, encoded in place by rs_group_encode_host_batch (the group splits
+    it with rs_group_slice and runs the slices on their devices concurrently).
+    Slice i holds member i's first E stripes, so the parity that comes back is
+    checked against that member's device-resident encode."""
+    import torch
+
+    n = len(members)
+    host = torch.empty((n * E, k + m, vec), dtype=torch.uint8, pin_memory=True)
+    for i, (_c, _d, _st, data, _p) in enumerate(members):
+        lo, hi = g.slice(n * E, i)
+        assert hi - lo == E
+        host[lo:hi, :k].copy_(data[:E])
+    host[:, k:].fill_(0xA5)
+    g.encode_host_batch(host)
+    for i, (_c, _d, _st, _data, parity) in enumerate(members):
+        lo, _hi = g.slice(n * E, i)
+        if not torch.equal(host[lo:lo + 2, k:], parity[:2].cpu()):
+            raise SystemExit(f"group end-to-end: member {i} parity differs from its device-resident encode")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.encode_host_batch(host)
+    el = time.perf_counter() - t0
+    del host
+    return {"value": round(n * E * (k + m) * vec * reps / el / 2 ** 30, 2), "unit": "GiB/s",
+            "stripes_per_member": E, "reps": reps,
+            "path": "one pinned host batch split over the group's members (rs_group_encode_host_batch), "
+                    "parity back in host memory; wall clock"}
+
+
 # ---------------------------------------------------------------- main
 
 def main(argv=None):
@@ -515,6 +672,10 @@ def main(argv=None):
     args = parse_args(raw)
     world, rank, local = dist_env()
     launched = "WORLD_SIZE" in os.environ
+    if args.group:
+        if launched or args.gpus != 1:
+            raise SystemExit("bench: --group N runs in one process (no launcher, no --gpus)")
+        return group_main(args)
     if not launched and args.gpus > 1:
         raise SystemExit(spawn_ranks(args.gpus, raw))
     check_world(args, world, launched)
@@ -644,7 +805,7 @@ def main(argv=None):
 
     result = None
     if rank == 0:
-        traffic, traffic_src = load_traffic(args.config)
+        traffic, traffic_src = load_traffic(args.config, bytes_per_step_rank)
         result = {
             "metric": metric_name(k, m, vec),
             "value": round(value, 2),
@@ -688,6 +849,7 @@ def main(argv=None):
         }
         result["cold"] = cold
         result["end_to_end"] = e2e
+        result["build"] = rs.build_info()
         if n_gpus == 1 and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(k, m, vec, args.cpu_seconds)
         else:

@@ -70,6 +70,10 @@ RS_API const char* rs_strerror(int code);
 /* Library / device information. */
 RS_API int rs_version(void);                /* 100*major + minor */
 RS_API int rs_device_count(void);           /* number of visible HIP devices, <0 on error */
+/* SHA-256 (64 hex digits) of the sources and compile flags this library was
+ * built from (reedsolomon_amd/build.py source_digest), so a measurement names
+ * the exact tree it ran; "unstamped" for a build outside build.py. */
+RS_API const char* rs_build_id(void);
 
 /* ------------------------------------------------------------------------
  * Codec lifetime.  Replaces New(dataNum, parityNum) rs.go:54-85.
@@ -88,6 +92,25 @@ RS_API int  rs_parity_num(const rs_t* rs);               /* RS.ParityNum rs.go:2
  * or -1 while it is "the current device at first use" and no call has bound
  * it yet.  No device call. */
 RS_API int  rs_device(const rs_t* rs);
+/* Reference-compat Update / Replace, per handle (DESIGN.md §4 "Reference
+ * defect").  rs.go's encodePart runs its sub-16-byte tail pass over the whole
+ * last chunk of getSplitSize (rs.go:158-173, 190-200), so under updateOnly
+ * the body of a last chunk whose length is >= 16 and not a multiple of 16 is
+ * XORed twice and keeps its old parity; which bytes those are depends on the
+ * host's L1D size (cpu.X86.Cache.L1D).  l1d = 0 (the default): Update /
+ * Replace compute the re-encode definition (rs_test.go:219-331) everywhere.
+ * l1d > 0 (>= 32): the bytes rs.go produces on a host with that L1D.
+ * l1d = -1: this host's L1D as rs_host_l1d reports it, 32 KiB when unknown
+ * (rs.go:159-161).  Affects only this handle's Update / Replace calls (host,
+ * device and batch forms) that start after the call.  RS_ERR_INVAL for other
+ * values. */
+RS_API int rs_set_ref_l1d(rs_t* rs, int l1d);
+/* The handle's current setting in bytes (0 = off). */
+RS_API int rs_ref_l1d(const rs_t* rs);
+/* cpu.X86.Cache.L1D on this host as the reference's getSplitSize reads it
+ * (rs.go:158-159): the L1 data cache bytes from CPUID, -1 when undetectable,
+ * 0 on a non-x86 host.  No device call. */
+RS_API int rs_host_l1d(void);
 /* Copies GenMatrix (p x d, row-major, G[j*d+i]) into out[p*d]. rs.go:31,65-68 */
 RS_API int  rs_gen_matrix(const rs_t* rs, uint8_t* out);
 /* Copies the (d+p) x d encoding matrix into out[(d+p)*d]. rs.go:30 */
@@ -468,10 +491,6 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * through the BAR, where the platform maps it for the CPU | 0 default: pinned
  * host memory, measured faster; taken by handles whose engine starts after
  * the change),
- * "ref_update_tail" (reference-compat Update / Replace: the L1D size in bytes
- * of the host whose rs.go bytes to reproduce, e.g. 32768 = rs.go's default
- * when the L1D is unknown; 0 default = the re-encode definition everywhere;
- * see DESIGN.md §4 "Reference defect"),
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit, the default since
  * round 4: every synchronous host call takes the chunked zero-copy pipeline),
  * "host_chunk" (bytes; host-memory call staging), "host_coalesce_max" (bytes per vector up to which

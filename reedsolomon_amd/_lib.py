@@ -42,6 +42,7 @@ c_layoutp = ctypes.POINTER(RSLayout)
 SIGNATURES = {
     "rs_strerror": (ctypes.c_char_p, [c_int]),
     "rs_version": (c_int, []),
+    "rs_build_id": (ctypes.c_char_p, []),
     "rs_device_count": (c_int, []),
     "rs_new": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_void)]),
     "rs_free": (None, [c_void]),
@@ -75,6 +76,9 @@ SIGNATURES = {
     "rs_group_codec": (c_void, [c_void, c_int]),
     "rs_group_slice": (c_int, [c_void, c_int, c_int, c_intp, c_intp]),
     "rs_device": (c_int, [c_void]),
+    "rs_set_ref_l1d": (c_int, [c_void, c_int]),
+    "rs_ref_l1d": (c_int, [c_void]),
+    "rs_host_l1d": (c_int, []),
     "rs_group_encode_host_batch": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz, c_int, c_int]),
     "rs_group_reconst_host_batch_multi": (c_int, [c_void, c_void, c_i64, c_i64, c_int, c_sz,
                                                   ctypes.POINTER(ctypes.c_uint64)]),

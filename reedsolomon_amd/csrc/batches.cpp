@@ -332,7 +332,7 @@ int rs_update_dev(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = update_matrix(rs, row);
-        return update_ranges(new_len, [&](uint64_t off, uint64_t n) {
+        return update_ranges(rs, new_len, [&](uint64_t off, uint64_t n) {
             const uint8_t* in[2] = {old_data + off, new_data + off};
             uint8_t* out[kMaxVects];
             for (int j = 0; j < rs->p; ++j) out[j] = parity[j] + off;
@@ -357,7 +357,7 @@ int rs_update_batch(rs_t* rs, const uint8_t* old_base, int64_t old_stride, const
         for (int j = 0; j < rs->p; ++j) osid[j] = 2;
         const int64_t ss[4] = {old_stride, new_stride, stripe_stride, 0};
         std::vector<uint8_t> gm = update_matrix(rs, row);
-        return update_ranges(len, [&](uint64_t off, uint64_t n) {
+        return update_ranges(rs, len, [&](uint64_t off, uint64_t n) {
             const uint8_t* in[2] = {old_base + off, new_base + off};
             uint8_t* out[kMaxVects];
             for (int j = 0; j < rs->p; ++j) out[j] = base + (rs->d + j) * vect_stride + off;
@@ -376,7 +376,7 @@ int rs_replace_dev(rs_t* rs, const uint8_t* const* data, const size_t* data_lens
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-        return update_ranges(data_lens[0], [&](uint64_t off, uint64_t n) {
+        return update_ranges(rs, data_lens[0], [&](uint64_t off, uint64_t n) {
             const uint8_t* in[kMaxVects];
             uint8_t* out[kMaxVects];
             for (int i = 0; i < nr; ++i) in[i] = data[i] + off;
@@ -401,7 +401,7 @@ int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_stripe_str
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-        return update_ranges(len, [&](uint64_t off, uint64_t n) {
+        return update_ranges(rs, len, [&](uint64_t off, uint64_t n) {
             const uint8_t* in[kMaxVects];
             uint8_t* out[kMaxVects];
             for (int i = 0; i < nr; ++i) in[i] = data_base + i * data_vect_stride + off;

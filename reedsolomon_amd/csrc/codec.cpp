@@ -16,6 +16,10 @@
 #include <cstdlib>
 
 #include "codec_internal.hpp"
+
+#if defined(__x86_64__) || defined(__i386__)
+#include <cpuid.h>
+#endif
 #include "jit.hpp"
 
 using namespace rsamd;
@@ -158,6 +162,7 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
         std::lock_guard<std::mutex> elk(rs->eng_mu);
         RS_TRY(engine_drain(rs));  // calls in flight complete first (a stopped instance would strand them)
         engine_stop(rs);
+        engines_quiesce();  // other handles' instances on this device would hold the sync for their idle window
         RS_TRY(hip_ok(hipDeviceSynchronize(), "table registry drain"));
         for (auto& kv : rs->tables) {
             (void)hipFree(kv.second.dev);
@@ -440,11 +445,9 @@ int check_replace(const rs_t* rs, const size_t* dlens, int nd, const int* rows, 
 
 // Update's matrix: p x 2, both columns G[j][row] (g*old ^ g*new == g*(old^new),
 // so xorsimd's step rs.go:432-433 folds into the product).
-int g_ref_update_tail = 0;
-
-bool ref_update_skip(uint64_t size, uint64_t* lo, uint64_t* hi) {
-    if (g_ref_update_tail <= 0) return false;
-    const uint64_t split = static_cast<uint64_t>(g_ref_update_tail) / 2;  // getSplitSize rs.go:158-173
+bool ref_update_skip(int l1d, uint64_t size, uint64_t* lo, uint64_t* hi) {
+    if (l1d <= 0) return false;
+    const uint64_t split = static_cast<uint64_t>(l1d) / 2;  // getSplitSize rs.go:158-173
     if (size < split) return false;  // chunks of (n>>4)<<4 bytes, then a < 16-byte tail on its own
     const uint64_t last = size % split;
     if (last < 16 || (last & 15) == 0) return false;
@@ -522,6 +525,75 @@ const char* rs_strerror(int code) {
 }
 
 int rs_version(void) { return 100; }
+
+// cpu.X86.Cache.L1D as the reference's getSplitSize reads it (rs.go:158-159):
+// the L1 data cache size of this host from CPUID, -1 when it cannot be
+// detected, 0 on a non-x86 host.  templexxx/cpu v0.0.1 (go.mod:4) is not in
+// the container; this restates the CPUID sources such a library reads:
+// deterministic cache parameters (leaf 4 on Intel, leaf 0x8000001D on AMD
+// with topology extensions), else AMD's leaf 0x80000005 ECX[31:24] KiB.
+int rs_host_l1d(void) {
+#if defined(__x86_64__) || defined(__i386__)
+    static const int l1d = [] {
+        unsigned a, b, c, d;
+        if (!__get_cpuid(0, &a, &b, &c, &d)) return -1;
+        const unsigned max_leaf = a;
+        const bool amd = b == 0x68747541u;  // "Auth"enticAMD
+        auto leaf_params = [](unsigned leaf) -> int {
+            for (unsigned sub = 0; sub < 16; ++sub) {
+                unsigned a2, b2, c2, d2;
+                __cpuid_count(leaf, sub, a2, b2, c2, d2);
+                const unsigned type = a2 & 31, level = (a2 >> 5) & 7;
+                if (type == 0) break;
+                if (type == 1 && level == 1)  // data cache, level 1
+                    return static_cast<int>(((b2 >> 22) + 1) * (((b2 >> 12) & 0x3ff) + 1) * ((b2 & 0xfff) + 1) *
+                                            (c2 + 1));
+            }
+            return -1;
+        };
+        if (!amd && max_leaf >= 4) {
+            const int v = leaf_params(4);
+            if (v > 0) return v;
+        }
+        if (amd && __get_cpuid(0x80000000u, &a, &b, &c, &d)) {
+            const unsigned max_ext = a;
+            if (max_ext >= 0x8000001Du && __get_cpuid(0x80000001u, &a, &b, &c, &d) && (c >> 22 & 1)) {
+                const int v = leaf_params(0x8000001Du);
+                if (v > 0) return v;
+            }
+            if (max_ext >= 0x80000005u && __get_cpuid(0x80000005u, &a, &b, &c, &d) && (c >> 24))
+                return static_cast<int>((c >> 24) * 1024);
+        }
+        return -1;
+    }();
+    return l1d;
+#else
+    return 0;
+#endif
+}
+
+int rs_set_ref_l1d(rs_t* rs, int l1d) {
+    if (!rs) return RS_ERR_INVAL;
+    if (l1d == -1) {
+        const int host = rs_host_l1d();
+        l1d = host > 0 ? host : 32 * 1024;  // rs.go:159-161: unknown (-1) or not x86 (0) -> 32 KiB
+    }
+    if (l1d != 0 && l1d < 32) return RS_ERR_INVAL;  // a split of at least 16 bytes (rs.go:169-172)
+    rs->ref_l1d.store(l1d, std::memory_order_relaxed);
+    return RS_OK;
+}
+
+int rs_ref_l1d(const rs_t* rs) { return rs ? rs->ref_l1d.load(std::memory_order_relaxed) : 0; }
+
+// Source digest stamped by reedsolomon_amd/build.py (SHA-256 over the build's
+// sources and flags).  The marker stays in .rodata so build.py can read the
+// digest of a library file without loading it.
+#ifndef RSAMD_BUILD_ID
+#define RSAMD_BUILD_ID "unstamped"
+#endif
+__attribute__((used)) static const char k_build_stamp[] = "RSAMD_BUILD_ID=" RSAMD_BUILD_ID;
+
+const char* rs_build_id(void) { return k_build_stamp + sizeof("RSAMD_BUILD_ID=") - 1; }
 
 int rs_device_count(void) {
     int n = 0;
@@ -614,7 +686,6 @@ int rs_tune(const char* name, int value) {
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
         else if (n == "wide_single_pass") t.wide_single_pass = value ? 1 : 0;
-        else if (n == "ref_update_tail") g_ref_update_tail = value >= 32 ? value : 0;
         else if (n == "host_engine") g_engine = value ? 1 : 0;
         else if (n == "host_engine_waves") g_engine_waves = value < 1 ? 1 : value > kEngineMaxGroups ? kEngineMaxGroups : value;
         else if (n == "host_engine_group_waves")

@@ -214,6 +214,10 @@ struct rs_codec {
     std::atomic<uint64_t> eng_calls{0}, eng_launches{0};
     std::atomic<int> eng_inflight{0};  // calls rung and not yet seen complete by their callers
 
+    // Reference-compat Update / Replace (rs_set_ref_l1d): the L1D bytes of the
+    // host whose rs.go bytes to reproduce, 0 = the re-encode definition.
+    std::atomic<int> ref_l1d{0};
+
     const uint8_t* gen() const { return enc.data() + static_cast<size_t>(d) * d; }
 
     ~rs_codec();
@@ -241,6 +245,9 @@ void engine_stop(rs_t* rs);  // caller holds eng_mu
 // follows.
 int engine_drain(rs_t* rs);
 void engine_shutdown(rs_t* rs);
+// Ask every handle's running engine instance to leave (its pending calls are
+// served first), ahead of a device-wide synchronisation by the library.
+void engines_quiesce();
 extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_life_us, g_engine_wg_units,
     g_engine_yield_us, g_engine_poll_gap, g_engine_vram, g_engine_split_rows;
 // Device memory the host can write through the BAR (uncached for the GPU:
@@ -447,8 +454,8 @@ int check_replace(const rs_t* rs, const size_t* dlens, int nd, const int* rows, 
 std::vector<uint8_t> update_matrix(const rs_t* rs, int row);
 std::vector<uint8_t> replace_matrix(const rs_t* rs, const int* rows, int nr);
 
-// Reference-compat mode for Update / Replace (rs_tune("ref_update_tail",
-// l1d_bytes); 0 = off, the default).  The reference's encodePart
+// Reference-compat mode for Update / Replace (rs_set_ref_l1d(rs,
+// l1d_bytes), per handle; 0 = off, the default).  The reference's encodePart
 // (rs.go:175-203) runs its sub-16-byte tail pass over the WHOLE last chunk
 // [start, end) of getSplitSize (rs.go:158-173: L1D/2 bytes), so under
 // updateOnly (Update rs.go:447, Replace rs.go:527) that chunk's 16-byte body
@@ -488,13 +495,13 @@ struct MaskView {
 int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, MaskView masks, void* stream);
 int check_masks(int d, int p, MaskView masks, int nstripes);
 
-extern int g_ref_update_tail;
-bool ref_update_skip(uint64_t size, uint64_t* lo, uint64_t* hi);
-// Run op(offset, length) over [0, size) minus the skipped range.
+bool ref_update_skip(int l1d, uint64_t size, uint64_t* lo, uint64_t* hi);
+// Run op(offset, length) over [0, size) minus the range the handle's
+// reference-compat setting skips (read once per call).
 template <class Op>
-int update_ranges(uint64_t size, Op op) {
+int update_ranges(const rs_t* rs, uint64_t size, Op op) {
     uint64_t lo = 0, hi = 0;
-    if (!ref_update_skip(size, &lo, &hi)) return op(uint64_t{0}, size);
+    if (!ref_update_skip(rs->ref_l1d.load(std::memory_order_relaxed), size, &lo, &hi)) return op(uint64_t{0}, size);
     if (lo > 0) RS_TRY(op(uint64_t{0}, lo));
     if (hi < size) RS_TRY(op(hi, size - hi));
     return RS_OK;

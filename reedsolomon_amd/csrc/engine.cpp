@@ -234,10 +234,36 @@ static void engine_dump(const rs_t* rs, const char* what) {  // diagnostics
     std::fprintf(stderr, "\n");
 }
 
-static void engine_signal_stop(rs_t* rs) {  // every slot: a wave polls whichever holds its next call
-    EngineSlot* slots = slots_of(rs);
-    for (int i = 0; i < kEngineSlots; ++i) __atomic_store_n(&slots[i].hdr.stop, rs->eng_epoch, __ATOMIC_RELEASE);
+static void signal_stop(EngineSlot* slots, uint64_t epoch) {  // every slot: a wave polls whichever holds its next call
+    for (int i = 0; i < kEngineSlots; ++i) __atomic_store_n(&slots[i].hdr.stop, epoch, __ATOMIC_RELEASE);
     _mm_sfence();  // (device-memory slots: write-combined stores leave now)
+}
+
+static void engine_signal_stop(rs_t* rs) { signal_stop(slots_of(rs), rs->eng_epoch); }
+
+// Running instances of every handle (slots, epoch), so that the library's own
+// device-wide drains (rs_host_unregister, the table registry's recycle, JIT
+// eviction) can ask them to leave first instead of waiting out their idle
+// window (up to host_engine_idle_us, 2 ms).  Taken after eng_mu, never
+// before it.  A stop word written this way is an ordinary early exit for the
+// handle: calls already rung are served first, and the next call finds the
+// instance gone and relaunches it (engine_relaunch_if_gone).  Slots are never
+// freed (rings and device slot blocks are pooled), so a stale entry can only
+// cost another instance an early exit, never a stray write.
+namespace {
+std::mutex g_active_mu;
+std::map<EngineSlot*, uint64_t> g_active;  // running instance's slots -> its epoch
+}  // namespace
+
+static void active_set(rs_t* rs, bool running) {
+    std::lock_guard<std::mutex> lk(g_active_mu);
+    if (running) g_active[slots_of(rs)] = rs->eng_epoch;
+    else g_active.erase(slots_of(rs));
+}
+
+void engines_quiesce() {
+    std::lock_guard<std::mutex> lk(g_active_mu);
+    for (auto& kv : g_active) signal_stop(kv.first, kv.second);
 }
 
 // Caller holds eng_mu.  Calls already rung are served first (a wave checks
@@ -264,6 +290,7 @@ void engine_stop(rs_t* rs) {
     }
     (void)hipStreamSynchronize(rs->eng_stream);
     rs->eng_running = false;
+    active_set(rs, false);
 }
 
 void engine_shutdown(rs_t* rs) {
@@ -350,6 +377,7 @@ static int engine_launch(rs_t* rs, int waves, int group_waves, uint64_t start) {
     rs->eng_life_us = g_engine_life_us;
     rs->eng_poll_gap = g_engine_poll_gap;
     rs->eng_launches.fetch_add(1, std::memory_order_relaxed);
+    active_set(rs, true);
     return RS_OK;
 }
 

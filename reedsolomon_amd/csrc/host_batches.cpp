@@ -50,9 +50,16 @@ int host_device_range(const void* p, size_t bytes, uint8_t** dev) {
 // reference on every span that covers part of it, registering only the pages
 // no span covers yet, so two caller ranges that share a page (heap buffers
 // side by side) never register that page twice and neither unregister pulls
-// it from under the other.  A span leaves the runtime when its last reference
-// goes, after every device this process launched on has been drained (a
-// kernel the caller queued over the range may still be reading it).  The
+// it from under the other.  A partial first or last page of a range is
+// registered as a span of its own, so the page a neighbour shares is the only
+// one that outlives the range's unregister (a span shared whole would keep the
+// range's own pages registered after the caller freed them, and a later
+// buffer at those addresses would get the runtime's stale pinning).  A span
+// leaves the runtime when its last reference goes, after every device this
+// process launched on has been drained (a kernel the caller queued over the
+// range may still be reading it); the drain runs without g_reg_mu, the spans
+// waiting for it are "dying": not found by lookups, and a registration that
+// touches one waits until it is gone.  The
 // library-owned pool (rs_host_alloc) holds a permanent reference on its
 // blocks: they are registered once and stay registered and mapped while the
 // process runs, however often they are handed out again.  Host calls look
@@ -69,7 +76,9 @@ struct PoolBlock {
     bool free;
 };
 std::mutex g_reg_mu;
+std::condition_variable g_reg_cv;                       // a dying span left the runtime
 std::map<uintptr_t, Span> g_spans;                      // disjoint page spans, by first address
+std::map<uintptr_t, uintptr_t> g_dying;                 // [lo, hi) spans unregistered, waiting for the drain
 struct UserReg {
     size_t bytes;
     std::vector<uintptr_t> spans;  // the spans it holds a reference on
@@ -106,7 +115,10 @@ int span_register(uintptr_t lo, uintptr_t hi) {
 }
 
 // Every device this process launched on has finished its queued work.
+// Resident host-call engines are asked to leave first (they would hold the
+// sync for their idle window).
 void drain_used_devices() {
+    engines_quiesce();
     const uint64_t used = g_devices_used.load(std::memory_order_acquire);
     for (int dv = 0; dv < 64; ++dv)
         if (used & (uint64_t{1} << dv)) {
@@ -116,18 +128,25 @@ void drain_used_devices() {
 }
 
 // Drops one reference on each span in `spans` (caller holds g_reg_mu);
-// spans whose last reference went are removed from the lookup and returned.
-std::vector<uintptr_t> spans_release(const std::vector<uintptr_t>& spans) {
-    std::vector<uintptr_t> dead;
+// spans whose last reference went are removed from the lookup and returned
+// as [lo, hi).
+std::vector<std::pair<uintptr_t, uintptr_t>> spans_release(const std::vector<uintptr_t>& spans) {
+    std::vector<std::pair<uintptr_t, uintptr_t>> dead;
     for (uintptr_t lo : spans) {
         auto it = g_spans.find(lo);
         if (it != g_spans.end() && --it->second.refs == 0) {
-            dead.push_back(lo);
+            dead.emplace_back(lo, it->second.hi);
             g_spans.erase(it);
         }
     }
     g_reg_count.store(static_cast<int>(g_spans.size()));
     return dead;
+}
+
+bool overlaps_dying(uintptr_t lo, uintptr_t hi) {  // caller holds g_reg_mu
+    auto it = g_dying.upper_bound(lo);
+    if (it != g_dying.begin() && std::prev(it)->second > lo) return true;
+    return it != g_dying.end() && it->first < hi;
 }
 }  // namespace
 std::atomic<int> g_reg_count{0};
@@ -144,7 +163,16 @@ uint8_t* registered_device_ptr(const void* p, size_t bytes) {
     auto it = g_spans.upper_bound(a);
     if (it == g_spans.begin()) return nullptr;
     --it;
-    if (a + bytes > it->second.hi) return nullptr;
+    if (a >= it->second.hi) return nullptr;
+    // the range may run over adjacent spans (a registration's own edge pages):
+    // zero-copy only when the runtime mapped them contiguously for the device
+    for (auto cur = it; a + bytes > cur->second.hi;) {
+        auto next = std::next(cur);
+        if (next == g_spans.end() || next->first != cur->second.hi ||
+            next->second.dev != cur->second.dev + (cur->second.hi - cur->first))
+            return nullptr;
+        cur = next;
+    }
     bool live = false;
     auto pb = g_pool.upper_bound(a);
     if (pb != g_pool.begin()) {
@@ -365,30 +393,42 @@ int rs_host_register(void* ptr, size_t bytes) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), ps = page_bytes();
         if (a + bytes < a) return RS_ERR_INVAL;
         const uintptr_t lo = a & ~(ps - 1), hi = (a + bytes + ps - 1) & ~(ps - 1);
-        std::lock_guard<std::mutex> lk(g_reg_mu);
+        std::unique_lock<std::mutex> lk(g_reg_mu);
         if (g_user.count(a)) return RS_ERR_INVAL;  // already registered at this address
-        std::vector<uintptr_t> held, created;
+        // pages of an unregister still draining: wait until they left the runtime
+        g_reg_cv.wait(lk, [&] { return !overlaps_dying(lo, hi); });
+        if (g_user.count(a)) return RS_ERR_INVAL;
+        // piece boundaries: a partial first / last page is a span of its own
+        uintptr_t cuts[3];
+        int ncut = 0;
+        if (a != lo && lo + ps < hi) cuts[ncut++] = lo + ps;
+        if (a + bytes != hi && hi - ps > lo && (ncut == 0 || hi - ps > cuts[0])) cuts[ncut++] = hi - ps;
+        cuts[ncut++] = hi;
+        std::vector<uintptr_t> held;
         uintptr_t cur = lo;
         int rc = RS_OK;
-        while (cur < hi && rc == RS_OK) {
-            auto it = g_spans.upper_bound(cur);  // the span covering cur, if any, precedes it
-            if (it != g_spans.begin() && std::prev(it)->second.hi > cur) {
-                Span& sp = std::prev(it)->second;
-                ++sp.refs;
-                held.push_back(std::prev(it)->first);
-                cur = sp.hi;
-                continue;
-            }
-            const uintptr_t end = it != g_spans.end() && it->first < hi ? it->first : hi;  // the gap up to the next span
-            rc = span_register(cur, end);
-            if (rc == RS_OK) {
-                held.push_back(cur);
-                created.push_back(cur);
-                cur = end;
+        for (int c = 0; c < ncut && rc == RS_OK; ++c) {
+            const uintptr_t piece_hi = cuts[c];
+            while (cur < piece_hi && rc == RS_OK) {
+                auto it = g_spans.upper_bound(cur);  // the span covering cur, if any, precedes it
+                if (it != g_spans.begin() && std::prev(it)->second.hi > cur) {
+                    Span& sp = std::prev(it)->second;
+                    ++sp.refs;
+                    held.push_back(std::prev(it)->first);
+                    cur = sp.hi;
+                    continue;
+                }
+                // the gap up to the next span, within this piece
+                const uintptr_t end = it != g_spans.end() && it->first < piece_hi ? it->first : piece_hi;
+                rc = span_register(cur, end);
+                if (rc == RS_OK) {
+                    held.push_back(cur);
+                    cur = end;
+                }
             }
         }
         if (rc != RS_OK) {  // roll back: nothing used the new spans yet
-            for (uintptr_t d : spans_release(held)) (void)hipHostUnregister(reinterpret_cast<void*>(d));
+            for (auto& d : spans_release(held)) (void)hipHostUnregister(reinterpret_cast<void*>(d.first));
             return rc;
         }
         g_user.emplace(a, UserReg{bytes, std::move(held)});
@@ -415,23 +455,29 @@ int rs_bind_thread_to_device(int device) {
 int rs_host_unregister(void* ptr) {
     return abi_guard([&]() -> int {
         if (!ptr) return RS_ERR_INVAL;
-        // (the lock is held until the runtime has let go of the dead spans: a
-        // registration of the same pages from another thread in between would
-        // find no span and ask the runtime to register pages it still holds)
-        std::lock_guard<std::mutex> lk(g_reg_mu);
+        std::unique_lock<std::mutex> lk(g_reg_mu);
         auto it = g_user.find(reinterpret_cast<uintptr_t>(ptr));
         if (it == g_user.end()) return RS_ERR_INVAL;
-        const std::vector<uintptr_t> dead = spans_release(it->second.spans);
+        const std::vector<std::pair<uintptr_t, uintptr_t>> dead = spans_release(it->second.spans);
         g_user.erase(it);
         if (dead.empty()) return RS_OK;  // every page still held by another registration or the pool
         // No longer found by the lookup; whatever the caller queued over the
-        // range finishes before the pages leave the runtime.
+        // range finishes before the pages leave the runtime.  The drain runs
+        // without g_reg_mu (host calls on other registered memory go on); a
+        // registration of these pages from another thread waits for it, so
+        // the runtime is never asked to register pages it still holds.
+        for (auto& d : dead) g_dying.emplace(d.first, d.second);
+        lk.unlock();
         drain_used_devices();
         int rc = RS_OK;
-        for (uintptr_t lo : dead) {
-            const int r = hip_ok(hipHostUnregister(reinterpret_cast<void*>(lo)), "hipHostUnregister");
+        for (auto& d : dead) {
+            const int r = hip_ok(hipHostUnregister(reinterpret_cast<void*>(d.first)), "hipHostUnregister");
             if (rc == RS_OK) rc = r;
         }
+        lk.lock();
+        for (auto& d : dead) g_dying.erase(d.first);
+        lk.unlock();
+        g_reg_cv.notify_all();
         return rc;
     });
 }

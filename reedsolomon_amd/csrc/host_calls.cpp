@@ -720,7 +720,7 @@ int rs_update(rs_t* rs, const uint8_t* old_data, size_t old_len, const uint8_t* 
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = update_matrix(rs, row);
-        return update_ranges(new_len, [&](uint64_t off, uint64_t n) {
+        return update_ranges(rs, new_len, [&](uint64_t off, uint64_t n) {
             const uint8_t* src[2] = {old_data + off, new_data + off};
             uint8_t* dst[kMaxVects];
             for (int j = 0; j < rs->p; ++j) dst[j] = parity[j] + off;
@@ -739,7 +739,7 @@ int rs_replace(rs_t* rs, const uint8_t* const* data, const size_t* data_lens, in
         RS_TRY(ensure_device(rs));
         DeviceGuard g(rs->device);
         std::vector<uint8_t> gm = replace_matrix(rs, replace_rows, nr);
-        return update_ranges(data_lens[0], [&](uint64_t off, uint64_t n) {
+        return update_ranges(rs, data_lens[0], [&](uint64_t off, uint64_t n) {
             const uint8_t* src[kMaxVects];
             uint8_t* dst[kMaxVects];
             for (int i = 0; i < nr; ++i) src[i] = data[i] + off;

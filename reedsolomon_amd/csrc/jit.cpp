@@ -150,6 +150,11 @@ int g_jit_disk_cache = [] {  // rs_tune("jit_disk_cache", 0 | 1); env RSAMD_JIT_
     return e ? (std::atoi(e) ? 1 : 0) : 1;
 }();
 
+void jit_evict_now();  // (below: the worker runs it)
+namespace detail {
+void engines_quiesce();  // engine.cpp
+}
+
 namespace {
 
 uint8_t gmul(uint8_t a, uint8_t b) {  // GF(2^8), polynomial 0x11d
@@ -634,6 +639,7 @@ struct Seen {
 };
 
 void jit_atexit_hook();
+void jit_atexit();
 
 struct Jit {
     std::mutex mu;
@@ -680,8 +686,15 @@ struct Jit {
     void work() {
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
-            cv.wait(lk, [&] { return stop || !queue.empty(); });
+            cv.wait(lk, [&] { return stop || !queue.empty() || evict_task; });
             if (stop) return;
+            if (evict_task) {  // posted by a launch (jit_launch_guard): done here, off the launch path
+                evict_task = false;
+                lk.unlock();
+                jit_evict_now();
+                lk.lock();
+                continue;
+            }
             std::shared_ptr<Entry> e = queue.front();
             queue.pop_front();
             e->state = Entry::kCompiling;
@@ -694,6 +707,22 @@ struct Jit {
     pid_t owner = 0;  // the process that started the worker
     uint64_t use_clock = 0;
     std::atomic<bool> evict_wanted{false};
+    bool evict_task = false;  // an eviction is queued for the worker (under mu)
+
+    // Caller holds mu.  Starts the worker thread if this process has none.
+    void ensure_worker() {
+        if (worker.joinable() && owner == getpid()) return;
+        if (worker.joinable()) worker.detach();  // (a forked child starts its own)
+        // load the compiler library hiprtc would load on its first compile
+        // now, so its static destructors are registered before jit_atexit and
+        // run after it (atexit order)
+        static void* const comgr = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
+        (void)comgr;
+        static const bool registered = std::atexit(jit_atexit) == 0;
+        (void)registered;
+        owner = getpid();
+        worker = std::thread([this] { work(); });
+    }
 };
 
 // Launches hold this shared from the lookup of a compiled kernel until it is
@@ -985,18 +1014,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
                 lk.lock();
             } else {
                 j.queue.push_back(e);
-                if (!j.worker.joinable() || j.owner != getpid()) {  // (a forked child starts its own)
-                    if (j.worker.joinable()) j.worker.detach();
-                    // load the compiler library hiprtc would load on its first
-                    // compile now, so its static destructors are registered
-                    // before jit_atexit and run after it (atexit order)
-                    static void* const comgr = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
-                    (void)comgr;
-                    static const bool registered = std::atexit(jit_atexit) == 0;
-                    (void)registered;
-                    j.owner = getpid();
-                    j.worker = std::thread([&j] { j.work(); });
-                }
+                j.ensure_worker();
                 j.cv.notify_one();
                 return {};
             }
@@ -1045,41 +1063,63 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     }
 }
 
-// The older half of the compiled kernels leaves: with every launch that
-// looked one up enqueued (exclusive g_evict_mu) and the devices drained, none
-// of their code can still be in use.
-static void jit_evict() {
-    std::unique_lock<std::shared_mutex> ex(g_evict_mu);
+// The older half of the compiled kernels leaves.  Under exclusive
+// g_evict_mu (every launch that looked one up is enqueued) they are taken out
+// of the lookup, so no later launch can find them; the locks are then
+// released (launches go on, on the kernels that stay) while the devices that
+// ran them drain, and only then are their modules unloaded.
+void jit_evict_now() {
     Jit& j = jit();
-    std::lock_guard<std::mutex> lk(j.mu);
-    if (!j.evict_wanted.load(std::memory_order_acquire)) return;
-    std::vector<std::pair<uint64_t, std::string>> loaded;
-    for (auto& kv : j.entries)
-        if (kv.second->state == Entry::kLoaded || kv.second->state == Entry::kFailed ||
-            kv.second->state == Entry::kReady)
-            loaded.emplace_back(kv.second->last_use, kv.first);
-    std::sort(loaded.begin(), loaded.end());
-    loaded.resize(std::max<size_t>(loaded.size() / 2, std::min<size_t>(loaded.size(), 1)));
+    std::vector<std::shared_ptr<Entry>> victims;
     std::set<int> devs;
-    for (auto& x : loaded) devs.insert(j.entries[x.second]->dev);
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    for (int dv : devs) {
-        (void)hipSetDevice(dv);
-        (void)hipDeviceSynchronize();
+    {
+        std::unique_lock<std::shared_mutex> ex(g_evict_mu);
+        std::lock_guard<std::mutex> lk(j.mu);
+        if (!j.evict_wanted.load(std::memory_order_acquire)) return;
+        std::vector<std::pair<uint64_t, std::string>> loaded;
+        for (auto& kv : j.entries)
+            if (kv.second->state == Entry::kLoaded || kv.second->state == Entry::kFailed ||
+                kv.second->state == Entry::kReady)
+                loaded.emplace_back(kv.second->last_use, kv.first);
+        std::sort(loaded.begin(), loaded.end());
+        loaded.resize(std::max<size_t>(loaded.size() / 2, std::min<size_t>(loaded.size(), 1)));
+        for (auto& x : loaded) {
+            auto it = j.entries.find(x.second);
+            if (it->second->module) devs.insert(it->second->dev);
+            victims.push_back(std::move(it->second));
+            j.entries.erase(it);
+        }
+        ++j.evictions;
+        j.evict_wanted.store(false, std::memory_order_release);
     }
-    (void)hipSetDevice(cur);
-    for (auto& x : loaded) {
-        auto it = j.entries.find(x.second);
-        if (it->second->module) (void)hipModuleUnload(it->second->module);
-        j.entries.erase(it);
+    if (!devs.empty()) {
+        detail::engines_quiesce();  // (resident host-call engines would hold the sync for their idle window)
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        for (int dv : devs) {
+            (void)hipSetDevice(dv);
+            (void)hipDeviceSynchronize();
+        }
+        (void)hipSetDevice(cur);
     }
-    ++j.evictions;
-    j.evict_wanted.store(false, std::memory_order_release);
+    for (auto& e : victims)
+        if (e->module) (void)hipModuleUnload(e->module);
 }
 
+static void jit_evict() { jit_evict_now(); }
+
+// A launch never drains the device itself: a full kernel table queues the
+// eviction on the worker (this launch takes the table kernels meanwhile).
 std::shared_lock<std::shared_mutex> jit_launch_guard() {
-    if (jit().evict_wanted.load(std::memory_order_acquire)) jit_evict();
+    Jit& j = jit();
+    if (j.evict_wanted.load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> lk(j.mu);
+        if (j.evict_wanted.load(std::memory_order_acquire) && !j.evict_task) {
+            j.evict_task = true;
+            j.ensure_worker();
+            j.cv.notify_one();
+        }
+    }
     return std::shared_lock<std::shared_mutex>(g_evict_mu);
 }
 

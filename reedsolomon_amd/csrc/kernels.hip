@@ -1179,12 +1179,14 @@ __global__ __launch_bounds__(512) void gf_engine(EngineRing* ring, const EngineS
         // this build (no threadgroup-split mode: a workgroup's waves share the
         // CU's L1 and the XCD's L2), but the memory model does not promise
         // that, and a lone call (the latency case) loads on the first wave
-        // only, so only overlapping calls pay for it.
+        // only, so only overlapping calls pay for it.  With shared rows a wave
+        // loads an input column (wave < cols) and, for XOR-accumulate calls,
+        // the old output of its own row (wave < rows).
         const int nwaves = static_cast<int>(blockDim.x >> 6), my_wave = static_cast<int>(threadIdx.x >> 6);
         const bool split_rows = (w5 & 16) != 0 && rows <= nwaves;
         const bool shared_rows = (w5 & 32) != 0 && rows <= nwaves && nwaves * kEngineShareCols >= cols;
         if (works && !poller &&
-            ((shared_rows && my_wave < cols) || (split_rows && my_wave < rows) ||
+            ((shared_rows && (my_wave < cols || (accumulate && my_wave < rows))) || (split_rows && my_wave < rows) ||
              ((threadIdx.x >> 6) * nwg + local) * 64u < nstripes * units))
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint64_t t_tab = __builtin_amdgcn_s_memrealtime();

@@ -192,6 +192,17 @@ class RS:
         self.GenMatrix = g            # p x d, row-major: G[j*d+i]   (rs.go:31)
         self.encMatrix = e            # (d+p) x d                      (rs.go:30)
 
+    def set_ref_l1d(self, l1d: int) -> None:
+        """Reference-compat Update / Replace for this codec (rs_set_ref_l1d):
+        0 = re-encode definition (default), n = rs.go's bytes on a host whose
+        L1D is n bytes, -1 = this host's L1D (rs.go:158-173, 190-200)."""
+        _check(lib().rs_set_ref_l1d(self._h, int(l1d)))
+
+    @property
+    def ref_l1d(self) -> int:
+        """The codec's reference-compat L1D setting in bytes (0 = off)."""
+        return int(lib().rs_ref_l1d(self._h))
+
     def device_ordinal(self) -> int:
         """The device the handle launches on (rs_device; -1 = not bound yet)."""
         return int(lib().rs_device(self._h))
@@ -578,6 +589,11 @@ def New(dataNum: int, parityNum: int, device: int = -1) -> RS:
 
 
 # ---------------------------------------------------------------- free helpers
+
+def host_l1d() -> int:
+    """cpu.X86.Cache.L1D of this host as rs.go:158-159 reads it (rs_host_l1d)."""
+    return int(lib().rs_host_l1d())
+
 
 def invert(m, n: int) -> np.ndarray:
     """matrix.go:85-147 (raises ErrNotSquare / ErrSingularMatrix)."""

@@ -3,6 +3,7 @@ include/rs_amd.h, and its host-side logic (checks, planning, matrices,
 inverse cache) equals the oracle's."""
 import itertools
 import os
+import platform
 import re
 
 import numpy as np
@@ -271,6 +272,32 @@ def test_group_handles(rslib):
         rslib.NewGroup(200, 57, [0])
     L = rslib.lib()
     assert L.rs_group_codec(g._g, 3) is None and L.rs_group_codec(g._g, -1) is None
+
+
+def test_ref_l1d_is_per_handle(rslib):
+    """rs_set_ref_l1d: per handle, no device call; -1 resolves to this host's
+    L1D (rs_host_l1d; 32 KiB when undetectable, rs.go:159-161); values below
+    32 are refused; the old process-wide knob is gone."""
+    a, b = rslib.New(10, 4), rslib.New(10, 4)
+    assert a.ref_l1d == 0 and b.ref_l1d == 0
+    a.set_ref_l1d(49152)
+    assert a.ref_l1d == 49152 and b.ref_l1d == 0
+    host = rslib.host_l1d()
+    b.set_ref_l1d(-1)
+    assert b.ref_l1d == (host if host > 0 else 32768)
+    if platform.machine() in ("x86_64", "AMD64"):
+        # CPUID's answer agrees with the kernel's view of this host's L1D
+        p = "/sys/devices/system/cpu/cpu0/cache/index0"
+        if os.path.exists(p + "/size") and open(p + "/type").read().strip() == "Data":
+            txt = open(p + "/size").read().strip()
+            assert host == int(txt.rstrip("K")) * 1024, (host, txt)
+    for bad in (1, 16, 31, -2):
+        with pytest.raises(rslib.ErrInvalidArgument):
+            a.set_ref_l1d(bad)
+    assert a.ref_l1d == 49152
+    a.set_ref_l1d(0)
+    assert a.ref_l1d == 0
+    assert rslib.lib().rs_tune(b"ref_update_tail", 32768) == 13
 
 
 def test_tune_accepts_every_documented_knob(rslib):

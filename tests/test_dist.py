@@ -229,3 +229,83 @@ def test_two_rank_gloo_device_groups_and_placement():
     assert res[0][2] == res[1][2] and res[0][2][0] == res[0][2][1]
     assert res[0][3] > 0 and res[1][3] > 0
     assert res[0][4] + res[1][4] == 2 * 37 * 14  # every shard has exactly one home
+
+
+@pytest.mark.timeout(400)
+def test_bench_eight_ranks_rehearsal():
+    """The driver's 8-GPU SCALE shape rehearsed on CPU: `bench.py --gpus 8`
+    with no launcher starts 8 gloo ranks, all join, rank 0 alone prints the
+    line with n_gpus 8 and ranks_seen 8."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "3",
+                        "--warmup", "1", "--rehearse-cpu"], capture_output=True, text=True, env=_bench_env(),
+                       timeout=380, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 8 and line["ranks_seen"] == 8, line
+
+
+def _eight_rank_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        barrier, max_over = bench.make_collectives(dist, torch.device("cpu"))
+        el = bench.timed_region(lambda _i: time.sleep(0.002 * (rank + 1)), 4, barrier, lambda: None, max_over)
+        q.put((rank, bench.stripe_range(rank, 256), el))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_eight_rank_gloo_timing_protocol():
+    """World 8: every rank reports the same max-over-ranks time, bounded by the
+    slowest rank, and the 8 stripe ranges tile [0, 8*S) with no overlap."""
+    world = 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_eight_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(250)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    times = {el for _, _, el in res}
+    assert len(times) == 1 and times.pop() >= 4 * 0.016
+    ranges = [rg for _, rg, _ in res]
+    assert ranges[0][0] == 0 and ranges[-1][1] == 8 * 256
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+
+
+def test_group_devices_rule():
+    """bench.py --group N: members on devices 0..N-1, or all on the pinned
+    device of a rehearsal; too few GPUs without a pin is refused."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.group_devices(4, 8, None) == [0, 1, 2, 3]
+    assert bench.group_devices(8, 1, 0) == [0] * 8
+    with pytest.raises(SystemExit):
+        bench.group_devices(8, 1, None)
+    with pytest.raises(SystemExit):
+        bench.group_devices(0, 8, None)
+
+
+def test_group_refuses_launcher():
+    import subprocess
+
+    env = _bench_env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--group", "2"], capture_output=True,
+                       text=True, env=env, timeout=100, cwd=ROOT)
+    assert r.returncode != 0 and "one process" in (r.stderr + r.stdout)

@@ -55,8 +55,10 @@ def test_register_free_reuse_sequence_in_child(rslib, orc):
 
 def test_registrations_sharing_pages(rslib, orc, torch_dev):
     """Two buffers that share a page registered one after the other: the
-    second takes a reference on the first's page span and registers only the
-    pages no span covers; unregistering the first leaves the second
+    second takes a reference on the shared page's span (a registration's
+    partial edge pages are spans of their own) and registers only the pages no
+    span covers; a's vectors that run over its edge-page spans stay zero-copy;
+    unregistering the first leaves the second
     zero-copy (its host calls run straight over it, never through the
     coalesced staging path) and correct; the span leaves the runtime with the
     last registration, after which the same vectors are staged."""
@@ -75,7 +77,9 @@ def test_registrations_sharing_pages(rslib, orc, torch_dev):
         vb = [b[4080 + i * size: 4080 + (i + 1) * size] for i in range(d + p)]  # b's vectors: its own pages
         rslib.host_register(a.ctypes.data, a.nbytes)
         rslib.host_register(b.ctypes.data, b.nbytes)
-        assert rslib.host_pool_stats()["spans"] - spans0 == 2  # a's pages, then b's pages a did not cover
+        # a: its partial first and last pages as spans of their own plus its
+        # middle; b: a reference on a's last-page span plus its own pages
+        assert rslib.host_pool_stats()["spans"] - spans0 == 4
         with pytest.raises(rslib.ErrInvalidArgument):
             rslib.host_register(a.ctypes.data, a.nbytes)  # same address twice
 
@@ -86,7 +90,8 @@ def test_registrations_sharing_pages(rslib, orc, torch_dev):
         assert _encode_ok(orc, r, d, p, va, rng) and _encode_ok(orc, r, d, p, vb, rng)
         assert staged() == s0  # both zero-copy
         rslib.host_unregister(a.ctypes.data)
-        assert rslib.host_pool_stats()["spans"] - spans0 == 2  # b still holds the shared page's span
+        # only the shared page outlives a: b holds its one-page span
+        assert rslib.host_pool_stats()["spans"] - spans0 == 2
         assert _encode_ok(orc, r, d, p, vb, rng)
         assert staged() == s0  # b still zero-copy
         assert _encode_ok(orc, r, d, p, va, rng)
@@ -166,4 +171,126 @@ def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
         t.join()
     del views, base
     m.close()
+    assert not errs, errs[:3]
+
+
+def _libc():
+    import ctypes
+
+    c = ctypes.CDLL(None, use_errno=True)
+    c.mmap.restype = ctypes.c_void_p
+    c.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    c.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    return c
+
+
+def test_unregister_releases_pages_a_neighbour_does_not_share(rslib, orc, torch_dev):
+    """Advisor round 4: A and B share one page; A is unregistered, A's own
+    pages are unmapped and mapped afresh at the same addresses (what an
+    allocator trim + regrow does), and a new buffer C registered there must
+    get new pinning: its zero-copy host calls write the pages the CPU sees.
+    Were A's whole span kept alive by B's reference, C would take that stale
+    pinning and the parity would land in the old physical pages."""
+    import ctypes
+
+    c = _libc()
+    PROT_RW, MAP_PRIV_ANON, MAP_FIXED = 0x3, 0x22, 0x10
+    page = 4096
+    npages = 24
+    base = c.mmap(None, npages * page, PROT_RW, MAP_PRIV_ANON, -1, 0)
+    assert base not in (None, ctypes.c_void_p(-1).value)
+    d, p, size = 4, 2, 16 * 1024  # 6 vectors x 16 KiB = 24 pages
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(5)
+    try:
+        a_lo, a_len = base + 64, 12 * page - 64 - 32  # A: pages 0..11, its last page shared with B
+        b_lo, b_len = a_lo + a_len, 4 * page + 32  # B: from the end of A (inside page 11) on
+        rslib.host_register(a_lo, a_len)
+        rslib.host_register(b_lo, b_len)
+        # A's host calls once, so its pages were used zero-copy
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * (npages * page)).from_address(base))
+        va = [arr[64 + i * 1024: 64 + (i + 1) * 1024] for i in range(d + p)]
+        assert _encode_ok(orc, r, d, p, va, rng)
+        rslib.host_unregister(a_lo)
+        # trim + regrow of A's exclusive pages 0..10: new physical pages, same addresses
+        assert c.munmap(base, 11 * page) == 0
+        got = c.mmap(base, 11 * page, PROT_RW, MAP_PRIV_ANON | MAP_FIXED, -1, 0)
+        assert got == base
+        # C: the fresh pages, page-aligned (no page shared with B)
+        rslib.host_register(base, 11 * page)
+        assert rslib.host_device_pointer(base, 11 * page)
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * (11 * page)).from_address(base))
+        vc = [arr[i * 4096: (i + 1) * 4096] for i in range(d + p)]
+        for it in range(3):
+            assert _encode_ok(orc, r, d, p, vc, rng), it
+        rslib.host_unregister(base)
+        rslib.host_unregister(b_lo)
+    finally:
+        c.munmap(base, npages * page)
+
+
+def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
+    """An unregister after a host call asks the resident engine to leave
+    instead of draining behind its idle window (advisor round 4): with the
+    idle window raised to 50 ms, register -> Encode -> unregister takes far
+    less than 50 ms, and the next call (engine relaunched) is still correct."""
+    import time
+
+    d, p, size = 10, 4, 8192
+    L = rslib.lib()
+    assert L.rs_tune(b"host_engine_idle_us", 50000) == 0
+    try:
+        r = rslib.New(d, p)
+        rng = np.random.default_rng(21)
+        buf = np.zeros((d + p) * size + 4096, np.uint8)
+        off = (-buf.ctypes.data) % 4096
+        v = [buf[off + i * size: off + (i + 1) * size] for i in range(d + p)]
+        times = []
+        for it in range(5):
+            rslib.host_register(buf[off:].ctypes.data, (d + p) * size)
+            assert _encode_ok(orc, r, d, p, v, rng), it
+            t0 = time.perf_counter()
+            rslib.host_unregister(buf[off:].ctypes.data)
+            times.append(time.perf_counter() - t0)
+            assert _encode_ok(orc, r, d, p, v, rng), it  # pageable now
+        print("unregister ms", [round(x * 1e3, 3) for x in times])
+        assert sorted(times)[2] < 0.02, times
+    finally:
+        L.rs_tune(b"host_engine_idle_us", 2000)
+
+
+def test_host_calls_proceed_during_unregister_drain(rslib, orc, torch_dev):
+    """rs_host_unregister drains the devices without holding the registry:
+    host calls on another registered buffer keep running (and stay correct)
+    while a third thread registers / unregisters in a loop."""
+    import threading
+
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    keep = rslib.host_alloc((d + p) * size)
+    vk = [keep[i * size:(i + 1) * size] for i in range(d + p)]
+    churn = np.zeros(64 * 4096, np.uint8)
+    stop = threading.Event()
+    errs = []
+
+    def churner():
+        try:
+            while not stop.is_set():
+                rslib.host_register(churn.ctypes.data, churn.nbytes)
+                rslib.host_unregister(churn.ctypes.data)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    t = threading.Thread(target=churner)
+    t.start()
+    try:
+        rng = np.random.default_rng(3)
+        for it in range(200):
+            if not _encode_ok(orc, r, d, p, vk, rng):
+                errs.append(("mismatch", it))
+                break
+    finally:
+        stop.set()
+        t.join(60)
+    rslib.host_free(keep)
     assert not errs, errs[:3]

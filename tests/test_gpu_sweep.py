@@ -207,7 +207,7 @@ def test_update_replace_at_reference_defect_sizes(rslib, orc, torch_dev, size):
 @pytest.mark.parametrize("l1d,size", [(32768, 17031), (32768, 49263), (32768, 236667), (49152, 24576 + 33),
                                       (49152, 3 * 24576 + 1000 + 5), (32768, 16384 * 3)])
 def test_update_replace_reference_compat_mode(rslib, orc, torch_dev, l1d, size):
-    """rs_tune("ref_update_tail", l1d) reproduces the reference's Update /
+    """rs_set_ref_l1d(handle, l1d) reproduces the reference's Update /
     Replace bytes (rs.go:190-200 tail pass, rs_oracle.c encode_part) on a host
     whose L1D is `l1d`: host API, single-stripe device call and device batch,
     byte for byte against the restated reference with the same L1D.  The last
@@ -221,7 +221,8 @@ def test_update_replace_reference_compat_mode(rslib, orc, torch_dev, l1d, size):
     assert orc.encode(d, p, enc) == 0
     new = _rand(rng, size)
     r = rslib.New(d, p)
-    assert L.rs_tune(b"ref_update_tail", l1d) == 0
+    r.set_ref_l1d(l1d)
+    assert r.ref_l1d == l1d
     orc.set_l1d(l1d)
     try:
         # Update: restated reference, then each librsamd entry point
@@ -266,8 +267,102 @@ def test_update_replace_reference_compat_mode(rslib, orc, torch_dev, l1d, size):
             for s_ in range(S):
                 assert np.array_equal(buf[s_, j].cpu().numpy(), ora[j]), ("replace_batch", l1d, size, s_, j)
     finally:
-        L.rs_tune(b"ref_update_tail", 0)
         orc.set_l1d(0)
+
+
+def test_update_replace_reference_compat_per_handle_concurrent(rslib, orc, torch_dev):
+    """The compat setting belongs to the handle (verdict round 4): three
+    handles in one process - re-encode (0), 32 KiB and 48 KiB L1D - run Update
+    and Replace concurrently from their own threads over sizes with a defect
+    range for both L1D values, and each one's bytes equal the restated
+    reference with ITS setting (orc.set_l1d), host API and device batch."""
+    import threading
+
+    torch = torch_dev
+    d, p, row, rows = 10, 4, 2, [0, 5, 7]
+    sizes = [3 * 16384 + 16 * 37 + 9, 2 * 24576 + 16 * 50 + 3]  # last chunk >= 16 B, not a multiple of 16
+    settings = [0, 32768, 49152]
+    rng = np.random.default_rng(77)
+    cases = []
+    for size in sizes:
+        data = [_rand(rng, size) for _ in range(d)]
+        enc = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+        assert orc.encode(d, p, enc) == 0
+        new = _rand(rng, size)
+        delta = [_rand(rng, size) for _ in rows]
+        exp = {}
+        for l1d in settings:
+            orc.set_l1d(l1d)
+            if l1d == 0:  # the re-encode definition
+                u = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                u[row] = new.copy()
+                assert orc.encode(d, p, u) == 0
+                rp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                for i, rr in enumerate(rows):
+                    rp[rr] = np.bitwise_xor(rp[rr], delta[i])
+                assert orc.encode(d, p, rp) == 0
+                exp[l1d] = ([x.copy() for x in u[d:]], [x.copy() for x in rp[d:]])
+            else:
+                u = [x.copy() for x in enc]
+                assert orc.update(d, p, u[row], new, row, u[d:]) == 0
+                rp = [x.copy() for x in enc]
+                assert orc.replace(d, p, [x.copy() for x in delta], rows, rp[d:]) == 0
+                exp[l1d] = (u[d:], rp[d:])
+        orc.set_l1d(0)
+        # the three expectations really differ pairwise at these sizes
+        for a in settings:
+            for b in settings:
+                if a < b:
+                    assert any(not np.array_equal(x, y) for x, y in zip(exp[a][0], exp[b][0])), (size, a, b)
+        cases.append((size, enc, new, delta, exp))
+    handles = {}
+    for l1d in settings:
+        h = rslib.New(d, p, device=0)
+        h.set_ref_l1d(l1d)
+        handles[l1d] = h
+    errors = []
+    start = threading.Barrier(len(settings))
+
+    def run(l1d):
+        try:
+            h = handles[l1d]
+            stream = torch.cuda.Stream(0)
+            start.wait()
+            for _rep in range(3):
+                for size, enc, new, delta, exp in cases:
+                    act = [x.copy() for x in enc]
+                    h.Update(act[row], new, row, act[d:])
+                    for j in range(p):
+                        if not np.array_equal(act[d + j], exp[l1d][0][j]):
+                            errors.append(("Update", l1d, size, j))
+                    act = [x.copy() for x in enc]
+                    h.Replace([x.copy() for x in delta], rows, act[d:])
+                    for j in range(p):
+                        if not np.array_equal(act[d + j], exp[l1d][1][j]):
+                            errors.append(("Replace", l1d, size, j))
+                    S = 2
+                    with torch.cuda.stream(stream):
+                        buf = torch.from_numpy(np.stack([np.stack(enc)] * S)).cuda(0)
+                        old_b = buf[:, row].clone()
+                        new_b = torch.from_numpy(np.stack([new] * S)).cuda(0)
+                    h.update_batch(old_b, new_b, row, buf, stream=stream)
+                    stream.synchronize()
+                    got = buf.cpu().numpy()
+                    for s_ in range(S):
+                        for j in range(p):
+                            if not np.array_equal(got[s_, d + j], exp[l1d][0][j]):
+                                errors.append(("update_batch", l1d, size, s_, j))
+        except Exception as e:  # noqa: BLE001
+            errors.append(("exception", l1d, repr(e)))
+
+    ts = [threading.Thread(target=run, args=(l1d,)) for l1d in settings]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:10]
+    assert [handles[x].ref_l1d for x in settings] == settings
 
 
 def _padded(torch, rng, S, nvec, n, device):

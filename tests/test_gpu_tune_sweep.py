@@ -45,7 +45,6 @@ SWEEP = {
     "host_engine_vram": [0, 1],
     "host_engine_split_rows": [1, 0, 2],
     "host_engine_max_bytes": [0, 1 << 20],
-    "ref_update_tail": [32768, 0],  # 64 KiB vectors: no rs.go tail-defect bytes, so equal to re-encode
     "host_pinned_max": [0, 4 << 20, 256 << 10],
     "host_zc_max": [0, 2 << 20, -1],
     "host_chunk": [4096, 128 << 10],

@@ -17,7 +17,12 @@ Mix per iteration (one of):
   dev   - device batch Encode + Reconst of 1..p lost (5-8 lost takes the
           run-time compiled kernels once they are ready; compiles start at the
           first sight of a matrix, jit_min_bytes 0);
-  multi - multi-pattern Reconst with a different erasure set per stripe.
+  multi - multi-pattern Reconst with a different erasure set per stripe;
+  wide  - (jit=policy) large device batches of wide rebuilds with a FRESH
+          erasure pattern each time, sized so that one launch crosses the
+          library's compile threshold (16+16 Reconst of 16 x 48 stripes @ 1 MiB,
+          100+28 Reconst of 20 x 80 stripes @ 256 KiB): first-sight machine-code
+          compiles from several threads at once under the shipped policy.
 Handles are shared between threads for one shape per class, so concurrent
 callers hit the same handle (rs.go's *RS is safe for concurrent use).
 Prints one JSON line; exits 1 on any mismatch or error.
@@ -49,8 +54,11 @@ def main():
     if MODE == "all":  # compile every matrix on first sight: hammer the compile and eviction paths
         assert rs.lib().rs_tune(b"jit", 2) == 0
     shared = {s: rs.New(*s) for s in SHAPES}
+    wide_shapes = [(16, 16, 1 << 20, 16, 48), (100, 28, 256 << 10, 20, 80)]  # d, p, size, lost, stripes
+    for d, p, *_ in wide_shapes:
+        shared[(d, p)] = rs.New(d, p)
     lock = threading.Lock()
-    stats = {"host": 0, "dev": 0, "multi": 0, "errors": []}
+    stats = {"host": 0, "dev": 0, "multi": 0, "wide": 0, "errors": []}
     t_end = time.time() + SECS
 
     def fail(msg):
@@ -135,6 +143,24 @@ def main():
         if not ok:
             fail(f"multi {d}+{p} S {S} n {n}")
 
+    def wide_op(rng, stream):
+        d, p, n, nl, S = wide_shapes[int(rng.integers(len(wide_shapes)))]
+        r = shared[(d, p)]
+        G = orc.gen_matrix(d, p).reshape(p, d)
+        one = rng.integers(0, 256, (1, d + p, n), dtype=np.uint8)
+        one[:, d:] = orc.encode_numpy(G, one[:, :d])  # the oracle's stripe, tiled S times on the GPU
+        lost = sorted(int(v) for v in rng.choice(d + p, nl, replace=False))  # fresh pattern
+        with torch.cuda.stream(stream):
+            ref = torch.from_numpy(one).cuda().expand(S, d + p, n).contiguous()
+            buf = ref.clone()
+            buf[:, lost] = 0x5A
+            r.reconst_batch(buf, [], lost, stream=stream)
+            ok = bool(torch.equal(buf, ref))
+            stream.synchronize()
+            del buf, ref
+        if not ok:
+            fail(f"wide reconst {d}+{p} S {S} n {n} lost {lost}")
+
     def worker(i):
         rng = np.random.default_rng(1000 + i)
         stream = torch.cuda.Stream()
@@ -145,9 +171,12 @@ def main():
                 r = shared[(d, p)]
             else:
                 r = private.setdefault((d, p), rs.New(d, p))
-            kind = ("host", "host", "dev", "multi")[int(rng.integers(4))]
+            kinds = ("host", "host", "dev", "multi") + (("wide",) if MODE == "policy" else ())
+            kind = kinds[int(rng.integers(len(kinds)))]
             try:
-                if kind == "host":
+                if kind == "wide":
+                    wide_op(rng, stream)
+                elif kind == "host":
                     host_op(rng, r, d, p)
                 elif kind == "dev":
                     dev_op(rng, r, d, p, stream)
@@ -167,11 +196,11 @@ def main():
         time.sleep(0.5)
         if time.time() - last > 20:
             last = time.time()
-            print(f"progress: {stats['host']} host, {stats['dev']} dev, {stats['multi']} multi, "
+            print(f"progress: {stats['host']} host, {stats['dev']} dev, {stats['multi']} multi, {stats['wide']} wide, "
                   f"{len(stats['errors'])} errors", flush=True)
     for t in th:
         t.join()
-    out = {"threads": T, "seconds": SECS, "jit_mode": MODE, "host": stats["host"], "dev": stats["dev"], "multi": stats["multi"],
+    out = {"threads": T, "seconds": SECS, "jit_mode": MODE, "host": stats["host"], "dev": stats["dev"], "multi": stats["multi"], "wide": stats["wide"],
            "errors": stats["errors"][:20], "jit": rs.jit_stats()}
     print(json.dumps(out), flush=True)
     sys.exit(1 if stats["errors"] else 0)
