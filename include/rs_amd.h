@@ -483,8 +483,11 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "host_engine_yield_us" (a caller waiting longer than this on its engine
  * call yields its core between polls; 0 default = always spin),
  * "host_engine_idle_us" (the engine leaves after this long without a call,
- * default 2000; a call that finds it gone pays a relaunch), "host_engine_life_us" (and once it has run this long, even
- * while calls keep coming: a device-wide synchronisation waits at most about
+ * default 2000), "host_engine_cold_launch" (1 default: a call that finds the
+ * engine gone, with no call pending, takes the launch path and the engine is
+ * relaunched while that call's kernel runs | 0: the call waits for the
+ * relaunch), "host_engine_life_us" (the engine also leaves once it has run
+ * this long, even while calls keep coming: a device-wide synchronisation waits at most about
  * this long for it; default 4000), "host_engine_max_bytes" (larger batches
  * launch; default 1 MiB), "host_engine_vram" (1: the engine's call slots and
  * the small calls' input staging live in device memory the host writes
@@ -531,6 +534,10 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * more VGPRs: 0 default | 1 | -1 = for 8-wave workgroups only),
  * "jit_share_cols" (shared columns: columns each wave loads per step, one
  * barrier per nw x n columns: 1 default | 2 | -1 = 2 for 8-wave workgroups),
+ * "jit_share_dma" (shared columns: 0 = each wave loads its next column into
+ * registers one step ahead | n = 2..8: each wave's columns stream into a
+ * private LDS ring of n steps through LDS-DMA loads, n - 1 steps ahead, with
+ * no load registers),
  * "jit_split_cols" (n > 0: products of 9-16 rows over at least n columns run
  * as two 8-row paths sharing the columns; 0 default: one path; measured
  * within -4..+4 %),

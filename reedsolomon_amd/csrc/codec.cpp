@@ -676,6 +676,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_path_rows") g_jit_path_rows = value < 1 ? 1 : value > 16 ? 16 : value;
         else if (n == "jit_share") g_jit_share = value ? 1 : 0;
         else if (n == "jit_share_deep") g_jit_share_deep = value < 0 ? -1 : value ? 1 : 0;
+        else if (n == "jit_share_dma") g_jit_share_dma = value < 2 ? 0 : value > 8 ? 8 : value;
         else if (n == "jit_split_cols") g_jit_split_cols = value < 0 ? 0 : value;
         else if (n == "jit_share_cols") g_jit_share_cols = value < 0 ? -1 : value > 2 ? 2 : value < 1 ? 1 : value;
         else if (n == "jit_wide_pf") g_jit_wide_pf = value < 1 ? 1 : value > 4 ? 4 : value;
@@ -696,6 +697,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_engine_idle_us") g_engine_idle_us = value < 20 ? 20 : value > 100000 ? 100000 : value;
         else if (n == "host_engine_vram") g_engine_vram = value ? 1 : 0;
         else if (n == "host_engine_split_rows") g_engine_split_rows = value < 0 ? 0 : value > 2 ? 2 : value;
+        else if (n == "host_engine_cold_launch") g_engine_cold_launch = value ? 1 : 0;
         else if (n == "host_engine_life_us") g_engine_life_us = value < 100 ? 100 : value > 1000000 ? 1000000 : value;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);

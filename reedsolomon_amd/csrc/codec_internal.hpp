@@ -213,6 +213,7 @@ struct rs_codec {
     std::vector<uint8_t> eng_tab_key;
     std::atomic<uint64_t> eng_calls{0}, eng_launches{0};
     std::atomic<int> eng_inflight{0};  // calls rung and not yet seen complete by their callers
+    std::atomic<bool> eng_warm_wanted{false};  // a call declined a cold engine: relaunch it (engine_warm)
 
     // Reference-compat Update / Replace (rs_set_ref_l1d): the L1D bytes of the
     // host whose rs.go bytes to reproduce, 0 = the re-encode definition.
@@ -245,11 +246,18 @@ void engine_stop(rs_t* rs);  // caller holds eng_mu
 // follows.
 int engine_drain(rs_t* rs);
 void engine_shutdown(rs_t* rs);
+// After a call that the engine declined because it was cold (idle exit) has
+// enqueued its kernel on the launch path: relaunch the engine now, while that
+// kernel runs, so the next call finds it (no-op unless a call declined).
+void engine_warm(rs_t* rs);
+// Would an engine call now be declined as cold (see engine_warm)?  Lets a
+// caller skip staging meant for the engine.
+bool engine_cold_now(rs_t* rs);
 // Ask every handle's running engine instance to leave (its pending calls are
 // served first), ahead of a device-wide synchronisation by the library.
 void engines_quiesce();
 extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_engine_life_us, g_engine_wg_units,
-    g_engine_yield_us, g_engine_poll_gap, g_engine_vram, g_engine_split_rows;
+    g_engine_yield_us, g_engine_poll_gap, g_engine_vram, g_engine_split_rows, g_engine_cold_launch;
 // Device memory the host can write through the BAR (uncached for the GPU:
 // its loads always see the host's latest bytes), or nullptr when the
 // platform maps no such memory for the CPU (engine.cpp).  Blocks are pooled

@@ -97,6 +97,12 @@ int g_engine_wg_units = 0;
 // is not cached), 10+4 @ 8 KiB Encode 10.8 -> 20.5 us, Reconst of 4 10.9 -> 20.4
 // (profiles/r03/host_latency_split_rows.log)
 int g_engine_split_rows = 2;
+// A call that finds the engine gone (idle exit) and no call pending is served
+// by the launch path, and the engine is relaunched while that call's kernel
+// runs (engine_warm), instead of the call waiting for the relaunch: ~39 us ->
+// the launch path's ~20-25 us for the first call after a quiet period;
+// rs_tune("host_engine_cold_launch", 1 default | 0).
+int g_engine_cold_launch = 1;
 // Waiters spin this long, then yield the core between polls; rs_tune("host_engine_yield_us"), 0 = never
 // (default): 8-64 threads on the box measured the same either way and a lone
 // caller ~1 us slower with it (profiles/r02/engine_yield.log)
@@ -486,6 +492,54 @@ int engine_drain(rs_t* rs) {
     return engine_wait(rs, rs->eng_seq, rs->eng_waves, 0, rs->eng_waves, true);
 }
 
+static void engine_shape(int* waves, int* gwaves) {
+    *waves = g_engine_waves < 1 ? 1 : g_engine_waves > kEngineMaxGroups ? kEngineMaxGroups : g_engine_waves;
+    *gwaves = g_engine_group_waves < 1                      ? 1
+              : g_engine_group_waves > kEngineMaxGroupWaves ? kEngineMaxGroupWaves
+                                                            : g_engine_group_waves;
+}
+
+// The knobs changed since the latest instance started (caller holds eng_mu).
+static bool engine_reshape(const rs_t* rs, int waves, int gwaves) {
+    return rs->eng_waves > 0 &&
+           (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us ||
+            rs->eng_life_us != g_engine_life_us || rs->eng_poll_gap != g_engine_poll_gap);
+}
+
+// Caller holds eng_mu.  An instance ran before, none is serving now (it left
+// after its idle window, or was stopped) and every call rung so far is
+// complete: a call now would wait for a relaunch.
+static bool engine_cold(const rs_t* rs) {
+    if (rs->eng_waves <= 0 || engine_low_done(rs) < rs->eng_seq) return false;
+    if (!rs->eng_running) return true;
+    for (int w = 0; w < rs->eng_waves; ++w)
+        if (__atomic_load_n(&rs->eng_ring->gone[w], __ATOMIC_ACQUIRE) == rs->eng_epoch) return true;
+    return false;
+}
+
+bool engine_cold_now(rs_t* rs) {
+    if (!g_engine_cold_launch || !g_engine) return false;
+    std::lock_guard<std::mutex> lk(rs->eng_mu);
+    int waves, gwaves;
+    engine_shape(&waves, &gwaves);
+    return !rs->eng_failed && rs->eng_ring && !engine_reshape(rs, waves, gwaves) && engine_cold(rs);
+}
+
+void engine_warm(rs_t* rs) {
+    if (!rs->eng_warm_wanted.load(std::memory_order_acquire)) return;
+    std::unique_lock<std::mutex> lk(rs->eng_mu, std::try_to_lock);
+    if (!lk.owns_lock()) return;  // a call holds it: that call (re)launches the engine itself
+    if (!rs->eng_warm_wanted.exchange(false, std::memory_order_acq_rel)) return;
+    if (rs->eng_failed || !rs->eng_ring) return;
+    Region region("engine warm (relaunch behind a launch-path call)");
+    int waves, gwaves;
+    engine_shape(&waves, &gwaves);
+    if (engine_reshape(rs, waves, gwaves)) return;  // the next engine call reshapes it
+    if (engine_relaunch_if_gone(rs) != RS_OK) return;
+    if (!rs->eng_running && engine_drain(rs) == RS_OK && !rs->eng_running)
+        (void)engine_launch(rs, waves, gwaves, rs->eng_seq);
+}
+
 static int engine_run(rs_t* rs, const EngineWork& wk) {
     const int rows = wk.rows, cols = wk.cols;
     const auto t_call = std::chrono::steady_clock::now();
@@ -528,13 +582,16 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
         for (uint32_t& t : rs->eng_slot_tab) t = 0;
     }
     EngineRing* ring = rs->eng_ring;
-    const int waves = g_engine_waves < 1 ? 1 : g_engine_waves > kEngineMaxGroups ? kEngineMaxGroups : g_engine_waves;
-    const int gwaves = g_engine_group_waves < 1                      ? 1
-                       : g_engine_group_waves > kEngineMaxGroupWaves ? kEngineMaxGroupWaves
-                                                                     : g_engine_group_waves;
-    if (rs->eng_waves > 0 &&
-        (rs->eng_waves != waves || rs->eng_group_waves != gwaves || rs->eng_idle_us != g_engine_idle_us ||
-         rs->eng_life_us != g_engine_life_us || rs->eng_poll_gap != g_engine_poll_gap)) {
+    int waves, gwaves;
+    engine_shape(&waves, &gwaves);
+    const bool reshape = engine_reshape(rs, waves, gwaves);
+    if (g_engine_cold_launch && !reshape && engine_cold(rs)) {
+        // idle exit with nothing pending: this call takes the launch path and
+        // the engine restarts behind it (engine_warm), for the calls that follow
+        rs->eng_warm_wanted.store(true, std::memory_order_release);
+        return RS_ERR_INVAL;
+    }
+    if (reshape) {
         // new shape: the calls in flight finish on the old one, and the old
         // instance is gone before the next one reads done words
         RS_TRY(engine_drain(rs));

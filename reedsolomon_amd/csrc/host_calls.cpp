@@ -423,6 +423,7 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     std::lock_guard<std::mutex> lk(rs->co_launch_mu);
     const int rc = matmul(rs, b.mat.data(), b.rows, b.cols, in, static_cast<int64_t>(b.stride), out,
                           static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
+    engine_warm(rs);  // (a cold engine declined this batch: it restarts while the kernel runs)
     const hipError_t e = hipStreamSynchronize(rs->co_stream);  // never leave a kernel on the buffer
     return rc ? rc : (e == hipSuccess ? RS_OK : dev_fail(e, "coalesced batch sync"));
 }
@@ -483,6 +484,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
                 RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
             if (rs->zc_pending) RS_TRY(sync(rs));
             const int rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, size, accumulate, rs->stream);
+            engine_warm(rs);  // (a cold engine declined this call: it restarts while the kernel runs)
             const int src_rc = sync(rs);
             return rc ? rc : src_rc;
         }
@@ -493,7 +495,7 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     }
     if (g_engine_direct) {
         const size_t pitch = rup(size, 64), stride = pitch * static_cast<size_t>(rows + cols);
-        if (engine_accepts(rows, cols, stride)) {
+        if (engine_accepts(rows, cols, stride) && !engine_cold_now(rs)) {
             using clk = std::chrono::steady_clock;
             clk::time_point t0, t1, t2;
             if (g_phase_trace) t0 = clk::now();

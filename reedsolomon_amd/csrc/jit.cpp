@@ -119,9 +119,13 @@ static bool jit_split_small(int rows, int cols) {
 // kernel loads per step, i.e. one barrier per nw x n columns (-1: 2 for 8-wave
 // workgroups, whose occupancy the 8 extra VGPRs do not change)
 int g_jit_share_cols = 1;
+// rs_tune("jit_share_dma", 0 | 2..8): shared-column kernels stream each wave's
+// columns into an LDS ring of n steps by LDS-DMA loads (n - 1 steps ahead, no
+// load registers) instead of one step ahead through VGPRs; 0 = off
+int g_jit_share_dma = 0;
 AsmShape jit_shape(int rows, int cols) {
     return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep,
-                     jit_split_small(rows, cols) ? 1 : 0, g_jit_share_cols);
+                     jit_split_small(rows, cols) ? 1 : 0, g_jit_share_cols, g_jit_share_dma);
 }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // Generated kernels of more than 16 rows (several code paths): two columns of
@@ -892,6 +896,7 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_backend ? g_jit_path_rows : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share_deep : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_share_dma : 0);
     k.text += static_cast<char>(g_jit_backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share_cols : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
@@ -929,6 +934,7 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(backend ? g_jit_path_rows : 0);
     key += static_cast<char>(backend ? g_jit_share : 0);
     key += static_cast<char>(backend ? g_jit_share_deep : 0);
+    key += static_cast<char>(backend ? g_jit_share_dma : 0);
     key += static_cast<char>(backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
     key += static_cast<char>(backend ? g_jit_share_cols : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);

@@ -99,6 +99,9 @@ enum class K : uint8_t {
     BufStore2,  // same
     DsWrite4,   // ds_write_b128: a = vaddr, b = first data VGPR, imm = offset
     DsRead4,    // ds_read_b128: a = first vdst, b = vaddr, imm = offset
+    DsRead2,    // ds_read_b64: a = first vdst, b = vaddr, imm = offset
+    BufLoadLds4,  // buffer_load_dwordx4 ... lds (LDS-DMA: 16 bytes per lane to LDS at M0 + 16 * lane):
+                  // b = vaddr, c = srsrc, sub = nt
 };
 
 enum Sub : uint8_t {
@@ -156,7 +159,11 @@ struct Prog {
     void buf_store2(int vdata, int vaddr, int srsrc, int off) { put(K::BufStore2, 1, vdata, vaddr, srsrc, off); }
     void ds_write4(int vaddr, int vdata, uint32_t off) { put(K::DsWrite4, kNone, vaddr, vdata, 0, 0, off); }
     void ds_read4(int vdst, int vaddr, uint32_t off) { put(K::DsRead4, kNone, vdst, vaddr, 0, 0, off); }
+    void ds_read2(int vdst, int vaddr, uint32_t off) { put(K::DsRead2, kNone, vdst, vaddr, 0, 0, off); }
+    void buf_load_lds4(int vaddr, int srsrc, bool nt) { put(K::BufLoadLds4, nt ? 1 : 0, 0, vaddr, srsrc); }
 };
+
+constexpr int kM0 = 124;  // SGPR operand number of M0
 
 // ---------------------------------------------------------------- text
 
@@ -166,9 +173,12 @@ std::string opnd(int x, uint32_t imm) {  // a 9-bit source operand as assembly t
     else if (x == kLit) std::snprintf(b, sizeof b, "0x%x", imm);
     else if (x >= 128 && x <= 192) std::snprintf(b, sizeof b, "%d", x - 128);
     else if (x >= 193 && x <= 208) std::snprintf(b, sizeof b, "%d", 192 - x);
+    else if (x == kM0) std::snprintf(b, sizeof b, "m0");
     else std::snprintf(b, sizeof b, "s%d", x);
     return b;
 }
+
+std::string sreg(int n) { return n == kM0 ? std::string("m0") : "s" + std::to_string(n); }
 
 std::string print(const Prog& p) {
     std::string out;
@@ -189,9 +199,11 @@ std::string print(const Prog& p) {
                 if (i.b == 1) line("s_load_dword s%d, s[%d:%d], 0x%x", i.a, i.c, i.c + 1, i.imm);
                 else line("s_load_dwordx2 s[%d:%d], s[%d:%d], 0x%x", i.a, i.a + 1, i.c, i.c + 1, i.imm);
                 break;
-            case K::SMovLit: line(i.d ? "s_mov_b32 s%d, 0x%08x" : "s_mov_b32 s%d, 0x%x", i.a, i.imm); break;
+            case K::SMovLit:
+                line(i.d ? "s_mov_b32 %s, 0x%08x" : "s_mov_b32 %s, 0x%x", sreg(i.a).c_str(), i.imm);
+                break;
             case K::SOp1:
-                if (i.sub == kMov) line("s_mov_b32 s%d, s%d", i.a, i.b);
+                if (i.sub == kMov) line("s_mov_b32 %s, %s", sreg(i.a).c_str(), sreg(i.b).c_str());
                 else if (i.sub == kGetpc) line("s_getpc_b64 s[%d:%d]", i.a, i.a + 1);
                 else line("s_setpc_b64 s[%d:%d]", i.b, i.b + 1);
                 break;
@@ -254,6 +266,12 @@ std::string print(const Prog& p) {
             case K::DsRead4:
                 line("ds_read_b128 v[%d:%d], v%d offset:%u", i.a, i.a + 3, i.b, i.imm);
                 break;
+            case K::DsRead2:
+                line("ds_read_b64 v[%d:%d], v%d offset:%u", i.a, i.a + 1, i.b, i.imm);
+                break;
+            case K::BufLoadLds4:
+                line("buffer_load_dwordx4 v%d, s[%d:%d], 0 offen%s lds", i.b, i.c, i.c + 3, i.sub ? " nt" : "");
+                break;
         }
     }
     return out;
@@ -267,7 +285,7 @@ int ins_size(const Ins& i) {
     switch (i.k) {
         case K::Label: return 0;
         case K::SLoad: case K::VBfi: case K::VXor3: case K::BufLoad2: case K::BufStore2: return 8;
-        case K::DsWrite4: case K::DsRead4: return 8;
+        case K::DsWrite4: case K::DsRead4: case K::DsRead2: case K::BufLoadLds4: return 8;
         case K::SMovLit: return 8;
         case K::SAddPcrel: return 8;
         case K::SOp2: return (i.b == kLit || i.c == kLit) ? 8 : 4;
@@ -388,9 +406,14 @@ bool encode(const Prog& p, std::vector<uint32_t>* out, std::string* err) {
                 w(static_cast<uint32_t>(i.a) | (static_cast<uint32_t>(i.b) << 8));
                 break;
             case K::DsRead4:  // DS op 0xff; addr, vdst << 24
+            case K::DsRead2:  // DS op 0x76 (ds_read_b64)
                 if (i.imm > 0xffffu) return bad("ds offset");
-                w(0xd8000000u | (0xffu << 17) | i.imm);
+                w(0xd8000000u | ((i.k == K::DsRead4 ? 0xffu : 0x76u) << 17) | i.imm);
                 w(static_cast<uint32_t>(i.b) | (static_cast<uint32_t>(i.a) << 24));
+                break;
+            case K::BufLoadLds4:  // MUBUF op 0x17 (dwordx4), lds = bit 16, nt = bit 17, offen, offset 0; soffset 0
+                w(0xe0000000u | (0x17u << 18) | (i.sub ? 1u << 17 : 0u) | (1u << 16) | (1u << 12));
+                w(0x80000000u | ((static_cast<uint32_t>(i.c) >> 2) << 16) | static_cast<uint32_t>(i.b));
                 break;
         }
     }
@@ -455,18 +478,25 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     const int npaths = (rows + rw - 1) / rw;
     const bool share = sh.share && !by_group && npaths > 1;
     const int K = share && sh.kcols > 1 ? sh.kcols : 1;  // own columns per wave and step
-    const bool deep = share && sh.deep && K == 1;
+    // (dma: each wave's columns stream into a private LDS ring D steps deep
+    // through LDS-DMA loads - no VGPRs held by loads in flight)
+    const int D = share && K == 1 && sh.dma >= 2 ? sh.dma : 0;
+    const bool deep = share && sh.deep && K == 1 && !D;
     Layout L;
     // (share: one column of loads in flight per wave, i.e. nw columns of the
     // workgroup - two with deep; the planes read back from LDS get registers
-    // of their own, two sets with deep)
-    L.pf = share ? (deep ? 2 : K) : pf < 1 ? 1 : pf > 4 ? 4 : pf;
+    // of their own, two sets with deep; dma: no load registers, the raw bytes
+    // are read from LDS into the plane registers and transposed there)
+    L.pf = share ? (D ? 0 : deep ? 2 : K) : pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
     const int kVPlanes = L.slots_end;
     L.sub = L.slots_end + (share ? (deep ? 16 : 8) : 0);  // 2 x 11 subset registers: the XORs of 2-4 planes of each half
     L.acc = L.sub + 22;
     const int kVT1 = L.sub + 21;  // (see kVT0)
     L.vgprs = L.acc + 8 * rw;
+    const int kVDma = L.vgprs;  // dma: the lane's LDS-DMA offsets, chunk * 2048 + 16 * lane (+ 1024)
+    if (D) L.vgprs += 2;
+    const uint32_t raw_base = static_cast<uint32_t>(2 * npaths * 2048);  // dma ring, after the plane buffers
     if (vgprs_out) *vgprs_out = L.vgprs;
 
     // mask[c][r][i]: input planes j of column c feeding plane i of row r
@@ -523,6 +553,11 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     P.wait_lgkm0();
     P.label(l_stripe_done);
     P.s_nop(4);  // (v_readfirstlane -> SGPR read hazard margin)
+    if (D) {
+        P.v_op2(kVAnd, kVDma, kLit, kVOff, 0x1f8);        // 8 * lane
+        P.v_op2(kVAdd, kVDma, V(kVOff), kVDma);            // chunk * 2048 + 16 * lane
+        P.v_op2(kVAdd, kVDma + 1, kLit, kVDma, 1024);
+    }
     if (by_group) {
         // Layout 1: workgroup x -> (chunk group cg, row group g) with the row
         // groups of one chunk group on one XCD, back to back in its dispatch
@@ -647,9 +682,28 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                 col_id[static_cast<size_t>(c)] = next_id++;
             }
         };
+        // dma: column c = c_first + k_ * c_step streams into this wave's ring
+        // slot k_ % D (2 KiB as two LDS-DMA loads of 1 KiB, lane-linear)
+        auto dma_slot = [&](int k_) { return raw_base + static_cast<uint32_t>(((k_ % std::max(D, 1)) * nw + w) * 2048); };
+        auto issue_dma = [&](int c) {  // stage(c) was issued into slot (c / c_step) & 1
+            const int k_ = c / c_step;
+            desc(k_ & 1, kSDescIn);
+            if (c + c_step < cols) stage(c + c_step, (k_ + 1) & 1);
+            for (int h = 0; h < 2; ++h) {
+                P.s_mov_lit(kM0, dma_slot(k_) + 1024u * static_cast<uint32_t>(h), false);
+                P.s_nop(0);  // (M0 write -> LDS-DMA: one wait state)
+                P.buf_load_lds4(kVDma + h, kSDescIn, in_nt);
+                vq.push_back(next_id);
+                col_id[static_cast<size_t>(c)] = next_id++;
+            }
+        };
         if (c_first < cols) {
             stage(c_first, 0);
-            for (int k_ = 0; k_ < L.pf && c_first + k_ * c_step < cols; ++k_) issue_col(c_first + k_ * c_step);
+            if (D) {
+                for (int k_ = 0; k_ < D - 1 && c_first + k_ * c_step < cols; ++k_) issue_dma(c_first + k_ * c_step);
+            } else {
+                for (int k_ = 0; k_ < L.pf && c_first + k_ * c_step < cols; ++k_) issue_col(c_first + k_ * c_step);
+            }
         }
         // subset m of a half (2-4 of its planes) -> one of 11 registers (the
         // single planes stay where the transpose left them)
@@ -734,18 +788,30 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                 for (int q = 0; q < K; ++q) {
                     const int c = st * per + q * npaths + w, k_ = st * K + q;
                     if (c >= cols) break;
-                    vmem_wait_for(col_id[static_cast<size_t>(c)]);
+                    if (D) {
+                        // the column D - 1 steps ahead into the ring slot this
+                        // wave read (and waited for) in the previous step
+                        if (c + (D - 1) * c_step < cols) issue_dma(c + (D - 1) * c_step);
+                        vmem_wait_for(col_id[static_cast<size_t>(c)]);
+                        // lane t's four 8-byte pieces (8 t + 512 k) from the ring slot
+                        P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
+                        P.v_op2(kVAdd, kVT0, kLit, kVT0, dma_slot(k_));
+                        for (int k = 0; k < 4; ++k) P.ds_read2(kVPlanes + 2 * k, kVT0, 512u * static_cast<uint32_t>(k));
+                        P.wait_lgkm0();
+                    } else {
+                        vmem_wait_for(col_id[static_cast<size_t>(c)]);
+                    }
                     int pr[8];
-                    for (int j = 0; j < 8; ++j) pr[j] = slot_reg(k_, j);
+                    for (int j = 0; j < 8; ++j) pr[j] = D ? kVPlanes + j : slot_reg(k_, j);
                     transpose8(P, pr, kVT1);
                     // LDS address of lane t: 16 t (kVT0 is free between transposes)
                     P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
                     P.v_op2(kVLshl, kVT0, C(1), kVT0);
                     const uint32_t off = buf + static_cast<uint32_t>(q * npaths + w) * 2048u;
-                    P.ds_write4(kVT0, slot_reg(k_, 0), off);
-                    P.ds_write4(kVT0, slot_reg(k_, 4), off + 1024u);
+                    P.ds_write4(kVT0, pr[0], off);
+                    P.ds_write4(kVT0, pr[4], off + 1024u);
                     P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
-                    if (c + L.pf * npaths < cols) {
+                    if (!D && c + L.pf * npaths < cols) {
                         issue_col(c + L.pf * npaths);
                         // (its scalar loads back before the LDS reads below, so
                         // lgkmcnt counts LDS reads only, in order)

@@ -51,13 +51,15 @@ struct AsmShape {
     int share = 0;   // layout 0, nw > 1: columns shared through LDS
     int deep = 0;    // share: two steps of loads in flight and the next column's planes read ahead
     int kcols = 1;   // share: columns each wave loads per step (one barrier per nw * kcols columns)
+    int dma = 0;     // share: each wave's columns stream into a private LDS ring of `dma` steps through
+                     // LDS-DMA loads (buffer_load_dwordx4 ... lds), dma - 1 steps ahead; 0 = register loads
 };
 // deep: -1 = when the workgroup has 8 waves (one workgroup per CU whatever
 // the registers: the extra 24 VGPRs cost no occupancy), 0 / 1 = off / on.
 // split_small: a product of 9-16 rows runs as two paths of at most 8 rows
 // (half the accumulator registers per wave) instead of one.
 inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0,
-                          int deep = -1, int split_small = 0, int kcols = 1) {
+                          int deep = -1, int split_small = 0, int kcols = 1, int dma = 0) {
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
     const int paths = rows <= 16 ? (split_small && rows > 8 ? 2 : 1) : (rows + pr - 1) / pr;
@@ -70,10 +72,14 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     s.deep = s.share && (deep < 0 ? s.nw >= 8 : deep > 0) ? 1 : 0;
     s.kcols = s.share ? (kcols < 0 ? (s.nw >= 8 ? 2 : 1) : kcols < 1 ? 1 : kcols > 2 ? 2 : kcols) : 1;
     if (s.kcols > 1) s.deep = 0;
+    s.dma = (s.share && s.kcols == 1 && dma >= 2) ? (dma > 8 ? 8 : dma) : 0;
+    if (s.dma) s.deep = 0;
     return s;
 }
 // LDS bytes per workgroup of a generated kernel.
-inline int asm_lds_bytes(const AsmShape& s) { return s.share ? 2 * s.nw * s.kcols * 2048 : 0; }
+//   dma (share): wave w's columns of steps s .. s + dma - 1 land in its ring
+//     slots (s % dma) behind the plane buffers, (2 + dma) x nw x 2 KiB in all.
+inline int asm_lds_bytes(const AsmShape& s) { return s.share ? (2 * s.kcols + s.dma) * s.nw * 2048 : 0; }
 // Waves per workgroup of layout 0 (16 rows per wave at most).
 inline int asm_waves(int rows) { return asm_shape(rows, 0, 1).nw; }
 // (path_rows: products of more than 16 rows run in code paths of at most

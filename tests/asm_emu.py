@@ -19,9 +19,12 @@ before it wrote: the hardware needs one wait state there and otherwise reads
 the old value (measured on MI355X, tools/asm_probe/wave_id.s).
 
 Workgroups with LDS (the shared-column kernels): ds_write_b128 /
-ds_read_b128 on a per-workgroup LDS of the size the kernel descriptor
-declares (bounds and 16-byte alignment checked); reads land at
-`lgkmcnt(0)` like scalar loads.  The waves of a workgroup run in rounds
+ds_read_b128 / ds_read_b64 on a per-workgroup LDS of the size the kernel
+descriptor declares (bounds and alignment checked); reads land at
+`lgkmcnt(0)` like scalar loads.  LDS-DMA loads (`buffer_load_dwordx4 ...
+lds`: 16 bytes per lane written to LDS at M0 + 16 * lane) count on vmcnt like
+other vector memory loads, and an LDS read of bytes whose DMA has not been
+waited for raises `WaitcntError`.  The waves of a workgroup run in rounds
 from one s_barrier to the next, in alternating order, and a wave that reads
 LDS bytes another wave wrote in the same round, or writes bytes another
 wave read or wrote in it, raises `LdsRaceError`: without the barrier
@@ -76,7 +79,9 @@ def _parse(src: str):
 
 
 def _regs(tok: str):
-    """'v[4:5]' -> ('v', 4, 2); 's12' -> ('s', 12, 1)"""
+    """'v[4:5]' -> ('v', 4, 2); 's12' -> ('s', 12, 1); 'm0' -> ('s', 124, 1)"""
+    if tok == "m0":
+        return "s", 124, 1
     m = re.match(r"^([sv])\[(\d+):(\d+)\]$", tok)
     if m:
         a, b = int(m.group(2)), int(m.group(3))
@@ -95,6 +100,20 @@ class LdsRaceError(AssertionError):
     pass
 
 
+class _Dma:
+    """An outstanding LDS-DMA load in a wave's vmcnt queue: the LDS bytes
+    [lo, hi) it writes (it has no VGPR destination)."""
+
+    def __init__(self, lo: int, hi: int):
+        self.lo, self.hi = lo, hi
+
+    def __contains__(self, vgpr) -> bool:
+        return False
+
+    def overlaps(self, lo: int, hi: int) -> bool:
+        return self.lo < hi and lo < self.hi
+
+
 class Lds:
     """A workgroup's LDS plus, per barrier round, who wrote / read each byte."""
 
@@ -108,10 +127,10 @@ class Lds:
         self.writer[:] = -1
         self.readers[:] = False
 
-    def _span(self, wave, addr, write):
-        if addr % 16 or addr < 0 or addr + 16 > self.size:
+    def _span(self, wave, addr, write, n=16):
+        if addr % n or addr < 0 or addr + n > self.size:
             raise AssertionError(f"wave {wave}: LDS access at {addr} out of bounds / unaligned (size {self.size})")
-        sl = slice(addr, addr + 16)
+        sl = slice(addr, addr + n)
         w = self.writer[sl]
         if np.any((w >= 0) & (w != wave)):
             raise LdsRaceError(f"wave {wave}: LDS bytes {addr}.. written by wave {int(w.max())} in this round")
@@ -213,6 +232,41 @@ class Wave:
                 continue
             if op == "s_nop":
                 continue
+            if op == "ds_read_b64":
+                assert self.lds is not None, "LDS access in a kernel without LDS"
+                off = 0
+                for m_ in rest.split():
+                    if m_.startswith("offset:"):
+                        off = int(m_.split(":")[1])
+                dr, ar = _regs(ops[0]), _regs(ops[1].split()[0])
+                self._chk("v", ar[1], 1)
+                self._chk("v", dr[1], 2, write=True)
+                addr = self.v[ar[1]].astype(np.int64) + off
+                lo, hi = int(addr.min()), int(addr.max()) + 8
+                if any(isinstance(d, _Dma) and d.overlaps(lo, hi) for d in self.vm):
+                    raise WaitcntError(f"pc {self.pc}: LDS bytes {lo}..{hi} read before their LDS-DMA was waited for")
+                for lane in range(64):
+                    sl = self.lds._span(self.wid, int(addr[lane]), False, 8)
+                    w = self.lds.buf[sl].view(np.uint32)
+                    self.v[dr[1], lane], self.v[dr[1] + 1, lane] = int(w[0]), int(w[1])
+                self.lds_q.append(({dr[1], dr[1] + 1}, False))
+                continue
+            if op == "buffer_load_dwordx4" and rest.split()[-1] == "lds":
+                assert self.lds is not None, "LDS-DMA in a kernel without LDS"
+                voff = self.vval(ops[0]).astype(np.int64)
+                sr = _regs(ops[1])
+                self._chk("s", sr[1], 4)
+                self._chk("s", 124, 1)
+                m0 = self.s[124]
+                d0, d1, d2 = self.s[sr[1]], self.s[sr[1] + 1], self.s[sr[1] + 2]
+                base, nrec = d0 | ((d1 & 0xFFFF) << 32), d2
+                assert "offset:" not in rest, "LDS-DMA with an instruction offset (its LDS semantics are not modelled)"
+                for lane in range(64):
+                    o = int(voff[lane])
+                    sl = self.lds._span(self.wid, m0 + 16 * lane, True)
+                    self.lds.buf[sl] = emu.mem.view(base + o, 16) if o + 16 <= nrec else 0
+                self.vm.append(_Dma(m0, m0 + 16 * 64))
+                continue
             if op in ("ds_write_b128", "ds_read_b128"):
                 assert self.lds is not None, "LDS access in a kernel without LDS"
                 mods = rest.split()
@@ -225,6 +279,9 @@ class Wave:
                     self._chk("v", ar[1], 1)
                     self._chk("v", dr[1], 4)
                     addr = self.v[ar[1]].astype(np.int64) + off
+                    lo, hi = int(addr.min()), int(addr.max()) + 16
+                    if any(isinstance(d, _Dma) and d.overlaps(lo, hi) for d in self.vm):
+                        raise WaitcntError(f"pc {self.pc}: LDS bytes {lo}..{hi} written while an LDS-DMA into them is outstanding")
                     for lane in range(64):
                         sl = self.lds._span(self.wid, int(addr[lane]), True)
                         self.lds.buf[sl] = np.array([self.v[dr[1] + q, lane] for q in range(4)],
@@ -235,6 +292,9 @@ class Wave:
                     self._chk("v", ar[1], 1)
                     self._chk("v", dr[1], 4, write=True)
                     addr = self.v[ar[1]].astype(np.int64) + off
+                    lo, hi = int(addr.min()), int(addr.max()) + 16
+                    if any(isinstance(d, _Dma) and d.overlaps(lo, hi) for d in self.vm):
+                        raise WaitcntError(f"pc {self.pc}: LDS bytes {lo}..{hi} read before their LDS-DMA was waited for")
                     for lane in range(64):
                         sl = self.lds._span(self.wid, int(addr[lane]), False)
                         w = self.lds.buf[sl].view(np.uint32)
@@ -243,7 +303,8 @@ class Wave:
                     self.lds_q.append(({dr[1] + q for q in range(4)}, False))
                 continue
             if ops and op not in ("s_cbranch_scc1", "s_cbranch_scc0", "s_branch", "s_cmp_eq_u64", "s_cmp_eq_u32",
-                                  "s_cmp_ge_u32", "s_setpc_b64", "buffer_store_dwordx2", "ds_write_b128"):
+                                  "s_cmp_ge_u32", "s_setpc_b64", "buffer_store_dwordx2", "ds_write_b128",
+                                  "buffer_load_dwordx4"):
                 self._use(ops[0], write=True)  # the destination
             if op == "s_load_dword" or op == "s_load_dwordx2":
                 d, base, off = ops[0], ops[1], int(ops[2], 0)

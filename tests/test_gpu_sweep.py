@@ -280,7 +280,8 @@ def test_update_replace_reference_compat_per_handle_concurrent(rslib, orc, torch
 
     torch = torch_dev
     d, p, row, rows = 10, 4, 2, [0, 5, 7]
-    sizes = [3 * 16384 + 16 * 37 + 9, 2 * 24576 + 16 * 50 + 3]  # last chunk >= 16 B, not a multiple of 16
+    # last chunk >= 16 B and not a multiple of 16 for both L1Ds, at different offsets
+    sizes = [40001, 70003]
     settings = [0, 32768, 49152]
     rng = np.random.default_rng(77)
     cases = []

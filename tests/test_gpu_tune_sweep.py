@@ -44,6 +44,7 @@ SWEEP = {
     "host_engine_life_us": [100, 4000],
     "host_engine_vram": [0, 1],
     "host_engine_split_rows": [1, 0, 2],
+    "host_engine_cold_launch": [0, 1],
     "host_engine_max_bytes": [0, 1 << 20],
     "host_pinned_max": [0, 4 << 20, 256 << 10],
     "host_zc_max": [0, 2 << 20, -1],
@@ -72,6 +73,7 @@ SWEEP = {
     "jit_wide_waves": [0, 2, 3],
     "jit_share": [0, 1],
     "jit_share_deep": [1, -1, 0],
+    "jit_share_dma": [3, 0],
     "jit_split_cols": [4, 0],
     "jit_share_cols": [2, -1, 1],
     "table_registry_max": [1, 1 << 14],

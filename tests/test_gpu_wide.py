@@ -279,6 +279,19 @@ def test_wide_asm_jit_shared_deep(rslib, orc, torch_dev, asm_jit, rows, cols):
         asm_jit.rs_tune(b"jit_share_deep", 0)
 
 
+@pytest.mark.parametrize("rows,cols,dma", [(64, 64, 3), (128, 128, 4), (33, 7, 2), (56, 200, 4), (17, 5, 8)])
+def test_wide_asm_jit_shared_dma(rslib, orc, torch_dev, asm_jit, rows, cols, dma):
+    """rs_tune("jit_share_dma", n): shared columns streamed into per-wave LDS
+    rings by LDS-DMA loads (buffer_load_dwordx4 ... lds), n - 1 steps ahead,
+    against the oracle on the GPU (overwrite and accumulate, aligned and
+    ragged sizes)."""
+    assert asm_jit.rs_tune(b"jit_share_dma", dma) == 0
+    try:
+        test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
+    finally:
+        asm_jit.rs_tune(b"jit_share_dma", 0)
+
+
 @pytest.mark.parametrize("d,p,S", [(64, 64, 4), (128, 128, 2), (200, 56, 2)])
 def test_wide_full_size_round_trip(rslib, orc, torch_dev, asm_jit, d, p, S):
     """Full-size wide stripes (1 MiB vectors) through the compiled shared-column

@@ -245,3 +245,54 @@ def test_asm_kernel_split_small(rslib, orc, rows, cols, acc):
     finally:
         L.rs_tune(b"jit_split_cols", 0)
     assert "ds_write_b128" in src and ".amdhsa_group_segment_fixed_size 8192" in src
+
+
+@pytest.mark.parametrize("rows,cols,acc,dma", [(33, 7, 0, 3), (40, 9, 1, 2), (17, 5, 0, 4), (64, 13, 0, 3),
+                                               (64, 1, 1, 4), (128, 19, 0, 3), (48, 30, 1, 6), (20, 2, 0, 8)])
+def test_asm_kernel_shared_columns_dma(rslib, orc, rows, cols, acc, dma):
+    """rs_tune("jit_share_dma", n): each wave's columns stream into a private
+    LDS ring of n steps through LDS-DMA loads (buffer_load_dwordx4 ... lds,
+    n - 1 steps ahead), are read back into the plane registers (ds_read_b64),
+    transposed and shared as before.  Against the oracle in the emulator,
+    which fails an LDS read of bytes whose DMA was not waited for (vmcnt) and
+    the usual cross-wave races; ragged steps and short columns included."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_share_dma", dma) == 0
+    try:
+        src = _check_kernel(rslib, orc, rows, cols, acc)
+    finally:
+        L.rs_tune(b"jit_share_dma", 0)
+    nw = (rows + 15) // 16
+    assert src.count(" lds") == 2 * cols  # two 1 KiB LDS-DMA loads per column
+    assert src.count("ds_read_b64") == 4 * cols
+    assert f".amdhsa_group_segment_fixed_size {(2 + dma) * nw * 2048}" in src
+
+
+def test_emulator_catches_an_unwaited_dma(rslib, orc):
+    """The DMA wait check is live: the same kernel with every vmcnt wait made
+    a no-op reads ring bytes whose LDS-DMA is still outstanding."""
+    import re
+
+    from asm_emu import WaitcntError
+
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_share_dma", 3) == 0
+    try:
+        with pytest.raises(WaitcntError):
+            _check_kernel(rslib, orc, 33, 7, 0, edit=lambda s: re.sub(r"vmcnt\(\d+\)", "vmcnt(63)", s))
+    finally:
+        L.rs_tune(b"jit_share_dma", 0)
+
+
+@pytest.mark.parametrize("rows,cols,acc,dma", [(64, 64, 0, 4), (128, 128, 1, 3), (56, 200, 0, 4), (33, 3, 1, 2)])
+def test_machine_code_equals_assembler_dma(rslib, rows, cols, acc, dma):
+    """The DMA-ring kernels' machine code (M0 writes, buffer_load_dwordx4 ...
+    lds, ds_read_b64) equals comgr's assembly of their text."""
+    L = rslib.lib()
+    mat = np.random.default_rng(rows * 41 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
+    assert L.rs_tune(b"jit_share_dma", dma) == 0
+    try:
+        n = rslib.jit_encoder_check(mat, bool(acc))
+    finally:
+        L.rs_tune(b"jit_share_dma", 0)
+    assert n > 0 and n % 4 == 0

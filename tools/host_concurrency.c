@@ -94,6 +94,22 @@ static void on_usr1(int sig) {
     backtrace_symbols_fd(frames, n, 2);
 }
 
+/* HL_TUNE="name=value,name=value": any rs_tune knobs (applied after the
+ * HL_* shorthands). */
+static void apply_tune_env(void) {
+    const char* e = getenv("HL_TUNE");
+    char buf[512], *tok, *save = NULL;
+    if (!e) return;
+    strncpy(buf, e, sizeof buf - 1);
+    buf[sizeof buf - 1] = 0;
+    for (tok = strtok_r(buf, ",", &save); tok; tok = strtok_r(NULL, ",", &save)) {
+        char* eq = strchr(tok, '=');
+        if (!eq) continue;
+        *eq = 0;
+        if (rs_tune(tok, atoi(eq + 1)) != RS_OK) fprintf(stderr, "HL_TUNE: unknown knob %s\n", tok);
+    }
+}
+
 int main(int argc, char** argv) {
     int a, t, j, nt;
     atexit(at_exit_last);
@@ -123,6 +139,7 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE_WG_UNITS")) rs_tune("host_engine_wg_units", atoi(getenv("HL_ENGINE_WG_UNITS")));
     if (getenv("HL_ENGINE_DIRECT")) rs_tune("host_engine_direct", atoi(getenv("HL_ENGINE_DIRECT")));
     if (getenv("HL_ENGINE_GROUP_WAVES")) rs_tune("host_engine_group_waves", atoi(getenv("HL_ENGINE_GROUP_WAVES")));
+    apply_tune_env();
     if (rs_device_count() < 1 || rs_new(D, P, -1, &g_rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;

@@ -101,6 +101,22 @@ static void report(const char* op, size_t vec, double bytes, int reps) {
     fflush(stdout);
 }
 
+/* HL_TUNE="name=value,name=value": any rs_tune knobs (applied after the
+ * HL_* shorthands). */
+static void apply_tune_env(void) {
+    const char* e = getenv("HL_TUNE");
+    char buf[512], *tok, *save = NULL;
+    if (!e) return;
+    strncpy(buf, e, sizeof buf - 1);
+    buf[sizeof buf - 1] = 0;
+    for (tok = strtok_r(buf, ",", &save); tok; tok = strtok_r(NULL, ",", &save)) {
+        char* eq = strchr(tok, '=');
+        if (!eq) continue;
+        *eq = 0;
+        if (rs_tune(tok, atoi(eq + 1)) != RS_OK) fprintf(stderr, "HL_TUNE: unknown knob %s\n", tok);
+    }
+}
+
 int main(int argc, char** argv) {
     size_t sizes[16] = {4096, 8192, 65536, 262144, 1048576, 4194304};
     size_t nsizes = 6;
@@ -132,6 +148,7 @@ int main(int argc, char** argv) {
     if (getenv("HL_ENGINE_IDLE")) rs_tune("host_engine_idle_us", atoi(getenv("HL_ENGINE_IDLE")));
     if (getenv("HL_ENGINE_LIFE")) rs_tune("host_engine_life_us", atoi(getenv("HL_ENGINE_LIFE")));
     if (getenv("HL_SPLIT_ROWS")) rs_tune("host_engine_split_rows", atoi(getenv("HL_SPLIT_ROWS")));
+    apply_tune_env();
     if (rs_device_count() < 1 || rs_new(D, P, -1, &rs) != RS_OK) {
         fprintf(stderr, "no device\n");
         return 1;
