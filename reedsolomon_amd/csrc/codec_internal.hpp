@@ -214,6 +214,7 @@ struct rs_codec {
     std::atomic<uint64_t> eng_calls{0}, eng_launches{0};
     std::atomic<int> eng_inflight{0};  // calls rung and not yet seen complete by their callers
     std::atomic<bool> eng_warm_wanted{false};  // a call declined a cold engine: relaunch it (engine_warm)
+    std::atomic<int64_t> eng_last_ns{0};       // steady-clock time of the latest engine call's completion
 
     // Reference-compat Update / Replace (rs_set_ref_l1d): the L1D bytes of the
     // host whose rs.go bytes to reproduce, 0 = the re-encode definition.

@@ -4,7 +4,7 @@
 // (gf_engine, kernels.hip) through a doorbell in host memory, instead of a
 // kernel launch plus a stream synchronisation per call.
 //
-// Measured on MI355X (tools/doorbell_probe3.hip, profiles/r02/doorbell_probe.log):
+// Measured on MI355X (round 2's doorbell probe, profiles/r02/doorbell_probe.log):
 // an empty call's round trip is 11.8 us with launch + hipStreamSynchronize,
 // 5.9 us with launch + a host-memory completion flag, 4.3 us through a
 // doorbell; with a 10+4 @ 8 KiB stripe read and written over PCIe 12.4 / 7.1 us
@@ -506,11 +506,20 @@ static bool engine_reshape(const rs_t* rs, int waves, int gwaves) {
             rs->eng_life_us != g_engine_life_us || rs->eng_poll_gap != g_engine_poll_gap);
 }
 
-// Caller holds eng_mu.  An instance ran before, none is serving now (it left
-// after its idle window, or was stopped) and every call rung so far is
-// complete: a call now would wait for a relaunch.
+static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Caller holds eng_mu.  An instance ran before, none is serving now, every
+// call rung so far is complete, and the handle has been quiet for at least
+// the idle window: a sporadic caller, whose call would wait for a relaunch.
+// (An instance that left at the end of its life while calls keep coming is
+// relaunched by the next call as before: that caller pays ~the launch path's
+// time anyway, and the calls behind it find the engine.)
 static bool engine_cold(const rs_t* rs) {
     if (rs->eng_waves <= 0 || engine_low_done(rs) < rs->eng_seq) return false;
+    if (now_ns() - rs->eng_last_ns.load(std::memory_order_relaxed) < int64_t{1000} * rs->eng_idle_us) return false;
     if (!rs->eng_running) return true;
     for (int w = 0; w < rs->eng_waves; ++w)
         if (__atomic_load_n(&rs->eng_ring->gone[w], __ATOMIC_ACQUIRE) == rs->eng_epoch) return true;
@@ -688,6 +697,7 @@ static int engine_run(rs_t* rs, const EngineWork& wk) {
     const auto t_ring = std::chrono::steady_clock::now();
     const int wrc = engine_wait(rs, seq, inst_waves, wg0, nwg, false);
     rs->eng_inflight.fetch_sub(1, std::memory_order_acq_rel);
+    rs->eng_last_ns.store(now_ns(), std::memory_order_relaxed);
     RS_TRY(wrc);
     const auto t_done = std::chrono::steady_clock::now();
     rs->eng_calls.fetch_add(1, std::memory_order_relaxed);

@@ -34,6 +34,7 @@ def engine(rslib):
     L.rs_tune(b"host_engine_max_bytes", 1 << 20)
     L.rs_tune(b"host_engine_wg_units", 0)
     L.rs_tune(b"host_engine_direct", 1)
+    L.rs_tune(b"host_engine_cold_launch", 1)
 
 
 def _rand(rng, n):
@@ -95,10 +96,15 @@ def test_engine_calls_vs_oracle(rslib, orc, torch_dev, engine, waves, group_wave
             assert calls > 0 and launches >= 1, (d, p, calls, launches)
 
 
-def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
-    """With a short idle window the engine leaves between spaced calls and a
-    new instance serves the next one; bursts share one instance."""
+@pytest.mark.parametrize("cold_launch", [1, 0])
+def test_engine_idle_relaunch(rslib, orc, torch_dev, engine, cold_launch):
+    """With a short idle window the engine leaves between spaced calls.
+    cold_launch=1 (default): a call that finds it gone is served by the
+    launch path and the engine restarts behind it, so only the first call
+    rides the engine and every call starts an instance; cold_launch=0: a new
+    instance serves each call.  Bursts share one instance either way."""
     assert engine.rs_tune(b"host_engine_idle_us", 50) == 0
+    assert engine.rs_tune(b"host_engine_cold_launch", cold_launch) == 0
     d, p, size = 10, 4, 8192
     r = rslib.New(d, p)
     rng = np.random.default_rng(7)
@@ -111,7 +117,7 @@ def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
         assert all(np.array_equal(v[j], exp[j]) for j in range(d, d + p)), k
         time.sleep(0.005)
     calls, launches = r.host_engine_stats()
-    assert calls == 6 and launches == 6, (calls, launches)
+    assert calls == (1 if cold_launch else 6) and launches == 6, (cold_launch, calls, launches)
     assert engine.rs_tune(b"host_engine_idle_us", 100000) == 0
     assert engine.rs_tune(b"host_engine_life_us", 1000000) == 0
     for k in range(50):  # a burst: one instance
@@ -119,7 +125,7 @@ def test_engine_idle_relaunch(rslib, orc, torch_dev, engine):
         r.Encode(v)
         assert all(np.array_equal(v[j], exp[j]) for j in range(d, d + p)), k
     calls2, launches2 = r.host_engine_stats()
-    assert calls2 == 56 and launches2 == launches + 1, (calls2, launches2)
+    assert calls2 == calls + 50 and launches2 == launches + 1, (calls2, launches2)
     assert engine.rs_tune(b"host_engine_idle_us", 2000) == 0
 
 

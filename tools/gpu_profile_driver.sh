@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-4 committed profiles of the headline kernel in one GPU call:
+# The committed profiles of the headline kernel, one GPU call per round:
 #  1. the driver's own command under rocprofv3 --kernel-trace --stats, and
 #     tools/trace_window.py cutting its timed window out (the headline kernel
 #     alone, no end-to-end or self-check launches)

@@ -4,17 +4,20 @@
 # instruction-cache counters of the rs_bs_asm kernel, one rocprofv3 --pmc pass
 # per counter group (MI355X_MICROARCH.md §rocprofv3 PMC slots), for each
 # shape given (tools/pmc_traffic.py specs, e.g. enc:64+64).  Summary:
-# gpurun_out/pmc_icache/summary.json (tools/pmc_sq_summary.py).
+# gpurun_out/pmc_icache/summary.json (tools/pmc_sq_summary.py).  PMC_GROUPS
+# picks the counter groups (default "SQ SQC"; "LDS" = the wait / LDS split).
 set -uo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$REPO/gpurun_out/pmc_icache"
+OUT="$REPO/gpurun_out/${PMC_OUT:-pmc_icache}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_IFETCH SQ_IFETCH_LEVEL GRBM_GUI_ACTIVE"
 SQC="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE"
+# LDS: where parked / stalled cycles come from (s_waitcnt + barrier vs LDS issue stalls and bank conflicts)
+LDS="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
 i=0
 for SPEC in "$@"; do
-  for GROUP in SQ SQC; do
+  for GROUP in ${PMC_GROUPS:-SQ SQC}; do
     i=$((i + 1))
     CTRS="${!GROUP}"
     echo "== p$i: $SPEC $GROUP"
