@@ -401,6 +401,13 @@ RS_API int rs_host_engine_stats(const rs_t* rs, uint64_t* calls, uint64_t* launc
  * NULL. */
 RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
 
+/* The run-time kernels' in-process table, process-wide: compiled kernels
+ * held now (at most 256) and evictions so far (each drops the older half;
+ * a launch never waits for one: it is queued on the library's worker thread,
+ * which drains the devices that ran the evicted kernels before unloading
+ * them).  Either pointer may be NULL. */
+RS_API int rs_jit_table_stats(uint64_t* entries, uint64_t* evictions);
+
 /* The run-time kernels' on-disk code-object cache (RSAMD_JIT_CACHE_DIR,
  * default $XDG_CACHE_HOME/rsamd/jit or ~/.cache/rsamd/jit; knob
  * "jit_disk_cache"), process-wide: first sights of a matrix whose code object

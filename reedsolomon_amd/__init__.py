@@ -11,7 +11,7 @@ from .rs import (  # noqa: F401
     ErrMismatchReplace, ErrNotSquare, ErrSingularMatrix, ErrInvalidArgument, ErrDevice, ErrNoMemory,
     invert, inverse_cache_key, host_l1d, gf_mul, device_count, host_register, host_unregister, host_device_pointer,
     host_alloc, host_free, host_pool_stats,
-    jit_stats, jit_cache_stats, jit_compile_check, jit_asm_source, jit_encoder_check,
+    jit_stats, jit_cache_stats, jit_table_stats, jit_compile_check, jit_asm_source, jit_encoder_check,
 )
 from ._lib import lib, LIB_PATH  # noqa: F401
 

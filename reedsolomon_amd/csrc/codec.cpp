@@ -779,6 +779,13 @@ int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, doubl
     });
 }
 
+int rs_jit_table_stats(uint64_t* entries, uint64_t* evictions) {
+    return abi_guard([&]() -> int {
+        jit_table_stats(entries, evictions);
+        return RS_OK;
+    });
+}
+
 int rs_jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects) {
     return abi_guard([&]() -> int {
         jit_cache_stats(hits, misses, writes, rejects);

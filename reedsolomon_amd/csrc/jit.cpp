@@ -853,6 +853,13 @@ void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double*
 
 void jit_count_launch() { jit().launches.fetch_add(1, std::memory_order_relaxed); }
 
+void jit_table_stats(uint64_t* entries, uint64_t* evictions) {
+    Jit& j = jit();
+    std::lock_guard<std::mutex> lk(j.mu);
+    if (entries) *entries = j.entries.size();
+    if (evictions) *evictions = j.evictions;
+}
+
 void jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects) {
     DiskStats& d = disk_stats();
     if (hits) *hits = d.hits.load();

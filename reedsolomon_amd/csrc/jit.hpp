@@ -96,6 +96,7 @@ int jit_encoder_check(const uint8_t* mat, int rows, int cols, bool accumulate, s
 // the kernel for a matrix now, whatever its launch history (rs_jit_prepare).
 int jit_prepare(const uint8_t* mat, int rows, int cols, bool accumulate, bool wait);
 void jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms);
+void jit_table_stats(uint64_t* entries, uint64_t* evictions);
 // On-disk code-object cache: first-sight lookups that found a valid file,
 // that found none, files written, files rejected on load (corrupt / stale).
 void jit_cache_stats(uint64_t* hits, uint64_t* misses, uint64_t* writes, uint64_t* rejects);

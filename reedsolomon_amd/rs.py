@@ -617,6 +617,13 @@ def jit_stats() -> dict:
     return {"compiled": c.value, "failed": f.value, "launches": n.value, "compile_ms": ms.value}
 
 
+def jit_table_stats() -> dict:
+    """Compiled run-time kernels held and evictions so far (rs_jit_table_stats)."""
+    e, v = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().rs_jit_table_stats(ctypes.byref(e), ctypes.byref(v)))
+    return {"entries": e.value, "evictions": v.value}
+
+
 def jit_cache_stats() -> dict:
     """The run-time kernels' on-disk code-object cache (rs_jit_cache_stats)."""
     v = [ctypes.c_uint64(0) for _ in range(4)]

@@ -418,3 +418,36 @@ def test_jit_disk_cache_across_processes(rslib, tmp_path):
         os.chmod(f, 0o600)
     g = run(1)
     assert g["ok"] and g["cache"]["hits"] == 1, g
+
+
+def test_jit_eviction_off_the_launch_path(rslib, orc, torch_dev, jit_sync):
+    """More distinct matrices than the kernel table holds (256), each compiled
+    on first sight (jit=2) and launched: the table fills, a launch queues the
+    eviction on the library's worker instead of draining the device itself
+    (advisor round 4), the worker drops the older half after the device
+    drain, and every launch before, during and after stays bit-exact against
+    the oracle (evicted matrices that come back are compiled again)."""
+    import time
+
+    torch = torch_dev
+    rng = np.random.default_rng(2024)
+    r = rslib.New(10, 4)
+    S, n = 2, 4096
+    src_h = rng.integers(0, 256, (S, 6, n), dtype=np.uint8)
+    src = torch.from_numpy(src_h).cuda()
+    t0 = rslib.jit_table_stats()
+    mats = [rng.integers(0, 256, (5, 6), dtype=np.uint8) for _ in range(300)]
+    for i, mat in enumerate(mats + mats[:20]):  # the first 20 again at the end: evicted, compiled afresh
+        dst = torch.zeros((S, 5, n), dtype=torch.uint8, device="cuda")
+        r.gf_matmul_batch(mat, src, None, dst, None)
+        if i % 7 == 0 or i >= 290:
+            torch.cuda.synchronize()
+            assert np.array_equal(dst.cpu().numpy(), orc.encode_numpy(mat, src_h)), i
+    torch.cuda.synchronize()
+    deadline = time.time() + 30  # the worker's eviction runs asynchronously
+    while rslib.jit_table_stats()["evictions"] == t0["evictions"] and time.time() < deadline:
+        time.sleep(0.05)
+    st = rslib.jit_table_stats()
+    assert st["evictions"] > t0["evictions"], (t0, st)
+    assert st["entries"] <= 256, st
+    assert rslib.jit_stats()["failed"] == 0

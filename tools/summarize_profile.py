@@ -68,8 +68,13 @@ dominant = statistics.mode([r["Kernel_Name"] for r in trace_all])
 trace = [r for r in trace_all if r["Kernel_Name"] == dominant]
 durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
 steps = int(os.environ.get("BENCH_STEPS", "1000"))  # tools/gpu_profile.sh runs --steps 1000
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (the config table: algorithmic bytes of this launch)
+
+_k, _m, _vec, _S = bench.CONFIGS[cfg]
 summary = {
     "config": cfg,
+    "algorithmic_bytes_per_launch": (_k + _m) * _vec * _S,
     "kernel": trace[0]["Kernel_Name"] if trace else None,
     "launches_traced": len(durs),
     "duration_ns_mean_all_launches": statistics.mean(durs) if durs else None,
@@ -87,6 +92,7 @@ summary = {
 json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 tpath = os.path.join(ROOT, "profiles", "traffic.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
-traffic[cfg] = {"hbm_bytes_per_launch": int(f_b + w_b), "source": f"profiles/{rnd}/pmc_summary.json"}
+traffic[cfg] = {"hbm_bytes_per_launch": int(f_b + w_b), "source": f"profiles/{rnd}/pmc_summary.json",
+                "algorithmic_bytes_per_launch": summary.get("algorithmic_bytes_per_launch")}
 json.dump(traffic, open(tpath, "w"), indent=1)
 print(json.dumps(summary, indent=1))
