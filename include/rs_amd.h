@@ -528,9 +528,13 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "jit_layout" (generated kernels of more than 16 rows: 0 default = the
  * rows over the waves of a workgroup, all on the same 2 KiB chunk | 1 = row
  * groups of up to 16 rows over workgroups whose waves take consecutive
- * chunks with the same code, the row groups of a chunk on one XCD),
+ * chunks with the same code, the row groups of a chunk on one XCD | 2 =
+ * with shared columns and more paths than jit_group_waves: workgroups of at
+ * most jit_group_waves waves, one path each, over one chunk, sharing its
+ * columns through LDS, G such workgroups per chunk on one XCD),
  * "jit_group_waves" (layout 1: waves per workgroup, 1, 2, 4 or 8 - other
- * values round down; default 4),
+ * values round down; layout 2: at most this many waves per workgroup,
+ * 2..8; default 4),
  * "jit_path_rows" (generated kernels of more than 16 rows: rows per code
  * path, 1..16, each row 8 VGPR accumulators; default 16),
  * "jit_share" (generated kernels of several waves, layout 0: 1 = each column

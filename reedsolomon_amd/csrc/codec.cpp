@@ -670,7 +670,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_pf") g_jit_pf = value < 1 ? 1 : value > 6 ? 6 : value;
         else if (n == "jit_sync") g_jit_sync = value < 0 ? 0 : value > 64 ? 64 : value;
         else if (n == "jit_waves") g_jit_waves = value < 0 ? 0 : value > 8 ? 8 : value;
-        else if (n == "jit_layout") g_jit_layout = value == 1 ? 1 : 0;
+        else if (n == "jit_layout") g_jit_layout = value == 1 || value == 2 ? value : 0;
         else if (n == "jit_group_waves")  // a power of two (the kernel shifts by log2): 1, 2, 4 or 8
             g_jit_group_waves = value >= 8 ? 8 : value >= 4 ? 4 : value >= 2 ? 2 : 1;
         else if (n == "jit_path_rows") g_jit_path_rows = value < 1 ? 1 : value > 16 ? 16 : value;

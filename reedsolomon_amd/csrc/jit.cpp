@@ -93,7 +93,8 @@ int g_jit_waves = [] {
 // waves take consecutive chunks with the same code (1, group_waves waves)
 int g_jit_layout = [] {
     const char* e = std::getenv("RSAMD_JIT_LAYOUT");
-    return e ? (std::atoi(e) == 1 ? 1 : 0) : 0;
+    const int v = e ? std::atoi(e) : 0;
+    return v == 1 || v == 2 ? v : 0;
 }();
 int g_jit_group_waves = 4;
 // rs_tune("jit_path_rows", 1..16): rows per code path of generated kernels of

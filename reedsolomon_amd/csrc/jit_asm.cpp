@@ -472,11 +472,16 @@ void transpose8(Prog& P, const int (&r)[8], int t1) {
 // AsmShape, jit_asm.hpp).
 Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& sh, int pf, int sync,
               int* vgprs_out) {
-    const bool by_group = sh.layout == 1;
+    // layout 1 and 2: row groups over XCD-mapped workgroups; layout 2's
+    // workgroup is nw waves with a path each over ONE chunk, sharing columns
+    const bool by_group = sh.layout == 1 || sh.layout == 2;
+    const bool grouped_share = sh.layout == 2;
     const int nw = sh.nw;
-    const int rw = sh.rw;  // rows per code path (per wave in layout 0, per workgroup in layout 1)
+    const int rw = sh.rw;  // rows per code path (per wave in layouts 0 / 2, per workgroup in layout 1)
     const int npaths = (rows + rw - 1) / rw;
-    const bool share = sh.share && !by_group && npaths > 1;
+    const int G = grouped_share ? sh.groups : npaths;  // row groups (workgroups per chunk group)
+    const int nsh = grouped_share ? nw : npaths;       // waves sharing a step's columns
+    const bool share = sh.share && (!by_group || grouped_share) && nsh > 1;
     const int K = share && sh.kcols > 1 ? sh.kcols : 1;  // own columns per wave and step
     // (dma: each wave's columns stream into a private LDS ring D steps deep
     // through LDS-DMA loads - no VGPRs held by loads in flight)
@@ -496,7 +501,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     L.vgprs = L.acc + 8 * rw;
     const int kVDma = L.vgprs;  // dma: the lane's LDS-DMA offsets, chunk * 2048 + 16 * lane (+ 1024)
     if (D) L.vgprs += 2;
-    const uint32_t raw_base = static_cast<uint32_t>(2 * npaths * 2048);  // dma ring, after the plane buffers
+    const uint32_t raw_base = static_cast<uint32_t>(2 * nsh * K * 2048);  // dma ring, after the plane buffers
     if (vgprs_out) *vgprs_out = L.vgprs;
 
     // mask[c][r][i]: input planes j of column c feeding plane i of row r
@@ -553,19 +558,14 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     P.wait_lgkm0();
     P.label(l_stripe_done);
     P.s_nop(4);  // (v_readfirstlane -> SGPR read hazard margin)
-    if (D) {
-        P.v_op2(kVAnd, kVDma, kLit, kVOff, 0x1f8);        // 8 * lane
-        P.v_op2(kVAdd, kVDma, V(kVOff), kVDma);            // chunk * 2048 + 16 * lane
-        P.v_op2(kVAdd, kVDma + 1, kLit, kVDma, 1024);
-    }
     if (by_group) {
         // Layout 1: workgroup x -> (chunk group cg, row group g) with the row
         // groups of one chunk group on one XCD, back to back in its dispatch
         // order (the hardware hands workgroup x to XCD x % 8):
         //   x = ((cg / 8) * G + g) * 8 + cg % 8
         // so the G workgroups reading the same input lines share that XCD's
-        // L2.  Wave w of the workgroup takes chunk cg * NW + w.
-        const int G = npaths;
+        // L2.  Wave w of the workgroup takes chunk cg * NW + w (layout 2: all
+        // waves take chunk cg, one path each: path g * NW + w).
         P.s_op2(kAnd, kSGrp + 1, kSWgX, C(7));       // cg % 8
         P.s_op2(kLshr, kSTmp, kSWgX, C(3));          // q = x / 8
         if (G > 1 && (G & (G - 1)) == 0) {
@@ -585,7 +585,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         P.s_op2(kOr, kSGrp + 1, kSGrp + 1, kSTmp);   // cg
         // chunk groups past the vector body: nothing to do
         int lg_nw = 0;
-        while ((1 << lg_nw) < nw) ++lg_nw;
+        while (!grouped_share && (1 << lg_nw) < nw) ++lg_nw;
         P.s_op2(kAdd, kSTmp, kSDescIn + 2, kLit, static_cast<uint32_t>((2048u << lg_nw) - 1));
         P.s_op2(kLshr, kSTmp, kSTmp, C(11 + lg_nw));
         const int l_go = P.new_label(".Lgo");
@@ -593,11 +593,25 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         P.branch(kScc0, l_go);  // (.Lidle lies past all the code: out of branch range)
         P.s_endpgm();
         P.label(l_go);
-        // lane offset = ((cg * NW + wave) << 11) + 8 * lane
-        P.s_op2(kLshl, kSTmp, kSGrp + 1, C(lg_nw));
-        P.s_op2(kAdd, kSTmp, kSTmp, kSWave);
-        P.s_op2(kLshl, kSTmp, kSTmp, C(11));
-        P.v_op2(kVAdd, kVOff, kSTmp, kVOff);
+        if (grouped_share) {
+            // lane offset = (cg << 11) + 8 * lane; path = g * NW + wave
+            if (G == 1) P.s_mov_lit(kSGrp, 0, false);
+            P.s_op2(kLshl, kSTmp, kSGrp + 1, C(11));
+            P.v_op2(kVAdd, kVOff, kSTmp, kVOff);
+            P.s_op2(kMul, kSTmp, kSGrp, C(nw));
+            P.s_op2(kAdd, kSGrp, kSTmp, kSWave);
+        } else {
+            // lane offset = ((cg * NW + wave) << 11) + 8 * lane
+            P.s_op2(kLshl, kSTmp, kSGrp + 1, C(lg_nw));
+            P.s_op2(kAdd, kSTmp, kSTmp, kSWave);
+            P.s_op2(kLshl, kSTmp, kSTmp, C(11));
+            P.v_op2(kVAdd, kVOff, kSTmp, kVOff);
+        }
+    }
+    if (D) {
+        P.v_op2(kVAnd, kVDma, kLit, kVOff, 0x1f8);        // 8 * lane
+        P.v_op2(kVAdd, kVDma, V(kVOff), kVDma);            // chunk * 2048 + 16 * lane
+        P.v_op2(kVAdd, kVDma + 1, kLit, kVDma, 1024);
     }
     // path p (layout 0: wave p; layout 1: row group p) -> its rows' code
     // (long jumps: a path's straight-line code can exceed the 16-bit branch
@@ -668,10 +682,11 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         // the same XCD) stay cached for them (measured with nt: 64+64 Encode
         // fetched 1.45x its input bytes from HBM, 128+128 2.8x;
         // profiles/r03/pmc_traffic_*.json)
-        const bool in_nt = npaths == 1 || share;
+        const bool in_nt = npaths == 1 || (share && G == 1) || (share && !grouped_share);
         // the columns this wave loads, in order: all of them, or (share) its
         // own column of each step, w, w + nw, ...
-        const int c_first = share ? w : 0, c_step = share ? npaths : 1;
+        const int wi = grouped_share ? w % nw : w;  // this path's wave in its workgroup
+        const int c_first = share ? wi : 0, c_step = share ? nsh : 1;
         auto issue_col = [&](int c) {  // stage(c) was issued into slot (c / c_step) & 1
             const int k_ = c / c_step;
             desc(k_ & 1, kSDescIn);
@@ -684,7 +699,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         };
         // dma: column c = c_first + k_ * c_step streams into this wave's ring
         // slot k_ % D (2 KiB as two LDS-DMA loads of 1 KiB, lane-linear)
-        auto dma_slot = [&](int k_) { return raw_base + static_cast<uint32_t>(((k_ % std::max(D, 1)) * nw + w) * 2048); };
+        auto dma_slot = [&](int k_) { return raw_base + static_cast<uint32_t>(((k_ % std::max(D, 1)) * nsh + wi) * 2048); };
         auto issue_dma = [&](int c) {  // stage(c) was issued into slot (c / c_step) & 1
             const int k_ = c / c_step;
             desc(k_ & 1, kSDescIn);
@@ -781,12 +796,12 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
             // step s before it passes the barrier of step s + 1.  With K > 1
             // (AsmShape::kcols) a step is K columns per wave (half the barriers),
             // column s * nw * K + q * nw + w being the wave's q-th of the step.
-            const int per = npaths * K;
+            const int per = nsh * K;
             const int steps = (cols + per - 1) / per;
             for (int st = 0; st < steps; ++st) {
                 const uint32_t buf = static_cast<uint32_t>(st & 1) * static_cast<uint32_t>(per) * 2048u;
                 for (int q = 0; q < K; ++q) {
-                    const int c = st * per + q * npaths + w, k_ = st * K + q;
+                    const int c = st * per + q * nsh + wi, k_ = st * K + q;
                     if (c >= cols) break;
                     if (D) {
                         // the column D - 1 steps ahead into the ring slot this
@@ -807,18 +822,18 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                     // LDS address of lane t: 16 t (kVT0 is free between transposes)
                     P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
                     P.v_op2(kVLshl, kVT0, C(1), kVT0);
-                    const uint32_t off = buf + static_cast<uint32_t>(q * npaths + w) * 2048u;
+                    const uint32_t off = buf + static_cast<uint32_t>(q * nsh + wi) * 2048u;
                     P.ds_write4(kVT0, pr[0], off);
                     P.ds_write4(kVT0, pr[4], off + 1024u);
                     P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
-                    if (!D && c + L.pf * npaths < cols) {
-                        issue_col(c + L.pf * npaths);
+                    if (!D && c + L.pf * nsh < cols) {
+                        issue_col(c + L.pf * nsh);
                         // (its scalar loads back before the LDS reads below, so
                         // lgkmcnt counts LDS reads only, in order)
                         if (deep) P.wait_lgkm0();
                     }
                 }
-                if (st * per + w >= cols) {  // no column of this wave in the step: the address still
+                if (st * per + wi >= cols) {  // no column of this wave in the step: the address still
                     P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
                     P.v_op2(kVLshl, kVT0, C(1), kVT0);
                 }

@@ -38,6 +38,12 @@ constexpr int kAsmChunk = 2048;                      // bytes of each vector per
 //     computing one row group [g * rw, g * rw + rw) with the same code; the G
 //     row groups of a chunk group are G workgroups placed on one XCD back to
 //     back (grid x = ceil(chunk groups / 8) * 8 * G), sharing its L2.
+//   layout 2 (with share, more than group_waves paths): a workgroup is nw
+//     waves over the same 2 KiB chunk, each computing its own path
+//     (g * nw + w) and sharing the columns through LDS as below; the G row
+//     groups of a chunk are G workgroups on one XCD back to back, as in
+//     layout 1, so their reads of the chunk's inputs hit that XCD's L2.
+//     Smaller workgroups than layout 0's for > 4 x 16 rows: several per CU.
 //   share (layout 0 with several waves): the waves share the column work
 //     through LDS instead of each loading and transposing every column:
 //     in step s wave w loads and transposes column s * nw + w and writes its
@@ -47,7 +53,7 @@ struct AsmShape {
     int layout = 0;
     int nw = 1;   // waves per workgroup
     int rw = 1;   // rows per code path
-    int groups = 1;  // layout 1: row groups G (= code paths)
+    int groups = 1;  // layouts 1 / 2: row groups G (layout 1: = code paths; layout 2: paths / nw)
     int share = 0;   // layout 0, nw > 1: columns shared through LDS
     int deep = 0;    // share: two steps of loads in flight and the next column's planes read ahead
     int kcols = 1;   // share: columns each wave loads per step (one barrier per nw * kcols columns)
@@ -63,6 +69,28 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
     const int paths = rows <= 16 ? (split_small && rows > 8 ? 2 : 1) : (rows + pr - 1) / pr;
+    if (layout == 2 && share && rows > 16) {
+        // row groups of shared-column workgroups: at most group_waves paths
+        // (waves) per workgroup, G workgroups per chunk, rows spread evenly
+        const int gw = group_waves < 2 ? 2 : group_waves > 8 ? 8 : group_waves;
+        const int G = (paths + gw - 1) / gw;
+        if (G > 1) {
+            s.layout = 2;
+            s.groups = G;
+            s.nw = (paths + G - 1) / G;
+            const int np = G * s.nw;
+            s.rw = (rows + np - 1) / np;
+            if ((np - 1) * s.rw < rows) {  // every path has rows
+                s.share = 1;
+                s.deep = 0;
+                s.kcols = 1;
+                s.dma = dma >= 2 ? (dma > 8 ? 8 : dma) : 0;
+                return s;
+            }
+            s = AsmShape{};
+        }
+        layout = 0;  // one group: layout 0 is the same kernel
+    }
     s.layout = layout == 1 ? 1 : 0;
     s.rw = (rows + paths - 1) / paths;
     // (layout 1: a power of two, the kernel maps chunks with shifts)

@@ -1630,8 +1630,9 @@ hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
                 // groups of nw chunks, G row groups each, in blocks of 8
                 // chunk groups (the kernel maps x back, jit_asm.cpp)
                 const uint64_t chunks = (a.body + kAsmChunk - 1) / kAsmChunk;
-                const uint64_t cgs = (chunks + k.nw - 1) / k.nw;
-                const unsigned gx = static_cast<unsigned>(k.layout == 1 ? (cgs + 7) / 8 * 8 * k.groups : chunks);
+                // (layout 2: chunk groups of one chunk, G row groups each)
+                const uint64_t cgs = k.layout == 2 ? chunks : (chunks + k.nw - 1) / k.nw;
+                const unsigned gx = static_cast<unsigned>(k.layout >= 1 ? (cgs + 7) / 8 * 8 * k.groups : chunks);
                 for (int y0 = 0; y0 < a.nstripes; y0 += 65535) {
                     x.stripe0 = static_cast<uint32_t>(y0);
                     const unsigned gy = static_cast<unsigned>(a.nstripes - y0 < 65535 ? a.nstripes - y0 : 65535);

@@ -292,6 +292,22 @@ def test_wide_asm_jit_shared_dma(rslib, orc, torch_dev, asm_jit, rows, cols, dma
         asm_jit.rs_tune(b"jit_share_dma", 0)
 
 
+@pytest.mark.parametrize("rows,cols,gw,dma", [(128, 128, 4, 0), (100, 28, 4, 0), (64, 64, 2, 0), (56, 200, 2, 0),
+                                              (128, 17, 4, 3), (40, 9, 2, 2)])
+def test_wide_asm_jit_grouped_shared(rslib, orc, torch_dev, asm_jit, rows, cols, gw, dma):
+    """rs_tune("jit_layout", 2): row groups of shared-column workgroups (at
+    most `gw` waves each, G workgroups per chunk, XCD-mapped), with and
+    without the LDS-DMA rings, against the oracle on the GPU."""
+    assert asm_jit.rs_tune(b"jit_layout", 2) == 0 and asm_jit.rs_tune(b"jit_group_waves", gw) == 0
+    assert asm_jit.rs_tune(b"jit_share_dma", dma) == 0
+    try:
+        test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
+    finally:
+        asm_jit.rs_tune(b"jit_layout", 0)
+        asm_jit.rs_tune(b"jit_group_waves", 4)
+        asm_jit.rs_tune(b"jit_share_dma", 0)
+
+
 @pytest.mark.parametrize("d,p,S", [(64, 64, 4), (128, 128, 2), (200, 56, 2)])
 def test_wide_full_size_round_trip(rslib, orc, torch_dev, asm_jit, d, p, S):
     """Full-size wide stripes (1 MiB vectors) through the compiled shared-column

@@ -63,7 +63,7 @@ def test_asm_kernel_row_group_layout(rslib, orc, rows, cols, acc, gw):
         L.rs_tune(b"jit_group_waves", 4)
 
 
-def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4, paths=None, edit=None):
+def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4, paths=None, edit=None, groups=1):
     rng = np.random.default_rng(rows * 1000 + cols * 10 + acc)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
     src = rslib.jit_asm_source(mat, bool(acc))
@@ -90,6 +90,9 @@ def _check_kernel(rslib, orc, rows, cols, acc, layout=0, gw=4, paths=None, edit=
     if layout == 1:  # the library's launch rule (kernels.hip): ceil(chunk groups / 8) * 8 * row groups
         nw, cgs = gw, (body // 2048 + gw - 1) // gw
         grid = ((cgs + 7) // 8 * 8 * paths, S)
+    elif layout == 2:  # chunk groups of one chunk, `groups` row groups of gw waves each
+        nw, cgs = gw, body // 2048
+        grid = ((cgs + 7) // 8 * 8 * groups, S)
     else:
         nw, grid = paths, (body // 2048, S)
     emu = Emu(mem)
@@ -294,5 +297,55 @@ def test_machine_code_equals_assembler_dma(rslib, rows, cols, acc, dma):
     try:
         n = rslib.jit_encoder_check(mat, bool(acc))
     finally:
+        L.rs_tune(b"jit_share_dma", 0)
+    assert n > 0 and n % 4 == 0
+
+
+def _layout2_shape(rows, gw):
+    """asm_shape(rows, layout 2, gw) (jit_asm.hpp): (row groups, waves per workgroup, rows per path)."""
+    paths = (rows + 15) // 16
+    G = (paths + gw - 1) // gw
+    nw = (paths + G - 1) // G
+    rw = (rows + G * nw - 1) // (G * nw)
+    return G, nw, rw
+
+
+@pytest.mark.parametrize("rows,cols,acc,gw,dma", [(128, 9, 0, 4, 0), (100, 7, 1, 4, 0), (65, 5, 1, 2, 0),
+                                                  (40, 13, 0, 2, 0), (128, 9, 1, 4, 3), (72, 11, 0, 2, 2)])
+def test_asm_kernel_grouped_shared_layout(rslib, orc, rows, cols, acc, gw, dma):
+    """rs_tune("jit_layout", 2): row groups of shared-column workgroups - a
+    workgroup is at most jit_group_waves waves over one 2 KiB chunk, each with
+    its own path (g * nw + w) of the rows, sharing the columns through LDS;
+    the G row groups of a chunk are G workgroups mapped XCD-aware as in
+    layout 1 (grid ceil(chunks / 8) * 8 * G).  Against the oracle in the
+    emulator with the LDS race and DMA wait checks; rows spread evenly over
+    the paths (100 rows: 8 paths of 13)."""
+    L = rslib.lib()
+    G, nw, rw = _layout2_shape(rows, gw)
+    assert G > 1 and (G * nw - 1) * rw < rows
+    assert L.rs_tune(b"jit_layout", 2) == 0 and L.rs_tune(b"jit_group_waves", gw) == 0
+    assert L.rs_tune(b"jit_share_dma", dma) == 0
+    try:
+        src = _check_kernel(rslib, orc, rows, cols, acc, layout=2, gw=nw, groups=G)
+    finally:
+        L.rs_tune(b"jit_layout", 0)
+        L.rs_tune(b"jit_group_waves", 4)
+        L.rs_tune(b"jit_share_dma", 0)
+    steps = (cols + nw - 1) // nw
+    assert src.count("s_barrier") == G * nw * steps  # every path's code has one barrier per step
+    assert f".amdhsa_group_segment_fixed_size {(2 + dma) * nw * 2048}" in src
+
+
+@pytest.mark.parametrize("rows,cols,acc,dma", [(128, 128, 0, 0), (128, 64, 1, 3), (100, 28, 0, 0)])
+def test_machine_code_equals_assembler_grouped(rslib, rows, cols, acc, dma):
+    """Layout 2's machine code (path dispatch on g * nw + w) equals comgr's
+    assembly of its text."""
+    L = rslib.lib()
+    mat = np.random.default_rng(rows * 43 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
+    assert L.rs_tune(b"jit_layout", 2) == 0 and L.rs_tune(b"jit_share_dma", dma) == 0
+    try:
+        n = rslib.jit_encoder_check(mat, bool(acc))
+    finally:
+        L.rs_tune(b"jit_layout", 0)
         L.rs_tune(b"jit_share_dma", 0)
     assert n > 0 and n % 4 == 0
