@@ -525,13 +525,14 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * workgroup meet at a barrier every n columns, 0 = never; default 0),
  * "jit_waves" (assembly kernels hold at most n waves per SIMD, 2..8, by
  * declaring more registers; 0 = as many as fit; default 2),
- * "jit_layout" (generated kernels of more than 16 rows: 0 default = the
+ * "jit_layout" (generated kernels of more than 16 rows: 0 = the
  * rows over the waves of a workgroup, all on the same 2 KiB chunk | 1 = row
  * groups of up to 16 rows over workgroups whose waves take consecutive
  * chunks with the same code, the row groups of a chunk on one XCD | 2 =
  * with shared columns and more paths than jit_group_waves: workgroups of at
  * most jit_group_waves waves, one path each, over one chunk, sharing its
- * columns through LDS, G such workgroups per chunk on one XCD),
+ * columns through LDS, G such workgroups per chunk on one XCD; layout 0 up
+ * to jit_group_waves paths; the default),
  * "jit_group_waves" (layout 1: waves per workgroup, 1, 2, 4 or 8 - other
  * values round down; layout 2: at most this many waves per workgroup,
  * 2..8; default 4),

@@ -89,11 +89,15 @@ int g_jit_waves = [] {
 }();
 // rs_tune("jit_layout", 0 | 1) / ("jit_group_waves", 1..8): how generated
 // kernels of more than 16 rows split their work (AsmShape, jit_asm.hpp):
-// rows over the waves of a workgroup (0) or row groups over workgroups whose
-// waves take consecutive chunks with the same code (1, group_waves waves)
+// rows over the waves of a workgroup (0), row groups over workgroups whose
+// waves take consecutive chunks with the same code (1, group_waves waves), or
+// (2, the default) as 0 up to group_waves paths and beyond that row groups of
+// shared-column workgroups of at most group_waves waves, several per CU:
+// 128+128 Encode 1.94 -> 2.00 TB/s; 2-wave groups were slower on 64+64 /
+// 200+56 (profiles/r05/ab_layout2_*.log)
 int g_jit_layout = [] {
     const char* e = std::getenv("RSAMD_JIT_LAYOUT");
-    const int v = e ? std::atoi(e) : 0;
+    const int v = e ? std::atoi(e) : 2;
     return v == 1 || v == 2 ? v : 0;
 }();
 int g_jit_group_waves = 4;

@@ -66,7 +66,7 @@ SWEEP = {
     "jit_waves": [0, 4, 2],
     "jit_disk_cache": [0, 1],
     "jit_backend": [0, 1, 2],
-    "jit_layout": [1, 2, 0],
+    "jit_layout": [1, 0, 2],
     "jit_group_waves": [2, 8, 4],
     "jit_path_rows": [5, 11, 16],
     "jit_wide_pf": [1, 3, 2],

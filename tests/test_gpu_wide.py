@@ -303,7 +303,7 @@ def test_wide_asm_jit_grouped_shared(rslib, orc, torch_dev, asm_jit, rows, cols,
     try:
         test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
     finally:
-        asm_jit.rs_tune(b"jit_layout", 0)
+        asm_jit.rs_tune(b"jit_layout", 2)
         asm_jit.rs_tune(b"jit_group_waves", 4)
         asm_jit.rs_tune(b"jit_share_dma", 0)
 

@@ -16,6 +16,17 @@ from asm_emu import Emu, Memory
 KMAXPTRS = 260
 
 
+@pytest.fixture(autouse=True)
+def _layout0_unless_set(rslib):
+    """These tests describe the kernels by layout 0's shape (nw = paths per
+    workgroup, one workgroup per chunk) unless they pick a layout themselves;
+    the library's default (2) is layout 0 up to jit_group_waves paths."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_layout", 0) == 0
+    yield
+    L.rs_tune(b"jit_layout", 2)
+
+
 def _karg(body, stripe0, stripe_ids, ptrs, strides16):
     b = struct.pack("<IIQ", body, stripe0, stripe_ids)
     p = list(ptrs) + [0] * (KMAXPTRS - len(ptrs))
