@@ -528,6 +528,8 @@ static bool engine_cold(const rs_t* rs) {
 
 bool engine_cold_now(rs_t* rs) {
     if (!g_engine_cold_launch || !g_engine) return false;
+    // (a busy handle answers without the lock: its last call is recent)
+    if (now_ns() - rs->eng_last_ns.load(std::memory_order_relaxed) < int64_t{1000} * g_engine_idle_us) return false;
     std::lock_guard<std::mutex> lk(rs->eng_mu);
     int waves, gwaves;
     engine_shape(&waves, &gwaves);
