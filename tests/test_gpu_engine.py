@@ -22,9 +22,13 @@ def torch_dev():
 
 @pytest.fixture
 def engine(rslib):
-    """Engine on with default settings; restored afterwards."""
+    """Engine on with default settings, except that a call after a quiet
+    period waits for the relaunch instead of taking the launch path (these
+    tests count engine calls; test_engine_idle_relaunch and
+    test_engine_cold_launch_concurrent cover that path); restored afterwards."""
     L = rslib.lib()
     assert L.rs_tune(b"host_engine", 1) == 0
+    assert L.rs_tune(b"host_engine_cold_launch", 0) == 0
     yield L
     L.rs_tune(b"host_engine", 1)
     L.rs_tune(b"host_engine_waves", 8)
@@ -502,3 +506,56 @@ def test_engine_drain_before_stop(rslib, orc, torch_dev, engine):
     assert not errors, errors[:5]
     calls, launches = r.host_engine_stats()
     assert calls >= 6 * 60 and launches > 2, (calls, launches)
+
+
+def test_engine_cold_launch_concurrent(rslib, orc, torch_dev, engine):
+    """The default cold path under concurrency: 8 threads call Encode /
+    Update on one handle with random pauses, some longer than the engine's
+    idle window, so calls after a quiet period take the launch path while the
+    engine restarts behind them and the others ride the engine; every result
+    against the oracle, and both paths were taken."""
+    assert engine.rs_tune(b"host_engine_cold_launch", 1) == 0
+    assert engine.rs_tune(b"host_engine_idle_us", 300) == 0
+    d, p, size = 10, 4, 8192
+    r = rslib.New(d, p)
+    errors = []
+    per = 25
+    sync = threading.Barrier(8, timeout=60)
+
+    def worker(tid):
+        rng = np.random.default_rng(700 + tid)
+        try:
+            for it in range(per):
+                if it % 5 == 0:  # every thread quiet at once for > the idle window, then all call
+                    sync.wait()
+                    time.sleep(0.002)
+                data = [_rand(rng, size) for _ in range(d)]
+                v = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                r.Encode(v)
+                exp = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, exp) == 0
+                if any(not np.array_equal(v[j], exp[j]) for j in range(d, d + p)):
+                    errors.append((tid, it, "encode"))
+                row = it % d
+                new = _rand(rng, size)
+                par = [x.copy() for x in v[d:]]
+                r.Update(v[row], new, row, par)
+                data[row] = new
+                exp2 = [x.copy() for x in data] + [np.zeros(size, np.uint8) for _ in range(p)]
+                assert orc.encode(d, p, exp2) == 0
+                if any(not np.array_equal(par[j], exp2[d + j]) for j in range(p)):
+                    errors.append((tid, it, "update"))
+        except Exception as e:  # noqa: BLE001
+            errors.append((tid, repr(e)))
+            sync.abort()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th)
+    assert not errors, errors[:5]
+    calls, launches = r.host_engine_stats()
+    assert 0 < calls < 8 * per * 2, (calls, launches)  # some calls rode the engine, some the launch path
+    assert launches >= 2, (calls, launches)

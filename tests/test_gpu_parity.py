@@ -619,6 +619,9 @@ def test_coalesced_host_calls(rslib, orc, torch_dev, direct):
             errors.append(repr(e))
 
     ts = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    # (a call after a quiet period would take the launch path, i.e. the
+    # coalescer this test counts: keep every call on its path)
+    assert L.rs_tune(b"host_engine_cold_launch", 0) == 0
     try:
         for t in ts:
             t.start()
@@ -627,6 +630,7 @@ def test_coalesced_host_calls(rslib, orc, torch_dev, direct):
     finally:
         assert L.rs_tune(b"host_coalesce_linger_us", 0) == 0
         assert L.rs_tune(b"host_engine_direct", 1) == 0
+        assert L.rs_tune(b"host_engine_cold_launch", 1) == 0
     assert not errors, errors[:10]
     launches, calls = r.host_call_stats()
     if direct:
