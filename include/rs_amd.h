@@ -493,7 +493,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * default 2000), "host_engine_cold_launch" (1 default: a call that finds the
  * engine gone, with no call pending, takes the launch path and the engine is
  * relaunched while that call's kernel runs | 0: the call waits for the
- * relaunch), "host_engine_life_us" (the engine also leaves once it has run
+ * relaunch), "host_flag_sync" (1 default: a host call served by a kernel
+ * launch waits for it through a pinned flag the stream writes after the
+ * kernel | 0: hipStreamSynchronize), "host_engine_life_us" (the engine also leaves once it has run
  * this long, even while calls keep coming: a device-wide synchronisation waits at most about
  * this long for it; default 4000), "host_engine_max_bytes" (larger batches
  * launch; default 1 MiB), "host_engine_vram" (1: the engine's call slots and

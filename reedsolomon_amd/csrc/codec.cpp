@@ -698,6 +698,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_engine_vram") g_engine_vram = value ? 1 : 0;
         else if (n == "host_engine_split_rows") g_engine_split_rows = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (n == "host_engine_cold_launch") g_engine_cold_launch = value ? 1 : 0;
+        else if (n == "host_flag_sync") g_host_flag_sync = value ? 1 : 0;
         else if (n == "host_engine_life_us") g_engine_life_us = value < 100 ? 100 : value > 1000000 ? 1000000 : value;
         else if (n == "host_engine_max_bytes") g_engine_max_bytes = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);

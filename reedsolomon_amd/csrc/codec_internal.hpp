@@ -171,6 +171,17 @@ struct rs_codec {
     hipEvent_t dma_ev[3][8] = {};
     hipStream_t co_stream = nullptr;
 
+    // Completion flags of the launch-path host calls (flag_sync,
+    // host_calls.cpp): pinned words the stream writes after the call's
+    // kernel, one per stream (stream under stage_mu, co_stream under
+    // co_launch_mu).
+    struct DoneFlag {
+        uint32_t* host = nullptr;
+        void* dev = nullptr;
+        uint32_t seq = 0;
+    };
+    DoneFlag stream_flag, co_flag;
+
     // Upload ring for per-call device descriptors (multi-pattern Reconst):
     // pinned host slot -> device slot on a private copy stream, so the copy
     // for call n+1 overlaps call n's kernel instead of stalling the stream.
@@ -250,7 +261,10 @@ void engine_shutdown(rs_t* rs);
 // After a call that the engine declined because it was cold (idle exit) has
 // enqueued its kernel on the launch path: relaunch the engine now, while that
 // kernel runs, so the next call finds it (no-op unless a call declined).
-void engine_warm(rs_t* rs);
+void engine_warm(rs_t* rs, bool wait_lock = false);
+// The same on the library's warmer thread: the caller only queues the request
+// (a cold call's latency stays the launch path's).
+void engine_warm_async(rs_t* rs);
 // Would an engine call now be declined as cold (see engine_warm)?  Lets a
 // caller skip staging meant for the engine.
 bool engine_cold_now(rs_t* rs);
@@ -337,6 +351,8 @@ inline void rs_codec::release_device() {
         for (hipStream_t s : dma_stream)
             if (s) (void)hipStreamDestroy(s);
         if (co_stream) (void)hipStreamDestroy(co_stream);
+        for (DoneFlag* f : {&stream_flag, &co_flag})
+            if (f->host) (void)hipHostFree(f->host);
         for (hipEvent_t e : chunk_ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -537,6 +553,9 @@ int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t
 // of the same shape (takes stage_mu itself).
 int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
               size_t size, bool accumulate);
+// Wait for everything queued on `st` so far (see host_calls.cpp).
+int flag_sync(hipStream_t st, rs_codec::DoneFlag& f, const char* where);
+extern int g_host_flag_sync;
 
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
 extern int g_host_batch_zc, g_host_dma_1d, g_bind_numa, g_host_pageable_stage;

@@ -36,6 +36,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <map>
+#include <condition_variable>
+#include <deque>
 #include <thread>
 
 #include <hip/hip_ext.h>
@@ -299,7 +301,78 @@ void engine_stop(rs_t* rs) {
     active_set(rs, false);
 }
 
+// ---- the warmer: relaunches engines that a cold call declined, off the
+// caller's thread (engine_warm_async).  One thread per process, started at
+// the first request and joined by an exit handler registered then (after the
+// HIP runtime was loaded, so it runs before the runtime's own teardown).
+namespace {
+struct Warmer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<rs_t*> q;
+    rs_t* cur = nullptr;  // the handle being warmed (engine_shutdown waits for it)
+    bool stop = false;
+    std::thread th;
+    pid_t owner = 0;
+};
+Warmer& warmer() {
+    static Warmer* w = new Warmer;  // never destroyed (see jit.cpp's Jit)
+    return *w;
+}
+void warmer_atexit() {
+    Warmer& w = warmer();
+    {
+        std::lock_guard<std::mutex> lk(w.mu);
+        if (!w.th.joinable() || w.owner != getpid()) return;
+        w.stop = true;
+    }
+    w.cv.notify_all();
+    w.th.join();
+}
+void warmer_loop() {
+    Warmer& w = warmer();
+    std::unique_lock<std::mutex> lk(w.mu);
+    for (;;) {
+        w.cv.wait(lk, [&] { return w.stop || !w.q.empty(); });
+        if (w.stop) return;
+        rs_t* rs = w.q.front();
+        w.q.pop_front();
+        w.cur = rs;
+        lk.unlock();
+        {
+            DeviceGuard g(rs->device);
+            engine_warm(rs, true);
+        }
+        lk.lock();
+        w.cur = nullptr;
+        w.cv.notify_all();
+    }
+}
+}  // namespace
+
+void engine_warm_async(rs_t* rs) {
+    if (!rs->eng_warm_wanted.load(std::memory_order_acquire)) return;
+    Warmer& w = warmer();
+    std::lock_guard<std::mutex> lk(w.mu);
+    if (w.stop) return;
+    if (w.cur != rs && std::find(w.q.begin(), w.q.end(), rs) == w.q.end()) w.q.push_back(rs);
+    if (!w.th.joinable() || w.owner != getpid()) {
+        if (w.th.joinable()) w.th.detach();  // (a forked child starts its own)
+        static const bool registered = std::atexit(warmer_atexit) == 0;
+        (void)registered;
+        w.owner = getpid();
+        w.th = std::thread(warmer_loop);
+    }
+    w.cv.notify_one();
+}
+
 void engine_shutdown(rs_t* rs) {
+    {  // no warm of this handle queued or running past this point
+        Warmer& w = warmer();
+        std::unique_lock<std::mutex> wl(w.mu);
+        w.q.erase(std::remove(w.q.begin(), w.q.end(), rs), w.q.end());
+        w.cv.wait(wl, [&] { return w.cur != rs; });
+    }
     std::lock_guard<std::mutex> lk(rs->eng_mu);
     if (!rs->eng_ring) return;
     DeviceGuard g(rs->device);
@@ -536,10 +609,11 @@ bool engine_cold_now(rs_t* rs) {
     return !rs->eng_failed && rs->eng_ring && !engine_reshape(rs, waves, gwaves) && engine_cold(rs);
 }
 
-void engine_warm(rs_t* rs) {
+void engine_warm(rs_t* rs, bool wait_lock) {
     if (!rs->eng_warm_wanted.load(std::memory_order_acquire)) return;
-    std::unique_lock<std::mutex> lk(rs->eng_mu, std::try_to_lock);
-    if (!lk.owns_lock()) return;  // a call holds it: that call (re)launches the engine itself
+    std::unique_lock<std::mutex> lk(rs->eng_mu, std::defer_lock);
+    if (wait_lock) lk.lock();
+    else if (!lk.try_lock()) return;  // a call holds it: that call (re)launches the engine itself
     if (!rs->eng_warm_wanted.exchange(false, std::memory_order_acq_rel)) return;
     if (rs->eng_failed || !rs->eng_ring) return;
     Region region("engine warm (relaunch behind a launch-path call)");

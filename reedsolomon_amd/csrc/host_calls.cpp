@@ -10,6 +10,8 @@
 #include "host_pool.hpp"
 #include "codec_internal.hpp"
 
+#include <immintrin.h>
+
 using namespace rsamd;
 using namespace rsamd::detail;
 
@@ -86,6 +88,46 @@ int d2h(rs_t* rs, uint8_t* dst, const uint8_t* src, size_t n) {
 }
 int sync(rs_t* rs) {
     return hip_ok(hipStreamSynchronize(rs->stream), "host-call stream sync");
+}
+
+// A launch-path host call waits for its kernel through a flag instead of
+// hipStreamSynchronize: the stream writes a sequence number into a pinned
+// word after the kernel (hipStreamWriteValue32, ordered behind it, so the
+// kernel's stores to host memory are complete) and the caller spins on the
+// word.  A launch + stream sync has a ~12 us floor on MI355X against ~6 us for
+// a launch + host flag (profiles/r02/doorbell_probe.log).  Falls back to the
+// stream sync when the write cannot be queued, or after 10 s without the
+// flag.  rs_tune("host_flag_sync", 1 default | 0).
+int g_host_flag_sync = 1;
+
+int flag_sync(hipStream_t st, rs_codec::DoneFlag& f, const char* where) {
+    if (g_host_flag_sync && !f.host) {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) == hipSuccess) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d) {
+                f.host = static_cast<uint32_t*>(h);
+                f.dev = d;
+                __atomic_store_n(f.host, f.seq, __ATOMIC_RELEASE);
+            } else {
+                (void)hipHostFree(h);
+            }
+        }
+        (void)hipGetLastError();
+    }
+    if (!g_host_flag_sync || !f.host) return hip_ok(hipStreamSynchronize(st), where);
+    const uint32_t v = ++f.seq;
+    if (hipStreamWriteValue32(st, f.dev, v, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return hip_ok(hipStreamSynchronize(st), where);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 1; __atomic_load_n(f.host, __ATOMIC_ACQUIRE) != v; ++spins) {
+        _mm_pause();
+        if ((spins & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+            return hip_ok(hipStreamSynchronize(st), where);
+    }
+    return RS_OK;
 }
 
 // Pageable vectors never go to the runtime's pageable copies (which pin the
@@ -423,9 +465,9 @@ static int run_batch(rs_t* rs, const CoBatch& b, int n) {
     std::lock_guard<std::mutex> lk(rs->co_launch_mu);
     const int rc = matmul(rs, b.mat.data(), b.rows, b.cols, in, static_cast<int64_t>(b.stride), out,
                           static_cast<int64_t>(b.stride), n, b.size, b.accumulate, rs->co_stream);
-    engine_warm(rs);  // (a cold engine declined this batch: it restarts while the kernel runs)
-    const hipError_t e = hipStreamSynchronize(rs->co_stream);  // never leave a kernel on the buffer
-    return rc ? rc : (e == hipSuccess ? RS_OK : dev_fail(e, "coalesced batch sync"));
+    engine_warm_async(rs);  // (a cold engine declined this batch: it restarts behind it, on the warmer thread)
+    const int src = flag_sync(rs->co_stream, rs->co_flag, "coalesced batch sync");  // never leave a kernel on the buffer
+    return rc ? rc : src;
 }
 
 // Wait for the next batch state change: spin briefly on co_gen (a futex
@@ -484,8 +526,8 @@ int host_call(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
                 RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
             if (rs->zc_pending) RS_TRY(sync(rs));
             const int rc = matmul(rs, mat, rows, cols, in, 0, out, 0, 1, size, accumulate, rs->stream);
-            engine_warm(rs);  // (a cold engine declined this call: it restarts while the kernel runs)
-            const int src_rc = sync(rs);
+            engine_warm_async(rs);  // (a cold engine declined this call: it restarts behind it, on the warmer thread)
+            const int src_rc = flag_sync(rs->stream, rs->stream_flag, "host-call stream sync");
             return rc ? rc : src_rc;
         }
     }

@@ -45,6 +45,7 @@ SWEEP = {
     "host_engine_vram": [0, 1],
     "host_engine_split_rows": [1, 0, 2],
     "host_engine_cold_launch": [0, 1],
+    "host_flag_sync": [0, 1],
     "host_engine_max_bytes": [0, 1 << 20],
     "host_pinned_max": [0, 4 << 20, 256 << 10],
     "host_zc_max": [0, 2 << 20, -1],
