@@ -365,6 +365,12 @@ def prewarm(step, stream, min_launches: int, max_launches: int, window: int = 20
             a, b = evs[done - 1]
             b.synchronize()
             durs.append(a.elapsed_time(b))
+            # release the pair now: destroying ~4,000 events at once when the
+            # list dies took longer than the 4 queued launches (a 1.6 ms idle
+            # gap before the warm-up, whose power transient then landed on the
+            # timed region; profiles/r05/driver_cmd)
+            evs[done - 1] = None
+            del a, b
             if len(durs) >= max(min_launches, 2 * window) and len(durs) % 2 == 0:
                 last, prev = durs[-window:], durs[-2 * window:-window]
                 m1, m0 = sum(last) / window, sum(prev) / window

@@ -552,6 +552,12 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * registers one step ahead | n = 2..8: each wave's columns stream into a
  * private LDS ring of n steps through LDS-DMA loads, n - 1 steps ahead, with
  * no load registers),
+ * "jit_share_ahead" (shared columns: 1 = the next column's planes are read
+ * from LDS while the current one combines, 8 more VGPRs; 0 default),
+ * "jit_gray" (1 = the low half's subsets are built one at a time in
+ * Gray-code order, 12 subset VGPRs instead of 22; 0 default; with
+ * jit_share_ahead the 16-row paths keep 3 waves per SIMD; both measured
+ * within -1..+1 %),
  * "jit_split_cols" (n > 0: products of 9-16 rows over at least n columns run
  * as two 8-row paths sharing the columns; 0 default: one path; measured
  * within -4..+4 %),

@@ -657,6 +657,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "nt_store") t.nt_store = value;
 #ifdef RSAMD_EXPERIMENTS  // code-shape experiments: librsamd_exp.so only (the product has no "var")
         else if (n == "var") t.var = value;
+        else if (n == "jit_nobar") g_jit_nobar = value ? 1 : 0;  // timing diagnostic, wrong results
 #endif
         else if (n == "lds_pad") t.lds_pad = value;
         else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;
@@ -677,6 +678,8 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_share") g_jit_share = value ? 1 : 0;
         else if (n == "jit_share_deep") g_jit_share_deep = value < 0 ? -1 : value ? 1 : 0;
         else if (n == "jit_share_dma") g_jit_share_dma = value < 2 ? 0 : value > 8 ? 8 : value;
+        else if (n == "jit_share_ahead") g_jit_share_ahead = value ? 1 : 0;
+        else if (n == "jit_gray") g_jit_gray = value ? 1 : 0;
         else if (n == "jit_split_cols") g_jit_split_cols = value < 0 ? 0 : value;
         else if (n == "jit_share_cols") g_jit_share_cols = value < 0 ? -1 : value > 2 ? 2 : value < 1 ? 1 : value;
         else if (n == "jit_wide_pf") g_jit_wide_pf = value < 1 ? 1 : value > 4 ? 4 : value;

@@ -128,9 +128,21 @@ int g_jit_share_cols = 1;
 // columns into an LDS ring of n steps by LDS-DMA loads (n - 1 steps ahead, no
 // load registers) instead of one step ahead through VGPRs; 0 = off
 int g_jit_share_dma = 0;
+// rs_tune("jit_share_ahead", 0 | 1): shared-column kernels read the next
+// column's planes from LDS while the current one combines (8 more VGPRs)
+int g_jit_share_ahead = 0;
+// rs_tune("jit_gray", 0 | 1): generated kernels build the low half's subsets
+// one at a time in Gray-code order (12 subset registers instead of 22)
+int g_jit_gray = 0;
+// rs_tune("jit_nobar", 1), experiments build only: a timing diagnostic that
+// drops the shared-column barriers (the results are wrong)
+int g_jit_nobar = 0;
 AsmShape jit_shape(int rows, int cols) {
-    return asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep,
-                     jit_split_small(rows, cols) ? 1 : 0, g_jit_share_cols, g_jit_share_dma);
+    AsmShape s = asm_shape(rows, g_jit_layout, g_jit_group_waves, g_jit_path_rows, g_jit_share, g_jit_share_deep,
+                           jit_split_small(rows, cols) ? 1 : 0, g_jit_share_cols, g_jit_share_dma, g_jit_share_ahead,
+                           g_jit_gray);
+    s.nobar = g_jit_nobar;
+    return s;
 }
 int g_jit_pf = 3;  // rs_tune("jit_pf", 1..6): columns whose loads are in flight ahead of the one combined
 // Generated kernels of more than 16 rows (several code paths): two columns of
@@ -911,6 +923,9 @@ static DiskKey disk_key(const std::string& arch, const MatmulArgs& a) {
     k.text += static_cast<char>(g_jit_backend ? g_jit_share_dma : 0);
     k.text += static_cast<char>(g_jit_backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
     k.text += static_cast<char>(g_jit_backend ? g_jit_share_cols : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_share_ahead : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_gray : 0);
+    k.text += static_cast<char>(g_jit_backend ? g_jit_nobar : 0);
     k.text.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     k.h1 = fnv1a(k.text.data(), k.text.size(), 0xcbf29ce484222325ull);
     k.h2 = hash2(k.text);
@@ -949,6 +964,9 @@ static JitKernel lookup(const MatmulArgs& a, int bs, uint64_t launch_bytes, int 
     key += static_cast<char>(backend ? g_jit_share_dma : 0);
     key += static_cast<char>(backend && jit_split_small(a.rows, a.cols) ? 1 : 0);
     key += static_cast<char>(backend ? g_jit_share_cols : 0);
+    key += static_cast<char>(backend ? g_jit_share_ahead : 0);
+    key += static_cast<char>(backend ? g_jit_gray : 0);
+    key += static_cast<char>(backend ? g_jit_nobar : 0);
     key.append(reinterpret_cast<const char*>(a.host_mat), static_cast<size_t>(a.rows) * a.cols);
     {
         auto it = j.entries.find(key);

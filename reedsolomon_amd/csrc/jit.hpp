@@ -44,6 +44,9 @@ extern int g_jit_share_deep;    // rs_tune("jit_share_deep")
 extern int g_jit_split_cols;    // rs_tune("jit_split_cols")
 extern int g_jit_share_cols;    // rs_tune("jit_share_cols")
 extern int g_jit_share_dma;     // rs_tune("jit_share_dma")
+extern int g_jit_share_ahead;   // rs_tune("jit_share_ahead")
+extern int g_jit_gray;          // rs_tune("jit_gray")
+extern int g_jit_nobar;         // rs_tune("jit_nobar"), experiments build only
 extern int g_jit_wide_pf, g_jit_wide_waves;  // rs_tune("jit_wide_pf" / "jit_wide_waves"): kernels of > 16 rows
 extern int g_jit_sync;
 extern int g_jit_waves;

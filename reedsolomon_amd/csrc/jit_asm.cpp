@@ -487,6 +487,10 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     // through LDS-DMA loads - no VGPRs held by loads in flight)
     const int D = share && K == 1 && sh.dma >= 2 ? sh.dma : 0;
     const bool deep = share && sh.deep && K == 1 && !D;
+    // (ahead: the next column's planes are read from LDS while this one
+    // combines - deep does that too, with a second step of loads)
+    const bool ahead = share && K == 1 && (deep || sh.ahead);
+    const bool gray = sh.gray != 0;
     Layout L;
     // (share: one column of loads in flight per wave, i.e. nw columns of the
     // workgroup - two with deep; the planes read back from LDS get registers
@@ -495,9 +499,12 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
     L.pf = share ? (D ? 0 : deep ? 2 : K) : pf < 1 ? 1 : pf > 4 ? 4 : pf;
     L.slots_end = kVSlots + 8 * L.pf;
     const int kVPlanes = L.slots_end;
-    L.sub = L.slots_end + (share ? (deep ? 16 : 8) : 0);  // 2 x 11 subset registers: the XORs of 2-4 planes of each half
-    L.acc = L.sub + 22;
-    const int kVT1 = L.sub + 21;  // (see kVT0)
+    // subset registers: the XORs of 2-4 planes of each half, 2 x 11; gray:
+    // the high half's 11 and one for the low half's subset of the moment
+    const int nsub = gray ? 12 : 22;
+    L.sub = L.slots_end + (share ? (ahead ? 16 : 8) : 0);
+    L.acc = L.sub + nsub;
+    const int kVT1 = L.sub + nsub - 1;  // (see kVT0)
     L.vgprs = L.acc + 8 * rw;
     const int kVDma = L.vgprs;  // dma: the lane's LDS-DMA offsets, chunk * 2048 + 16 * lane (+ 1024)
     if (D) L.vgprs += 2;
@@ -724,14 +731,27 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
         // single planes stay where the transpose left them)
         auto sub_reg = [&](int half, int m) {
             static const int8_t kIdx[16] = {-1, -1, -1, 0, -1, 1, 2, 3, -1, 4, 5, 6, 7, 8, 9, 10};
-            return L.sub + half * 11 + kIdx[m];
+            return L.sub + (gray ? 0 : half * 11) + kIdx[m];
         };
         auto acc_reg = [&](int r, int i) { return L.acc + 8 * r + i; };
+        // output plane (r, i) ^= the column's terms t[0..nt) (the first column sets it)
+        auto update = [&](int c, int r, int i, const int* t, int nt) {
+            const int a = acc_reg(r - r0, i);
+            if (c == 0) {
+                if (nt == 0) P.v_mov(a, C(0));
+                else if (nt == 1) P.v_mov(a, V(t[0]));
+                else P.v_op2(kVXor, a, V(t[0]), t[1]);
+            } else if (nt == 2) {
+                P.v_xor3(a, a, t[0], t[1]);
+            } else if (nt == 1) {
+                P.v_op2(kVXor, a, V(a), t[0]);
+            }
+        };
         // column c's planes in pr[]: its subsets of each half that this
         // path's rows use, then one xor3 per output plane and row
         auto combine = [&](int c, const int (&pr)[8]) {
             int reg[2][16];
-            for (int half = 0; half < 2; ++half) {
+            for (int half = gray ? 1 : 0; half < 2; ++half) {
                 bool have[16] = {}, used[16] = {}, need[16] = {};
                 for (int b = 0; b < 4; ++b) {
                     have[1 << b] = true;
@@ -754,24 +774,65 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                         have[m] = true;
                     }
             }
+            if (!gray) {
+                for (int r = r0; r < r0 + nr; ++r)
+                    for (int i = 0; i < 8; ++i) {
+                        const int m = mask[(static_cast<size_t>(c) * rows + r) * 8 + i];
+                        int t[2];
+                        int nt = 0;
+                        if (m & 15) t[nt++] = reg[0][m & 15];
+                        if (m >> 4) t[nt++] = reg[1][m >> 4];
+                        update(c, r, i, t, nt);
+                    }
+                return;
+            }
+            // gray: the outputs grouped by their low-half subset; the subsets
+            // visited in Gray-code order, each built in register tl with one
+            // XOR / xor3 from the one before or from the planes (single planes
+            // are used where they are), its outputs updated right after
+            std::vector<std::pair<int, int>> by_lo[16];
             for (int r = r0; r < r0 + nr; ++r)
-                for (int i = 0; i < 8; ++i) {
-                    const int m = mask[(static_cast<size_t>(c) * rows + r) * 8 + i];
+                for (int i = 0; i < 8; ++i)
+                    by_lo[mask[(static_cast<size_t>(c) * rows + r) * 8 + i] & 15].emplace_back(r, i);
+            const int tl = L.sub + 11;
+            static const int kGray[15] = {1, 3, 2, 6, 7, 5, 4, 12, 13, 15, 14, 10, 11, 9, 8};
+            int cur = 0;  // the subset tl holds (0: none)
+            for (int gi = -1; gi < 15; ++gi) {
+                const int a = gi < 0 ? 0 : kGray[gi];
+                if (by_lo[a].empty()) continue;
+                int src = -1;
+                if (a && (a & (a - 1)) == 0) {
+                    src = pr[__builtin_ctz(static_cast<unsigned>(a))];
+                } else if (a) {
+                    int b[4], nb = 0;
+                    const int d = a ^ cur;
+                    if (cur && __builtin_popcount(static_cast<unsigned>(d)) <= 2) {
+                        for (int x = 0; x < 4; ++x)
+                            if (d >> x & 1) b[nb++] = pr[x];
+                        if (nb == 1) P.v_op2(kVXor, tl, V(tl), b[0]);
+                        else P.v_xor3(tl, tl, b[0], b[1]);
+                    } else {
+                        for (int x = 0; x < 4; ++x)
+                            if (a >> x & 1) b[nb++] = pr[x];
+                        if (nb == 2) {
+                            P.v_op2(kVXor, tl, V(b[0]), b[1]);
+                        } else {
+                            P.v_xor3(tl, b[0], b[1], b[2]);
+                            if (nb == 4) P.v_op2(kVXor, tl, V(tl), b[3]);
+                        }
+                    }
+                    cur = a;
+                    src = tl;
+                }
+                for (const auto& ri : by_lo[a]) {
+                    const int m = mask[(static_cast<size_t>(c) * rows + ri.first) * 8 + ri.second];
                     int t[2];
                     int nt = 0;
-                    if (m & 15) t[nt++] = reg[0][m & 15];
+                    if (src >= 0) t[nt++] = src;
                     if (m >> 4) t[nt++] = reg[1][m >> 4];
-                    const int a = acc_reg(r - r0, i);
-                    if (c == 0) {
-                        if (nt == 0) P.v_mov(a, C(0));
-                        else if (nt == 1) P.v_mov(a, V(t[0]));
-                        else P.v_op2(kVXor, a, V(t[0]), t[1]);
-                    } else if (nt == 2) {
-                        P.v_xor3(a, a, t[0], t[1]);
-                    } else if (nt == 1) {
-                        P.v_op2(kVXor, a, V(a), t[0]);
-                    }
+                    update(c, ri.first, ri.second, t, nt);
                 }
+            }
         };
         if (!share) {
             for (int c = 0; c < cols; ++c) {
@@ -837,26 +898,30 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                     P.v_op2(kVAnd, kVT0, kLit, kVOff, 0x1f8);
                     P.v_op2(kVLshl, kVT0, C(1), kVT0);
                 }
-                P.s_barrier();
+                if (!sh.nobar) P.s_barrier();
                 const int ncol = std::min(per, cols - st * per);
                 auto read = [&](int j) {
                     const uint32_t off = buf + static_cast<uint32_t>(j) * 2048u;
-                    const int d = kVPlanes + (deep ? 8 * (j & 1) : 0);
+                    const int d = kVPlanes + (ahead ? 8 * (j & 1) : 0);
                     P.ds_read4(d, kVT0, off);
                     P.ds_read4(d + 4, kVT0, off + 1024u);
                 };
                 read(0);
                 for (int j = 0; j < ncol; ++j) {
-                    if (deep && j + 1 < ncol) {
-                        read(j + 1);  // the next column's planes arrive while this one combines
+                    if (ahead && j + 1 < ncol) {
+                        // the next column's planes arrive while this one combines
+                        // (a count of LDS reads only: the scalar loads still out
+                        // are staging, not waited for here, and LDS reads return
+                        // in order, so 2 outstanding means read(j) is in)
+                        read(j + 1);
                         P.wait_lgkm(2);
                     } else {
                         P.wait_lgkm0();
                     }
                     int pr[8];
-                    for (int q = 0; q < 8; ++q) pr[q] = kVPlanes + (deep ? 8 * (j & 1) : 0) + q;
+                    for (int q = 0; q < 8; ++q) pr[q] = kVPlanes + (ahead ? 8 * (j & 1) : 0) + q;
                     combine(st * per + j, pr);
-                    if (!deep && j + 1 < ncol) read(j + 1);
+                    if (!ahead && j + 1 < ncol) read(j + 1);
                 }
             }
         }

@@ -59,13 +59,18 @@ struct AsmShape {
     int kcols = 1;   // share: columns each wave loads per step (one barrier per nw * kcols columns)
     int dma = 0;     // share: each wave's columns stream into a private LDS ring of `dma` steps through
                      // LDS-DMA loads (buffer_load_dwordx4 ... lds), dma - 1 steps ahead; 0 = register loads
+    int ahead = 0;   // share: the next column's planes are read from LDS while this one combines
+                     // (a second set of 8 plane registers; the loads stay one step ahead)
+    int nobar = 0;   // DIAGNOSTIC (experiments build only, wrong results): shared columns without barriers
+    int gray = 0;    // the low half's subsets are built one at a time into one register, in Gray-code
+                     // order, the outputs they feed updated right after (12 subset registers, not 22)
 };
 // deep: -1 = when the workgroup has 8 waves (one workgroup per CU whatever
 // the registers: the extra 24 VGPRs cost no occupancy), 0 / 1 = off / on.
 // split_small: a product of 9-16 rows runs as two paths of at most 8 rows
 // (half the accumulator registers per wave) instead of one.
-inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0,
-                          int deep = -1, int split_small = 0, int kcols = 1, int dma = 0) {
+inline AsmShape asm_shape_base(int rows, int layout, int group_waves, int path_rows, int share, int deep,
+                               int split_small, int kcols, int dma) {
     AsmShape s;
     const int pr = path_rows < 1 ? 1 : path_rows > 16 ? 16 : path_rows;
     const int paths = rows <= 16 ? (split_small && rows > 8 ? 2 : 1) : (rows + pr - 1) / pr;
@@ -102,6 +107,14 @@ inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows =
     if (s.kcols > 1) s.deep = 0;
     s.dma = (s.share && s.kcols == 1 && dma >= 2) ? (dma > 8 ? 8 : dma) : 0;
     if (s.dma) s.deep = 0;
+    return s;
+}
+inline AsmShape asm_shape(int rows, int layout, int group_waves, int path_rows = 16, int share = 0,
+                          int deep = -1, int split_small = 0, int kcols = 1, int dma = 0, int ahead = 0,
+                          int gray = 0) {
+    AsmShape s = asm_shape_base(rows, layout, group_waves, path_rows, share, deep, split_small, kcols, dma);
+    s.gray = gray ? 1 : 0;
+    s.ahead = (ahead && s.share && s.kcols == 1 && !s.deep) ? 1 : 0;
     return s;
 }
 // LDS bytes per workgroup of a generated kernel.

@@ -21,7 +21,8 @@ the old value (measured on MI355X, tools/asm_probe/wave_id.s).
 Workgroups with LDS (the shared-column kernels): ds_write_b128 /
 ds_read_b128 / ds_read_b64 on a per-workgroup LDS of the size the kernel
 descriptor declares (bounds and alignment checked); reads land at
-`lgkmcnt(0)` like scalar loads.  LDS-DMA loads (`buffer_load_dwordx4 ...
+`lgkmcnt(0)`, or at `lgkmcnt(N)` for all but the newest N (LDS reads
+return in order; scalar loads may still be out then).  LDS-DMA loads (`buffer_load_dwordx4 ...
 lds`: 16 bytes per lane written to LDS at M0 + 16 * lane) count on vmcnt like
 other vector memory loads, and an LDS read of bytes whose DMA has not been
 waited for raises `WaitcntError`.  The waves of a workgroup run in rounds
@@ -220,10 +221,10 @@ class Wave:
                         self.lgkm.clear()
                         self.lds_q.clear()
                     else:
-                        # scalar loads return out of order: a nonzero count is
-                        # only meaningful with none outstanding
-                        if self.lgkm:
-                            raise WaitcntError(f"pc {self.pc}: lgkmcnt({n}) with scalar loads outstanding")
+                        # LDS reads return in order, scalar loads in any order:
+                        # a nonzero count retires the LDS reads older than the
+                        # newest n (whatever scalar loads are still out, they
+                        # only add to the count) and no scalar load
                         while len(self.lds_q) > n:
                             self.lds_q.pop(0)
                 continue

@@ -75,6 +75,8 @@ SWEEP = {
     "jit_share": [0, 1],
     "jit_share_deep": [1, -1, 0],
     "jit_share_dma": [3, 0],
+    "jit_share_ahead": [1, 0],
+    "jit_gray": [1, 0],
     "jit_split_cols": [4, 0],
     "jit_share_cols": [2, -1, 1],
     "table_registry_max": [1, 1 << 14],

@@ -360,3 +360,70 @@ def test_machine_code_equals_assembler_grouped(rslib, rows, cols, acc, dma):
         L.rs_tune(b"jit_layout", 0)
         L.rs_tune(b"jit_share_dma", 0)
     assert n > 0 and n % 4 == 0
+
+
+def _vgprs_used(src):
+    import re
+    return int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", src).group(1))
+
+
+@pytest.mark.parametrize("rows,cols,acc,layout,gw,dma", [(5, 10, 0, 0, 4, 0), (16, 16, 1, 0, 4, 0), (33, 7, 0, 0, 4, 0),
+                                                         (40, 9, 1, 0, 4, 0), (64, 13, 0, 0, 4, 3), (17, 2, 1, 0, 4, 0),
+                                                         (128, 9, 0, 2, 4, 0), (100, 7, 1, 2, 4, 0),
+                                                         (72, 11, 0, 2, 2, 2), (33, 5, 1, 1, 4, 0)])
+@pytest.mark.parametrize("gray,ahead", [(1, 0), (0, 1), (1, 1)])
+def test_asm_kernel_gray_subsets_and_read_ahead(rslib, orc, rows, cols, acc, layout, gw, dma, gray, ahead):
+    """rs_tune("jit_gray", 1): the low half's subsets are built one at a time
+    into one register in Gray-code order (one XOR / xor3 each, from the subset
+    before or from the planes) with the outputs they feed updated right after
+    - 12 subset registers instead of 22.  rs_tune("jit_share_ahead", 1): a
+    shared-column kernel reads the next column's planes from LDS while this
+    one combines (lgkmcnt(2) with the staging scalar loads possibly still
+    out: LDS reads return in order).  Against the oracle in the emulator
+    (LDS races, wait counts) for every layout, accumulate included."""
+    L = rslib.lib()
+    assert L.rs_tune(b"jit_layout", layout) == 0 and L.rs_tune(b"jit_group_waves", gw) == 0
+    assert L.rs_tune(b"jit_share_dma", dma) == 0
+    # (no occupancy cap: the kernel declares the VGPRs it uses)
+    assert L.rs_tune(b"jit_waves", 0) == 0 and L.rs_tune(b"jit_wide_waves", 0) == 0
+    mat = np.random.default_rng(rows * 1000 + cols * 10 + acc).integers(0, 256, (rows, cols), dtype=np.uint8)
+    base = _vgprs_used(rslib.jit_asm_source(mat, bool(acc)))
+    assert L.rs_tune(b"jit_gray", gray) == 0 and L.rs_tune(b"jit_share_ahead", ahead) == 0
+    try:
+        paths = 1 if rows <= 16 else (rows + 15) // 16
+        if layout == 2:
+            G, nw, _rw = _layout2_shape(rows, gw)
+            src = _check_kernel(rslib, orc, rows, cols, acc, layout=2, gw=nw, groups=G)
+        else:
+            src = _check_kernel(rslib, orc, rows, cols, acc, layout=layout, gw=gw, paths=paths)
+    finally:
+        L.rs_tune(b"jit_gray", 0)
+        L.rs_tune(b"jit_share_ahead", 0)
+        L.rs_tune(b"jit_layout", 0)
+        L.rs_tune(b"jit_group_waves", 4)
+        L.rs_tune(b"jit_share_dma", 0)
+        L.rs_tune(b"jit_waves", 2)
+        L.rs_tune(b"jit_wide_waves", 3)
+    shared = layout != 1 and paths > 1
+    assert ("lgkmcnt(2)" in src) == bool(ahead and shared and cols > 1)
+    # registers: 10 fewer with gray, 8 more with the read-ahead plane set
+    # (declared VGPRs round up to 4)
+    want = base - (10 if gray else 0) + (8 if ahead and shared else 0)
+    assert abs(_vgprs_used(src) - want) <= 3
+
+
+@pytest.mark.parametrize("rows,cols,acc,layout", [(128, 128, 0, 2), (64, 64, 1, 0), (56, 200, 0, 0), (16, 16, 1, 0)])
+def test_machine_code_equals_assembler_gray_ahead(rslib, rows, cols, acc, layout):
+    """The gray / read-ahead kernels' machine code equals comgr's assembly of
+    their text."""
+    L = rslib.lib()
+    mat = np.random.default_rng(rows * 47 + cols).integers(0, 256, (rows, cols), dtype=np.uint8)
+    assert L.rs_tune(b"jit_layout", layout) == 0
+    assert L.rs_tune(b"jit_gray", 1) == 0 and L.rs_tune(b"jit_share_ahead", 1) == 0
+    try:
+        n = rslib.jit_encoder_check(mat, bool(acc))
+    finally:
+        L.rs_tune(b"jit_gray", 0)
+        L.rs_tune(b"jit_share_ahead", 0)
+        L.rs_tune(b"jit_layout", 0)
+    assert n > 0 and n % 4 == 0

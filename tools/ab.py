@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 # "var=..." code-shape experiments live only in the experiments build
 # (librsamd_exp.so, -DRSAMD_EXPERIMENTS); the product library rejects "var".
-EXPERIMENTS = any("var=" in s for s in sys.argv[1:])
+EXPERIMENTS = any("var=" in s or "jit_nobar=" in s for s in sys.argv[1:])
 if EXPERIMENTS:
     os.environ["RSAMD_LIB_VARIANT"] = "experiments"
 
@@ -37,7 +37,8 @@ ITERS = int(os.environ.get("AB_ITERS", "20"))
 DEFAULTS = {"max_grid": 0, "vpt": 1, "nt_store": 1, "lds_pad": 0, "lane_bytes": 8, "block8": 128,
             "bitslice": 1, "bs_block": 0, "bs_waves": 2, "wide_block": 256, "jit": 2, "jit_pf": 3, "jit_sync": 0, "jit_waves": 2, "jit_min_acc_cols": 1, "jit_min_rows": 5,
             "jit_backend": 2, "jit_layout": 2, "jit_group_waves": 4, "jit_path_rows": 16,
-            "jit_wide_pf": 2, "jit_wide_waves": 3, "jit_share": 1, "jit_share_deep": 0, "jit_split_cols": 0, "jit_share_cols": 1, "jit_share_dma": 0}
+            "jit_wide_pf": 2, "jit_wide_waves": 3, "jit_share": 1, "jit_share_deep": 0, "jit_split_cols": 0, "jit_share_cols": 1, "jit_share_dma": 0,
+            "jit_share_ahead": 0, "jit_gray": 0}
 LOST = {"rec1": [0], "rec2": [0, 11], "rec4": [0, 2, 5, 9], "rec5": [0, 2, 4, 6, 8], "rec6": [0, 1, 3, 5, 7, 9],
         "rec8": [0, 1, 2, 3, 4, 5, 6, 7], "rec8p": [0, 2, 4, 6, 10, 12, 14, 16], "rec12": list(range(12)),
         "rec16": list(range(16)), "rec24": list(range(24)), "rec32": list(range(32))}
@@ -52,6 +53,7 @@ def parse(spec):
 
 if EXPERIMENTS:
     DEFAULTS["var"] = -1
+    DEFAULTS["jit_nobar"] = 0
 
 
 def main():

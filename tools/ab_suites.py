@@ -112,6 +112,16 @@ SUITES = {
                                                "block8=256", "block8=256,layout=inter"]),
                 (dict(AB_K="10", AB_M="4", AB_VEC="8192"), ["op=rep1", "op=rep1,lane_bytes=16", "op=upd",
                                                             "op=upd,lane_bytes=16", "op=rep1,block8=256"])],
+    # round 5: the low half's subsets built one at a time in Gray-code order (12 subset
+    # registers, not 22), which makes room for reading the next column's planes from LDS
+    # while one combines (jit_share_ahead) at 3 waves per SIMD, or for 4 waves per SIMD
+    # with 11-13-row paths
+    "gray_ahead": [(dict(AB_K=str(k), AB_M=str(m), AB_S=str(s)),
+                    ["", "jit_gray=1", "jit_share_ahead=1", "jit_gray=1,jit_share_ahead=1",
+                     "jit_gray=1,jit_path_rows=12,jit_wide_waves=4",
+                     "jit_gray=1,jit_share_ahead=1,jit_path_rows=11,jit_wide_waves=4",
+                     "jit_gray=1,jit_share_dma=3,jit_path_rows=13,jit_wide_waves=4"])
+                   for k, m, s in ((64, 64, 28), (128, 128, 14), (200, 56, 14), (32, 32, 56))],
 }
 
 

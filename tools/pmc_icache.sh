@@ -5,7 +5,8 @@
 # per counter group (MI355X_MICROARCH.md §rocprofv3 PMC slots), for each
 # shape given (tools/pmc_traffic.py specs, e.g. enc:64+64).  Summary:
 # gpurun_out/pmc_icache/summary.json (tools/pmc_sq_summary.py).  PMC_GROUPS
-# picks the counter groups (default "SQ SQC"; "LDS" = the wait / LDS split).
+# picks the counter groups (default "SQ SQC"; "LDS" = the wait / LDS split;
+# "VALU" = SIMD VALU cycles against the waves').
 set -uo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$REPO/gpurun_out/${PMC_OUT:-pmc_icache}"
@@ -15,6 +16,8 @@ SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_I
 SQC="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE"
 # LDS: where parked / stalled cycles come from (s_waitcnt + barrier vs LDS issue stalls and bank conflicts)
 LDS="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+# VALU: SIMD-side VALU cycles against the waves' (is the SIMD or the wave the limit?)
+VALU="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"
 i=0
 for SPEC in "$@"; do
   for GROUP in ${PMC_GROUPS:-SQ SQC}; do

@@ -37,6 +37,12 @@ for d in sorted(glob.glob(os.path.join(out, "p*"))):
         "share_wait_inst_any": mean.get("SQ_WAIT_INST_ANY", 0) / wc,
         "share_active_inst_any": mean.get("SQ_ACTIVE_INST_ANY", 0) / wc,
         "share_active_valu": mean.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+        "share_wait_inst_lds": mean.get("SQ_WAIT_INST_LDS", 0) / wc,
+        "share_active_lds": mean.get("SQ_ACTIVE_INST_LDS", 0) / wc,
+        "share_active_misc": mean.get("SQ_ACTIVE_INST_MISC", 0) / wc,
+        "lds_bank_conflict_per_lds_inst": mean.get("SQ_LDS_BANK_CONFLICT", 0) / max(mean.get("SQ_INSTS_LDS", 0), 1),
+        "valu_simd_cycles_per_valu_inst": mean.get("SQ_INST_CYCLES_VALU", 0) / max(mean.get("SQ_INSTS_VALU", 0), 1),
+        "valu_simd_cycles_per_busy_cycle": mean.get("SQ_INST_CYCLES_VALU", 0) / max(mean.get("SQ_BUSY_CYCLES", 0), 1),
         "ifetch_per_wave": mean.get("SQ_IFETCH", 0) / max(mean.get("SQ_WAVES", 1), 1),
         "icache_miss_rate": mean.get("SQC_ICACHE_MISSES", 0) / max(mean.get("SQC_ICACHE_REQ", 0), 1),
         "icache_hit_rate": mean.get("SQC_ICACHE_HITS", 0) / max(mean.get("SQC_ICACHE_REQ", 0), 1),
