@@ -657,7 +657,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "nt_store") t.nt_store = value;
 #ifdef RSAMD_EXPERIMENTS  // code-shape experiments: librsamd_exp.so only (the product has no "var")
         else if (n == "var") t.var = value;
-        else if (n == "jit_nobar") g_jit_nobar = value ? 1 : 0;  // timing diagnostic, wrong results
+        else if (n == "jit_nobar") g_jit_nobar = value < 0 ? 0 : value > 3 ? 3 : value;  // timing diagnostic, wrong results
 #endif
         else if (n == "lds_pad") t.lds_pad = value;
         else if (n == "lane_bytes") t.lane_bytes = value == 16 ? 16 : 8;

@@ -874,7 +874,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                         P.v_op2(kVAdd, kVT0, kLit, kVT0, dma_slot(k_));
                         for (int k = 0; k < 4; ++k) P.ds_read2(kVPlanes + 2 * k, kVT0, 512u * static_cast<uint32_t>(k));
                         P.wait_lgkm0();
-                    } else {
+                    } else if (sh.nobar < 2) {
                         vmem_wait_for(col_id[static_cast<size_t>(c)]);
                     }
                     int pr[8];
@@ -886,7 +886,7 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                     const uint32_t off = buf + static_cast<uint32_t>(q * nsh + wi) * 2048u;
                     P.ds_write4(kVT0, pr[0], off);
                     P.ds_write4(kVT0, pr[4], off + 1024u);
-                    P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
+                    if (sh.nobar < 3) P.wait_lgkm0();  // (the slot registers are read before the next load lands in them)
                     if (!D && c + L.pf * nsh < cols) {
                         issue_col(c + L.pf * nsh);
                         // (its scalar loads back before the LDS reads below, so
@@ -914,8 +914,8 @@ Prog generate(const uint8_t* mat, int rows, int cols, bool acc, const AsmShape& 
                         // are staging, not waited for here, and LDS reads return
                         // in order, so 2 outstanding means read(j) is in)
                         read(j + 1);
-                        P.wait_lgkm(2);
-                    } else {
+                        if (sh.nobar < 3) P.wait_lgkm(2);
+                    } else if (sh.nobar < 3) {
                         P.wait_lgkm0();
                     }
                     int pr[8];

@@ -62,6 +62,7 @@ struct AsmShape {
     int ahead = 0;   // share: the next column's planes are read from LDS while this one combines
                      // (a second set of 8 plane registers; the loads stay one step ahead)
     int nobar = 0;   // DIAGNOSTIC (experiments build only, wrong results): shared columns without barriers
+                     // (1), also without the column loads' vmcnt waits (2), also without the LDS waits (3)
     int gray = 0;    // the low half's subsets are built one at a time into one register, in Gray-code
                      // order, the outputs they feed updated right after (12 subset registers, not 22)
 };

@@ -292,6 +292,23 @@ def test_wide_asm_jit_shared_dma(rslib, orc, torch_dev, asm_jit, rows, cols, dma
         asm_jit.rs_tune(b"jit_share_dma", 0)
 
 
+@pytest.mark.parametrize("rows,cols,layout,gray,ahead", [(64, 64, 0, 1, 1), (128, 128, 2, 1, 1), (33, 7, 0, 1, 0),
+                                                        (56, 200, 2, 0, 1), (16, 16, 0, 1, 0), (100, 28, 2, 1, 1)])
+def test_wide_asm_jit_gray_ahead(rslib, orc, torch_dev, asm_jit, rows, cols, layout, gray, ahead):
+    """rs_tune("jit_gray", 1) (low-half subsets built one at a time in
+    Gray-code order) and rs_tune("jit_share_ahead", 1) (the next column's
+    planes read from LDS while one combines, lgkmcnt(2)), alone and together,
+    in layout 0 and the row-group layout 2, against the oracle on the GPU."""
+    assert asm_jit.rs_tune(b"jit_layout", layout) == 0
+    assert asm_jit.rs_tune(b"jit_gray", gray) == 0 and asm_jit.rs_tune(b"jit_share_ahead", ahead) == 0
+    try:
+        test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols)
+    finally:
+        asm_jit.rs_tune(b"jit_layout", 2)
+        asm_jit.rs_tune(b"jit_gray", 0)
+        asm_jit.rs_tune(b"jit_share_ahead", 0)
+
+
 @pytest.mark.parametrize("rows,cols,gw,dma", [(128, 128, 4, 0), (100, 28, 4, 0), (64, 64, 2, 0), (56, 200, 2, 0),
                                               (128, 17, 4, 3), (40, 9, 2, 2)])
 def test_wide_asm_jit_grouped_shared(rslib, orc, torch_dev, asm_jit, rows, cols, gw, dma):
