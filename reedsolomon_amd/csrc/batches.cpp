@@ -4,7 +4,6 @@
 // the generic product.  All asynchronous on the caller's stream.
 #include <algorithm>
 #include <array>
-#include <unordered_map>
 
 #include "codec_internal.hpp"
 
@@ -148,12 +147,19 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         // Group stripes by erasure pattern (host, O(S)); validate every pattern
         // before any launch.  Batches hold few distinct patterns, often in runs:
         // the previous stripe's pattern, then a scan of the first 16 patterns,
-        // then a hash map (32768 stripes through an unordered_map of vectors
-        // cost ~1 ms per call, more than the 0.55 ms kernel it feeds).
+        // then an open-addressing hash of pattern indexes (a node-based map
+        // cost ~150 ns per new pattern, most of a 1,470-pattern call once the
+        // GPU plans the patterns).
         std::vector<int32_t> pat_of(static_cast<size_t>(nstripes), -1);
         std::vector<Mask256> keys;
         std::vector<size_t> counts;
-        std::unordered_map<Mask256, int, Mask256Hash> index;
+        std::vector<int32_t> slots;  // pattern index per hash slot, -1 = empty (power-of-two size)
+        const Mask256Hash hasher;
+        auto slot_of = [&](const Mask256& key) -> size_t {  // the key's slot, or the empty one it would take
+            size_t h = hasher(key) & (slots.size() - 1);
+            while (slots[h] >= 0 && keys[static_cast<size_t>(slots[h])] != key) h = (h + 1) & (slots.size() - 1);
+            return h;
+        };
         int last = -1;
         constexpr int kScan = 16;
         for (int s = 0; s < nstripes; ++s) {
@@ -168,15 +174,21 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
                 const int n = static_cast<int>(keys.size());
                 for (int k = 0; k < n && k < kScan && gi < 0; ++k)
                     if (keys[k] == key) gi = k;
-                if (gi < 0 && n > kScan) {
-                    auto it = index.find(key);
-                    if (it != index.end()) gi = it->second;
+                size_t h = 0;
+                if (gi < 0 && n >= kScan) {
+                    if (slots.empty() || 2 * (n - kScan + 1) > static_cast<int>(slots.size())) {
+                        // (re)build at load <= 1/2 from the patterns past the scanned ones
+                        slots.assign(slots.empty() ? 256 : slots.size() * 2, -1);
+                        for (int k = kScan; k < n; ++k) slots[slot_of(keys[static_cast<size_t>(k)])] = k;
+                    }
+                    h = slot_of(key);
+                    if (slots[h] >= 0) gi = slots[h];
                 }
                 if (gi < 0) {
                     gi = n;
                     keys.push_back(key);
                     counts.push_back(0);
-                    if (gi >= kScan) index.emplace(key, gi);
+                    if (gi >= kScan) slots[h] = gi;
                 }
             }
             pat_of[s] = gi;
@@ -184,6 +196,85 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             last = gi;
         }
         if (keys.empty()) return RS_OK;
+        // Every pattern's plan_reconst error before any device work: with no
+        // survivor list the needed vectors are the mask's, and more than p of
+        // them is RS_ERR_TOO_MANY_LOST (nothing else can fail there).
+        int nn_max = 0;
+        for (const Mask256& k : keys) {
+            int nn = 0;
+            for (int w = 0; w < masks.words; ++w) nn += __builtin_popcountll(k[w]);
+            if (nn > p) return RS_ERR_TOO_MANY_LOST;
+            nn_max = nn > nn_max ? nn : nn_max;
+        }
+        if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
+        RS_TRY(ensure_device(rs));
+        DeviceGuard g(rs->device);
+        hipStream_t st = as_stream(stream);
+
+        // Single launch over all stripes when every pattern has <= 4 outputs and
+        // the layout takes the 16-byte vector path; otherwise one launch per
+        // pattern over a stripe-id list (below).
+        bool single = nn_max <= 4 && len % 16 == 0 && len < (size_t{1} << 31) &&
+                      (len / 1024 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
+        for (int v = 0; v < d + p && single; ++v)
+            single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
+        single = single && (L->data_stripe_stride & 15) == 0 && (L->parity_stripe_stride & 15) == 0;
+        const int gpu_plan = tuning().multi_gpu_plan;
+        if (single && gpu_plan > 0 && keys.size() >= static_cast<size_t>(gpu_plan)) {
+            // Plan on the GPU (gf_plan_multi, kernels.hip): upload the encoding
+            // matrix, the field tables, the distinct masks and the stripe ->
+            // pattern map; the planner writes the table images and descriptors
+            // behind them in the same device slot, then the multi kernel runs.
+            const int npat = static_cast<int>(keys.size());
+            const int tdw = multi_table_dwords(d);
+            auto al16 = [](size_t x) { return (x + 15) & ~size_t{15}; };
+            const size_t enc_b = al16(static_cast<size_t>(d + p) * d), gf_b = 768;
+            const size_t mask_b = al16(static_cast<size_t>(npat) * masks.words * 8);
+            const size_t pat_b = al16(static_cast<size_t>(nstripes) * 4);
+            const size_t head = enc_b + gf_b + mask_b + pat_b;
+            const size_t tab_b = static_cast<size_t>(npat) * tdw * 4;
+            const size_t desc_b = static_cast<size_t>(npat) * sizeof(PatternDesc);
+            UploadLease lease(rs);
+            uint8_t* host = nullptr;
+            RS_TRY(lease.acquire(head, &host, head + tab_b + desc_b));
+            std::memcpy(host, rs->enc.data(), static_cast<size_t>(d + p) * d);
+            std::memcpy(host + enc_b, gf().log, 256);
+            std::memcpy(host + enc_b + 256, gf().exp, 512);
+            uint64_t* hm = reinterpret_cast<uint64_t*>(host + enc_b + gf_b);
+            for (int gi = 0; gi < npat; ++gi)
+                for (int w = 0; w < masks.words; ++w) hm[static_cast<size_t>(gi) * masks.words + w] = keys[gi][w];
+            std::memcpy(host + enc_b + gf_b + mask_b, pat_of.data(), static_cast<size_t>(nstripes) * 4);
+            uint8_t* dev = nullptr;
+            RS_TRY(lease.upload(st, &dev));
+            PlanArgs pa;
+            pa.enc = dev;
+            pa.gf = dev + enc_b;
+            pa.masks = reinterpret_cast<const uint64_t*>(dev + enc_b + gf_b);
+            pa.tabs = reinterpret_cast<uint32_t*>(dev + head);
+            pa.descs = reinterpret_cast<PatternDesc*>(dev + head + tab_b);
+            pa.npat = npat;
+            pa.words = masks.words;
+            pa.d = d;
+            pa.p = p;
+            pa.tdw = tdw;
+            RS_TRY(hip_ok(launch_gf_plan_multi(pa, st), "multi-pattern planner launch"));
+            MatmulArgs a;
+            std::memset(&a, 0, sizeof a);
+            a.tables = pa.tabs;
+            a.rows = nn_max;
+            a.cols = d;
+            a.nstripes = nstripes;
+            a.len = len;
+            a.ss[0] = L->data_stripe_stride;
+            a.ss[1] = L->parity_stripe_stride;
+            const LayoutAddr A{L, d};
+            for (int v = 0; v < d + p; ++v) {
+                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
+                a.sid[v] = A.sid(v);
+            }
+            return hip_ok(launch_gf_multi(a, pa.descs, reinterpret_cast<const int32_t*>(dev + enc_b + gf_b + mask_b), st),
+                          "multi-pattern kernel launch");
+        }
         struct Group {
             ReconstPlan pl;
             size_t off, n;
@@ -197,26 +288,12 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             for (int v = 0; v < d + p; ++v)
                 if (keys[gi][v >> 6] >> (v & 63) & 1) need[nn++] = v;
             int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
-            if (rc) return rc;  // RS_ERR_TOO_MANY_LOST for a pattern beyond p erasures
+            if (rc) return rc;  // (validated above)
             gr.off = off;
             gr.n = counts[gi];
             off += gr.n;
             plan.push_back(gr);
         }
-        if (!L->data_base || !L->parity_base) return RS_ERR_INVAL;
-        RS_TRY(ensure_device(rs));
-        DeviceGuard g(rs->device);
-        hipStream_t st = as_stream(stream);
-
-        // Single launch over all stripes when every pattern has <= 4 outputs and
-        // the layout takes the 16-byte vector path; otherwise one launch per
-        // pattern over a stripe-id list (below).
-        bool single = len % 16 == 0 && len < (size_t{1} << 31) &&
-                      (len / 1024 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
-        for (const Group& gr : plan) single = single && gr.pl.nnr <= 4;
-        for (int v = 0; v < d + p && single; ++v)
-            single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
-        single = single && (L->data_stripe_stride & 15) == 0 && (L->parity_stripe_stride & 15) == 0;
         if (single) {
             const int npat = static_cast<int>(plan.size());
             const int tdw = multi_table_dwords(d);

@@ -189,7 +189,7 @@ struct rs_codec {
     struct UploadSlot {
         uint8_t* host = nullptr;
         uint8_t* dev = nullptr;
-        size_t cap = 0;
+        size_t cap = 0, dcap = 0;  // host / device bytes
         hipEvent_t copied = nullptr, done = nullptr;
         bool in_flight = false;
     };
@@ -391,8 +391,10 @@ public:
             slot_->in_flight = true;
         }
     }
-    // A pinned host buffer of `bytes` to fill (slot free for reuse on return).
-    int acquire(size_t bytes, uint8_t** host) {
+    // A pinned host buffer of `bytes` to fill (slot free for reuse on return),
+    // whose device copy has room for `dev_bytes` (at least `bytes`): the part
+    // past `bytes` is the consumer kernels' to write (the GPU planner).
+    int acquire(size_t bytes, uint8_t** host, size_t dev_bytes = 0) {
         rs_codec::UploadSlot& u = rs_->up[rs_->up_next];
         rs_->up_next = (rs_->up_next + 1) % rs_codec::kUploadSlots;
         if (!rs_->up_stream) {
@@ -411,24 +413,29 @@ public:
                 *ev = nullptr;
                 return RS_ERR_DEVICE;
             }
+        auto round = [](size_t b) { return (b + (size_t{64} << 10) - 1) & ~((size_t{64} << 10) - 1); };
         if (u.cap < bytes) {
             if (u.host) (void)hipHostFree(u.host);
-            if (u.dev) (void)hipFree(u.dev);
             u.host = nullptr;
-            u.dev = nullptr;
             u.cap = 0;
-            size_t cap = (bytes + (size_t{64} << 10) - 1) & ~((size_t{64} << 10) - 1);
+            const size_t cap = round(bytes);
             if (hipHostMalloc(reinterpret_cast<void**>(&u.host), cap, hipHostMallocDefault) != hipSuccess) {
                 u.host = nullptr;
                 return RS_ERR_NOMEM;
             }
+            u.cap = cap;
+        }
+        const size_t dneed = dev_bytes > bytes ? dev_bytes : bytes;
+        if (u.dcap < dneed) {
+            if (u.dev) (void)hipFree(u.dev);
+            u.dev = nullptr;
+            u.dcap = 0;
+            const size_t cap = round(dneed);
             if (hipMalloc(reinterpret_cast<void**>(&u.dev), cap) != hipSuccess) {
-                (void)hipHostFree(u.host);
-                u.host = nullptr;
                 u.dev = nullptr;
                 return RS_ERR_NOMEM;
             }
-            u.cap = cap;
+            u.dcap = cap;
         }
         slot_ = &u;
         bytes_ = bytes;

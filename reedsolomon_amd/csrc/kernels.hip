@@ -74,6 +74,7 @@ LaunchTuning& tuning() {
         // 6.28 TB/s, 8+5 interleaved 6.06 -> 6.53; profiles/r03/ab_bs_waves.log)
         const char* bw = std::getenv("RSAMD_BS_WAVES");
         x.bs_waves = bw ? std::atoi(bw) : 2;
+        x.multi_gpu_plan = 8;
         return x;
     }();
     return t;
@@ -1557,6 +1558,228 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
 }
 
 int multi_table_dwords(int cols) { return (cols == 10 ? 10 : ((cols + 3) / 4) * 4) * 20; }
+
+// ---------------------------------------------------------------------------
+// GPU planner of rs_reconst_batch_multi (SURVEY.md §8f.1 "a small GPU
+// Gauss-Jordan"): one wave per distinct erasure pattern writes the table
+// image and descriptor that reconst_multi (batches.cpp) would otherwise build
+// on the host (plan_reconst, the inverse, combined_matrix, perm_table), so a
+// batch whose stripes carry hundreds of patterns does not wait for the host.
+//
+// With no survivor list the survivors are every vector not needed, vs[0..d)
+// the first d in index order (checkReconst rs.go:264-325): the d - dn
+// surviving data vectors K, then the first dn surviving parity vectors P.
+// The dn lost data vectors L satisfy enc[P][L] D_L = P ^ enc[P][K] D_K, so
+// with Minv = (enc[P][L])^-1 (dn x dn, dn <= 4, Gauss-Jordan in one lane):
+//   lost data L_l : coef(q) = Minv[l][j]                       (vs[q] = P_j)
+//                             ^_j Minv[l][j] * enc[P_j][vs[q]]  (vs[q] in K)
+//   lost parity v : coef(q) = enc[v][vs[q]] (vs[q] < d) ^ ^_l enc[v][L_l] * coef_l(q)
+// A vector's coefficients over d independent survivors are unique, so these
+// are the rows of the host's combined matrix (rows of the inverse of the
+// d x d survivor submatrix, codec.cpp) byte for byte.  Every d x d row
+// submatrix of [I; Cauchy] is invertible, so a zero pivot cannot occur; the
+// code still leaves such a pattern's rows zero rather than loop or fault.
+// ---------------------------------------------------------------------------
+constexpr int kPlanWaves = 4;
+
+// c * 2^b for b = 0..7 (multiplication by x, reduced by 0x11d): the columns
+// of multiplication by c as a GF(2)-linear map, from which c * e for any e is
+// the XOR of the entries of e's bits (no table lookups)
+__device__ __forceinline__ void gf_basis(uint32_t c, uint32_t (&cb)[8]) {
+    cb[0] = c;
+#pragma unroll
+    for (int b = 1; b < 8; ++b) cb[b] = ((cb[b - 1] << 1) ^ ((cb[b - 1] & 0x80u) ? 0x11du : 0u)) & 0xffu;
+}
+// x * y in registers (shift-and-add with the 0x11d reduction): no LDS table
+// round trips in the planner's dependent chains
+__device__ __forceinline__ uint32_t gf_mul_alu(uint32_t x, uint32_t y) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        r ^= (y >> b & 1u) ? x : 0u;
+        x = ((x << 1) ^ ((x & 0x80u) ? 0x11du : 0u)) & 0xffu;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs a) {
+    __shared__ uint8_t lg[256], ex[512];
+    __shared__ uint16_t s_vs[kPlanWaves][256];
+    __shared__ uint8_t s_rows[kPlanWaves][4][256];  // enc rows P_0..P_{dn-1}, then the lost parity rows (nn <= 4)
+    __shared__ uint8_t s_minv[kPlanWaves][4][4];
+    __shared__ int s_nr[kPlanWaves][4];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = a.gf[i];
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = a.gf[256 + i];
+    const int w = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
+    const int gi = static_cast<int>(blockIdx.x) * kPlanWaves + w;
+    const bool live = gi < a.npat;  // (every wave reaches every barrier)
+    const int d = a.d, n = a.d + a.p;
+    auto mul = [](uint32_t x, uint32_t y) -> uint32_t { return gf_mul_alu(x, y); };
+    // 1. survivors vs[0, d) and needed vectors nr[0, nn) in index order
+    //    (loops unrolled over the 4 mask words: constant indexes, no scratch)
+    int nn = 0, dn = 0;
+    if (live) {
+        const uint64_t* mk = a.masks + static_cast<size_t>(gi) * a.words;
+        int ns = 0;
+        const uint64_t lt = __lanemask_lt();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int v0 = 64 * k;
+            if (v0 >= n) break;
+            const uint64_t mwk = mk[k];
+            const int v = v0 + lane;
+            const bool in = v < n;
+            const bool need = in && ((mwk >> lane) & 1u);
+            const uint64_t bs = __ballot(in && !need), bn = __ballot(need), bd = __ballot(need && v < d);
+            if (in && !need) {
+                const int rk = ns + __popcll(bs & lt);
+                if (rk < d) s_vs[w][rk] = static_cast<uint16_t>(v);
+            }
+            if (need) {
+                const int rk = nn + __popcll(bn & lt);
+                if (rk < 4) s_nr[w][rk] = v;
+            }
+            ns += __popcll(bs);
+            nn += __popcll(bn);
+            dn += __popcll(bd);
+        }
+    }
+    __syncthreads();
+    // 2. the encoding-matrix rows this pattern uses, into LDS: the parity
+    //    survivors P_j that stand in for the lost data (rows 0..dn), then the
+    //    lost parity rows (rows dn..nn)
+    //    (the rows' loads of one lane issued together, then stored)
+    if (live)
+        for (int q = lane; q < d; q += 64) {
+            uint8_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int row = k < dn ? s_vs[w][d - dn + k] : s_nr[w][k < nn ? k : 0];
+                v[k] = k < nn ? a.enc[static_cast<size_t>(row) * d + q] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s_rows[w][k][q] = v[k];
+        }
+    __syncthreads();
+    // 3. Minv (lane 0): [M | I] -> [I | Minv], M[j][l] = enc[P_j][L_l]; the
+    //    loops unrolled to 4 x 8 with guards so the matrix stays in registers
+    if (live && lane == 0 && dn > 0) {
+        uint32_t m[4][8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                m[j][l] = (j < dn && l < dn) ? s_rows[w][j][s_nr[w][l]] : 0u;
+                m[j][4 + l] = j == l ? 1u : 0u;
+            }
+        bool ok = true;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c >= dn || !ok) break;
+            int pr = -1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (r >= c && r < dn && pr < 0 && m[r][c]) pr = r;
+            if (pr < 0) {
+                ok = false;
+                break;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (r > c && r == pr)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t t = m[r][k];
+                        m[r][k] = m[c][k];
+                        m[c][k] = t;
+                    }
+            const uint32_t iv = ex[255 - lg[m[c][c]]];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) m[c][k] = mul(m[c][k], iv);
+#pragma unroll
+            for (int r2 = 0; r2 < 4; ++r2) {
+                if (r2 == c || r2 >= dn) continue;
+                const uint32_t f = m[r2][c];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) m[r2][k] ^= mul(f, m[c][k]);
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (l < dn && j < dn) s_minv[w][l][j] = ok ? static_cast<uint8_t>(m[l][4 + j]) : 0;
+    }
+    __syncthreads();
+    if (!live) return;  // (no barrier below)
+    // 4. coefficients (the lost data rows, then the lost parity rows from
+    //    them), each column's table image ([column][4 rows x 5 dwords],
+    //    perm_table in gf256.hpp; zero past the rows and columns) and the
+    //    descriptor
+    uint32_t* img = a.tabs + static_cast<size_t>(gi) * a.tdw;
+    const int ncol = a.tdw / 20;
+    for (int q = lane; q < ncol; q += 64) {
+        // (every loop over rows unrolled to 4 with guards: the coefficients
+        // stay in registers, no scratch)
+        uint32_t coef[4] = {0, 0, 0, 0};
+        if (q < d) {
+            const int u = s_vs[w][q];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                if (l >= dn) break;
+                uint32_t c = 0;
+                if (u >= d) {
+                    c = s_minv[w][l][q - (d - dn)];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (j < dn) c ^= mul(s_minv[w][l][j], s_rows[w][j][u]);
+                }
+                coef[l] = c;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (r < dn || r >= nn) continue;
+                uint32_t c = u < d ? s_rows[w][r][u] : 0u;
+#pragma unroll
+                for (int l = 0; l < 4; ++l)
+                    if (l < dn) c ^= mul(s_rows[w][r][s_nr[w][l]], coef[l]);
+                coef[r] = c;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            uint32_t cb[8];
+            gf_basis(coef[r], cb);
+            // c * e for the 3-bit groups as XORs of the basis (e's bits)
+            const uint32_t a3 = cb[0] ^ cb[1];
+            uint32_t t[5];
+            t[0] = (cb[0] << 8) | (cb[1] << 16) | (a3 << 24);
+            t[1] = cb[2] | (cb[2] ^ cb[0]) << 8 | (cb[2] ^ cb[1]) << 16 | (cb[2] ^ a3) << 24;
+            const uint32_t b3 = cb[3] ^ cb[4];
+            t[2] = (cb[3] << 8) | (cb[4] << 16) | (b3 << 24);
+            t[3] = cb[5] | (cb[5] ^ cb[3]) << 8 | (cb[5] ^ cb[4]) << 16 | (cb[5] ^ b3) << 24;
+            t[4] = (cb[6] << 8) | (cb[7] << 16) | ((cb[6] ^ cb[7]) << 24);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) img[q * 20 + r * 5 + k] = t[k];
+        }
+    }
+    PatternDesc* P = a.descs + gi;
+    for (int i = lane; i < 256; i += 64) P->in_idx[i] = i < d ? s_vs[w][i] : 0;
+    if (lane < 4) P->out_idx[lane] = lane < nn ? static_cast<uint32_t>(s_nr[w][lane]) : 0u;
+    if (lane == 0) {
+        P->tab_off = static_cast<uint32_t>(gi) * static_cast<uint32_t>(a.tdw);
+        P->nout = static_cast<uint32_t>(nn);
+    }
+}
+
+hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream) {
+    if (a.npat <= 0) return hipSuccess;
+    (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
+    const unsigned grid = static_cast<unsigned>((a.npat + kPlanWaves - 1) / kPlanWaves);
+    hipLaunchKernelGGL(gf_plan_multi, dim3(grid), dim3(64 * kPlanWaves), 0, stream, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_gf_matmul(MatmulArgs& a, hipStream_t stream) {
     if (a.len == 0 || a.nstripes <= 0 || a.rows <= 0 || a.cols <= 0) return hipSuccess;

@@ -54,6 +54,19 @@ struct PatternDesc {
 };
 int multi_table_dwords(int cols);
 hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream);
+// GPU planner of the multi-pattern kernel's inputs (gf_plan_multi): for each
+// distinct need mask, the pattern's table image (tdw dwords at tabs + i * tdw)
+// and its descriptor, as reconst_multi builds them on the host.  Every pattern
+// must need 1-4 vectors, none past d + p (validated on the host).
+struct PlanArgs {
+    const uint64_t* masks;  // npat x words need masks
+    const uint8_t* enc;     // (d + p) x d encoding matrix (matrix.go:37-54)
+    const uint8_t* gf;      // the field's log[256], then exp[512] (gf256.hpp)
+    uint32_t* tabs;
+    PatternDesc* descs;
+    int npat, words, d, p, tdw;
+};
+hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream);
 
 // Host-call engine (engine.cpp): a resident kernel that serves small
 // synchronous host calls through doorbells in host memory instead of one
@@ -133,6 +146,7 @@ struct LaunchTuning {
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
     int wide_single_pass;  // > 8 rows without a compiled network: single-pass wide kernels (1) | row groups of 8 (0)
     int bs_waves;     // bit-sliced Encode: at most this many waves per SIMD (LDS padding; 0 = as many as fit; default 2)
+    int multi_gpu_plan;  // rs_reconst_batch_multi: plan on the GPU from this many distinct patterns (0 = host)
 };
 LaunchTuning& tuning();
 

@@ -902,6 +902,71 @@ def test_reconst_batch_multi_single_launch(rslib, torch_dev, d, p, n):
     assert torch.equal(data, ref_d) and torch.equal(parity, ref_p)
 
 
+def _distinct_patterns(d, p, count, seed):
+    """`count` distinct need masks of 1-4 erasures (every one of them when
+    count is the number that exists), as Python ints."""
+    from itertools import combinations
+    from math import comb
+
+    n = d + p
+    kmax = min(4, p)
+    total = sum(comb(n, k) for k in range(1, kmax + 1))
+    if count >= total:
+        return [sum(1 << v for v in c) for k in range(1, kmax + 1) for c in combinations(range(n), k)]
+    rng = np.random.default_rng(seed)
+    seen, out = set(), []
+    while len(out) < count:
+        lost = rng.choice(n, int(rng.integers(1, kmax + 1)), replace=False)
+        m = sum(1 << int(v) for v in lost)
+        if m not in seen:
+            seen.add(m)
+            out.append(m)
+    return out
+
+
+@pytest.mark.parametrize("d,p,n,npat", [(10, 4, 8192, 1470), (100, 28, 4096, 300), (6, 3, 16, 129),
+                                        (32, 32, 1024, 512), (60, 4, 2048, 9)])
+def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat):
+    """rs_tune("multi_gpu_plan", n): a batch with at least n distinct erasure
+    patterns has its pattern tables and descriptors built on the GPU
+    (gf_plan_multi, kernels.hip: the lost data from a dn x dn inverse) instead
+    of by the host (the d x d inverse, combined_matrix).  Every pattern of 1-4
+    erasures (10+4: all 1,470 of C(14, 1..4), one stripe each; 100+28: 256-bit
+    masks reaching past bit 64) is rebuilt bit-exact through both planners,
+    stripes shuffled, a few stripes untouched."""
+    torch = torch_dev
+    L = rslib.lib()
+    pats = _distinct_patterns(d, p, npat, d * 1000 + p)
+    assert len(pats) == npat
+    S = npat + 3
+    rng = np.random.default_rng(npat)
+    order = rng.permutation(S)
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(d * 37 + p)
+    data = torch.randint(0, 256, (S, d, n), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    torch.cuda.synchronize()
+    ref_d, ref_p = data.clone(), parity.clone()
+    masks = [0] * S
+    for i, m in enumerate(pats):
+        masks[int(order[i])] = m   # (the 3 stripes past the patterns stay untouched)
+    arg = masks if d + p > 64 else np.array(masks, dtype=np.uint64)
+    try:
+        for plan in (1, 0):
+            assert L.rs_tune(b"multi_gpu_plan", plan) == 0
+            for s, m in enumerate(masks):
+                for v in range(d + p):
+                    if m >> v & 1:
+                        (data[s, v] if v < d else parity[s, v - d]).fill_(0x5A)
+            r.reconst_batch_multi(data, parity, arg)
+            torch.cuda.synchronize()
+            bad = [s for s in range(S) if not (torch.equal(data[s], ref_d[s]) and torch.equal(parity[s], ref_p[s]))]
+            assert not bad, (plan, bad[:5], [bin(masks[s]) for s in bad[:5]])
+    finally:
+        L.rs_tune(b"multi_gpu_plan", 8)
+
+
 @pytest.mark.parametrize("d,p", [(10, 8), (8, 8), (10, 6)])
 def test_reconst_batch_multi_parity_rows_bitsliced(rslib, orc, torch_dev, d, p):
     """Stripes that lose only parity rows p' in 5..p: the grouped fallback's

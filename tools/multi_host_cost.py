@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
-"""Host-side cost of rs_reconst_batch_multi: many distinct erasure patterns,
-1-4 erasures each, tiny vectors (the kernel is negligible), wall time of the synchronous call.
-Cold = first call on a fresh handle (every inverse computed), warm = the
-same masks again (inverses from the cache where the reference would cache).
-Usage: python tools/multi_host_cost.py   (writes gpurun_out/multi_host_cost.json)
+"""Planning cost of rs_reconst_batch_multi with many distinct erasure
+patterns (1-4 erasures each), host planner (rs_tune("multi_gpu_plan", 0):
+the d x d inverse through the cache, combined_matrix and perm tables per
+pattern) against the GPU planner (gf_plan_multi, one wave per pattern).
+Wall time of the synchronous call (launch + sync) and the device-resident
+rate it amounts to, per shape; cold = first call on a fresh handle, warm =
+the same masks again (median of 8 calls).  Writes gpurun_out/multi_host_cost.json.
 """
 import json
 import os
 import sys
 import time
+from itertools import combinations
+from math import comb
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -20,38 +24,55 @@ import reedsolomon_amd as rs  # noqa: E402
 
 
 def masks_for(d, p, n, seed):
+    """n distinct masks of 1-4 erasures (all of them when n is their count)."""
+    kmax = min(4, p)
+    total = sum(comb(d + p, k) for k in range(1, kmax + 1))
+    if n >= total:
+        return [sum(1 << v for v in c) for k in range(1, kmax + 1) for c in combinations(range(d + p), k)]
     rng = np.random.default_rng(seed)
     seen, out = set(), []
     while len(out) < n:
-        lost = rng.choice(d + p, int(rng.integers(1, min(p, 4) + 1)), replace=False)
-        if not any(v < d for v in lost):
-            continue
+        lost = rng.choice(d + p, int(rng.integers(1, kmax + 1)), replace=False)
         mk = sum(1 << int(v) for v in lost)
         if mk not in seen:
             seen.add(mk)
             out.append(mk)
-    return np.array(out, dtype=np.uint64)
+    return out
 
 
 def main():
     res = {}
-    vec = 1024
-    for d, p, npat in ((10, 4, 1000), (20, 12, 4096), (32, 32, 4096)):
+    L = rs.lib()
+    for d, p, npat, vec in ((10, 4, 1470, 8192), (10, 4, 1470, 1024), (20, 12, 4096, 1024), (32, 32, 4096, 1024),
+                            (100, 28, 1000, 4096)):
         masks = masks_for(d, p, npat, d * 100 + p)
         S = len(masks)
+        arg = masks if d + p > 64 else np.array(masks, dtype=np.uint64)
+        nbytes = sum((d + bin(m).count("1")) * vec for m in masks)
         data = torch.zeros((S, d, vec), dtype=torch.uint8, device="cuda")
         parity = torch.zeros((S, p, vec), dtype=torch.uint8, device="cuda")
-        r = rs.New(d, p)
-        row = {}
-        for phase in ("cold", "warm"):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            r.reconst_batch_multi(data, parity, masks)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            row[phase + "_ms"] = round(dt * 1e3, 2)
-            row[phase + "_us_per_pattern"] = round(dt * 1e6 / S, 2)
-        key = f"{d}+{p} {S} patterns"
+        row = {"stripes": S, "distinct_patterns": S, "vec": vec}
+        for plan, name in ((0, "host"), (1, "gpu")):
+            assert L.rs_tune(b"multi_gpu_plan", plan) == 0
+            r = rs.New(d, p)
+            walls, hosts = [], []
+            for _ in range(9):  # the first call cold (fresh handle), then 8 warm ones (the upload ring holds 4 slots)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                r.reconst_batch_multi(data, parity, arg)
+                hosts.append(time.perf_counter() - t0)  # host side: the call returns once its work is queued
+                torch.cuda.synchronize()
+                walls.append(time.perf_counter() - t0)
+            row[f"{name}_cold_ms"] = round(walls[0] * 1e3, 3)
+            warm = sorted(walls[1:])
+            med = warm[len(warm) // 2]
+            row[f"{name}_warm_median_ms"] = round(med * 1e3, 3)
+            row[f"{name}_warm_min_ms"] = round(warm[0] * 1e3, 3)
+            row[f"{name}_warm_host_median_ms"] = round(sorted(hosts[1:])[len(hosts[1:]) // 2] * 1e3, 3)
+            row[f"{name}_warm_GiBps"] = round(nbytes / med / 2 ** 30, 1)
+            row[f"{name}_us_per_pattern_warm"] = round(med * 1e6 / S, 3)
+        L.rs_tune(b"multi_gpu_plan", 8)
+        key = f"{d}+{p} {S} patterns @ {vec}"
         res[key] = row
         print(key, row, flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
