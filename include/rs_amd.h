@@ -280,8 +280,13 @@ RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stri
  * rs_host_unregister(ptr) takes the address given to rs_host_register
  * (RS_ERR_INVAL for any other); a page leaves the runtime when the last
  * registration holding it goes, after every device this process launched on
- * has been drained.  The caller may then free the memory and reuse the range
- * like any other (the reference retains nothing after a call: rs.go:101-111).
+ * has been drained.  The library then holds nothing of the range (the
+ * reference retains nothing after a call: rs.go:101-111).  Caution, outside
+ * the library: with ROCm 7.x the HIP runtime's own pageable copies
+ * (hipMemcpy from ordinary memory) have faulted on a range that was
+ * registered, unregistered, freed and reused by a new heap allocation
+ * (DESIGN.md §5.8); buffers registered once for the process's life, or
+ * rs_host_alloc blocks, avoid that pattern.
  * No rs_host_register equivalent exists in the reference; it replaces the
  * pinning a cgo caller would otherwise do per call. */
 RS_API int rs_host_register(void* ptr, size_t bytes);

@@ -440,7 +440,8 @@ class RS:
 
     def jit_prepare(self, mat=None, accumulate: bool = False, wait: bool = True) -> None:
         """Compile the run-time bit-sliced kernel for `mat` (rows x cols,
-        5 <= rows <= 16) on this codec's device now (rs_jit_prepare); default
+        5 <= rows <= 128, cols <= 256) on this codec's device now
+        (rs_jit_prepare; a full kernel table is made room in first); default
         mat = GenMatrix, i.e. this code's Encode."""
         m = (self.GenMatrix.reshape(self.ParityNum, self.DataNum) if mat is None
              else np.ascontiguousarray(mat, dtype=np.uint8))

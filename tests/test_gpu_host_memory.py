@@ -14,6 +14,9 @@ import sys
 import numpy as np
 import pytest
 
+# mappings a test registered and unregistered, kept for the session (never unmapped)
+_KEEP_MAPPED = []
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -69,7 +72,9 @@ def test_registrations_sharing_pages(rslib, orc, torch_dev):
         r = rslib.New(d, p)
         rng = np.random.default_rng(11)
         spans0 = rslib.host_pool_stats()["spans"]
-        arena = np.zeros(2 * (d + p) * size + 3 * 4096, np.uint8)
+        from conftest import host_arena  # (registered memory is never freed: conftest.host_arena)
+
+        arena = host_arena(2 * (d + p) * size + 3 * 4096)
         off = (-arena.ctypes.data) % 4096 + 16  # a starts 16 bytes into a page
         a = arena[off: off + (d + p) * size]  # ends 16 bytes into its last page
         b = arena[off + a.nbytes: off + a.nbytes + 4080 + (d + p) * size]  # starts in that page
@@ -160,9 +165,10 @@ def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
 
     import reedsolomon_amd as rs
 
+    from conftest import host_arena  # (registered memory is never unmapped: conftest.host_arena)
+
     page = mmap.PAGESIZE
-    m = mmap.mmap(-1, 8 * page)
-    base = np.frombuffer(m, dtype=np.uint8)
+    base = host_arena(8 * page)
     views = [base[page // 2: 3 * page + page // 2], base[3 * page: 6 * page]]  # share the page at 3 * page
     errs = []
 
@@ -180,7 +186,6 @@ def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
     for t in th:
         t.join()
     del views, base
-    m.close()
     assert not errs, errs[:3]
 
 
@@ -236,7 +241,10 @@ def test_unregister_releases_pages_a_neighbour_does_not_share(rslib, orc, torch_
         rslib.host_unregister(base)
         rslib.host_unregister(b_lo)
     finally:
-        c.munmap(base, npages * page)
+        # the range stays mapped for the rest of the session (conftest.host_arena:
+        # a registered-then-unregistered range that is unmapped and reused by a
+        # later heap array has made the runtime's pageable copies from it fault)
+        _KEEP_MAPPED.append((base, npages * page))
 
 
 def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
@@ -252,7 +260,9 @@ def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
     try:
         r = rslib.New(d, p)
         rng = np.random.default_rng(21)
-        buf = np.zeros((d + p) * size + 4096, np.uint8)
+        from conftest import host_arena  # (registered memory is never freed: conftest.host_arena)
+
+        buf = host_arena((d + p) * size + 4096)
         off = (-buf.ctypes.data) % 4096
         v = [buf[off + i * size: off + (i + 1) * size] for i in range(d + p)]
         times = []
@@ -279,7 +289,9 @@ def test_host_calls_proceed_during_unregister_drain(rslib, orc, torch_dev):
     r = rslib.New(d, p)
     keep = rslib.host_alloc((d + p) * size)
     vk = [keep[i * size:(i + 1) * size] for i in range(d + p)]
-    churn = np.zeros(64 * 4096, np.uint8)
+    from conftest import host_arena  # (registered memory is never freed: conftest.host_arena)
+
+    churn = host_arena(64 * 4096)
     stop = threading.Event()
     errs = []
 

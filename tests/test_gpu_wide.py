@@ -212,6 +212,11 @@ def test_wide_asm_jit_vs_oracle(rslib, orc, torch_dev, asm_jit, rows, cols):
     rng = np.random.default_rng(rows * 7000 + cols)
     mat = rng.integers(0, 256, (rows, cols), dtype=np.uint8)
     r = rslib.New(10, 4)
+    # compiled up front (rs_jit_prepare): a launch that finds the kernel table
+    # full takes the table kernels while the worker evicts (by design), which
+    # a long test session reaches; preparing makes room on this thread first
+    r.jit_prepare(mat)
+    r.jit_prepare(mat, accumulate=True)
     before = rslib.jit_stats()["launches"]
     for S, n, pad in [(3, 2048, 0), (2, 4096 + 5, 11), (2, 65536 + 48, 16)]:
         src, hsrc = _padded(torch, rng, S, cols, n, pad)
