@@ -211,10 +211,10 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         DeviceGuard g(rs->device);
         hipStream_t st = as_stream(stream);
 
-        // Single launch over all stripes when every pattern has <= 4 outputs and
+        // Single launch over all stripes when every pattern has <= 8 outputs and
         // the layout takes the 16-byte vector path; otherwise one launch per
         // pattern over a stripe-id list (below).
-        bool single = nn_max <= 4 && len % 16 == 0 && len < (size_t{1} << 31) &&
+        bool single = nn_max <= kMultiMaxOut && len % 16 == 0 && len < (size_t{1} << 31) &&
                       (len / 1024 + 1) * static_cast<uint64_t>(nstripes) < (uint64_t{1} << 31);  // grid < 2^31 chunks
         for (int v = 0; v < d + p && single; ++v)
             single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
@@ -226,7 +226,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             // pattern map; the planner writes the table images and descriptors
             // behind them in the same device slot, then the multi kernel runs.
             const int npat = static_cast<int>(keys.size());
-            const int tdw = multi_table_dwords(d);
+            const int tdw = multi_table_dwords(d, nn_max);
             auto al16 = [](size_t x) { return (x + 15) & ~size_t{15}; };
             const size_t enc_b = al16(static_cast<size_t>(d + p) * d), gf_b = 768;
             const size_t mask_b = al16(static_cast<size_t>(npat) * masks.words * 8);
@@ -257,6 +257,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             pa.d = d;
             pa.p = p;
             pa.tdw = tdw;
+            pa.img_rows = multi_image_rows(nn_max);
             RS_TRY(hip_ok(launch_gf_plan_multi(pa, st), "multi-pattern planner launch"));
             MatmulArgs a;
             std::memset(&a, 0, sizeof a);
@@ -296,7 +297,8 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         }
         if (single) {
             const int npat = static_cast<int>(plan.size());
-            const int tdw = multi_table_dwords(d);
+            const int tdw = multi_table_dwords(d, nn_max);
+            const int cw = multi_image_rows(nn_max) * 5;
             const size_t tab_bytes = static_cast<size_t>(npat) * tdw * 4;
             const size_t desc_bytes = static_cast<size_t>(npat) * sizeof(PatternDesc);
             const size_t pat_bytes = static_cast<size_t>(nstripes) * 4;
@@ -316,7 +318,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
                 RS_TRY(combined_matrix(rs, gr.pl.vs, gr.pl.nr, gr.pl.nnr, gr.pl.dn, m));
                 uint32_t* img = tabs + static_cast<size_t>(gi) * tdw;
                 for (int i = 0; i < d; ++i)
-                    for (int r = 0; r < gr.pl.nnr; ++r) perm_table(m[static_cast<size_t>(r) * d + i], img + i * 20 + r * 5);
+                    for (int r = 0; r < gr.pl.nnr; ++r) perm_table(m[static_cast<size_t>(r) * d + i], img + i * cw + r * 5);
                 PatternDesc& pd = descs[gi];
                 pd.tab_off = static_cast<uint32_t>(gi * tdw);
                 pd.nout = static_cast<uint32_t>(gr.pl.nnr);

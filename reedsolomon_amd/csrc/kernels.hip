@@ -501,14 +501,16 @@ __device__ __forceinline__ void multi_chunk(const MatmulArgs& a, const PatternDe
     const int cols = KFIX ? KB : a.cols;
     const int ncols_pad = KFIX ? KB : ((cols + KB - 1) / KB) * KB;
     const uint32_t* img = a.tables + P->tab_off;
-    // image columns are 20 dwords (4 rows x 5); keep the first COLD of each
+    // image columns are CW dwords (4 or 8 rows x 5, a.rows = the batch's most
+    // outputs); keep the first COLD of each
+    const int CW = multi_image_rows(a.rows) * 5;
     auto stage = [&]() {
-        if (COLD == 20) {  // 4-row body: the image is the LDS layout
+        if (COLD == CW) {  // the image is the LDS layout
             for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) lds32[idx] = img[idx];
         } else {
             for (int idx = threadIdx.x; idx < ncols_pad * COLD; idx += BS) {
                 const int c = idx / COLD;
-                lds32[idx] = img[c * 20 + (idx - c * COLD)];
+                lds32[idx] = img[c * CW + (idx - c * COLD)];
             }
         }
         __syncthreads();
@@ -536,8 +538,11 @@ __global__ __launch_bounds__(BS) void gf_matmul_multi(const MatmulArgs a, const 
     if (pid < 0) return;  // stripe not in the batch's work (uniform: whole workgroup)
     const PatternDesc* P = pats + pid;
     const uint32_t nout = P->nout;
+    if constexpr (MC > 4) {
+        if (nout > 4) return multi_chunk<MC, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
+    }
     if constexpr (MC > 2) {
-        if (nout > 2) return multi_chunk<MC, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
+        if (nout > 2) return multi_chunk<4, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
     }
     if constexpr (MC > 1) {
         if (nout == 2) return multi_chunk<2, KB, KFIX, BS, LQ, VAR>(a, P, s, cb, lds32);
@@ -1522,9 +1527,9 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     a.cps_shift = -1;
     for (int sh = 0; sh < 31; ++sh)
         if ((int64_t{1} << sh) == a.chunks_per_stripe) a.cps_shift = sh;
-    // a.rows = the largest output count over the batch's patterns (<= 4)
+    // a.rows = the largest output count over the batch's patterns (<= 8)
     const bool k10 = a.cols == 10;
-    const int mc = a.rows <= 1 ? 1 : (a.rows == 2 ? 2 : 4);
+    const int mc = a.rows <= 1 ? 1 : a.rows == 2 ? 2 : a.rows <= 4 ? 4 : 8;
     const int ncols_pad = k10 ? 10 : ((a.cols + 3) / 4) * 4;
     const size_t lds = static_cast<size_t>(ncols_pad) * (((mc * 5 + 3) / 4) * 4) * 4;
     const dim3 grid(static_cast<unsigned>(a.total_chunks));
@@ -1547,17 +1552,21 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
     if (k10) {
         if (mc == 1) RSAMD_MULTI(10, true, 1);
         else if (mc == 2) RSAMD_MULTI(10, true, 2);
-        else RSAMD_MULTI(10, true, 4);
+        else if (mc == 4) RSAMD_MULTI(10, true, 4);
+        else RSAMD_MULTI(10, true, 8);
     } else {
         if (mc == 1) RSAMD_MULTI(4, false, 1);
         else if (mc == 2) RSAMD_MULTI(4, false, 2);
-        else RSAMD_MULTI(4, false, 4);
+        else if (mc == 4) RSAMD_MULTI(4, false, 4);
+        else RSAMD_MULTI(4, false, 8);
     }
 #undef RSAMD_MULTI
     return hipGetLastError();
 }
 
-int multi_table_dwords(int cols) { return (cols == 10 ? 10 : ((cols + 3) / 4) * 4) * 20; }
+int multi_table_dwords(int cols, int max_out) {
+    return (cols == 10 ? 10 : ((cols + 3) / 4) * 4) * multi_image_rows(max_out) * 5;
+}
 
 // ---------------------------------------------------------------------------
 // GPU planner of rs_reconst_batch_multi (SURVEY.md §8f.1 "a small GPU
@@ -1570,7 +1579,7 @@ int multi_table_dwords(int cols) { return (cols == 10 ? 10 : ((cols + 3) / 4) * 
 // the first d in index order (checkReconst rs.go:264-325): the d - dn
 // surviving data vectors K, then the first dn surviving parity vectors P.
 // The dn lost data vectors L satisfy enc[P][L] D_L = P ^ enc[P][K] D_K, so
-// with Minv = (enc[P][L])^-1 (dn x dn, dn <= 4, Gauss-Jordan in one lane):
+// with Minv = (enc[P][L])^-1 (dn x dn, dn <= nn <= 8, Gauss-Jordan in one lane):
 //   lost data L_l : coef(q) = Minv[l][j]                       (vs[q] = P_j)
 //                             ^_j Minv[l][j] * enc[P_j][vs[q]]  (vs[q] in K)
 //   lost parity v : coef(q) = enc[v][vs[q]] (vs[q] < d) ^ ^_l enc[v][L_l] * coef_l(q)
@@ -1602,12 +1611,17 @@ __device__ __forceinline__ uint32_t gf_mul_alu(uint32_t x, uint32_t y) {
     return r;
 }
 
+// N: the most outputs a pattern of the launch has, rounded to 4 or 8 (the
+// register arrays below are N wide: a batch of 1-4-loss patterns keeps the
+// small instance)
+template <int N>
 __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs a) {
     __shared__ uint8_t lg[256], ex[512];
     __shared__ uint16_t s_vs[kPlanWaves][256];
-    __shared__ uint8_t s_rows[kPlanWaves][4][256];  // enc rows P_0..P_{dn-1}, then the lost parity rows (nn <= 4)
-    __shared__ uint8_t s_minv[kPlanWaves][4][4];
-    __shared__ int s_nr[kPlanWaves][4];
+    __shared__ uint8_t s_rows[kPlanWaves][N][256];  // enc rows P_0..P_{dn-1}, then the lost parity rows (nn <= N)
+    __shared__ uint8_t s_minv[kPlanWaves][N][N];
+    __shared__ uint8_t s_gj[kPlanWaves][N][2 * N];  // the wave's Gauss-Jordan matrix
+    __shared__ int s_nr[kPlanWaves][N];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = a.gf[i];
     for (int i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = a.gf[256 + i];
     const int w = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
@@ -1637,7 +1651,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
             }
             if (need) {
                 const int rk = nn + __popcll(bn & lt);
-                if (rk < 4) s_nr[w][rk] = v;
+                if (rk < N) s_nr[w][rk] = v;
             }
             ns += __popcll(bs);
             nn += __popcll(bn);
@@ -1651,64 +1665,56 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
     //    (the rows' loads of one lane issued together, then stored)
     if (live)
         for (int q = lane; q < d; q += 64) {
-            uint8_t v[4];
+            uint8_t v[N];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < N; ++k) {
                 const int row = k < dn ? s_vs[w][d - dn + k] : s_nr[w][k < nn ? k : 0];
                 v[k] = k < nn ? a.enc[static_cast<size_t>(row) * d + q] : 0;
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) s_rows[w][k][q] = v[k];
+            for (int k = 0; k < N; ++k) s_rows[w][k][q] = v[k];
         }
     __syncthreads();
-    // 3. Minv (lane 0): [M | I] -> [I | Minv], M[j][l] = enc[P_j][L_l]; the
-    //    loops unrolled to 4 x 8 with guards so the matrix stays in registers
-    if (live && lane == 0 && dn > 0) {
-        uint32_t m[4][8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                m[j][l] = (j < dn && l < dn) ? s_rows[w][j][s_nr[w][l]] : 0u;
-                m[j][4 + l] = j == l ? 1u : 0u;
-            }
+    // 3. Minv: [M | I] -> [I | Minv], M[j][l] = enc[P_j][L_l], Gauss-Jordan
+    //    by the whole wave on an N x 2N matrix in LDS (a lane per entry and
+    //    step; the wave's LDS reads and writes land in program order, and
+    //    every read of a step is issued before its writes)
+    if (live && dn > 0) {
+        uint8_t(&m)[N][2 * N] = s_gj[w];
+        auto wave_fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+        for (int e = lane; e < N * 2 * N; e += 64) {
+            const int r = e / (2 * N), k = e % (2 * N);
+            m[r][k] = k < N ? ((r < dn && k < dn) ? s_rows[w][r][s_nr[w][k]] : 0) : (k - N == r ? 1 : 0);
+        }
+        wave_fence();
         bool ok = true;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (c >= dn || !ok) break;
-            int pr = -1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (r >= c && r < dn && pr < 0 && m[r][c]) pr = r;
-            if (pr < 0) {
+        for (int c = 0; c < dn; ++c) {
+            const uint64_t piv = __ballot(lane < dn && lane >= c && m[lane < N ? lane : 0][c] != 0);
+            if (!piv) {
                 ok = false;
                 break;
             }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (r > c && r == pr)
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const uint32_t t = m[r][k];
-                        m[r][k] = m[c][k];
-                        m[c][k] = t;
-                    }
-            const uint32_t iv = ex[255 - lg[m[c][c]]];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) m[c][k] = mul(m[c][k], iv);
-#pragma unroll
-            for (int r2 = 0; r2 < 4; ++r2) {
-                if (r2 == c || r2 >= dn) continue;
-                const uint32_t f = m[r2][c];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) m[r2][k] ^= mul(f, m[c][k]);
+            const int pr = __ffsll(static_cast<unsigned long long>(piv)) - 1;
+            if (pr != c && lane < 2 * N) {
+                const uint8_t t = m[pr][lane];
+                m[pr][lane] = m[c][lane];
+                m[c][lane] = t;
             }
+            wave_fence();
+            const uint32_t iv = ex[255 - lg[m[c][c]]];
+            if (lane < 2 * N) m[c][lane] = static_cast<uint8_t>(mul(m[c][lane], iv));
+            wave_fence();
+            for (int e = lane; e < N * 2 * N; e += 64) {
+                const int r = e / (2 * N), k = e % (2 * N);
+                const uint32_t f = m[r][c], pv = m[c][k];
+                if (r != c && r < dn && f) m[r][k] ^= static_cast<uint8_t>(mul(f, pv));
+            }
+            wave_fence();
         }
-#pragma unroll
-        for (int l = 0; l < 4; ++l)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (l < dn && j < dn) s_minv[w][l][j] = ok ? static_cast<uint8_t>(m[l][4 + j]) : 0;
+        for (int e = lane; e < N * N; e += 64) {
+            const int l = e / N, j2 = e % N;
+            if (l < dn && j2 < dn) s_minv[w][l][j2] = ok ? m[l][N + j2] : 0;
+        }
     }
     __syncthreads();
     if (!live) return;  // (no barrier below)
@@ -1717,38 +1723,42 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
     //    perm_table in gf256.hpp; zero past the rows and columns) and the
     //    descriptor
     uint32_t* img = a.tabs + static_cast<size_t>(gi) * a.tdw;
-    const int ncol = a.tdw / 20;
+    const int cw = a.img_rows * 5;  // dwords per image column
+    const int ncol = a.tdw / cw;
     for (int q = lane; q < ncol; q += 64) {
-        // (every loop over rows unrolled to 4 with guards: the coefficients
+        // (every loop over rows unrolled to N with guards: the coefficients
         // stay in registers, no scratch)
-        uint32_t coef[4] = {0, 0, 0, 0};
+        uint32_t coef[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) coef[r] = 0;
         if (q < d) {
             const int u = s_vs[w][q];
 #pragma unroll
-            for (int l = 0; l < 4; ++l) {
+            for (int l = 0; l < N; ++l) {
                 if (l >= dn) break;
                 uint32_t c = 0;
                 if (u >= d) {
                     c = s_minv[w][l][q - (d - dn)];
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < N; ++j)
                         if (j < dn) c ^= mul(s_minv[w][l][j], s_rows[w][j][u]);
                 }
                 coef[l] = c;
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < N; ++r) {
                 if (r < dn || r >= nn) continue;
                 uint32_t c = u < d ? s_rows[w][r][u] : 0u;
 #pragma unroll
-                for (int l = 0; l < 4; ++l)
+                for (int l = 0; l < N; ++l)
                     if (l < dn) c ^= mul(s_rows[w][r][s_nr[w][l]], coef[l]);
                 coef[r] = c;
             }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < N; ++r) {
+            if (r >= a.img_rows) break;  // (img_rows == N)
             uint32_t cb[8];
             gf_basis(coef[r], cb);
             // c * e for the 3-bit groups as XORs of the basis (e's bits)
@@ -1761,12 +1771,12 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
             t[3] = cb[5] | (cb[5] ^ cb[3]) << 8 | (cb[5] ^ cb[4]) << 16 | (cb[5] ^ b3) << 24;
             t[4] = (cb[6] << 8) | (cb[7] << 16) | ((cb[6] ^ cb[7]) << 24);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) img[q * 20 + r * 5 + k] = t[k];
+            for (int k = 0; k < 5; ++k) img[q * cw + r * 5 + k] = t[k];
         }
     }
     PatternDesc* P = a.descs + gi;
     for (int i = lane; i < 256; i += 64) P->in_idx[i] = i < d ? s_vs[w][i] : 0;
-    if (lane < 4) P->out_idx[lane] = lane < nn ? static_cast<uint32_t>(s_nr[w][lane]) : 0u;
+    if (lane < N) P->out_idx[lane] = lane < nn ? static_cast<uint32_t>(s_nr[w][lane]) : 0u;
     if (lane == 0) {
         P->tab_off = static_cast<uint32_t>(gi) * static_cast<uint32_t>(a.tdw);
         P->nout = static_cast<uint32_t>(nn);
@@ -1777,7 +1787,10 @@ hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream) {
     if (a.npat <= 0) return hipSuccess;
     (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
     const unsigned grid = static_cast<unsigned>((a.npat + kPlanWaves - 1) / kPlanWaves);
-    hipLaunchKernelGGL(gf_plan_multi, dim3(grid), dim3(64 * kPlanWaves), 0, stream, a);
+    if (a.img_rows > 4)
+        hipLaunchKernelGGL(gf_plan_multi<8>, dim3(grid), dim3(64 * kPlanWaves), 0, stream, a);
+    else
+        hipLaunchKernelGGL(gf_plan_multi<4>, dim3(grid), dim3(64 * kPlanWaves), 0, stream, a);
     return hipGetLastError();
 }
 

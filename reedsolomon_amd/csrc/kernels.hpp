@@ -44,20 +44,23 @@ struct MatmulArgs {
 
 // Multi-pattern mode: one pattern of rs_reconst_batch_multi.  tab_off is the
 // dword offset (in MatmulArgs::tables) of the pattern's LDS image:
-// multi_table_dwords(cols) dwords laid out [column][4 rows x 5 dwords], zero
-// padded (rows >= nout, columns >= cols).
+// multi_table_dwords(cols, max_out) dwords laid out [column][R rows x 5
+// dwords], R = multi_image_rows(max_out) (4, or 8 when a pattern of the batch
+// has more than 4 outputs), zero padded (rows >= nout, columns >= cols).
+constexpr int kMultiMaxOut = 8;
 struct PatternDesc {
     uint32_t tab_off;
-    uint32_t nout;        // <= 4 outputs
+    uint32_t nout;        // <= kMultiMaxOut outputs
     uint16_t in_idx[256];  // the d input vectors (indexes into MatmulArgs::ptr; d+p <= 256)
-    uint32_t out_idx[4];  // the output vectors
+    uint32_t out_idx[kMultiMaxOut];  // the output vectors
 };
-int multi_table_dwords(int cols);
+__host__ __device__ inline int multi_image_rows(int max_out) { return max_out > 4 ? 8 : 4; }
+int multi_table_dwords(int cols, int max_out);
 hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t* stripe_pat, hipStream_t stream);
 // GPU planner of the multi-pattern kernel's inputs (gf_plan_multi): for each
 // distinct need mask, the pattern's table image (tdw dwords at tabs + i * tdw)
 // and its descriptor, as reconst_multi builds them on the host.  Every pattern
-// must need 1-4 vectors, none past d + p (validated on the host).
+// must need 1-kMultiMaxOut vectors, none past d + p (validated on the host).
 struct PlanArgs {
     const uint64_t* masks;  // npat x words need masks
     const uint8_t* enc;     // (d + p) x d encoding matrix (matrix.go:37-54)
@@ -65,6 +68,7 @@ struct PlanArgs {
     uint32_t* tabs;
     PatternDesc* descs;
     int npat, words, d, p, tdw;
+    int img_rows;           // multi_image_rows(the batch's most outputs): 4 or 8
 };
 hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream);
 

@@ -879,8 +879,8 @@ def test_xor_batch(rslib, torch_dev):
 
 @pytest.mark.parametrize("d,p,n", [(10, 4, 8192), (6, 3, 4096), (10, 4, 65536), (8, 6, 4096), (3, 2, 16)])
 def test_reconst_batch_multi_single_launch(rslib, torch_dev, d, p, n):
-    """Aligned lengths take the single-launch pattern kernel (nout <= 4);
-    8+6 also has patterns with 5-6 outputs (grouped fallback)."""
+    """Aligned lengths take the single-launch pattern kernel (nout <= 8: 8+6's
+    patterns of 5-6 outputs too, in the image with 8 rows per column)."""
     torch = torch_dev
     S = 200
     r = rslib.New(d, p)
@@ -902,14 +902,14 @@ def test_reconst_batch_multi_single_launch(rslib, torch_dev, d, p, n):
     assert torch.equal(data, ref_d) and torch.equal(parity, ref_p)
 
 
-def _distinct_patterns(d, p, count, seed):
-    """`count` distinct need masks of 1-4 erasures (every one of them when
+def _distinct_patterns(d, p, count, seed, kmax=4):
+    """`count` distinct need masks of 1-kmax erasures (every one of them when
     count is the number that exists), as Python ints."""
     from itertools import combinations
     from math import comb
 
     n = d + p
-    kmax = min(4, p)
+    kmax = min(kmax, p)
     total = sum(comb(n, k) for k in range(1, kmax + 1))
     if count >= total:
         return [sum(1 << v for v in c) for k in range(1, kmax + 1) for c in combinations(range(n), k)]
@@ -924,19 +924,22 @@ def _distinct_patterns(d, p, count, seed):
     return out
 
 
-@pytest.mark.parametrize("d,p,n,npat", [(10, 4, 8192, 1470), (100, 28, 4096, 300), (6, 3, 16, 129),
-                                        (32, 32, 1024, 512), (60, 4, 2048, 9)])
-def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat):
+@pytest.mark.parametrize("d,p,n,npat,kmax", [(10, 4, 8192, 1470, 4), (100, 28, 4096, 300, 4), (6, 3, 16, 129, 4),
+                                             (32, 32, 1024, 512, 4), (60, 4, 2048, 9, 4), (10, 8, 4096, 800, 8),
+                                             (20, 12, 1024, 600, 8), (40, 30, 2048 + 16, 100, 8), (8, 6, 64, 6475, 6)])
+def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
     """rs_tune("multi_gpu_plan", n): a batch with at least n distinct erasure
     patterns has its pattern tables and descriptors built on the GPU
     (gf_plan_multi, kernels.hip: the lost data from a dn x dn inverse) instead
     of by the host (the d x d inverse, combined_matrix).  Every pattern of 1-4
     erasures (10+4: all 1,470 of C(14, 1..4), one stripe each; 100+28: 256-bit
-    masks reaching past bit 64) is rebuilt bit-exact through both planners,
-    stripes shuffled, a few stripes untouched."""
+    masks reaching past bit 64), and patterns of up to 8 (10+8, 20+12, 40+30;
+    8+6: all 6,475 of C(14, 1..6)) in the one launch whose tables hold 8 rows,
+    rebuilt bit-exact through both planners, stripes shuffled, a few stripes
+    untouched."""
     torch = torch_dev
     L = rslib.lib()
-    pats = _distinct_patterns(d, p, npat, d * 1000 + p)
+    pats = _distinct_patterns(d, p, npat, d * 1000 + p, kmax)
     assert len(pats) == npat
     S = npat + 3
     rng = np.random.default_rng(npat)

@@ -23,9 +23,9 @@ import torch  # noqa: E402
 import reedsolomon_amd as rs  # noqa: E402
 
 
-def masks_for(d, p, n, seed):
-    """n distinct masks of 1-4 erasures (all of them when n is their count)."""
-    kmax = min(4, p)
+def masks_for(d, p, n, seed, kmax=4):
+    """n distinct masks of 1-kmax erasures (all of them when n is their count)."""
+    kmax = min(kmax, p)
     total = sum(comb(d + p, k) for k in range(1, kmax + 1))
     if n >= total:
         return [sum(1 << v for v in c) for k in range(1, kmax + 1) for c in combinations(range(d + p), k)]
@@ -43,9 +43,10 @@ def masks_for(d, p, n, seed):
 def main():
     res = {}
     L = rs.lib()
-    for d, p, npat, vec in ((10, 4, 1470, 8192), (10, 4, 1470, 1024), (20, 12, 4096, 1024), (32, 32, 4096, 1024),
-                            (100, 28, 1000, 4096)):
-        masks = masks_for(d, p, npat, d * 100 + p)
+    for d, p, npat, vec, kmax in ((10, 4, 1470, 8192, 4), (10, 4, 1470, 1024, 4), (20, 12, 4096, 1024, 4),
+                                  (32, 32, 4096, 1024, 4), (100, 28, 1000, 4096, 4), (10, 8, 4096, 8192, 8),
+                                  (20, 12, 4096, 1024, 8)):
+        masks = masks_for(d, p, npat, d * 100 + p, kmax)
         S = len(masks)
         arg = masks if d + p > 64 else np.array(masks, dtype=np.uint64)
         nbytes = sum((d + bin(m).count("1")) * vec for m in masks)
@@ -72,7 +73,7 @@ def main():
             row[f"{name}_warm_GiBps"] = round(nbytes / med / 2 ** 30, 1)
             row[f"{name}_us_per_pattern_warm"] = round(med * 1e6 / S, 3)
         L.rs_tune(b"multi_gpu_plan", 8)
-        key = f"{d}+{p} {S} patterns @ {vec}"
+        key = f"{d}+{p} {S} patterns of 1-{kmax} lost @ {vec}"
         res[key] = row
         print(key, row, flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
