@@ -466,9 +466,10 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * per workgroup of the 8-byte-lane kernels: 128 default | 256), "bitslice"
  * (1 default: bit-sliced Encode for the generated 5-8-parity shapes | 0),
  * "multi_gpu_plan" (rs_reconst_batch_multi and its host-batch / group
- * variants: from this many distinct patterns in one call (default 8) the
- * pattern tables are planned on the GPU, one wave per pattern, instead of on
- * the host; 0 = always on the host; patterns of 1-8 erasures on the
+ * variants: from this many distinct patterns in one call the pattern tables
+ * are planned on the GPU, one wave per pattern, instead of on the host;
+ * -1 default = when patterns x d >= 160, where the GPU planner starts to
+ * pay; 0 = always on the host; patterns of 1-8 erasures on the
  * single-launch path only),
  * "bs_block" (lanes per workgroup of the bit-sliced kernels: 64 | 128 | 256;
  * 0 default = 64, or 256 for interleaved stripes of d+p >= 18), "bs_waves"

@@ -219,8 +219,13 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         for (int v = 0; v < d + p && single; ++v)
             single = (reinterpret_cast<uintptr_t>(LayoutAddr{L, d}.ptr(v)) & 15) == 0;
         single = single && (L->data_stripe_stride & 15) == 0 && (L->parity_stripe_stride & 15) == 0;
+        // (the GPU planner costs ~6 us more than the host's for a handful of
+        // patterns and less from ~16 patterns at d = 10, ~8 at 20, ~5 at 32:
+        // profiles/r05/multi_planner_small_counts.log)
         const int gpu_plan = tuning().multi_gpu_plan;
-        if (single && gpu_plan > 0 && keys.size() >= static_cast<size_t>(gpu_plan)) {
+        const bool use_gpu_plan = gpu_plan < 0 ? keys.size() * static_cast<size_t>(d) >= 160
+                                               : gpu_plan > 0 && keys.size() >= static_cast<size_t>(gpu_plan);
+        if (single && use_gpu_plan) {
             // Plan on the GPU (gf_plan_multi, kernels.hip): upload the encoding
             // matrix, the field tables, the distinct masks and the stripe ->
             // pattern map; the planner writes the table images and descriptors

@@ -687,7 +687,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "jit_disk_cache") g_jit_disk_cache = value ? 1 : 0;
         else if (n == "jit_backend") g_jit_backend = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (n == "jit_min_bytes") g_jit_min_bytes = value < 0 ? 0 : static_cast<uint64_t>(value);
-        else if (n == "multi_gpu_plan") t.multi_gpu_plan = value < 0 ? 0 : value;
+        else if (n == "multi_gpu_plan") t.multi_gpu_plan = value < 0 ? -1 : value;
         else if (n == "bs_block") t.bs_block = (value == 64 || value == 128 || value == 256) ? value : 0;
         else if (n == "wide_block") t.wide_block = value == 128 ? 128 : 256;
         else if (n == "wide_single_pass") t.wide_single_pass = value ? 1 : 0;

@@ -74,7 +74,7 @@ LaunchTuning& tuning() {
         // 6.28 TB/s, 8+5 interleaved 6.06 -> 6.53; profiles/r03/ab_bs_waves.log)
         const char* bw = std::getenv("RSAMD_BS_WAVES");
         x.bs_waves = bw ? std::atoi(bw) : 2;
-        x.multi_gpu_plan = 8;
+        x.multi_gpu_plan = -1;
         return x;
     }();
     return t;

@@ -150,7 +150,8 @@ struct LaunchTuning {
     int wide_block;   // 16-byte-unit one-chunk kernels (3-8 rows over runtime columns): lanes (256 | 128)
     int wide_single_pass;  // > 8 rows without a compiled network: single-pass wide kernels (1) | row groups of 8 (0)
     int bs_waves;     // bit-sliced Encode: at most this many waves per SIMD (LDS padding; 0 = as many as fit; default 2)
-    int multi_gpu_plan;  // rs_reconst_batch_multi: plan on the GPU from this many distinct patterns (0 = host)
+    int multi_gpu_plan;  // rs_reconst_batch_multi: plan on the GPU from this many distinct patterns (0 = host,
+                         // -1 = when patterns x d >= 160, where it starts to pay)
 };
 LaunchTuning& tuning();
 

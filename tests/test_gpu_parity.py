@@ -967,7 +967,7 @@ def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
             bad = [s for s in range(S) if not (torch.equal(data[s], ref_d[s]) and torch.equal(parity[s], ref_p[s]))]
             assert not bad, (plan, bad[:5], [bin(masks[s]) for s in bad[:5]])
     finally:
-        L.rs_tune(b"multi_gpu_plan", 8)
+        L.rs_tune(b"multi_gpu_plan", -1)
 
 
 @pytest.mark.parametrize("d,p", [(10, 8), (8, 8), (10, 6)])

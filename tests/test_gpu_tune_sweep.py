@@ -80,7 +80,7 @@ SWEEP = {
     "jit_split_cols": [4, 0],
     "jit_share_cols": [2, -1, 1],
     "table_registry_max": [1, 1 << 14],
-    "multi_gpu_plan": [1, 0, 8],
+    "multi_gpu_plan": [1, 0, 8, -1],
 }
 
 # 20+12: 12 output rows (the wide single-pass kernels, or a compiled network)
@@ -142,6 +142,15 @@ def _check_all(rslib, torch, cases, tag):
         r.reconst_batch(buf, [], lost)
         torch.cuda.synchronize()
         assert np.array_equal(buf.cpu().numpy(), full), (tag, d, p, "reconst_batch")
+        # multi-pattern Reconst: a different erasure set per stripe (the
+        # single launch up to 8 lost vectors, grouped launches beyond)
+        pats = [lost[:1], lost[:max(2, len(lost) // 2)], lost]
+        masks = np.array([sum(1 << v for v in pat) for pat in pats], dtype=np.uint64)
+        for s, pat in enumerate(pats):
+            buf[s, pat] = 0x4D
+        r.reconst_batch_multi(buf[:, :d], buf[:, d:], masks)
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), full), (tag, d, p, "reconst_batch_multi")
         # Update of one data row
         old_t = buf[:, UPD_ROW].clone()
         new_t = torch.from_numpy(new).cuda()

@@ -43,9 +43,13 @@ def masks_for(d, p, n, seed, kmax=4):
 def main():
     res = {}
     L = rs.lib()
-    for d, p, npat, vec, kmax in ((10, 4, 1470, 8192, 4), (10, 4, 1470, 1024, 4), (20, 12, 4096, 1024, 4),
-                                  (32, 32, 4096, 1024, 4), (100, 28, 1000, 4096, 4), (10, 8, 4096, 8192, 8),
-                                  (20, 12, 4096, 1024, 8)):
+    shapes = ((10, 4, 1470, 8192, 4), (10, 4, 1470, 1024, 4), (20, 12, 4096, 1024, 4),
+              (32, 32, 4096, 1024, 4), (100, 28, 1000, 4096, 4), (10, 8, 4096, 8192, 8),
+              (20, 12, 4096, 1024, 8))
+    if "--small" in sys.argv:  # where the GPU planner starts to pay (rs_tune("multi_gpu_plan") threshold)
+        shapes = tuple((d, p, n, vec, 4) for d, p, vec in ((10, 4, 8192), (20, 12, 1024), (32, 32, 1024))
+                       for n in (4, 8, 16, 32, 64, 128))
+    for d, p, npat, vec, kmax in shapes:
         masks = masks_for(d, p, npat, d * 100 + p, kmax)
         S = len(masks)
         arg = masks if d + p > 64 else np.array(masks, dtype=np.uint64)
@@ -65,6 +69,7 @@ def main():
                 torch.cuda.synchronize()
                 walls.append(time.perf_counter() - t0)
             row[f"{name}_cold_ms"] = round(walls[0] * 1e3, 3)
+            # (planner forced: 1 = the GPU whatever the count, 0 = the host)
             warm = sorted(walls[1:])
             med = warm[len(warm) // 2]
             row[f"{name}_warm_median_ms"] = round(med * 1e3, 3)
@@ -72,12 +77,13 @@ def main():
             row[f"{name}_warm_host_median_ms"] = round(sorted(hosts[1:])[len(hosts[1:]) // 2] * 1e3, 3)
             row[f"{name}_warm_GiBps"] = round(nbytes / med / 2 ** 30, 1)
             row[f"{name}_us_per_pattern_warm"] = round(med * 1e6 / S, 3)
-        L.rs_tune(b"multi_gpu_plan", 8)
+        L.rs_tune(b"multi_gpu_plan", -1)
         key = f"{d}+{p} {S} patterns of 1-{kmax} lost @ {vec}"
         res[key] = row
         print(key, row, flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
-    json.dump(res, open("gpurun_out/multi_host_cost.json", "w"), indent=1)
+    json.dump(res, open("gpurun_out/multi_host_cost" + ("_small" if "--small" in sys.argv else "") + ".json", "w"),
+              indent=1)
 
 
 if __name__ == "__main__":
