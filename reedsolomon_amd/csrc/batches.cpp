@@ -222,6 +222,25 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         // (the GPU planner costs ~6 us more than the host's for a handful of
         // patterns and less from ~16 patterns at d = 10, ~8 at 20, ~5 at 32:
         // profiles/r05/multi_planner_small_counts.log)
+        // the one launch over every stripe, from the tables / descriptors /
+        // stripe -> pattern map in device memory (a.rows: the most outputs)
+        auto launch_single = [&](const uint32_t* tabs, const PatternDesc* descs, const int32_t* spat) {
+            MatmulArgs a;
+            std::memset(&a, 0, sizeof a);
+            a.tables = tabs;
+            a.rows = nn_max;
+            a.cols = d;
+            a.nstripes = nstripes;
+            a.len = len;
+            a.ss[0] = L->data_stripe_stride;
+            a.ss[1] = L->parity_stripe_stride;
+            const LayoutAddr A{L, d};
+            for (int v = 0; v < d + p; ++v) {
+                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
+                a.sid[v] = A.sid(v);
+            }
+            return hip_ok(launch_gf_multi(a, descs, spat, st), "multi-pattern kernel launch");
+        };
         const int gpu_plan = tuning().multi_gpu_plan;
         const bool use_gpu_plan = gpu_plan < 0 ? keys.size() * static_cast<size_t>(d) >= 160
                                                : gpu_plan > 0 && keys.size() >= static_cast<size_t>(gpu_plan);
@@ -264,22 +283,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             pa.tdw = tdw;
             pa.img_rows = multi_image_rows(nn_max);
             RS_TRY(hip_ok(launch_gf_plan_multi(pa, st), "multi-pattern planner launch"));
-            MatmulArgs a;
-            std::memset(&a, 0, sizeof a);
-            a.tables = pa.tabs;
-            a.rows = nn_max;
-            a.cols = d;
-            a.nstripes = nstripes;
-            a.len = len;
-            a.ss[0] = L->data_stripe_stride;
-            a.ss[1] = L->parity_stripe_stride;
-            const LayoutAddr A{L, d};
-            for (int v = 0; v < d + p; ++v) {
-                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
-                a.sid[v] = A.sid(v);
-            }
-            return hip_ok(launch_gf_multi(a, pa.descs, reinterpret_cast<const int32_t*>(dev + enc_b + gf_b + mask_b), st),
-                          "multi-pattern kernel launch");
+            return launch_single(pa.tabs, pa.descs, reinterpret_cast<const int32_t*>(dev + enc_b + gf_b + mask_b));
         }
         struct Group {
             ReconstPlan pl;
@@ -307,8 +311,6 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             const size_t tab_bytes = static_cast<size_t>(npat) * tdw * 4;
             const size_t desc_bytes = static_cast<size_t>(npat) * sizeof(PatternDesc);
             const size_t pat_bytes = static_cast<size_t>(nstripes) * 4;
-            int nout_max = 0;
-            for (const Group& gr : plan) nout_max = gr.pl.nnr > nout_max ? gr.pl.nnr : nout_max;
             UploadLease lease(rs);
             uint8_t* host = nullptr;
             RS_TRY(lease.acquire(tab_bytes + desc_bytes + pat_bytes, &host));
@@ -332,23 +334,8 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             }
             uint8_t* dev = nullptr;
             RS_TRY(lease.upload(st, &dev));
-            MatmulArgs a;
-            std::memset(&a, 0, sizeof a);
-            a.tables = reinterpret_cast<const uint32_t*>(dev);
-            a.rows = nout_max;
-            a.cols = d;
-            a.nstripes = nstripes;
-            a.len = len;
-            a.ss[0] = L->data_stripe_stride;
-            a.ss[1] = L->parity_stripe_stride;
-            const LayoutAddr A{L, d};
-            for (int v = 0; v < d + p; ++v) {
-                a.ptr[v] = reinterpret_cast<uint64_t>(A.ptr(v));
-                a.sid[v] = A.sid(v);
-            }
-            return hip_ok(launch_gf_multi(a, reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
-                                          reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes), st),
-                          "multi-pattern kernel launch");
+            return launch_single(reinterpret_cast<const uint32_t*>(dev), reinterpret_cast<const PatternDesc*>(dev + tab_bytes),
+                                 reinterpret_cast<const int32_t*>(dev + tab_bytes + desc_bytes));
         }
 
         // stripe ids grouped by pattern, in stripe order within a pattern
