@@ -91,6 +91,11 @@ struct rs_codec {
     std::atomic<uint64_t> cache_n{0};
     std::mutex cache_mu;
     std::unordered_map<uint64_t, std::vector<uint8_t>> cache;
+    // codes beyond 64 vectors (no reference cache, rs.go:70-74): the combined
+    // Reconst matrices of recent patterns, keyed by the survivor and need
+    // bitmaps (codec.cpp combined_matrix; bounded, cleared when full)
+    std::mutex wide_mu;
+    std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
 
     // device state (created lazily; the handle works on a GPU-less host)
     std::mutex dev_mu;

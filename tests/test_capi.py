@@ -160,6 +160,35 @@ def test_reconst_matrix_and_cache(rslib, orc):
                                           if any(i < d for i in lost)})
 
 
+@pytest.mark.parametrize("d,p,nlost", [(40, 30, 30), (100, 28, 28), (100, 28, 3), (200, 56, 56), (129, 127, 100),
+                                        (200, 56, 1)])
+def test_wide_reconst_matrix_equals_full_inverse(rslib, orc, d, p, nlost):
+    """Codes beyond 64 vectors (no reference cache) build Reconst matrices
+    from the u x u block that couples the unknown data to the parity
+    survivors standing in for them (codec.cpp unknown_data_rows); every row
+    equals the full d x d inverse's row (the oracle's restated matrix.go
+    Gauss-Jordan), for survivor lists in and out of index order and a needed
+    survivor (its unit row); a repeated survivor is singular as before."""
+    rng = np.random.default_rng(d * 7 + nlost)
+    r = rslib.New(d, p)
+    em = orc.make_encode_matrix(d, p).reshape(d + p, d)
+    for trial in range(3):
+        lost = sorted(int(v) for v in rng.choice(d, nlost, replace=False))
+        par = sorted(int(v) for v in rng.choice(np.arange(d, d + p), nlost, replace=False))
+        surv = [i for i in range(d) if i not in lost] + par
+        if trial == 1:
+            surv = [int(v) for v in rng.permutation(surv)]  # any order
+        rc, inv = orc.invert(np.ascontiguousarray(em[surv]).ravel(), d)
+        assert rc == 0
+        need = lost + [min(x for x in surv if x < d)] if nlost < d else lost  # (+ a survivor: its unit row)
+        got = r.reconst_matrix(surv, need).reshape(len(need), d)
+        exp = inv.reshape(d, d)[need]
+        assert np.array_equal(got, exp), (d, p, nlost, trial)
+    with pytest.raises(rslib.ErrSingularMatrix):
+        r.reconst_matrix([0] + list(range(0, d - 1)), [d - 1])
+    assert r.inverse_cache_size() == 0
+
+
 def test_cache_disabled_when_wide(rslib):  # rs.go:70 (d+p <= 64 only)
     r = rslib.New(40, 30)
     r.reconst_matrix(list(range(1, 41)), [0])
