@@ -54,6 +54,14 @@ int main(int argc, char** argv) {
                 CHECK_RC(rs_reconst_matrix(rs, vs, nd, k, out));
             }
             (void)rs_inverse_cache_key(surv, ns < 64 ? ns : 64);
+            if (d > 0 && d <= 80) {
+                /* any survivor list (repeats, parity only, out of order): the
+                 * full inverse (d + p <= 64) or the reduced system beyond */
+                int sd[80], nd2[80], k2 = rr(0, d < 8 ? d : 8);
+                for (i = 0; i < d; ++i) sd[i] = rr(0, 3) ? i : rr(0, d + p - 1);
+                for (i = 0; i < k2; ++i) nd2[i] = rr(0, d - 1);
+                CHECK_RC(rs_reconst_matrix(rs, sd, nd2, k2, out));
+            }
         }
         {
             uint8_t* v[80];
