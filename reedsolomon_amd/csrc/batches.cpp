@@ -125,13 +125,92 @@ int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vec
 
 namespace {
 typedef std::array<uint64_t, 4> Mask256;
-struct Mask256Hash {
-    size_t operator()(const Mask256& m) const {
+
+// Group stripes by erasure pattern (host, O(S)): pat_of[s] = the pattern
+// index of stripe s (-1 for a zero mask), keys / counts per pattern in
+// first-seen order.  Batches hold few distinct patterns, often in runs: the
+// previous stripe's pattern, then a linear scan while there are at most kScan
+// patterns, then an open-addressing hash of pattern indexes holding every
+// pattern.  W is the mask width in words (1 or 4), so the common one-word
+// masks compare and hash as one integer (a node-based map cost ~150 ns per new
+// pattern, 4-word keys with a 16-key scan ahead of the hash ~80: most of a
+// 1,470-pattern call once the GPU plans the patterns).  Returns
+// RS_ERR_ILLEGAL_VECTS for a bit at or above nvec.
+template <int W>
+int group_patterns(const uint64_t* m, int nstripes, int nvec, std::vector<int32_t>& pat_of, std::vector<Mask256>& out,
+                   std::vector<size_t>& counts) {
+    typedef std::array<uint64_t, W> Key;
+    auto hash = [](const Key& k) {
         uint64_t h = 0x9E3779B97F4A7C15ull;
-        for (uint64_t w : m) h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
-        return static_cast<size_t>(h ^ (h >> 31));
+        for (uint64_t w : k) h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+        // a product's low bits see only the low bits of its input: fold the
+        // high half down twice so a code's top vectors (bits 32-63 for 32+32)
+        // reach the slot index too
+        h = (h ^ (h >> 32)) * 0x94D049BB133111EBull;
+        return static_cast<size_t>(h ^ (h >> 32));
+    };
+    uint64_t top[W];  // bits a stripe may set, per word
+    for (int w = 0; w < W; ++w) {
+        const int lo = w * 64;
+        top[w] = nvec >= lo + 64 ? ~uint64_t{0} : nvec <= lo ? 0 : (uint64_t{1} << (nvec - lo)) - 1;
     }
-};
+    std::vector<Key> keys;
+    std::vector<int32_t> slots;  // pattern index per hash slot, -1 = empty (power-of-two size)
+    auto slot_of = [&](const Key& key) -> size_t {  // the key's slot, or the empty one it would take
+        size_t h = hash(key) & (slots.size() - 1);
+        while (slots[h] >= 0 && keys[static_cast<size_t>(slots[h])] != key) h = (h + 1) & (slots.size() - 1);
+        return h;
+    };
+    auto rehash = [&](size_t size) {  // every pattern into a table of `size` slots
+        slots.assign(size, -1);
+        for (size_t k = 0; k < keys.size(); ++k) slots[slot_of(keys[k])] = static_cast<int32_t>(k);
+    };
+    constexpr int kScan = 16;
+    int last = -1;
+    for (int s = 0; s < nstripes; ++s) {
+        Key key;
+        uint64_t any = 0, bad = 0;
+        for (int w = 0; w < W; ++w) {
+            key[w] = m[static_cast<size_t>(s) * W + w];
+            any |= key[w];
+            bad |= key[w] & ~top[w];
+        }
+        if (!any) continue;
+        if (bad) return RS_ERR_ILLEGAL_VECTS;
+        int gi = -1;
+        if (last >= 0 && keys[static_cast<size_t>(last)] == key) {
+            gi = last;
+        } else {
+            const int n = static_cast<int>(keys.size());
+            size_t h = 0;
+            if (slots.empty()) {
+                for (int k = 0; k < n && gi < 0; ++k)
+                    if (keys[static_cast<size_t>(k)] == key) gi = k;
+            } else {
+                h = slot_of(key);
+                gi = slots[h];
+            }
+            if (gi < 0) {
+                gi = n;
+                keys.push_back(key);
+                counts.push_back(0);
+                if (!slots.empty() && 2 * (n + 1) <= static_cast<int>(slots.size()))
+                    slots[h] = gi;
+                else if (n + 1 >= kScan)  // build at kScan patterns, then double at load 1/2
+                    rehash(slots.empty() ? 256 : slots.size() * 2);
+            }
+        }
+        pat_of[static_cast<size_t>(s)] = gi;
+        ++counts[static_cast<size_t>(gi)];
+        last = gi;
+    }
+    out.resize(keys.size());
+    for (size_t k = 0; k < keys.size(); ++k) {
+        out[k] = Mask256{};
+        for (int w = 0; w < W; ++w) out[k][w] = keys[k][w];
+    }
+    return RS_OK;
+}
 }  // namespace
 
 namespace rsamd {
@@ -144,57 +223,14 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         const int d = rs->d, p = rs->p;
         if (d + p > 64 * masks.words) return RS_ERR_INVAL;  // the mask cannot name every vector
         if (len == 0) return RS_ERR_ZERO_VECT_SIZE;
-        // Group stripes by erasure pattern (host, O(S)); validate every pattern
-        // before any launch.  Batches hold few distinct patterns, often in runs:
-        // the previous stripe's pattern, then a scan of the first 16 patterns,
-        // then an open-addressing hash of pattern indexes (a node-based map
-        // cost ~150 ns per new pattern, most of a 1,470-pattern call once the
-        // GPU plans the patterns).
+        // Group stripes by erasure pattern and validate every pattern before
+        // any launch (group_patterns above).
         std::vector<int32_t> pat_of(static_cast<size_t>(nstripes), -1);
         std::vector<Mask256> keys;
         std::vector<size_t> counts;
-        std::vector<int32_t> slots;  // pattern index per hash slot, -1 = empty (power-of-two size)
-        const Mask256Hash hasher;
-        auto slot_of = [&](const Mask256& key) -> size_t {  // the key's slot, or the empty one it would take
-            size_t h = hasher(key) & (slots.size() - 1);
-            while (slots[h] >= 0 && keys[static_cast<size_t>(slots[h])] != key) h = (h + 1) & (slots.size() - 1);
-            return h;
-        };
-        int last = -1;
-        constexpr int kScan = 16;
-        for (int s = 0; s < nstripes; ++s) {
-            if (!masks.any(s)) continue;
-            if (masks.beyond(s, d + p)) return RS_ERR_ILLEGAL_VECTS;
-            Mask256 key{};
-            for (int w = 0; w < masks.words; ++w) key[w] = masks.row(s)[w];
-            int gi = -1;
-            if (last >= 0 && keys[last] == key) {
-                gi = last;
-            } else {
-                const int n = static_cast<int>(keys.size());
-                for (int k = 0; k < n && k < kScan && gi < 0; ++k)
-                    if (keys[k] == key) gi = k;
-                size_t h = 0;
-                if (gi < 0 && n >= kScan) {
-                    if (slots.empty() || 2 * (n - kScan + 1) > static_cast<int>(slots.size())) {
-                        // (re)build at load <= 1/2 from the patterns past the scanned ones
-                        slots.assign(slots.empty() ? 256 : slots.size() * 2, -1);
-                        for (int k = kScan; k < n; ++k) slots[slot_of(keys[static_cast<size_t>(k)])] = k;
-                    }
-                    h = slot_of(key);
-                    if (slots[h] >= 0) gi = slots[h];
-                }
-                if (gi < 0) {
-                    gi = n;
-                    keys.push_back(key);
-                    counts.push_back(0);
-                    if (gi >= kScan) slots[h] = gi;
-                }
-            }
-            pat_of[s] = gi;
-            ++counts[gi];
-            last = gi;
-        }
+        const int rc_g = masks.words == 1 ? group_patterns<1>(masks.m, nstripes, d + p, pat_of, keys, counts)
+                                          : group_patterns<4>(masks.m, nstripes, d + p, pat_of, keys, counts);
+        if (rc_g) return rc_g;
         if (keys.empty()) return RS_OK;
         // Every pattern's plan_reconst error before any device work: with no
         // survivor list the needed vectors are the mask's, and more than p of

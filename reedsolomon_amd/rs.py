@@ -511,13 +511,11 @@ def _masks_for(need_masks, S: int, nvec: int, fn64: str):
         raise TypeError("need_masks must hold one mask per stripe")
     if nvec <= 64 and all(0 <= v < (1 << 64) for v in vals):
         return np.asarray(vals, dtype=np.uint64), fn64
-    m = np.zeros((S, 4), np.uint64)
-    for s, v in enumerate(vals):
-        if v < 0 or v >> 256:
-            raise ErrIllegalVects()
-        for w in range(4):
-            m[s, w] = (v >> (64 * w)) & 0xFFFFFFFFFFFFFFFF
-    return m, fn64 + "256"
+    try:  # 32 little-endian bytes per mask = 4 words, vector v at bit v % 64 of word v // 64
+        raw = b"".join(v.to_bytes(32, "little") for v in vals)
+    except OverflowError:  # negative, or a bit past 255
+        raise ErrIllegalVects() from None
+    return np.frombuffer(raw, dtype="<u8").astype(np.uint64).reshape(S, 4), fn64 + "256"
 
 
 def host_device_pointer(ptr: int, nbytes: int) -> int:

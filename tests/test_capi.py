@@ -389,6 +389,27 @@ def test_multi_pattern_mask_validation_wide(rslib):
                                                 m.ctypes.data_as(u64p)) == 6
     finally:
         L.rs_free(h)
+    # 64-bit masks through the hashed grouping (thousands of distinct
+    # patterns, repeats, runs): one bad stripe anywhere fails the whole call
+    from itertools import combinations
+
+    for d, p in ((10, 4), (32, 32)):
+        assert L.rs_new(d, p, -1, ctypes.byref(h)) == 0
+        try:
+            lay = RSLayout(0x1000, 1 << 20, 4096, 0x2000, 1 << 20, 4096)
+            good = [sum(1 << v for v in c) for k in (1, 2, 3) for c in combinations(range(d + p), k)][:3000]
+            good = np.array(good + good[::-1] + [good[7]] * 50, dtype=np.uint64)
+            for at, bad, rc in ((len(good) - 1, 1 << (d + p), 1), (len(good) // 2, (1 << (p + 1)) - 1, 6), (5, 0, 14)):
+                if d + p == 64 and rc == 1:
+                    continue  # every bit of a 64-bit mask is a vector of 32+32
+                m = good.copy()
+                if bad:
+                    m[at] = np.uint64(bad)
+                # rc 14: every mask valid, so the call gets as far as the device (none here)
+                assert L.rs_reconst_batch_multi(h, ctypes.byref(lay), len(m), 4096, m.ctypes.data_as(u64p),
+                                                None) in ((rc,) if rc != 14 else (14, 0)), (d, p, at, bad)
+        finally:
+            L.rs_free(h)
     # small codecs keep the 64-bit API
     m, fn = rslib.rs._masks_for([1, 2, 3], 3, 14, "rs_reconst_batch_multi")
     assert fn == "rs_reconst_batch_multi" and m.dtype == np.uint64 and m.shape == (3,)
