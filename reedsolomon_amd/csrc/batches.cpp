@@ -281,35 +281,35 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         const bool use_gpu_plan = gpu_plan < 0 ? keys.size() * static_cast<size_t>(d) >= 160
                                                : gpu_plan > 0 && keys.size() >= static_cast<size_t>(gpu_plan);
         if (single && use_gpu_plan) {
-            // Plan on the GPU (gf_plan_multi, kernels.hip): upload the encoding
-            // matrix, the field tables, the distinct masks and the stripe ->
-            // pattern map; the planner writes the table images and descriptors
-            // behind them in the same device slot, then the multi kernel runs.
+            // Plan on the GPU (gf_plan_multi, kernels.hip): upload the field
+            // tables, the distinct masks and the stripe -> pattern map (the
+            // encoding matrix's parity rows are Cauchy, so the planner derives
+            // its entries from the tables); the planner writes the table images
+            // and descriptors behind them in the same device slot, then the
+            // multi kernel runs.
             const int npat = static_cast<int>(keys.size());
             const int tdw = multi_table_dwords(d, nn_max);
             auto al16 = [](size_t x) { return (x + 15) & ~size_t{15}; };
-            const size_t enc_b = al16(static_cast<size_t>(d + p) * d), gf_b = 768;
+            const size_t gf_b = 768;
             const size_t mask_b = al16(static_cast<size_t>(npat) * masks.words * 8);
             const size_t pat_b = al16(static_cast<size_t>(nstripes) * 4);
-            const size_t head = enc_b + gf_b + mask_b + pat_b;
+            const size_t head = gf_b + mask_b + pat_b;
             const size_t tab_b = static_cast<size_t>(npat) * tdw * 4;
             const size_t desc_b = static_cast<size_t>(npat) * sizeof(PatternDesc);
             UploadLease lease(rs);
             uint8_t* host = nullptr;
             RS_TRY(lease.acquire(head, &host, head + tab_b + desc_b));
-            std::memcpy(host, rs->enc.data(), static_cast<size_t>(d + p) * d);
-            std::memcpy(host + enc_b, gf().log, 256);
-            std::memcpy(host + enc_b + 256, gf().exp, 512);
-            uint64_t* hm = reinterpret_cast<uint64_t*>(host + enc_b + gf_b);
+            std::memcpy(host, gf().log, 256);
+            std::memcpy(host + 256, gf().exp, 512);
+            uint64_t* hm = reinterpret_cast<uint64_t*>(host + gf_b);
             for (int gi = 0; gi < npat; ++gi)
                 for (int w = 0; w < masks.words; ++w) hm[static_cast<size_t>(gi) * masks.words + w] = keys[gi][w];
-            std::memcpy(host + enc_b + gf_b + mask_b, pat_of.data(), static_cast<size_t>(nstripes) * 4);
+            std::memcpy(host + gf_b + mask_b, pat_of.data(), static_cast<size_t>(nstripes) * 4);
             uint8_t* dev = nullptr;
             RS_TRY(lease.upload(st, &dev));
             PlanArgs pa;
-            pa.enc = dev;
-            pa.gf = dev + enc_b;
-            pa.masks = reinterpret_cast<const uint64_t*>(dev + enc_b + gf_b);
+            pa.gf = dev;
+            pa.masks = reinterpret_cast<const uint64_t*>(dev + gf_b);
             pa.tabs = reinterpret_cast<uint32_t*>(dev + head);
             pa.descs = reinterpret_cast<PatternDesc*>(dev + head + tab_b);
             pa.npat = npat;
@@ -319,7 +319,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             pa.tdw = tdw;
             pa.img_rows = multi_image_rows(nn_max);
             RS_TRY(hip_ok(launch_gf_plan_multi(pa, st), "multi-pattern planner launch"));
-            return launch_single(pa.tabs, pa.descs, reinterpret_cast<const int32_t*>(dev + enc_b + gf_b + mask_b));
+            return launch_single(pa.tabs, pa.descs, reinterpret_cast<const int32_t*>(dev + gf_b + mask_b));
         }
         struct Group {
             ReconstPlan pl;

@@ -1569,25 +1569,35 @@ int multi_table_dwords(int cols, int max_out) {
 }
 
 // ---------------------------------------------------------------------------
-// GPU planner of rs_reconst_batch_multi (SURVEY.md §8f.1 "a small GPU
-// Gauss-Jordan"): one wave per distinct erasure pattern writes the table
-// image and descriptor that reconst_multi (batches.cpp) would otherwise build
-// on the host (plan_reconst, the inverse, combined_matrix, perm_table), so a
-// batch whose stripes carry hundreds of patterns does not wait for the host.
+// GPU planner of rs_reconst_batch_multi: one wave per
+// distinct erasure pattern writes the table image and descriptor that
+// reconst_multi (batches.cpp) would otherwise build on the host (plan_reconst,
+// the inverse, combined_matrix, perm_table), so a batch whose stripes carry
+// hundreds of patterns does not wait for the host.
 //
 // With no survivor list the survivors are every vector not needed, vs[0..d)
 // the first d in index order (checkReconst rs.go:264-325): the d - dn
 // surviving data vectors K, then the first dn surviving parity vectors P.
 // The dn lost data vectors L satisfy enc[P][L] D_L = P ^ enc[P][K] D_K, so
-// with Minv = (enc[P][L])^-1 (dn x dn, dn <= nn <= 8, Gauss-Jordan in one lane):
+// with Minv = (enc[P][L])^-1 (dn x dn, dn <= nn <= 8):
 //   lost data L_l : coef(q) = Minv[l][j]                       (vs[q] = P_j)
 //                             ^_j Minv[l][j] * enc[P_j][vs[q]]  (vs[q] in K)
 //   lost parity v : coef(q) = enc[v][vs[q]] (vs[q] < d) ^ ^_l enc[v][L_l] * coef_l(q)
 // A vector's coefficients over d independent survivors are unique, so these
 // are the rows of the host's combined matrix (rows of the inverse of the
-// d x d survivor submatrix, codec.cpp) byte for byte.  Every d x d row
-// submatrix of [I; Cauchy] is invertible, so a zero pivot cannot occur; the
-// code still leaves such a pattern's rows zero rather than loop or fault.
+// d x d survivor submatrix, codec.cpp) byte for byte.
+//
+// The parity rows are Cauchy (matrix.go:37-54, codec.cpp make_encode_matrix):
+// enc[i][j] = 1 / (i ^ j) for a parity row i and a data column j, so every
+// entry the planner needs is an inverse from the field tables, and
+// enc[P][L] is the Cauchy matrix of x_j = P_j, y_l = L_l, whose inverse has a
+// closed form (in characteristic 2, where minus is plus):
+//   Minv[l][j] = prod_k (x_j + y_k) * prod_k (x_k + y_l)
+//              / ((x_j + y_l) * prod_{k != j} (x_j + x_k) * prod_{k != l} (y_l + y_k))
+// (every factor is non-zero: the x are distinct parity indexes, the y
+// distinct data indexes).  A lane per entry sums the factors' logarithms: no
+// Gauss-Jordan chain, no encoding-matrix reads.  tests/test_gpu_parity.py
+// compares every planned row with the oracle's inverse.
 // ---------------------------------------------------------------------------
 constexpr int kPlanWaves = 4;
 
@@ -1599,36 +1609,22 @@ __device__ __forceinline__ void gf_basis(uint32_t c, uint32_t (&cb)[8]) {
 #pragma unroll
     for (int b = 1; b < 8; ++b) cb[b] = ((cb[b - 1] << 1) ^ ((cb[b - 1] & 0x80u) ? 0x11du : 0u)) & 0xffu;
 }
-// x * y in registers (shift-and-add with the 0x11d reduction): no LDS table
-// round trips in the planner's dependent chains
-__device__ __forceinline__ uint32_t gf_mul_alu(uint32_t x, uint32_t y) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        r ^= (y >> b & 1u) ? x : 0u;
-        x = ((x << 1) ^ ((x & 0x80u) ? 0x11du : 0u)) & 0xffu;
-    }
-    return r;
-}
 
 // N: the most outputs a pattern of the launch has, rounded to 4 or 8 (the
-// register arrays below are N wide: a batch of 1-4-loss patterns keeps the
-// small instance)
+// image rows; a batch of 1-4-loss patterns keeps the small instance)
 template <int N>
 __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs a) {
     __shared__ uint8_t lg[256], ex[512];
     __shared__ uint16_t s_vs[kPlanWaves][256];
-    __shared__ uint8_t s_rows[kPlanWaves][N][256];  // enc rows P_0..P_{dn-1}, then the lost parity rows (nn <= N)
-    __shared__ uint8_t s_minv[kPlanWaves][N][N];
-    __shared__ uint8_t s_gj[kPlanWaves][N][2 * N];  // the wave's Gauss-Jordan matrix
     __shared__ int s_nr[kPlanWaves][N];
+    __shared__ uint8_t s_minv[kPlanWaves][N][N];
+    __shared__ uint8_t s_coef[kPlanWaves][N][256];  // the lost data rows' coefficients per survivor column
     for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = a.gf[i];
     for (int i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = a.gf[256 + i];
     const int w = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
     const int gi = static_cast<int>(blockIdx.x) * kPlanWaves + w;
-    const bool live = gi < a.npat;  // (every wave reaches every barrier)
+    const bool live = gi < a.npat;  // (every wave reaches the barrier)
     const int d = a.d, n = a.d + a.p;
-    auto mul = [](uint32_t x, uint32_t y) -> uint32_t { return gf_mul_alu(x, y); };
     // 1. survivors vs[0, d) and needed vectors nr[0, nn) in index order
     //    (loops unrolled over the 4 mask words: constant indexes, no scratch)
     int nn = 0, dn = 0;
@@ -1658,121 +1654,83 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
             dn += __popcll(bd);
         }
     }
-    __syncthreads();
-    // 2. the encoding-matrix rows this pattern uses, into LDS: the parity
-    //    survivors P_j that stand in for the lost data (rows 0..dn), then the
-    //    lost parity rows (rows dn..nn)
-    //    (the rows' loads of one lane issued together, then stored)
-    if (live)
-        for (int q = lane; q < d; q += 64) {
-            uint8_t v[N];
+    __syncthreads();  // (the field tables)
+    if (!live) return;  // (no barrier below: the rest is the wave's own)
+    // the wave's LDS writes land before its later reads (program order, waited)
+    auto wave_fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+    // log / exp lookups: the products and inverses below are independent of
+    // one another, so their LDS latencies overlap
+    auto tmul = [&](uint32_t x, uint32_t y) -> uint32_t { return (x && y) ? ex[lg[x] + lg[y]] : 0u; };
+    auto cinv = [&](uint32_t z) -> uint32_t { return ex[255 - lg[z]]; };  // z != 0
+    // 2. Minv by the closed form, a lane per entry (x_k = P_k = vs[d - dn + k],
+    //    y_k = L_k = nr[k]: the lost data come first in nr)
+    for (int e = lane; e < N * N; e += 64) {
+        const int l = e / N, j = e % N;
+        if (l >= dn || j >= dn) continue;
+        const uint32_t xj = s_vs[w][d - dn + j], yl = static_cast<uint32_t>(s_nr[w][l]);
+        int num = 0, den = lg[xj ^ yl];
 #pragma unroll
-            for (int k = 0; k < N; ++k) {
-                const int row = k < dn ? s_vs[w][d - dn + k] : s_nr[w][k < nn ? k : 0];
-                v[k] = k < nn ? a.enc[static_cast<size_t>(row) * d + q] : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < N; ++k) s_rows[w][k][q] = v[k];
+        for (int k = 0; k < N; ++k) {
+            if (k >= dn) break;
+            const uint32_t xk = s_vs[w][d - dn + k], yk = static_cast<uint32_t>(s_nr[w][k]);
+            num += lg[xj ^ yk] + lg[xk ^ yl];
+            if (k != j) den += lg[xj ^ xk];
+            if (k != l) den += lg[yl ^ yk];
         }
-    __syncthreads();
-    // 3. Minv: [M | I] -> [I | Minv], M[j][l] = enc[P_j][L_l], Gauss-Jordan
-    //    by the whole wave on an N x 2N matrix in LDS (a lane per entry and
-    //    step; the wave's LDS reads and writes land in program order, and
-    //    every read of a step is issued before its writes)
-    if (live && dn > 0) {
-        uint8_t(&m)[N][2 * N] = s_gj[w];
-        auto wave_fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
-        for (int e = lane; e < N * 2 * N; e += 64) {
-            const int r = e / (2 * N), k = e % (2 * N);
-            m[r][k] = k < N ? ((r < dn && k < dn) ? s_rows[w][r][s_nr[w][k]] : 0) : (k - N == r ? 1 : 0);
-        }
-        wave_fence();
-        bool ok = true;
-        for (int c = 0; c < dn; ++c) {
-            const uint64_t piv = __ballot(lane < dn && lane >= c && m[lane < N ? lane : 0][c] != 0);
-            if (!piv) {
-                ok = false;
-                break;
-            }
-            const int pr = __ffsll(static_cast<unsigned long long>(piv)) - 1;
-            if (pr != c && lane < 2 * N) {
-                const uint8_t t = m[pr][lane];
-                m[pr][lane] = m[c][lane];
-                m[c][lane] = t;
-            }
-            wave_fence();
-            const uint32_t iv = ex[255 - lg[m[c][c]]];
-            if (lane < 2 * N) m[c][lane] = static_cast<uint8_t>(mul(m[c][lane], iv));
-            wave_fence();
-            for (int e = lane; e < N * 2 * N; e += 64) {
-                const int r = e / (2 * N), k = e % (2 * N);
-                const uint32_t f = m[r][c], pv = m[c][k];
-                if (r != c && r < dn && f) m[r][k] ^= static_cast<uint8_t>(mul(f, pv));
-            }
-            wave_fence();
-        }
-        for (int e = lane; e < N * N; e += 64) {
-            const int l = e / N, j2 = e % N;
-            if (l < dn && j2 < dn) s_minv[w][l][j2] = ok ? m[l][N + j2] : 0;
-        }
+        s_minv[w][l][j] = ex[(num + 255 * 4 * N - den) % 255];
     }
-    __syncthreads();
-    if (!live) return;  // (no barrier below)
-    // 4. coefficients (the lost data rows, then the lost parity rows from
-    //    them), each column's table image ([column][4 rows x 5 dwords],
+    wave_fence();
+    // 3. the lost data rows' coefficients, a lane per (column, row) pair so a
+    //    short code (10 columns) still keeps the wave busy
+    for (int e = lane; e < d * N; e += 64) {
+        const int q = e / N, l = e % N;
+        if (l >= dn) continue;
+        const uint32_t u = s_vs[w][q];
+        uint32_t c = 0;
+        if (static_cast<int>(u) >= d) {
+            c = s_minv[w][l][q - (d - dn)];
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (j < dn) c ^= tmul(s_minv[w][l][j], cinv(static_cast<uint32_t>(s_vs[w][d - dn + j]) ^ u));
+        }
+        s_coef[w][l][q] = static_cast<uint8_t>(c);
+    }
+    wave_fence();
+    // 4. every row's coefficient (the lost parity rows from the lost data
+    //    ones), its column's table image ([column][img_rows x 5 dwords],
     //    perm_table in gf256.hpp; zero past the rows and columns) and the
     //    descriptor
     uint32_t* img = a.tabs + static_cast<size_t>(gi) * a.tdw;
-    const int cw = a.img_rows * 5;  // dwords per image column
+    const int cw = a.img_rows * 5;  // dwords per image column (img_rows == N)
     const int ncol = a.tdw / cw;
-    for (int q = lane; q < ncol; q += 64) {
-        // (every loop over rows unrolled to N with guards: the coefficients
-        // stay in registers, no scratch)
-        uint32_t coef[N];
-#pragma unroll
-        for (int r = 0; r < N; ++r) coef[r] = 0;
-        if (q < d) {
-            const int u = s_vs[w][q];
-#pragma unroll
-            for (int l = 0; l < N; ++l) {
-                if (l >= dn) break;
-                uint32_t c = 0;
-                if (u >= d) {
-                    c = s_minv[w][l][q - (d - dn)];
-                } else {
-#pragma unroll
-                    for (int j = 0; j < N; ++j)
-                        if (j < dn) c ^= mul(s_minv[w][l][j], s_rows[w][j][u]);
-                }
-                coef[l] = c;
-            }
-#pragma unroll
-            for (int r = 0; r < N; ++r) {
-                if (r < dn || r >= nn) continue;
-                uint32_t c = u < d ? s_rows[w][r][u] : 0u;
+    for (int e = lane; e < ncol * N; e += 64) {
+        const int q = e / N, r = e % N;
+        uint32_t coef = 0;
+        if (q < d && r < nn) {
+            if (r < dn) {
+                coef = s_coef[w][r][q];
+            } else {
+                const uint32_t u = s_vs[w][q], v = static_cast<uint32_t>(s_nr[w][r]);
+                coef = static_cast<int>(u) < d ? cinv(v ^ u) : 0u;
 #pragma unroll
                 for (int l = 0; l < N; ++l)
-                    if (l < dn) c ^= mul(s_rows[w][r][s_nr[w][l]], coef[l]);
-                coef[r] = c;
+                    if (l < dn) coef ^= tmul(cinv(v ^ static_cast<uint32_t>(s_nr[w][l])), s_coef[w][l][q]);
             }
         }
+        uint32_t cb[8];
+        gf_basis(coef, cb);
+        // c * e for the 3-bit groups as XORs of the basis (e's bits)
+        const uint32_t a3 = cb[0] ^ cb[1];
+        uint32_t t[5];
+        t[0] = (cb[0] << 8) | (cb[1] << 16) | (a3 << 24);
+        t[1] = cb[2] | (cb[2] ^ cb[0]) << 8 | (cb[2] ^ cb[1]) << 16 | (cb[2] ^ a3) << 24;
+        const uint32_t b3 = cb[3] ^ cb[4];
+        t[2] = (cb[3] << 8) | (cb[4] << 16) | (b3 << 24);
+        t[3] = cb[5] | (cb[5] ^ cb[3]) << 8 | (cb[5] ^ cb[4]) << 16 | (cb[5] ^ b3) << 24;
+        t[4] = (cb[6] << 8) | (cb[7] << 16) | ((cb[6] ^ cb[7]) << 24);
 #pragma unroll
-        for (int r = 0; r < N; ++r) {
-            if (r >= a.img_rows) break;  // (img_rows == N)
-            uint32_t cb[8];
-            gf_basis(coef[r], cb);
-            // c * e for the 3-bit groups as XORs of the basis (e's bits)
-            const uint32_t a3 = cb[0] ^ cb[1];
-            uint32_t t[5];
-            t[0] = (cb[0] << 8) | (cb[1] << 16) | (a3 << 24);
-            t[1] = cb[2] | (cb[2] ^ cb[0]) << 8 | (cb[2] ^ cb[1]) << 16 | (cb[2] ^ a3) << 24;
-            const uint32_t b3 = cb[3] ^ cb[4];
-            t[2] = (cb[3] << 8) | (cb[4] << 16) | (b3 << 24);
-            t[3] = cb[5] | (cb[5] ^ cb[3]) << 8 | (cb[5] ^ cb[4]) << 16 | (cb[5] ^ b3) << 24;
-            t[4] = (cb[6] << 8) | (cb[7] << 16) | ((cb[6] ^ cb[7]) << 24);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) img[q * cw + r * 5 + k] = t[k];
-        }
+        for (int k = 0; k < 5; ++k) img[q * cw + r * 5 + k] = t[k];
     }
     PatternDesc* P = a.descs + gi;
     for (int i = lane; i < 256; i += 64) P->in_idx[i] = i < d ? s_vs[w][i] : 0;
@@ -1785,6 +1743,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
 
 hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream) {
     if (a.npat <= 0) return hipSuccess;
+    if (a.img_rows != 4 && a.img_rows != 8) return hipErrorInvalidValue;  // the instance's N is its image rows
     (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
     const unsigned grid = static_cast<unsigned>((a.npat + kPlanWaves - 1) / kPlanWaves);
     if (a.img_rows > 4)

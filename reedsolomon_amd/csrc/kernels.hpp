@@ -63,7 +63,6 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
 // must need 1-kMultiMaxOut vectors, none past d + p (validated on the host).
 struct PlanArgs {
     const uint64_t* masks;  // npat x words need masks
-    const uint8_t* enc;     // (d + p) x d encoding matrix (matrix.go:37-54)
     const uint8_t* gf;      // the field's log[256], then exp[512] (gf256.hpp)
     uint32_t* tabs;
     PatternDesc* descs;
