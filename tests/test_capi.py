@@ -471,3 +471,34 @@ def test_host_memory_entry_points_without_device(rslib):
     assert L.rs_host_alloc(0, ctypes.byref(out)) == inval and not out.value
     st = rslib.host_pool_stats()
     assert st["in_use"] == 0 and set(st) == {"mapped", "in_use", "blocks", "spans"}
+
+
+def test_cauchy_closed_form_inverse(orc):
+    """The GPU planner (kernels.hip gf_plan_multi) inverts enc[P][L], the
+    block coupling the lost data L to the parity survivors P, by the Cauchy
+    closed form instead of Gauss-Jordan: enc[i][j] = 1/(i ^ j) for a parity
+    row (matrix.go:37-54), and for x_j = P_j, y_l = L_l
+      Minv[l][j] = prod_k (x_j+y_k)(x_k+y_l) / ((x_j+y_l) prod_{k!=j} (x_j+x_k) prod_{k!=l} (y_l+y_k)).
+    The same log sums as the kernel, against the oracle's Gauss-Jordan
+    (matrix.go:85-147 restated) on random blocks of 1-8 lost data."""
+    t = orc.tables()
+    lg = t["log"].astype(np.int64)
+    ex = np.concatenate([t["exp"], t["exp"]])
+    rng = np.random.default_rng(77)
+    for _ in range(400):
+        d = int(rng.integers(1, 200))
+        p = int(rng.integers(1, 257 - d))
+        n = int(rng.integers(1, min(8, p, d) + 1))
+        x = sorted(int(v) for v in rng.choice(np.arange(d, d + p), n, replace=False))
+        y = sorted(int(v) for v in rng.choice(d, n, replace=False))
+        em = orc.make_encode_matrix(d, p).reshape(d + p, d)
+        block = np.ascontiguousarray(em[np.ix_(x, y)])
+        rc, inv = orc.invert(block.ravel(), n)
+        assert rc == 0
+        want = inv.reshape(n, n)
+        for l in range(n):
+            for j in range(n):
+                num = sum(lg[x[j] ^ y[k]] + lg[x[k] ^ y[l]] for k in range(n))
+                den = lg[x[j] ^ y[l]] + sum(lg[x[j] ^ x[k]] for k in range(n) if k != j) + \
+                    sum(lg[y[l] ^ y[k]] for k in range(n) if k != l)
+                assert ex[(num + 255 * 4 * 8 - den) % 255] == want[l, j], (d, p, x, y, l, j)
