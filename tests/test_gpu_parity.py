@@ -970,6 +970,48 @@ def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
         L.rs_tune(b"multi_gpu_plan", -1)
 
 
+@pytest.mark.parametrize("d,p,npat", [(10, 4, 300), (32, 32, 700)])
+def test_reconst_batch_multi_repeated_patterns(rslib, torch_dev, d, p, npat):
+    """The host groups stripes by pattern (batches.cpp group_patterns): the
+    previous stripe's pattern, a scan of the first 16, then a hash that grows
+    as patterns arrive.  Stripes here repeat their patterns in runs, in
+    interleaved order and after the hash has grown (32+32: masks up to bit
+    63), with untouched stripes between; both planners rebuild every stripe
+    bit-exact and leave the untouched ones alone."""
+    torch = torch_dev
+    L = rslib.lib()
+    n = 1024
+    pats = _distinct_patterns(d, p, npat, d * 7 + p, 4)
+    rng = np.random.default_rng(npat + d)
+    seq = []
+    for k in range(npat):  # runs of 1-3 as patterns first appear
+        seq += [pats[k]] * int(rng.integers(1, 4))
+    seq += [pats[int(i)] for i in rng.integers(0, npat, 2 * npat)]  # repeats after the hash has grown
+    seq += [0] * 50
+    masks = [seq[int(i)] for i in rng.permutation(len(seq))[:len(seq) // 2]] + seq  # interleaved, then in order
+    S = len(masks)
+    r = rslib.New(d, p)
+    g = torch.Generator(device="cuda").manual_seed(d * 11 + p)
+    data = torch.randint(0, 256, (S, d, n), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((S, p, n), dtype=torch.uint8, device="cuda")
+    r.encode_batch_split(data, parity)
+    torch.cuda.synchronize()
+    ref_d, ref_p = data.clone(), parity.clone()
+    arg = np.array(masks, dtype=np.uint64)
+    try:
+        for plan in (1, 0):
+            assert L.rs_tune(b"multi_gpu_plan", plan) == 0
+            for s, m in enumerate(masks):
+                for v in range(d + p):
+                    if m >> v & 1:
+                        (data[s, v] if v < d else parity[s, v - d]).fill_(0x3C)
+            r.reconst_batch_multi(data, parity, arg)
+            torch.cuda.synchronize()
+            assert torch.equal(data, ref_d) and torch.equal(parity, ref_p), plan
+    finally:
+        L.rs_tune(b"multi_gpu_plan", -1)
+
+
 @pytest.mark.parametrize("d,p", [(10, 8), (8, 8), (10, 6)])
 def test_reconst_batch_multi_parity_rows_bitsliced(rslib, orc, torch_dev, d, p):
     """Stripes that lose only parity rows p' in 5..p: the grouped fallback's
