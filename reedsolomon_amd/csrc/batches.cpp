@@ -124,20 +124,21 @@ int rs_reconst_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vec
 }  // extern "C"
 
 namespace {
-typedef std::array<uint64_t, 4> Mask256;
 
 // Group stripes by erasure pattern (host, O(S)): pat_of[s] = the pattern
-// index of stripe s (-1 for a zero mask), keys / counts per pattern in
-// first-seen order.  Batches hold few distinct patterns, often in runs: the
+// index of stripe s (-1 for a zero mask); keyw holds each pattern's W mask
+// words in first-seen order (npat x W, the layout the GPU planner reads),
+// counts its stripes.  Batches hold few distinct patterns, often in runs: the
 // previous stripe's pattern, then a linear scan while there are at most kScan
 // patterns, then an open-addressing hash of pattern indexes holding every
 // pattern.  W is the mask width in words (1 or 4), so the common one-word
 // masks compare and hash as one integer (a node-based map cost ~150 ns per new
-// pattern, 4-word keys with a 16-key scan ahead of the hash ~80: most of a
-// 1,470-pattern call once the GPU plans the patterns).  Returns
-// RS_ERR_ILLEGAL_VECTS for a bit at or above nvec.
+// pattern, 4-word keys with a 16-key scan ahead of the hash ~80, and copying
+// 4,096 patterns out as 32-byte keys took a fresh mmap'ed block and its page
+// faults on every call: most of a many-pattern call once the GPU plans the
+// patterns).  Returns RS_ERR_ILLEGAL_VECTS for a bit at or above nvec.
 template <int W>
-int group_patterns(const uint64_t* m, int nstripes, int nvec, std::vector<int32_t>& pat_of, std::vector<Mask256>& out,
+int group_patterns(const uint64_t* m, int nstripes, int nvec, std::vector<int32_t>& pat_of, std::vector<uint64_t>& keyw,
                    std::vector<size_t>& counts) {
     typedef std::array<uint64_t, W> Key;
     auto hash = [](const Key& k) {
@@ -154,16 +155,20 @@ int group_patterns(const uint64_t* m, int nstripes, int nvec, std::vector<int32_
         const int lo = w * 64;
         top[w] = nvec >= lo + 64 ? ~uint64_t{0} : nvec <= lo ? 0 : (uint64_t{1} << (nvec - lo)) - 1;
     }
-    std::vector<Key> keys;
+    auto key_at = [&](size_t k) {
+        Key r;
+        for (int w = 0; w < W; ++w) r[w] = keyw[k * W + w];
+        return r;
+    };
     std::vector<int32_t> slots;  // pattern index per hash slot, -1 = empty (power-of-two size)
     auto slot_of = [&](const Key& key) -> size_t {  // the key's slot, or the empty one it would take
         size_t h = hash(key) & (slots.size() - 1);
-        while (slots[h] >= 0 && keys[static_cast<size_t>(slots[h])] != key) h = (h + 1) & (slots.size() - 1);
+        while (slots[h] >= 0 && key_at(static_cast<size_t>(slots[h])) != key) h = (h + 1) & (slots.size() - 1);
         return h;
     };
     auto rehash = [&](size_t size) {  // every pattern into a table of `size` slots
         slots.assign(size, -1);
-        for (size_t k = 0; k < keys.size(); ++k) slots[slot_of(keys[k])] = static_cast<int32_t>(k);
+        for (size_t k = 0; k < counts.size(); ++k) slots[slot_of(key_at(k))] = static_cast<int32_t>(k);
     };
     constexpr int kScan = 16;
     int last = -1;
@@ -178,21 +183,21 @@ int group_patterns(const uint64_t* m, int nstripes, int nvec, std::vector<int32_
         if (!any) continue;
         if (bad) return RS_ERR_ILLEGAL_VECTS;
         int gi = -1;
-        if (last >= 0 && keys[static_cast<size_t>(last)] == key) {
+        if (last >= 0 && key_at(static_cast<size_t>(last)) == key) {
             gi = last;
         } else {
-            const int n = static_cast<int>(keys.size());
+            const int n = static_cast<int>(counts.size());
             size_t h = 0;
             if (slots.empty()) {
                 for (int k = 0; k < n && gi < 0; ++k)
-                    if (keys[static_cast<size_t>(k)] == key) gi = k;
+                    if (key_at(static_cast<size_t>(k)) == key) gi = k;
             } else {
                 h = slot_of(key);
                 gi = slots[h];
             }
             if (gi < 0) {
                 gi = n;
-                keys.push_back(key);
+                for (int w = 0; w < W; ++w) keyw.push_back(key[w]);
                 counts.push_back(0);
                 if (!slots.empty() && 2 * (n + 1) <= static_cast<int>(slots.size()))
                     slots[h] = gi;
@@ -203,11 +208,6 @@ int group_patterns(const uint64_t* m, int nstripes, int nvec, std::vector<int32_
         pat_of[static_cast<size_t>(s)] = gi;
         ++counts[static_cast<size_t>(gi)];
         last = gi;
-    }
-    out.resize(keys.size());
-    for (size_t k = 0; k < keys.size(); ++k) {
-        out[k] = Mask256{};
-        for (int w = 0; w < W; ++w) out[k][w] = keys[k][w];
     }
     return RS_OK;
 }
@@ -226,19 +226,21 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
         // Group stripes by erasure pattern and validate every pattern before
         // any launch (group_patterns above).
         std::vector<int32_t> pat_of(static_cast<size_t>(nstripes), -1);
-        std::vector<Mask256> keys;
+        std::vector<uint64_t> keyw;  // npat x masks.words
         std::vector<size_t> counts;
-        const int rc_g = masks.words == 1 ? group_patterns<1>(masks.m, nstripes, d + p, pat_of, keys, counts)
-                                          : group_patterns<4>(masks.m, nstripes, d + p, pat_of, keys, counts);
+        const int rc_g = masks.words == 1 ? group_patterns<1>(masks.m, nstripes, d + p, pat_of, keyw, counts)
+                                          : group_patterns<4>(masks.m, nstripes, d + p, pat_of, keyw, counts);
         if (rc_g) return rc_g;
-        if (keys.empty()) return RS_OK;
+        const size_t npat_all = counts.size();
+        auto key_word = [&](size_t gi, int w) { return keyw[gi * static_cast<size_t>(masks.words) + w]; };
+        if (npat_all == 0) return RS_OK;
         // Every pattern's plan_reconst error before any device work: with no
         // survivor list the needed vectors are the mask's, and more than p of
         // them is RS_ERR_TOO_MANY_LOST (nothing else can fail there).
         int nn_max = 0;
-        for (const Mask256& k : keys) {
+        for (size_t gi = 0; gi < npat_all; ++gi) {
             int nn = 0;
-            for (int w = 0; w < masks.words; ++w) nn += __builtin_popcountll(k[w]);
+            for (int w = 0; w < masks.words; ++w) nn += __builtin_popcountll(key_word(gi, w));
             if (nn > p) return RS_ERR_TOO_MANY_LOST;
             nn_max = nn > nn_max ? nn : nn_max;
         }
@@ -278,8 +280,8 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             return hip_ok(launch_gf_multi(a, descs, spat, st), "multi-pattern kernel launch");
         };
         const int gpu_plan = tuning().multi_gpu_plan;
-        const bool use_gpu_plan = gpu_plan < 0 ? keys.size() * static_cast<size_t>(d) >= 160
-                                               : gpu_plan > 0 && keys.size() >= static_cast<size_t>(gpu_plan);
+        const bool use_gpu_plan = gpu_plan < 0 ? npat_all * static_cast<size_t>(d) >= 160
+                                               : gpu_plan > 0 && npat_all >= static_cast<size_t>(gpu_plan);
         if (single && use_gpu_plan) {
             // Plan on the GPU (gf_plan_multi, kernels.hip): upload the field
             // tables, the distinct masks and the stripe -> pattern map (the
@@ -287,7 +289,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             // its entries from the tables); the planner writes the table images
             // and descriptors behind them in the same device slot, then the
             // multi kernel runs.
-            const int npat = static_cast<int>(keys.size());
+            const int npat = static_cast<int>(npat_all);
             const int tdw = multi_table_dwords(d, nn_max);
             auto al16 = [](size_t x) { return (x + 15) & ~size_t{15}; };
             const size_t gf_b = 768;
@@ -301,9 +303,7 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             RS_TRY(lease.acquire(head, &host, head + tab_b + desc_b));
             std::memcpy(host, gf().log, 256);
             std::memcpy(host + 256, gf().exp, 512);
-            uint64_t* hm = reinterpret_cast<uint64_t*>(host + gf_b);
-            for (int gi = 0; gi < npat; ++gi)
-                for (int w = 0; w < masks.words; ++w) hm[static_cast<size_t>(gi) * masks.words + w] = keys[gi][w];
+            std::memcpy(host + gf_b, keyw.data(), keyw.size() * sizeof(uint64_t));  // (npat x words, as grouped)
             std::memcpy(host + gf_b + mask_b, pat_of.data(), static_cast<size_t>(nstripes) * 4);
             uint8_t* dev = nullptr;
             RS_TRY(lease.upload(st, &dev));
@@ -326,13 +326,13 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             size_t off, n;
         };
         std::vector<Group> plan;
-        plan.reserve(keys.size());
+        plan.reserve(npat_all);
         size_t off = 0;
-        for (size_t gi = 0; gi < keys.size(); ++gi) {
+        for (size_t gi = 0; gi < npat_all; ++gi) {
             Group gr;
             int need[kMaxVects], nn = 0;
             for (int v = 0; v < d + p; ++v)
-                if (keys[gi][v >> 6] >> (v & 63) & 1) need[nn++] = v;
+                if (key_word(gi, v >> 6) >> (v & 63) & 1) need[nn++] = v;
             int rc = plan_reconst(rs, nullptr, 0, need, nn, gr.pl.vs, &gr.pl.nvs, gr.pl.nr, &gr.pl.nnr, &gr.pl.dn);
             if (rc) return rc;  // (validated above)
             gr.off = off;
