@@ -193,6 +193,7 @@ struct rs_codec {
     static constexpr int kUploadSlots = 4;
     struct UploadSlot {
         uint8_t* host = nullptr;
+        const uint8_t* host_dev = nullptr;  // the host buffer's device address (mapped pinned memory)
         uint8_t* dev = nullptr;
         size_t cap = 0, dcap = 0;  // host / device bytes
         hipEvent_t copied = nullptr, done = nullptr;
@@ -422,12 +423,17 @@ public:
         if (u.cap < bytes) {
             if (u.host) (void)hipHostFree(u.host);
             u.host = nullptr;
+            u.host_dev = nullptr;
             u.cap = 0;
             const size_t cap = round(bytes);
-            if (hipHostMalloc(reinterpret_cast<void**>(&u.host), cap, hipHostMallocDefault) != hipSuccess) {
+            // coherent and mapped: a kernel may read it in place (map() below)
+            if (hipHostMalloc(reinterpret_cast<void**>(&u.host), cap,
+                              hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
                 u.host = nullptr;
                 return RS_ERR_NOMEM;
             }
+            void* hd = nullptr;
+            if (hipHostGetDevicePointer(&hd, u.host, 0) == hipSuccess) u.host_dev = static_cast<const uint8_t*>(hd);
             u.cap = cap;
         }
         const size_t dneed = dev_bytes > bytes ? dev_bytes : bytes;
@@ -454,6 +460,17 @@ public:
                       "upload copy"));
         RS_TRY(hip_ok(hipEventRecord(slot_->copied, rs_->up_stream), "upload event record"));
         RS_TRY(hip_ok(hipStreamWaitEvent(st, slot_->copied, 0), "upload stream wait"));
+        *dev = slot_->dev;
+        return RS_OK;
+    }
+
+    // No copy: the consumer kernels on `st` read the filled host buffer in
+    // place through its device address (and may write the device slot); the
+    // slot is reused only after they finish (the destructor's `done` event).
+    int map(hipStream_t st, const uint8_t** host_dev, uint8_t** dev) {
+        if (!slot_->host_dev) return dev_fail(hipErrorInvalidValue, "upload slot device address");
+        st_ = st;
+        *host_dev = slot_->host_dev;
         *dev = slot_->dev;
         return RS_OK;
     }

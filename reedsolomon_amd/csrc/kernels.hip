@@ -1601,6 +1601,26 @@ int multi_table_dwords(int cols, int max_out) {
 // ---------------------------------------------------------------------------
 constexpr int kPlanWaves = 4;
 
+// The field's log / exp tables as device constants (gf256.hpp's GfTables:
+// 0x11d, exp doubled), so a launch uploads nothing for them
+struct GfLogExp {
+    uint8_t log[256];
+    uint8_t exp[512];
+};
+constexpr GfLogExp make_gf_log_exp() {
+    GfLogExp t{};
+    unsigned v = 1;
+    for (int i = 0; i < 255; ++i) {
+        t.exp[i] = static_cast<uint8_t>(v);
+        t.log[v] = static_cast<uint8_t>(i);
+        v <<= 1;
+        if (v & 0x100) v ^= 0x11d;
+    }
+    for (int i = 255; i < 512; ++i) t.exp[i] = t.exp[i - 255];
+    return t;
+}
+__constant__ GfLogExp kGfLogExp = make_gf_log_exp();
+
 // c * 2^b for b = 0..7 (multiplication by x, reduced by 0x11d): the columns
 // of multiplication by c as a GF(2)-linear map, from which c * e for any e is
 // the XOR of the entries of e's bits (no table lookups)
@@ -1619,8 +1639,13 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
     __shared__ int s_nr[kPlanWaves][N];
     __shared__ uint8_t s_minv[kPlanWaves][N][N];
     __shared__ uint8_t s_coef[kPlanWaves][N][256];  // the lost data rows' coefficients per survivor column
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = a.gf[i];
-    for (int i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = a.gf[256 + i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lg[i] = kGfLogExp.log[i];
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) ex[i] = kGfLogExp.exp[i];
+    // the stripe -> pattern map into device memory for the multi kernel
+    // (grid-stride over every thread of the launch)
+    for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < a.nstripes;
+         i += static_cast<int>(gridDim.x * blockDim.x))
+        a.pat_dst[i] = a.pat_src[i];
     const int w = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
     const int gi = static_cast<int>(blockIdx.x) * kPlanWaves + w;
     const bool live = gi < a.npat;  // (every wave reaches the barrier)

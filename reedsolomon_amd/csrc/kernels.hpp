@@ -62,12 +62,13 @@ hipError_t launch_gf_multi(MatmulArgs& a, const PatternDesc* pats, const int32_t
 // and its descriptor, as reconst_multi builds them on the host.  Every pattern
 // must need 1-kMultiMaxOut vectors, none past d + p (validated on the host).
 struct PlanArgs {
-    const uint64_t* masks;  // npat x words need masks
-    const uint8_t* gf;      // the field's log[256], then exp[512] (gf256.hpp)
+    const uint64_t* masks;    // npat x words need masks (mapped pinned host memory, read in place)
+    const int32_t* pat_src;   // stripe -> pattern map, nstripes (mapped pinned host memory)
+    int32_t* pat_dst;         // its device copy, for the multi kernel (the planner copies it)
     uint32_t* tabs;
     PatternDesc* descs;
-    int npat, words, d, p, tdw;
-    int img_rows;           // multi_image_rows(the batch's most outputs): 4 or 8
+    int npat, words, d, p, tdw, nstripes;
+    int img_rows;             // multi_image_rows(the batch's most outputs): 4 or 8
 };
 hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream);
 
