@@ -1766,6 +1766,24 @@ __global__ __launch_bounds__(64 * kPlanWaves) void gf_plan_multi(const PlanArgs 
     }
 }
 
+// 16 bytes per lane, grid-stride (kernels.hpp launch_copy_in)
+__global__ __launch_bounds__(256) void copy_in(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n) {
+    for (size_t i = blockIdx.x * size_t{256} + threadIdx.x; i < n; i += size_t{gridDim.x} * 256) dst[i] = src[i];
+}
+
+hipError_t launch_copy_in(uint8_t* dst, const uint8_t* src_host_dev, size_t bytes, hipStream_t stream) {
+    if (bytes == 0) return hipSuccess;
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || (reinterpret_cast<uintptr_t>(src_host_dev) & 15))
+        return hipErrorInvalidValue;
+    (void)hipGetLastError();  // report this launch only (see launch_gf_multi)
+    const size_t n = bytes / 16;
+    const size_t want = (n + 255) / 256;
+    const unsigned grid = static_cast<unsigned>(want < 1024 ? want : 1024);
+    hipLaunchKernelGGL(copy_in, dim3(grid), dim3(256), 0, stream, reinterpret_cast<uint4*>(dst),
+                       reinterpret_cast<const uint4*>(src_host_dev), n);
+    return hipGetLastError();
+}
+
 hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream) {
     if (a.npat <= 0) return hipSuccess;
     if (a.img_rows != 4 && a.img_rows != 8) return hipErrorInvalidValue;  // the instance's N is its image rows

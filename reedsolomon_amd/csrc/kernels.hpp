@@ -71,6 +71,10 @@ struct PlanArgs {
     int img_rows;             // multi_image_rows(the batch's most outputs): 4 or 8
 };
 hipError_t launch_gf_plan_multi(const PlanArgs& a, hipStream_t stream);
+// Copy `bytes` (a multiple of 16) from mapped pinned host memory (its device
+// address) to device memory with a kernel on `stream`: the upload ring's copy
+// (UploadLease::upload) without a DMA engine or a cross-stream wait.
+hipError_t launch_copy_in(uint8_t* dst, const uint8_t* src_host_dev, size_t bytes, hipStream_t stream);
 
 // Host-call engine (engine.cpp): a resident kernel that serves small
 // synchronous host calls through doorbells in host memory instead of one
