@@ -49,7 +49,7 @@ def rec(name, nbytes, t, **kw):
     print(f"{name:44s} {nbytes / t / GiB:10.2f} GiB/s  {t * 1e6:10.2f} us/call", flush=True)
 
 
-SECTIONS = ["encode", "shapes", "split", "rec8", "rec4", "multi", "upd", "wide", "first", "host", "api"]
+SECTIONS = ["encode", "shapes", "split", "rec8", "rec4", "multi", "upd", "wide", "first", "first_small", "host", "api"]
 
 
 def want(name):
@@ -141,6 +141,47 @@ def first_sight(g):
     L.rs_tune(b"jit", 2)
 
 
+def first_small(g):
+    """Small synchronous Reconst calls"""
+    import numpy as np
+
+    L = rs.lib()
+    rng = np.random.default_rng(12)
+    # Small synchronous Reconst calls (16 stripes of 10+4 @ 8 KiB): a new
+    # pattern's first call (its decode matrix, perm tables and their upload)
+    # against a repeat of a pattern already seen; wall time per call with the
+    # stream synchronised, median of 100 (default policy: too small to compile)
+    L.rs_tune(b"jit", 1)
+    k, m, vec, S = 10, 4, 8192, 16
+    r = rs.New(k, m)
+    buf = torch.randint(0, 256, (S, k + m, vec), dtype=torch.uint8, device="cuda", generator=g)
+    r.encode_batch(buf)
+    ref = buf.clone()
+    seen = set()
+    fresh = []
+    while len(fresh) < 101:
+        pt = tuple(sorted(int(x) for x in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False)))
+        if pt not in seen:
+            seen.add(pt)
+            fresh.append(list(pt))
+    def per_call(pats):
+        ts = []
+        for pt in pats:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.reconst_batch(buf, [], pt)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
+    r.reconst_batch(buf, [], fresh[0])
+    t_new = per_call(fresh[1:])
+    t_rep = per_call([fresh[1]] * 100)
+    assert torch.equal(buf, ref), "small first-sight reconst changed the stripes"
+    for label, t in (("first call of a new pattern", t_new), ("a pattern already seen", t_rep)):
+        rec(f"reconst 10+4 8KiB x{S}, synchronous, {label}", S * (k + 2) * vec, t)
+    L.rs_tune(b"jit", 2)
+
+
 def main():
     g = torch.Generator(device="cuda").manual_seed(42)
     # run-time bit-sliced kernels (5-8 output rows) compile on first use here,
@@ -151,6 +192,8 @@ def main():
         wide(g)
     if want("first"):
         first_sight(g)
+    if want("first_small"):
+        first_small(g)
     if want("encode"):
         # ---- encode, device-resident
         for k, m, vec, S in ((10, 4, 1 << 20, 256), (12, 4, 1 << 20, 256), (10, 4, 8 << 10, 32768), (10, 4, 8 << 10, 1)):
