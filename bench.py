@@ -11,8 +11,10 @@ A step = one launch of the HIP encode over one batch of S synthetic stripes
 (default S=256 stripes of 10+4 x 1 MiB = 3.5 GiB per GPU, far beyond the
 256 MiB Infinity Cache) that are already resident in HBM.  Stripes are
 independent, so N GPUs each encode their own S stripes with no collective on
-the data path (weak scaling); the only collectives are the timing barrier and
-the max-over-ranks of the elapsed time.
+the data path (weak scaling); the only collectives are the timing barrier,
+the max-over-ranks of the elapsed time, the rank count and the per-rank
+device list, all on a gloo group over the host (RSAMD_BENCH_BACKEND=nccl opts
+in to RCCL; the line's `backend` and `rank_devices` say which ran).
 
 `--gpus N` without a launcher starts N ranks itself (torch.distributed.run
 as a child process, before any GPU call); under a launcher WORLD_SIZE must
@@ -35,6 +37,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -95,6 +98,30 @@ def dist_env():
 def stripe_range(rank: int, stripes_per_rank: int):
     """Global ids of the stripes a rank owns (weak scaling: fixed per rank)."""
     return rank * stripes_per_rank, (rank + 1) * stripes_per_rank
+
+
+def timing_backend(env=None) -> str:
+    """Process-group backend of the timing collectives.  The data path has no
+    collective: the group only carries the timing barrier, the
+    max over ranks, the rank count and the per-rank device list, none of which
+    needs a GPU transport, so the default is gloo over the host's loopback /
+    TCP, and RCCL is not on the SCALE path at all.  RSAMD_BENCH_BACKEND=nccl
+    opts in to RCCL (one process per GPU, device_id bound)."""
+    env = os.environ if env is None else env
+    b = env.get("RSAMD_BENCH_BACKEND", "gloo")
+    if b not in ("gloo", "nccl"):
+        raise SystemExit(f"bench: RSAMD_BENCH_BACKEND={b!r}: gloo (default) or nccl")
+    return b
+
+
+def rank_devices(pg, me: dict) -> list:
+    """Every rank's device record, in rank order (all_gather_object over the
+    timing group; [me] without one)."""
+    if pg is None:
+        return [me]
+    out = [None] * pg.get_world_size()
+    pg.all_gather_object(out, me)
+    return out
 
 
 def make_collectives(pg, device):
@@ -472,10 +499,14 @@ def rehearse_cpu(args, world: int, rank: int) -> dict | None:
     import torch.distributed as dist
 
     pg = None
+    backend = timing_backend()
     if world > 1:
+        if backend != "gloo":
+            raise SystemExit("bench: --rehearse-cpu runs on gloo only (no GPU)")
         dist.init_process_group("gloo")
         pg = dist
     ranks_seen = count_ranks(pg, torch.device("cpu"))
+    devices = rank_devices(pg, {"rank": rank, "device": "cpu", "pid": os.getpid()})
     if ranks_seen != args.gpus:
         raise SystemExit(f"bench: {ranks_seen} ranks joined, --gpus {args.gpus}")
     barrier, max_over = make_collectives(pg, torch.device("cpu"))
@@ -498,6 +529,7 @@ def rehearse_cpu(args, world: int, rank: int) -> dict | None:
     out = None
     if rank == 0:
         out = {"metric": "REHEARSAL (no GPU, no kernel)", "value": None, "n_gpus": world, "ranks_seen": ranks_seen,
+               "backend": backend if pg is not None else None, "rank_devices": devices,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
                "data": "rehearsal: numpy XOR stand-in, not a measurement",
                "prewarm": prewarm_summary(len(pw), sum(pw), sum(pw[-20:]) / len(pw[-20:]), True, pw, 0),
@@ -694,10 +726,11 @@ def main(argv=None):
     import reedsolomon_amd as rs
 
     # One process per GPU.  RSAMD_BENCH_DEVICE pins every rank to one device
-    # and RSAMD_BENCH_BACKEND overrides the process-group backend: used only to
-    # rehearse the multi-rank path on a 1-GPU box (gloo, ranks sharing cuda:0).
+    # (used only to rehearse the multi-rank path on a 1-GPU box, ranks sharing
+    # cuda:0).  The timing collectives run on gloo unless RSAMD_BENCH_BACKEND
+    # asks for nccl (timing_backend): no RCCL call is on the SCALE path.
     dev_idx = int(os.environ.get("RSAMD_BENCH_DEVICE", local))
-    backend = os.environ.get("RSAMD_BENCH_BACKEND", "nccl")
+    backend = timing_backend()
     if "RSAMD_BENCH_DEVICE" not in os.environ and torch.cuda.device_count() < world:
         raise SystemExit(f"bench: {world} ranks but only {torch.cuda.device_count()} visible GPUs")
     torch.cuda.set_device(dev_idx)
@@ -774,6 +807,9 @@ def main(argv=None):
     ranks_seen = count_ranks(pg, dev)
     if ranks_seen != args.gpus:
         raise SystemExit(f"bench: {ranks_seen} ranks joined the process group, --gpus {args.gpus}")
+    props = torch.cuda.get_device_properties(dev)
+    devices = rank_devices(pg, {"rank": rank, "local_rank": local, "device": dev_idx,
+                                "pci_bus_id": getattr(props, "pci_bus_id", None), "host": socket.gethostname()})
     barrier()
     max_over(0.0)
 
@@ -818,6 +854,8 @@ def main(argv=None):
             "unit": "GiB/s",
             "n_gpus": n_gpus,
             "ranks_seen": ranks_seen,
+            "backend": backend if pg is not None else None,
+            "rank_devices": devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),

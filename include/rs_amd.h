@@ -97,8 +97,10 @@ RS_API int  rs_device(const rs_t* rs);
  * last chunk of getSplitSize (rs.go:158-173, 190-200), so under updateOnly
  * the body of a last chunk whose length is >= 16 and not a multiple of 16 is
  * XORed twice and keeps its old parity; which bytes those are depends on the
- * host's L1D size (cpu.X86.Cache.L1D).  l1d = 0 (the default): Update /
+ * host's L1D size (cpu.X86.Cache.L1D).  l1d = 0 (rs_new's setting): Update /
  * Replace compute the re-encode definition (rs_test.go:219-331) everywhere.
+ * The cgo binding's New sets -1, so a Go drop-in returns
+ * rs.go's bytes on its host by default.
  * l1d > 0 (>= 32): the bytes rs.go produces on a host with that L1D.
  * l1d = -1: this host's L1D as rs_host_l1d reports it, 32 KiB when unknown
  * (rs.go:159-161).  Affects only this handle's Update / Replace calls (host,
@@ -413,6 +415,14 @@ RS_API int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches
  * them).  Either pointer may be NULL. */
 RS_API int rs_jit_table_stats(uint64_t* entries, uint64_t* evictions);
 
+/* A handle's coefficient tables (the perm-table kernels' per-matrix tables):
+ * uploads to device memory so far, and launches that read a new matrix's
+ * tables in place from a mapped staging slot (the first sight of a matrix in
+ * a launch of at most rs_tune("table_inplace_max") input bytes, default
+ * 2 MiB; its second use uploads).  Either pointer may be NULL.  No device
+ * call. */
+RS_API int rs_coef_table_stats(const rs_t* rs, uint64_t* uploads, uint64_t* inplace);
+
 /* The run-time kernels' on-disk code-object cache (RSAMD_JIT_CACHE_DIR,
  * default $XDG_CACHE_HOME/rsamd/jit or ~/.cache/rsamd/jit; knob
  * "jit_disk_cache"), process-wide: first sights of a matrix whose code object
@@ -583,7 +593,11 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * code objects are kept in an on-disk cache shared by processes, see
  * rs_jit_cache_stats | 0: compile in every process),
  * "table_registry_max" (distinct coefficient matrices
- * kept on the device per handle before the registry is recycled).  Returns
+ * kept on the device per handle before the registry is recycled),
+ * "table_inplace_max" (bytes of input vectors up to which a launch reads a
+ * matrix it sees for the first time with its tables in place from a mapped
+ * staging slot, the matrix's second use uploading them; default 2 MiB, 0 =
+ * upload at first sight; see rs_coef_table_stats).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name.  The code-shape experiments of
  * earlier rounds (the knob named var, env RSAMD_VAR; some are XOR-only
  * diagnostics) exist only in the separate experiments build librsamd_exp.so:

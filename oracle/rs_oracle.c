@@ -195,7 +195,7 @@ uint64_t orc_inverse_cache_key(const int* survived, int ns) {
  * for Update / Replace (updateOnly) it does, see encode_part. */
 static size_t g_l1d = 32 * 1024;
 /* cpu.X86.Cache.L1D as the reference would read it on another host (tests of
- * librsamd's rs_tune("ref_update_tail") compat mode); 0 restores 32 KiB. */
+ * librsamd's rs_set_ref_l1d compat mode); 0 restores 32 KiB. */
 void orc_set_l1d(size_t l1d) { g_l1d = l1d ? l1d : 32 * 1024; }
 
 static size_t split_size(size_t n) {

@@ -111,6 +111,7 @@ SIGNATURES = {
                              ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]),
     "rs_jit_cache_stats": (c_int, [ctypes.POINTER(ctypes.c_uint64)] * 4),
     "rs_jit_table_stats": (c_int, [ctypes.POINTER(ctypes.c_uint64)] * 2),
+    "rs_coef_table_stats": (c_int, [c_void, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "rs_jit_prepare": (c_int, [c_void, ctypes.c_void_p, c_int, c_int, c_int, c_int]),
     "rs_jit_compile_check": (c_int, [ctypes.c_void_p, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_double)]),
     "rs_jit_encoder_check": (c_int, [ctypes.c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_sz)]),

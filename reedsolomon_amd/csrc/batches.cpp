@@ -301,26 +301,30 @@ int reconst_multi(rs_t* rs, const rs_layout_t* L, int nstripes, size_t len, Mask
             UploadLease lease(rs);
             uint8_t* host = nullptr;
             RS_TRY(lease.acquire(mask_b + pat_b, &host, pat_b + tab_b + desc_b));
-            std::memcpy(host, keyw.data(), keyw.size() * sizeof(uint64_t));  // (npat x words, as grouped)
-            std::memcpy(host + mask_b, pat_of.data(), static_cast<size_t>(nstripes) * 4);
-            const uint8_t* hdev = nullptr;
-            uint8_t* dev = nullptr;
-            RS_TRY(lease.map(st, &hdev, &dev));
-            PlanArgs pa;
-            pa.masks = reinterpret_cast<const uint64_t*>(hdev);
-            pa.pat_src = reinterpret_cast<const int32_t*>(hdev + mask_b);
-            pa.pat_dst = reinterpret_cast<int32_t*>(dev);
-            pa.tabs = reinterpret_cast<uint32_t*>(dev + pat_b);
-            pa.descs = reinterpret_cast<PatternDesc*>(dev + pat_b + tab_b);
-            pa.npat = npat;
-            pa.words = masks.words;
-            pa.d = d;
-            pa.p = p;
-            pa.tdw = tdw;
-            pa.nstripes = nstripes;
-            pa.img_rows = multi_image_rows(nn_max);
-            RS_TRY(hip_ok(launch_gf_plan_multi(pa, st), "multi-pattern planner launch"));
-            return launch_single(pa.tabs, pa.descs, pa.pat_dst);
+            // (a pinned slot without a device address cannot be read in
+            // place: the host planner below serves the call instead, advisor r05)
+            if (lease.mappable()) {
+                std::memcpy(host, keyw.data(), keyw.size() * sizeof(uint64_t));  // (npat x words, as grouped)
+                std::memcpy(host + mask_b, pat_of.data(), static_cast<size_t>(nstripes) * 4);
+                const uint8_t* hdev = nullptr;
+                uint8_t* dev = nullptr;
+                RS_TRY(lease.map(st, &hdev, &dev));
+                PlanArgs pa;
+                pa.masks = reinterpret_cast<const uint64_t*>(hdev);
+                pa.pat_src = reinterpret_cast<const int32_t*>(hdev + mask_b);
+                pa.pat_dst = reinterpret_cast<int32_t*>(dev);
+                pa.tabs = reinterpret_cast<uint32_t*>(dev + pat_b);
+                pa.descs = reinterpret_cast<PatternDesc*>(dev + pat_b + tab_b);
+                pa.npat = npat;
+                pa.words = masks.words;
+                pa.d = d;
+                pa.p = p;
+                pa.tdw = tdw;
+                pa.nstripes = nstripes;
+                pa.img_rows = multi_image_rows(nn_max);
+                RS_TRY(hip_ok(launch_gf_plan_multi(pa, st), "multi-pattern planner launch"));
+                return launch_single(pa.tabs, pa.descs, pa.pat_dst);
+            }
         }
         struct Group {
             ReconstPlan pl;

@@ -113,6 +113,12 @@ int ensure_device(rs_t* rs) {
 std::atomic<uint64_t> g_devices_used{0};
 
 size_t g_registry_max = size_t{1} << 14;
+// First sight of a matrix in a small launch (at most this many bytes of input
+// vectors): the launch reads the tables in place from the mapped staging
+// slot, with no device allocation, upload copy or upload event on the
+// caller's path; the matrix's second use uploads them (get_tables).
+// rs_tune("table_inplace_max", bytes), 0 = always upload at first sight.
+size_t g_tab_inplace_max = size_t{2} << 20;
 
 thread_local char g_last_dev_err[192] = {0};
 
@@ -135,8 +141,20 @@ int dev_fail(hipError_t e, const char* where) {
 // another stream waits for the upload's event.  Caller holds tab_mu until its
 // launch is enqueued: a full registry is recycled after a device sync, so no
 // table may be handed out and launched across a recycle.
+//
+// First sight in a small launch (launch_in_bytes <= table_inplace_max, and
+// the caller passes inplace_slot): the tables are built into a coherent,
+// mapped staging slot and the launch reads them there in place (a few KiB
+// over PCIe per workgroup); *inplace_slot names the slot, and the caller
+// records the slot's `done` event behind its launch (the slot is reused only
+// after that).  No registry entry is made: the matrix's next use uploads.  A
+// small synchronous Reconst of a pattern new to the process spent ~12 of its
+// 33 us in the upload's host calls (hipMalloc, hipMemcpyAsync, event create
+// and two records; profiles/r05/first_sight_api_trace/), and a rebuild storm
+// of one-off patterns never reuses its tables.
 int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t stream, const uint32_t** out,
-               int* rows_pad_out) {
+               int* rows_pad_out, uint64_t launch_in_bytes, int* inplace_slot) {
+    if (inplace_slot) *inplace_slot = -1;
     const int rows_pad = static_cast<int>(rup(rows, 8));
     std::string key(reinterpret_cast<const char*>(&rows), sizeof rows);
     key.append(reinterpret_cast<const char*>(&cols), sizeof cols);
@@ -170,6 +188,11 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
         }
         rs->tables.clear();
     }
+    bool inplace = false;
+    if (inplace_slot && g_tab_inplace_max && launch_in_bytes <= g_tab_inplace_max) {
+        if (rs->tab_seen.size() >= 4096) rs->tab_seen.clear();
+        inplace = rs->tab_seen.emplace(key, 0u).second;  // first sight: in place; a second one uploads
+    }
     const size_t main_dw = static_cast<size_t>(cols) * rows_pad * 5;
     const size_t img_dw = rows <= 4 ? rup(cols, 4) * 20 : 0;
     // wide kernels (rows > 8): [column pair][rows_pad][12] dwords, per (pair,
@@ -188,12 +211,18 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     if (st.cap < bytes) {
         if (st.host) (void)hipHostFree(st.host);
         st.host = nullptr;
+        st.dev_host = nullptr;
         st.cap = 0;
         const size_t cap = rup(bytes, size_t{64} << 10);
-        if (hipHostMalloc(reinterpret_cast<void**>(&st.host), cap, hipHostMallocDefault) != hipSuccess) {
+        // coherent and mapped: a first-sight launch reads it in place
+        if (hipHostMalloc(reinterpret_cast<void**>(&st.host), cap,
+                          hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
             (void)hipGetLastError();
             return RS_ERR_NOMEM;
         }
+        void* hd = nullptr;
+        if (hipHostGetDevicePointer(&hd, st.host, 0) == hipSuccess) st.dev_host = static_cast<const uint8_t*>(hd);
+        (void)hipGetLastError();
         st.cap = cap;
     }
     uint32_t* host = reinterpret_cast<uint32_t*>(st.host);
@@ -214,6 +243,13 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
                 w[8 + h] = t[4];
             }
         }
+    if (inplace && st.dev_host) {
+        *inplace_slot = static_cast<int>(&st - rs->tab_stage);
+        *out = reinterpret_cast<const uint32_t*>(st.dev_host);
+        *rows_pad_out = rows_pad;
+        ++rs->tab_inplace;
+        return RS_OK;
+    }
     uint32_t* dptr = nullptr;
     if (hipMalloc(&dptr, bytes) != hipSuccess) {
         (void)hipGetLastError();
@@ -233,6 +269,7 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
         return dev_fail(e, "table upload");
     }
     st.pending = true;
+    ++rs->tab_uploads;
     rs->tables.emplace(std::move(key), te);
     *out = dptr;
     *rows_pad_out = rows_pad;
@@ -250,7 +287,9 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
     MatmulArgs a;
     std::memset(&a, 0, sizeof a);
     std::lock_guard<std::mutex> lk(rs->tab_mu);  // table lookup through launch (get_tables)
-    int rc = get_tables(rs, mat, rows, cols, stream, &a.tables, &a.rows_pad);
+    int slot = -1;
+    int rc = get_tables(rs, mat, rows, cols, stream, &a.tables, &a.rows_pad,
+                        static_cast<uint64_t>(nstripes) * len * static_cast<uint64_t>(cols), &slot);
     if (rc) return rc;
     a.img4 = rows <= 4 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
     a.wide = rows > 8 ? a.tables + static_cast<size_t>(cols) * a.rows_pad * 5 : nullptr;
@@ -270,7 +309,14 @@ int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* c
         a.ptr[cols + r] = reinterpret_cast<uint64_t>(out_ptrs[r]);
         a.sid[cols + r] = out_sid ? out_sid[r] : 1;
     }
-    const hipError_t e = launch_gf_matmul(a, stream);
+    hipError_t e = launch_gf_matmul(a, stream);
+    if (slot >= 0) {  // tables read in place: the slot is reused after this launch
+        rs_t::TabStage& st = rs->tab_stage[slot];
+        const hipError_t er = hipEventRecord(st.done, stream);
+        if (er == hipSuccess) st.pending = true;
+        else (void)hipStreamSynchronize(stream);
+        if (e == hipSuccess) e = er;
+    }
     return e == hipSuccess ? RS_OK : dev_fail(e, "kernel launch");
 }
 
@@ -834,6 +880,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_pageable_stage") g_host_pageable_stage = value;
         else if (n == "bind_numa") g_bind_numa = value;
         else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
+        else if (n == "table_inplace_max") g_tab_inplace_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_coalesce_linger_us") g_coalesce_linger_us = value < 0 ? 0 : value;
         else if (n == "host_engine_direct") g_engine_direct = value ? 1 : 0;
         else if (n == "host_coalesce_running") g_co_running = value < 1 ? 1 : value > 2 ? 2 : value;
@@ -902,6 +949,16 @@ int rs_reconst_matrix(rs_t* rs, const int* survived_d, const int* need, int nn, 
 int rs_jit_stats(uint64_t* compiled, uint64_t* failed, uint64_t* launches, double* compile_ms) {
     return abi_guard([&]() -> int {
         jit_stats(compiled, failed, launches, compile_ms);
+        return RS_OK;
+    });
+}
+
+int rs_coef_table_stats(const rs_t* rs, uint64_t* uploads, uint64_t* inplace) {
+    return abi_guard([&]() -> int {
+        if (!rs) return RS_ERR_INVAL;
+        std::lock_guard<std::mutex> lk(const_cast<rs_t*>(rs)->tab_mu);
+        if (uploads) *uploads = rs->tab_uploads;
+        if (inplace) *inplace = rs->tab_inplace;
         return RS_OK;
     });
 }

@@ -39,6 +39,7 @@ namespace detail {
 constexpr int kMaxVects = 256;                              // rs.go:47
 constexpr uint64_t kMaxInverseCacheBytes = 16ull << 20;     // rs.go:50
 extern size_t g_registry_max;  // coefficient-table registry cap (distinct matrices per handle)
+extern size_t g_tab_inplace_max;  // launches up to this many input bytes read a new matrix's tables in place
 
 // Record which HIP call failed (thread-local, read by rs_last_device_error)
 // and return RS_ERR_DEVICE.
@@ -114,6 +115,7 @@ struct rs_codec {
     // once the copy enqueued from it kRing uploads earlier has finished.
     struct TabStage {
         uint8_t* host = nullptr;
+        const uint8_t* dev_host = nullptr;  // its device address (coherent, mapped: read in place)
         size_t cap = 0;
         hipEvent_t done = nullptr;
         bool pending = false;
@@ -121,6 +123,11 @@ struct rs_codec {
     static constexpr int kTabStages = 4;
     TabStage tab_stage[kTabStages];
     int tab_stage_next = 0;
+    // Matrices a small launch has used once with its tables read in place
+    // from a staging slot (get_tables): the second sight uploads them.
+    // Bounded (cleared when full).
+    std::unordered_map<std::string, uint32_t> tab_seen;
+    uint64_t tab_uploads = 0, tab_inplace = 0;  // (rs_coef_table_stats)
 
     std::mutex stage_mu;  // staging for the host-memory entry points
     uint8_t* stage = nullptr;
@@ -377,7 +384,7 @@ uint64_t cache_key(const int* survived, int ns);                    // rs.go:414
 // ---------------------------------------------------------------- device product (codec.cpp)
 int ensure_device(rs_t* rs);
 int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t stream, const uint32_t** out,
-               int* rows_pad_out);
+               int* rows_pad_out, uint64_t launch_in_bytes = ~uint64_t{0}, int* inplace_slot = nullptr);
 int matmul_ex(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* in_ptrs,
               const uint8_t* in_sid, uint8_t* const* out_ptrs, const uint8_t* out_sid, const int64_t ss[4],
               int nstripes, uint64_t len, bool accumulate, hipStream_t stream, const int32_t* stripe_ids = nullptr);
@@ -476,6 +483,8 @@ public:
     // No copy: the consumer kernels on `st` read the filled host buffer in
     // place through its device address (and may write the device slot); the
     // slot is reused only after they finish (the destructor's `done` event).
+    // Does the acquired slot have a device address for map()?
+    bool mappable() const { return slot_ && slot_->host_dev; }
     int map(hipStream_t st, const uint8_t** host_dev, uint8_t** dev) {
         if (!slot_->host_dev) return dev_fail(hipErrorInvalidValue, "upload slot device address");
         st_ = st;

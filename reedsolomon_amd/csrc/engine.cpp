@@ -30,6 +30,7 @@
 // already finished a call (done word) skip it, so no unit is computed twice
 // (Update / Replace XOR into their outputs).
 #include <immintrin.h>
+#include <pthread.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -315,9 +316,19 @@ struct Warmer {
     std::thread th;
     pid_t owner = 0;
 };
+// Never destroyed (see jit.cpp's Jit).  A forked child inherits the object
+// but not the thread, possibly with `mu` held by it at the fork, and a queue
+// of the parent's handles: its pthread_atfork handler gives the child a fresh
+// Warmer (the inherited one is left alone; advisor r05).
+Warmer* g_warmer = nullptr;
+void warmer_fork_child() { g_warmer = new Warmer; }
 Warmer& warmer() {
-    static Warmer* w = new Warmer;  // never destroyed (see jit.cpp's Jit)
-    return *w;
+    static const bool init = [] {
+        g_warmer = new Warmer;
+        return pthread_atfork(nullptr, nullptr, warmer_fork_child) == 0;
+    }();
+    (void)init;
+    return *g_warmer;
 }
 void warmer_atexit() {
     Warmer& w = warmer();
@@ -356,8 +367,7 @@ void engine_warm_async(rs_t* rs) {
     std::lock_guard<std::mutex> lk(w.mu);
     if (w.stop) return;
     if (w.cur != rs && std::find(w.q.begin(), w.q.end(), rs) == w.q.end()) w.q.push_back(rs);
-    if (!w.th.joinable() || w.owner != getpid()) {
-        if (w.th.joinable()) w.th.detach();  // (a forked child starts its own)
+    if (!w.th.joinable()) {  // (a forked child's fresh Warmer starts its own)
         static const bool registered = std::atexit(warmer_atexit) == 0;
         (void)registered;
         w.owner = getpid();

@@ -43,6 +43,7 @@
 #include <hip/hiprtc.h>
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <pthread.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -730,10 +731,10 @@ struct Jit {
     std::atomic<bool> evict_wanted{false};
     bool evict_task = false;  // an eviction is queued for the worker (under mu)
 
-    // Caller holds mu.  Starts the worker thread if this process has none.
+    // Caller holds mu.  Starts the worker thread if this object has none (a
+    // forked child works on a fresh object: jit() below).
     void ensure_worker() {
-        if (worker.joinable() && owner == getpid()) return;
-        if (worker.joinable()) worker.detach();  // (a forked child starts its own)
+        if (worker.joinable()) return;
         // load the compiler library hiprtc would load on its first compile
         // now, so its static destructors are registered before jit_atexit and
         // run after it (atexit order)
@@ -746,17 +747,37 @@ struct Jit {
     }
 };
 
+// Never destroyed (a std::thread destructor on a joinable thread aborts); the
+// process that started the worker joins it at exit: the compile in flight
+// finishes (hiprtc only), queued ones are dropped.  A forked child inherits
+// the object but not its worker thread, possibly with `mu` or the eviction
+// lock held by that thread at the fork and with modules loaded into the
+// parent's HIP context: the child's pthread_atfork handler gives it a fresh
+// Jit and eviction lock instead (the inherited ones are left alone, never
+// destroyed; advisor r05).
+Jit* g_jit = nullptr;
 // Launches hold this shared from the lookup of a compiled kernel until it is
 // enqueued; eviction holds it exclusively, drains the devices and unloads.
-std::shared_mutex g_evict_mu;
+std::shared_mutex* g_evict_mu = nullptr;
 
-// Never destroyed (a std::thread destructor on a joinable thread aborts, and a
-// forked child inherits the object but not the thread); the process that
-// started the worker joins it at exit: the compile in flight finishes
-// (hiprtc only), queued ones are dropped.
+void jit_fork_child() {
+    g_jit = new Jit;
+    g_evict_mu = new std::shared_mutex;
+}
+
 Jit& jit() {
-    static Jit* j = new Jit;
-    return *j;
+    static const bool init = [] {
+        g_jit = new Jit;
+        g_evict_mu = new std::shared_mutex;
+        return pthread_atfork(nullptr, nullptr, jit_fork_child) == 0;
+    }();
+    (void)init;
+    return *g_jit;
+}
+
+std::shared_mutex& evict_mu() {
+    (void)jit();
+    return *g_evict_mu;
 }
 
 void jit_trace_report() {
@@ -1109,7 +1130,7 @@ void jit_evict_now() {
     std::vector<std::shared_ptr<Entry>> victims;
     std::set<int> devs;
     {
-        std::unique_lock<std::shared_mutex> ex(g_evict_mu);
+        std::unique_lock<std::shared_mutex> ex(evict_mu());
         std::lock_guard<std::mutex> lk(j.mu);
         if (!j.evict_wanted.load(std::memory_order_acquire)) return;
         std::vector<std::pair<uint64_t, std::string>> loaded;
@@ -1156,7 +1177,7 @@ std::shared_lock<std::shared_mutex> jit_launch_guard() {
             j.cv.notify_one();
         }
     }
-    return std::shared_lock<std::shared_mutex>(g_evict_mu);
+    return std::shared_lock<std::shared_mutex>(evict_mu());
 }
 
 JitKernel jit_kernel_for(const MatmulArgs& a, int bs, uint64_t launch_bytes) {

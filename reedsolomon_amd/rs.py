@@ -454,6 +454,12 @@ class RS:
         _check(lib().rs_host_engine_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
         return int(a.value), int(b.value)
 
+    def coef_table_stats(self) -> tuple:
+        """(uploads, in-place first sights) of this codec's coefficient tables (rs_coef_table_stats)."""
+        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(lib().rs_coef_table_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return int(a.value), int(b.value)
+
     def host_call_stats(self) -> tuple:
         """(launches, calls) of coalesced host calls since New (see rs_host_call_stats)."""
         a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)

@@ -63,23 +63,3 @@ def rslib():
 
     build.build()
     return reedsolomon_amd
-
-
-_ARENAS = []
-
-
-def host_arena(nbytes: int):
-    """A page-aligned uint8 numpy array over its own anonymous mapping, kept
-    for the whole session, for tests that rs_host_register memory.  The HIP
-    runtime's pageable-copy path faulted (hipErrorIllegalAddress at a later
-    torch `.cuda()` of a new numpy array) when registered-then-unregistered
-    ranges shared pages with, or were freed and reused by, ordinary heap
-    arrays; a mapping of its own that is never unmapped rules both out."""
-    import mmap
-
-    import numpy as np
-
-    size = max(4096, (nbytes + 4095) // 4096 * 4096)
-    m = mmap.mmap(-1, size)
-    _ARENAS.append(m)
-    return np.frombuffer(m, dtype=np.uint8, count=nbytes)

@@ -1,0 +1,86 @@
+"""What the HIP runtime and ROCr still know about a host address range.
+
+Test helper for the registration lifecycle (Weak #1): after
+rs_host_register -> rs_host_unregister, no page of the range may still be
+registered with either runtime layer, or a later pageable copy from a new
+allocation at those addresses could be served through a stale mapping.
+
+  * hipPointerGetAttributes: the HIP runtime's memory-object map
+    (hipMemoryTypeHost = registered or pinned host memory);
+  * hsa_amd_pointer_info: ROCr's view (HSA_EXT_POINTER_TYPE_LOCKED = a range
+    locked through ROCr; HSA = a runtime allocation).
+
+Calibrated on the MI355X box (tools/ptr_state_probe.py,
+profiles/r06/ptr_state_probe.log): a hipHostRegister'ed page (directly or
+through rs_host_register) is hipMemoryTypeHost to HIP and UNKNOWN to ROCr
+(the runtime registers user memory below ROCr's allocation map), a pageable
+page is hipMemoryTypeUnregistered / UNKNOWN, a hipHostMalloc'ed one is Host /
+HSA.  So "registered" is HIP's answer; ROCr's LOCKED is still reported where
+it appears.  Both are host-side queries: no GPU work is enqueued.
+"""
+import ctypes
+import mmap
+
+PAGE = mmap.PAGESIZE
+HSA_LOCKED = 2
+HIP_HOST = 1
+
+
+class _PtrInfo(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_uint32), ("type", ctypes.c_uint32), ("agentBaseAddress", ctypes.c_void_p),
+                ("hostBaseAddress", ctypes.c_void_p), ("sizeInBytes", ctypes.c_size_t),
+                ("userData", ctypes.c_void_p), ("agentOwner", ctypes.c_uint64), ("global_flags", ctypes.c_uint32),
+                ("registered", ctypes.c_bool)]
+
+
+class _HipAttr(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+_LIBS = []
+
+
+def _libs():
+    if not _LIBS:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hsa = ctypes.CDLL("libhsa-runtime64.so.1")
+        hip.hipPointerGetAttributes.argtypes = [ctypes.POINTER(_HipAttr), ctypes.c_void_p]
+        hip.hipGetLastError.restype = ctypes.c_int
+        hsa.hsa_amd_pointer_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(_PtrInfo), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        _LIBS.extend([hip, hsa])
+    return _LIBS
+
+
+def page_state(addr: int):
+    """(rocr type, rocr base, rocr size, hip type) of the page holding addr;
+    a negative type is the call's error code."""
+    hip, hsa = _libs()
+    pi = _PtrInfo()
+    pi.size = ctypes.sizeof(_PtrInfo)
+    rc = hsa.hsa_amd_pointer_info(ctypes.c_void_p(addr), ctypes.byref(pi), None, None, None)
+    rt = pi.type if rc == 0 else -rc
+    ha = _HipAttr()
+    hrc = hip.hipPointerGetAttributes(ctypes.byref(ha), ctypes.c_void_p(addr))
+    if hrc != 0:
+        hip.hipGetLastError()
+    return rt, (pi.hostBaseAddress or 0) if rt > 0 else 0, pi.sizeInBytes if rt > 0 else 0, (
+        ha.type if hrc == 0 else -hrc)
+
+
+def known_pages(lo: int, hi: int, skip=()):
+    """Pages of [lo, hi) that either layer still reports as registered / pinned
+    host memory (pages whose start is in `skip` are not asked)."""
+    out = []
+    for pg in range(lo & ~(PAGE - 1), hi, PAGE):
+        if pg in skip:
+            continue
+        rt, base, size, ht = page_state(pg)
+        if rt == HSA_LOCKED or ht == HIP_HOST:
+            out.append((hex(pg), rt, hex(base), size, ht))
+    return out
+
+
+def registered(addr: int) -> bool:
+    return page_state(addr)[3] == HIP_HOST

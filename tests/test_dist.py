@@ -244,6 +244,24 @@ def test_bench_eight_ranks_rehearsal():
     assert r.returncode == 0, r.stderr[-3000:]
     line = _last_json(r.stdout)
     assert line["n_gpus"] == 8 and line["ranks_seen"] == 8, line
+    # the timing group is the default backend (gloo: no RCCL on the SCALE
+    # path), and every rank's device record came back in rank order
+    assert line["backend"] == "gloo", line
+    assert [d["rank"] for d in line["rank_devices"]] == list(range(8)), line
+    assert len({d["pid"] for d in line["rank_devices"]}) == 8, line
+
+
+def test_timing_backend_default_is_gloo():
+    """the driver's first 8-GPU run must not depend on an RCCL
+    init that never ran on hardware; the timing collectives default to gloo,
+    nccl is an explicit opt-in, anything else is refused."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.timing_backend({}) == "gloo"
+    assert bench.timing_backend({"RSAMD_BENCH_BACKEND": "nccl"}) == "nccl"
+    with pytest.raises(SystemExit):
+        bench.timing_backend({"RSAMD_BENCH_BACKEND": "mpi"})
 
 
 def _eight_rank_worker(rank, world, port, q):

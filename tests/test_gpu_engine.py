@@ -273,10 +273,10 @@ def test_engine_on_off_identical(rslib, torch_dev, engine):
 def _registered_arena(rslib, nvec, size):
     """nvec vectors of `size` bytes, 4 KiB apart, in one page-aligned range
     registered with rs_host_register (unregister the returned base)."""
-    from conftest import host_arena
-
     pitch = (size + 4095) // 4096 * 4096
-    base = host_arena(nvec * pitch)
+    arena = np.zeros(nvec * pitch + 4096, np.uint8)  # an ordinary heap array (freed with base)
+    off = (-arena.ctypes.data) % 4096
+    base = arena[off: off + nvec * pitch]
     rslib.host_register(base.ctypes.data, base.nbytes)
     return base, [base[i * pitch: i * pitch + size] for i in range(nvec)]
 

@@ -2,11 +2,14 @@
 (page spans shared by reference, device drain before a span leaves the
 runtime) and the library-owned pool (rs_host_alloc / rs_host_free).
 
-Round 3's GPU suite faulted (hipErrorIllegalAddress at a later pageable
-`.cuda()` copy) after tests registered heap numpy memory, unregistered it and
-let it be freed; the reference's callers reuse their buffers freely
-(rs.go:101-111 retains nothing), so the supported API must allow exactly that
-sequence.  Every result is checked against the oracle (rs_oracle.c)."""
+The reference's callers reuse their buffers freely (rs.go:101-111 retains
+nothing), so the supported API must allow register -> unregister -> free ->
+reuse of ordinary heap memory: the tests below register plain numpy heap
+arrays (whose edge pages neighbouring heap objects share) and mappings they
+unmap afterwards, and after every unregister ask both runtime layers
+(tests/hip_ptr.py: hipPointerGetAttributes, hsa_amd_pointer_info) that no page
+the library released is still registered.  Every result is checked against
+the oracle (rs_oracle.c)."""
 import os
 import subprocess
 import sys
@@ -14,8 +17,7 @@ import sys
 import numpy as np
 import pytest
 
-# mappings a test registered and unregistered, kept for the session (never unmapped)
-_KEEP_MAPPED = []
+import hip_ptr
 
 pytestmark = pytest.mark.gpu
 
@@ -72,9 +74,7 @@ def test_registrations_sharing_pages(rslib, orc, torch_dev):
         r = rslib.New(d, p)
         rng = np.random.default_rng(11)
         spans0 = rslib.host_pool_stats()["spans"]
-        from conftest import host_arena  # (registered memory is never freed: conftest.host_arena)
-
-        arena = host_arena(2 * (d + p) * size + 3 * 4096)
+        arena = np.zeros(2 * (d + p) * size + 3 * 4096, np.uint8)  # an ordinary heap array
         off = (-arena.ctypes.data) % 4096 + 16  # a starts 16 bytes into a page
         a = arena[off: off + (d + p) * size]  # ends 16 bytes into its last page
         b = arena[off + a.nbytes: off + a.nbytes + 4080 + (d + p) * size]  # starts in that page
@@ -97,18 +97,23 @@ def test_registrations_sharing_pages(rslib, orc, torch_dev):
         rslib.host_unregister(a.ctypes.data)
         # only the shared page outlives a: b holds its one-page span
         assert rslib.host_pool_stats()["spans"] - spans0 == 2
+        shared = (a.ctypes.data + a.nbytes) & ~4095
+        assert hip_ptr.known_pages(a.ctypes.data, a.ctypes.data + a.nbytes, skip=(shared,)) == []
+        assert hip_ptr.registered(shared)
         assert _encode_ok(orc, r, d, p, vb, rng)
         assert staged() == s0  # b still zero-copy
         assert _encode_ok(orc, r, d, p, va, rng)
         assert staged() == s0 + 1  # a staged now
         rslib.host_unregister(b.ctypes.data)
         assert rslib.host_pool_stats()["spans"] == spans0
+        assert hip_ptr.known_pages(arena.ctypes.data, arena.ctypes.data + arena.nbytes) == []
         with pytest.raises(rslib.ErrInvalidArgument):
             rslib.host_unregister(b.ctypes.data)
         assert _encode_ok(orc, r, d, p, vb, rng)
         assert staged() == s0 + 2
     finally:
         L.rs_tune(b"host_engine_direct", 1)
+    del va, vb, a, b, arena  # freed: the heap may hand these addresses out again
 
 
 def test_pool_blocks_reused_and_zero_copy(rslib, orc, torch_dev):
@@ -165,10 +170,9 @@ def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
 
     import reedsolomon_amd as rs
 
-    from conftest import host_arena  # (registered memory is never unmapped: conftest.host_arena)
-
     page = mmap.PAGESIZE
-    base = host_arena(8 * page)
+    m = mmap.mmap(-1, 8 * page)
+    base = np.frombuffer(m, dtype=np.uint8)
     views = [base[page // 2: 3 * page + page // 2], base[3 * page: 6 * page]]  # share the page at 3 * page
     errs = []
 
@@ -185,8 +189,10 @@ def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
         t.start()
     for t in th:
         t.join()
-    del views, base
     assert not errs, errs[:3]
+    assert hip_ptr.known_pages(base.ctypes.data, base.ctypes.data + base.nbytes) == []
+    del views, base
+    m.close()  # unmapped: the next mapping may land here
 
 
 def _libc():
@@ -227,6 +233,9 @@ def test_unregister_releases_pages_a_neighbour_does_not_share(rslib, orc, torch_
         va = [arr[64 + i * 1024: 64 + (i + 1) * 1024] for i in range(d + p)]
         assert _encode_ok(orc, r, d, p, va, rng)
         rslib.host_unregister(a_lo)
+        # A's own pages left both runtime layers; the page B shares did not
+        assert hip_ptr.known_pages(base, base + 11 * page) == []
+        assert hip_ptr.registered(base + 11 * page)
         # trim + regrow of A's exclusive pages 0..10: new physical pages, same addresses
         assert c.munmap(base, 11 * page) == 0
         got = c.mmap(base, 11 * page, PROT_RW, MAP_PRIV_ANON | MAP_FIXED, -1, 0)
@@ -240,11 +249,9 @@ def test_unregister_releases_pages_a_neighbour_does_not_share(rslib, orc, torch_
             assert _encode_ok(orc, r, d, p, vc, rng), it
         rslib.host_unregister(base)
         rslib.host_unregister(b_lo)
+        assert hip_ptr.known_pages(base, base + npages * page) == []
     finally:
-        # the range stays mapped for the rest of the session (conftest.host_arena:
-        # a registered-then-unregistered range that is unmapped and reused by a
-        # later heap array has made the runtime's pageable copies from it fault)
-        _KEEP_MAPPED.append((base, npages * page))
+        c.munmap(base, npages * page)
 
 
 def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
@@ -260,9 +267,7 @@ def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
     try:
         r = rslib.New(d, p)
         rng = np.random.default_rng(21)
-        from conftest import host_arena  # (registered memory is never freed: conftest.host_arena)
-
-        buf = host_arena((d + p) * size + 4096)
+        buf = np.zeros((d + p) * size + 4096, np.uint8)  # an ordinary heap array
         off = (-buf.ctypes.data) % 4096
         v = [buf[off + i * size: off + (i + 1) * size] for i in range(d + p)]
         times = []
@@ -272,6 +277,7 @@ def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
             t0 = time.perf_counter()
             rslib.host_unregister(buf[off:].ctypes.data)
             times.append(time.perf_counter() - t0)
+            assert hip_ptr.known_pages(buf.ctypes.data, buf.ctypes.data + buf.nbytes) == [], it
             assert _encode_ok(orc, r, d, p, v, rng), it  # pageable now
         print("unregister ms", [round(x * 1e3, 3) for x in times])
         assert sorted(times)[2] < 0.02, times
@@ -282,16 +288,20 @@ def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
 def test_host_calls_proceed_during_unregister_drain(rslib, orc, torch_dev):
     """rs_host_unregister drains the devices without holding the registry:
     host calls on another registered buffer keep running (and stay correct)
-    while a third thread registers / unregisters in a loop."""
+    while a second thread registers / unregisters an ordinary heap array in a
+    loop.  Then the round-5 fault's sequence: the array is freed, arrays of
+    the sizes the next test allocated (tests/test_gpu_jit.py::_padded, the
+    1.3 MB copy that failed) are allocated and copied to the device through
+    the runtime's pageable path, every byte checked, with no page of them
+    still registered beforehand."""
     import threading
 
+    torch = torch_dev
     d, p, size = 10, 4, 8192
     r = rslib.New(d, p)
     keep = rslib.host_alloc((d + p) * size)
     vk = [keep[i * size:(i + 1) * size] for i in range(d + p)]
-    from conftest import host_arena  # (registered memory is never freed: conftest.host_arena)
-
-    churn = host_arena(64 * 4096)
+    churn = np.zeros(64 * 4096, np.uint8)  # an ordinary heap array
     stop = threading.Event()
     errs = []
 
@@ -316,3 +326,14 @@ def test_host_calls_proceed_during_unregister_drain(rslib, orc, torch_dev):
         t.join(60)
     rslib.host_free(keep)
     assert not errs, errs[:3]
+    lo, hi = churn.ctypes.data, churn.ctypes.data + churn.nbytes
+    assert hip_ptr.known_pages(lo, hi) == []
+    del churn
+    rng = np.random.default_rng(510)
+    for shape in [(3, 10, 16), (2, 10, 2064), (3, 10, 4112), (2, 10, 65632), (2, 5, 65632), (2, 10, (1 << 20) + 16),
+                  (64 * 4096,)]:
+        host = rng.integers(0, 256, shape, dtype=np.uint8)
+        assert hip_ptr.known_pages(host.ctypes.data, host.ctypes.data + host.nbytes) == [], shape
+        dev = torch.from_numpy(host).cuda()
+        torch.cuda.synchronize()
+        assert np.array_equal(dev.cpu().numpy(), host), shape

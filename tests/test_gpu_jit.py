@@ -218,9 +218,42 @@ def test_jit_background_compile(rslib, orc, torch_dev):
         torch.cuda.synchronize()
         assert np.array_equal(dst.cpu().numpy(), exp)
         assert rslib.jit_stats()["launches"] == st0["launches"] + 1
+        _fork_child_sees_fresh_jit(rslib)
     finally:
         L.rs_tune(b"jit_min_bytes", 8 << 20)
         L.rs_tune(b"jit_backend", 2)
+
+
+def _fork_child_sees_fresh_jit(rslib):
+    """Advisor r05: a forked child inherits the compile worker's object but not
+    its thread (and possibly its mutex held).  The pthread_atfork handler gives
+    the child a fresh one: its counters start at zero, and taking the lock
+    cannot hang.  The child makes no HIP call and leaves with os._exit."""
+    import os
+
+    assert rslib.jit_stats()["compiled"] > 0
+    rfd, wfd = os.pipe()
+    pid = os.fork()
+    if pid == 0:  # child
+        try:
+            os.write(wfd, str(rslib.jit_stats()["compiled"]).encode())
+        finally:
+            os._exit(0)
+    os.close(wfd)
+    t0 = time.time()
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() - t0 > 20:
+            os.kill(pid, 9)
+            os.waitpid(pid, 0)
+            raise AssertionError("forked child hung in rs_jit_stats (inherited lock)")
+        time.sleep(0.01)
+    got = os.read(rfd, 64).decode()
+    os.close(rfd)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+    assert got == "0", got
 
 
 def test_jit_concurrent_threads_background(rslib, orc, torch_dev):

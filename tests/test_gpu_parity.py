@@ -11,6 +11,8 @@ import threading
 import numpy as np
 import pytest
 
+import hip_ptr
+
 pytestmark = pytest.mark.gpu
 
 
@@ -303,6 +305,68 @@ def test_reconst_batch_every_pattern(rslib, orc, torch_dev):
             v[i][:] = 0x3C
         assert orc.reconst(d, p, v, [], lost) == 0
         assert all(np.array_equal(v[i], got[s, i]) for i in lost), s
+
+
+def test_first_sight_tables_in_place(rslib, orc, torch_dev):
+    """A matrix's first use in a small launch reads its perm tables in place
+    from the mapped staging slot (no upload); its second use uploads them;
+    a large launch uploads at first sight; table_inplace_max 0 always
+    uploads.  Eight new patterns back to back on one stream with no sync in
+    between reuse the four staging slots (each waits for the launch that read
+    it).  Every rebuilt stripe equals the oracle's Reconst (rs.go:221-380)."""
+    torch = torch_dev
+    L = rslib.lib()
+    d, p, S, n = 10, 4, 16, 8192
+    r = rslib.New(d, p)
+    rng = np.random.default_rng(77)
+    host = _rand(rng, S, d + p, n)
+    for s in range(S):
+        v = [x for x in host[s]]
+        assert orc.encode(d, p, v) == 0
+    buf = torch.from_numpy(host.copy()).cuda()
+    pats = [[0], [1, 12], [2, 5, 11], [3, 4, 6, 13], [7], [8, 9], [0, 10], [1, 2, 3], [5, 6]]
+
+    def rebuild(lost, sync=True, b=None, h=None):
+        b = buf if b is None else b
+        for v in lost:
+            b[:, v] = 0x77
+        r.reconst_batch(b, [], lost)
+        if sync:
+            torch.cuda.synchronize()
+            assert torch.equal(b.cpu(), torch.from_numpy(host if h is None else h)), lost
+
+    up0, ip0 = r.coef_table_stats()
+    rebuild(pats[0])
+    up1, ip1 = r.coef_table_stats()
+    assert (up1 - up0, ip1 - ip0) == (0, 1)  # first sight: in place
+    rebuild(pats[0])
+    up2, ip2 = r.coef_table_stats()
+    assert (up2 - up1, ip2 - ip1) == (1, 0)  # second sight: uploaded
+    rebuild(pats[0])
+    assert r.coef_table_stats() == (up2, ip2)  # registry hit
+    for lost in pats[1:]:  # 8 new patterns, no sync between them: slots reused behind their launches
+        rebuild(lost, sync=False)
+    torch.cuda.synchronize()
+    assert torch.equal(buf.cpu(), torch.from_numpy(host))
+    up3, ip3 = r.coef_table_stats()
+    assert (up3 - up2, ip3 - ip2) == (0, 8)
+    # a large launch (> table_inplace_max input bytes) uploads at first sight
+    big_h = np.concatenate([host] * 2, axis=2)  # 16 KiB vectors: 16 x 10 x 16 KiB = 2.5 MiB of input
+    big = torch.from_numpy(big_h.copy()).cuda()
+    rebuild([4, 9], b=big, h=big_h)
+    assert r.coef_table_stats() == (up3 + 1, ip3)
+    assert L.rs_tune(b"table_inplace_max", 0) == 0
+    try:
+        rebuild([6, 11])
+        assert r.coef_table_stats() == (up3 + 2, ip3)
+    finally:
+        L.rs_tune(b"table_inplace_max", 2 << 20)
+    # the oracle rebuilds the same stripe from the same survivors
+    v = [x.copy() for x in host[3]]
+    for i in (2, 5, 11):
+        v[i][:] = 0
+    assert orc.reconst(d, p, v, [], [2, 5, 11]) == 0
+    assert all(np.array_equal(v[i], host[3, i]) for i in range(d + p))
 
 
 def test_reconst_dev_and_explicit_survived(rslib, orc, torch_dev):
@@ -650,10 +714,10 @@ def test_host_calls_on_registered_memory(rslib, orc, torch_dev):
     r = rslib.New(d, p)
     rng = np.random.default_rng(404)
     for size in (4096, 65536, 1 << 20, 1000):
-        from conftest import host_arena
-
         pitch = (size + 4095) // 4096 * 4096
-        base = host_arena((d + p + 1) * pitch)
+        arena = np.zeros((d + p + 1) * pitch + 4096, np.uint8)  # an ordinary heap array
+        off = (-arena.ctypes.data) % 4096
+        base = arena[off: off + (d + p + 1) * pitch]
         rslib.host_register(base.ctypes.data, base.nbytes)
         try:
             v = [base[i * pitch: i * pitch + size] for i in range(d + p)]
@@ -683,6 +747,8 @@ def test_host_calls_on_registered_memory(rslib, orc, torch_dev):
             assert np.array_equal(mixed[d], exp[0]), (size, "mixed")
         finally:
             rslib.host_unregister(base.ctypes.data)
+        assert hip_ptr.known_pages(base.ctypes.data, base.ctypes.data + base.nbytes) == [], size
+        del v, base, arena  # freed: its addresses go back to the heap
 
 
 def test_encode_host_batch_pipeline(rslib, orc, torch_dev):
@@ -732,12 +798,8 @@ def test_host_batch_zero_copy(rslib, orc, torch_dev):
     rng = np.random.default_rng(122)
     host = _rand(rng, S, d + p, n)
     exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
-    # registered pageable numpy buffer -> device-mapped (a mapping of its own,
-    # kept for the session: conftest.host_arena)
-    from conftest import host_arena
-
-    reg = host_arena(host.nbytes).reshape(host.shape)
-    reg[:] = host
+    # registered pageable numpy heap buffer -> device-mapped, freed afterwards
+    reg = host.copy()
     rslib.host_register(reg.ctypes.data, reg.nbytes)
     try:
         dp = rslib.host_device_pointer(reg.ctypes.data, reg.nbytes)
@@ -746,6 +808,8 @@ def test_host_batch_zero_copy(rslib, orc, torch_dev):
         assert np.array_equal(reg[:, d:], exp)
     finally:
         rslib.host_unregister(reg.ctypes.data)
+    assert hip_ptr.known_pages(reg.ctypes.data, reg.ctypes.data + reg.nbytes) == []
+    del reg
     full = host.copy()
     full[:, d:] = exp
     masks = np.zeros(S, np.uint64)
@@ -927,7 +991,7 @@ def _distinct_patterns(d, p, count, seed, kmax=4):
 @pytest.mark.parametrize("d,p,n,npat,kmax", [(10, 4, 8192, 1470, 4), (100, 28, 4096, 300, 4), (6, 3, 16, 129, 4),
                                              (32, 32, 1024, 512, 4), (60, 4, 2048, 9, 4), (10, 8, 4096, 800, 8),
                                              (20, 12, 1024, 600, 8), (40, 30, 2048 + 16, 100, 8), (8, 6, 64, 6475, 6)])
-def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
+def test_reconst_batch_multi_gpu_planner(rslib, orc, torch_dev, d, p, n, npat, kmax):
     """rs_tune("multi_gpu_plan", n): a batch with at least n distinct erasure
     patterns has its pattern tables and descriptors built on the GPU
     (gf_plan_multi, kernels.hip: the lost data from a dn x dn inverse) instead
@@ -936,7 +1000,11 @@ def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
     masks reaching past bit 64), and patterns of up to 8 (10+8, 20+12, 40+30;
     8+6: all 6,475 of C(14, 1..6)) in the one launch whose tables hold 8 rows,
     rebuilt bit-exact through both planners, stripes shuffled, a few stripes
-    untouched."""
+    untouched.  A sample of the stripes of every shape (patterns of every
+    erasure count, and masks past bit 64 for 100+28) is also rebuilt by the
+    oracle from the same survivors (orc.reconst: rs.go:327-373 restated) and
+    must equal the GPU planner's bytes, so the planner is pinned to the
+    oracle, not only to the HIP encoder's round trip."""
     torch = torch_dev
     L = rslib.lib()
     pats = _distinct_patterns(d, p, npat, d * 1000 + p, kmax)
@@ -955,6 +1023,7 @@ def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
     for i, m in enumerate(pats):
         masks[int(order[i])] = m   # (the 3 stripes past the patterns stay untouched)
     arg = masks if d + p > 64 else np.array(masks, dtype=np.uint64)
+    sample = _planner_sample(pats, order, d + p)
     try:
         for plan in (1, 0):
             assert L.rs_tune(b"multi_gpu_plan", plan) == 0
@@ -962,16 +1031,46 @@ def test_reconst_batch_multi_gpu_planner(rslib, torch_dev, d, p, n, npat, kmax):
                 for v in range(d + p):
                     if m >> v & 1:
                         (data[s, v] if v < d else parity[s, v - d]).fill_(0x5A)
+            broken = _host_stripes(data, parity, sample) if plan == 1 else None
             r.reconst_batch_multi(data, parity, arg)
             torch.cuda.synchronize()
             bad = [s for s in range(S) if not (torch.equal(data[s], ref_d[s]) and torch.equal(parity[s], ref_p[s]))]
             assert not bad, (plan, bad[:5], [bin(masks[s]) for s in bad[:5]])
+            if plan == 1:
+                _oracle_rebuilds_sample(orc, d, p, broken, masks, data, parity, sample)
     finally:
         L.rs_tune(b"multi_gpu_plan", -1)
 
 
+def _planner_sample(pats, order, nvec, k=48):
+    """Stripes (indexes) of up to k patterns spread over the pattern list (the
+    exhaustive lists run by erasure count, so every count is hit), plus up to
+    8 whose masks reach past bit 63 when the code is that wide."""
+    idx = sorted(set(np.linspace(0, len(pats) - 1, min(len(pats), k)).astype(int).tolist()))
+    if nvec > 64:
+        idx += [i for i, m in enumerate(pats) if m >> 64][:8]
+    return sorted({int(order[i]) for i in idx})
+
+
+def _host_stripes(data, parity, stripes):
+    return {s: ([x.copy() for x in data[s].cpu().numpy()], [x.copy() for x in parity[s].cpu().numpy()])
+            for s in stripes}
+
+
+def _oracle_rebuilds_sample(orc, d, p, broken, masks, data, parity, sample):
+    """The oracle rebuilds each sampled stripe from the same survivors the
+    GPU saw (the broken copy); every vector must equal the GPU's."""
+    for s in sample:
+        v = broken[s][0] + broken[s][1]
+        lost = [i for i in range(d + p) if masks[s] >> i & 1]
+        assert orc.reconst(d, p, v, [], lost) == 0, (s, lost)
+        got = np.concatenate([data[s].cpu().numpy(), parity[s].cpu().numpy()])
+        bad = [i for i in range(d + p) if not np.array_equal(v[i], got[i])]
+        assert not bad, ("GPU planner vs oracle", s, lost, bad[:4])
+
+
 @pytest.mark.parametrize("d,p,npat", [(10, 4, 300), (32, 32, 700)])
-def test_reconst_batch_multi_repeated_patterns(rslib, torch_dev, d, p, npat):
+def test_reconst_batch_multi_repeated_patterns(rslib, orc, torch_dev, d, p, npat):
     """The host groups stripes by pattern (batches.cpp group_patterns): the
     previous stripe's pattern, a scan of the first 16, then a hash that grows
     as patterns arrive.  Stripes here repeat their patterns in runs, in
@@ -998,6 +1097,8 @@ def test_reconst_batch_multi_repeated_patterns(rslib, torch_dev, d, p, npat):
     torch.cuda.synchronize()
     ref_d, ref_p = data.clone(), parity.clone()
     arg = np.array(masks, dtype=np.uint64)
+    lossy = [s for s, m in enumerate(masks) if m]
+    sample = sorted(set(lossy[i] for i in np.linspace(0, len(lossy) - 1, 40).astype(int).tolist()))
     try:
         for plan in (1, 0):
             assert L.rs_tune(b"multi_gpu_plan", plan) == 0
@@ -1005,9 +1106,12 @@ def test_reconst_batch_multi_repeated_patterns(rslib, torch_dev, d, p, npat):
                 for v in range(d + p):
                     if m >> v & 1:
                         (data[s, v] if v < d else parity[s, v - d]).fill_(0x3C)
+            broken = _host_stripes(data, parity, sample) if plan == 1 else None
             r.reconst_batch_multi(data, parity, arg)
             torch.cuda.synchronize()
             assert torch.equal(data, ref_d) and torch.equal(parity, ref_p), plan
+            if plan == 1:  # pinned to the oracle, not only to the HIP encoder's round trip
+                _oracle_rebuilds_sample(orc, d, p, broken, masks, data, parity, sample)
     finally:
         L.rs_tune(b"multi_gpu_plan", -1)
 

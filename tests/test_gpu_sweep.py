@@ -205,13 +205,19 @@ def test_update_replace_at_reference_defect_sizes(rslib, orc, torch_dev, size):
 
 
 @pytest.mark.parametrize("l1d,size", [(32768, 17031), (32768, 49263), (32768, 236667), (49152, 24576 + 33),
-                                      (49152, 3 * 24576 + 1000 + 5), (32768, 16384 * 3)])
+                                      (49152, 3 * 24576 + 1000 + 5), (32768, 16384 * 3),
+                                      (-1, 16384 + 17), (-1, 49152 + 17), (-1, 100000 + 3)])
 def test_update_replace_reference_compat_mode(rslib, orc, torch_dev, l1d, size):
     """rs_set_ref_l1d(handle, l1d) reproduces the reference's Update /
     Replace bytes (rs.go:190-200 tail pass, rs_oracle.c encode_part) on a host
     whose L1D is `l1d`: host API, single-stripe device call and device batch,
-    byte for byte against the restated reference with the same L1D.  The last
-    size has no defect range (a whole number of chunks): compat = re-encode."""
+    byte for byte against the restated reference with the same L1D.  The
+    sixth size has no defect range (a whole number of chunks): compat =
+    re-encode.  l1d = -1 is the cgo binding's default (its New calls
+    rs_set_ref_l1d(h, -1)): THIS host's L1D as rs.go reads it,
+    so a Go drop-in gets the reference's bytes at defect sizes such as
+    16 KiB + 17 (a defect on 32 KiB-L1D hosts) and 48 KiB + 17 (on both 32 and
+    48 KiB hosts)."""
     torch = torch_dev
     L = rslib.lib()
     d, p, row, rows = 10, 4, 3, [1, 6, 9]
@@ -222,6 +228,10 @@ def test_update_replace_reference_compat_mode(rslib, orc, torch_dev, l1d, size):
     new = _rand(rng, size)
     r = rslib.New(d, p)
     r.set_ref_l1d(l1d)
+    if l1d == -1:  # the binding's New: this host's L1D, 32 KiB when CPUID has none (rs.go:159-161)
+        host = rslib.host_l1d()
+        l1d = host if host > 0 else 32768
+        print("host L1D", host, "defect range", orc.update_quirk_range(size, l1d))
     assert r.ref_l1d == l1d
     orc.set_l1d(l1d)
     try:
