@@ -282,13 +282,11 @@ RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stri
  * rs_host_unregister(ptr) takes the address given to rs_host_register
  * (RS_ERR_INVAL for any other); a page leaves the runtime when the last
  * registration holding it goes, after every device this process launched on
- * has been drained.  The library then holds nothing of the range (the
- * reference retains nothing after a call: rs.go:101-111).  Caution, outside
- * the library: with ROCm 7.x the HIP runtime's own pageable copies
- * (hipMemcpy from ordinary memory) have faulted on a range that was
- * registered, unregistered, freed and reused by a new heap allocation
- * (DESIGN.md §5.8); buffers registered once for the process's life, or
- * rs_host_alloc blocks, avoid that pattern.
+ * has been drained.  The library then holds nothing of the range, and the
+ * runtime reports no page of it registered any more (hipPointerGetAttributes,
+ * checked after every unregister of the GPU tests): the
+ * caller may free the memory and the allocator may reuse the addresses (the
+ * reference retains nothing after a call: rs.go:101-111).
  * No rs_host_register equivalent exists in the reference; it replaces the
  * pinning a cgo caller would otherwise do per call. */
 RS_API int rs_host_register(void* ptr, size_t bytes);
@@ -298,8 +296,7 @@ RS_API int rs_host_register(void* ptr, size_t bytes);
  * (page-aligned; size classes of powers of two from 64 KiB), device-mapped
  * like registered memory; rs_host_free returns it to the library, which keeps
  * it registered and mapped for reuse and never gives the pages back while the
- * process runs (no register / unregister / unmap churn, so no freed range is
- * ever reused by the runtime's own pageable copies).  A reused block holds its
+ * process runs (no per-buffer register / unregister cost).  A reused block holds its
  * previous bytes.  rs_host_free(NULL) is a no-op; any other pointer that is
  * not a live block gives RS_ERR_INVAL.  Thread-safe. */
 RS_API int rs_host_alloc(size_t bytes, void** out);
@@ -597,7 +594,11 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "table_inplace_max" (bytes of input vectors up to which a launch reads a
  * matrix it sees for the first time with its tables in place from a mapped
  * staging slot, the matrix's second use uploading them; default 2 MiB, 0 =
- * upload at first sight; see rs_coef_table_stats).  Returns
+ * upload at first sight; see rs_coef_table_stats), "table_stage_vram" (1:
+ * the tables' staging slots in device memory the host writes through the
+ * BAR, where the platform maps it, so a first-sight launch reads them from
+ * HBM; 0: coherent pinned host memory, read across PCIe; slots allocated
+ * after the change).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name.  The code-shape experiments of
  * earlier rounds (the knob named var, env RSAMD_VAR; some are XOR-only
  * diagnostics) exist only in the separate experiments build librsamd_exp.so:

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <immintrin.h>
+
 #include "codec_internal.hpp"
 
 #if defined(__x86_64__) || defined(__i386__)
@@ -119,6 +121,13 @@ size_t g_registry_max = size_t{1} << 14;
 // caller's path; the matrix's second use uploads them (get_tables).
 // rs_tune("table_inplace_max", bytes), 0 = always upload at first sight.
 size_t g_tab_inplace_max = size_t{2} << 20;
+// Table staging slots in device memory the host writes through the BAR
+// (uncached, hipDeviceMallocUncached; the engine's host_writable_vram_get):
+// a first-sight launch then reads its tables from local HBM instead of
+// across PCIe, and an upload is a device-to-device copy.  Platforms that map
+// no device memory for the CPU keep coherent pinned host memory.  Taken by
+// slots allocated after a change; rs_tune("table_stage_vram", 1 default | 0).
+int g_tab_stage_vram = 1;
 
 thread_local char g_last_dev_err[192] = {0};
 
@@ -209,24 +218,38 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     }
     if (!st.done) RS_TRY(hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "table staging event"));
     if (st.cap < bytes) {
-        if (st.host) (void)hipHostFree(st.host);
+        if (st.host && st.vram) host_writable_vram_put(rs->device, st.host, st.cap);
+        else if (st.host) (void)hipHostFree(st.host);
         st.host = nullptr;
         st.dev_host = nullptr;
         st.cap = 0;
         const size_t cap = rup(bytes, size_t{64} << 10);
-        // coherent and mapped: a first-sight launch reads it in place
-        if (hipHostMalloc(reinterpret_cast<void**>(&st.host), cap,
-                          hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+        size_t vcap = 0;
+        uint8_t* v = g_tab_stage_vram ? host_writable_vram_get(rs->device, cap, &vcap) : nullptr;
+        if (v) {  // device memory the host writes: read in place from HBM
+            st.host = v;
+            st.dev_host = v;
+            st.cap = vcap;
+            st.vram = true;
+        } else {  // coherent and mapped pinned host memory: read in place over PCIe
+            if (hipHostMalloc(reinterpret_cast<void**>(&st.host), cap,
+                              hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+                (void)hipGetLastError();
+                return RS_ERR_NOMEM;
+            }
+            void* hd = nullptr;
+            if (hipHostGetDevicePointer(&hd, st.host, 0) == hipSuccess) st.dev_host = static_cast<const uint8_t*>(hd);
             (void)hipGetLastError();
-            return RS_ERR_NOMEM;
+            st.cap = cap;
+            st.vram = false;
         }
-        void* hd = nullptr;
-        if (hipHostGetDevicePointer(&hd, st.host, 0) == hipSuccess) st.dev_host = static_cast<const uint8_t*>(hd);
-        (void)hipGetLastError();
-        st.cap = cap;
     }
-    uint32_t* host = reinterpret_cast<uint32_t*>(st.host);
-    std::memset(host, 0, bytes);
+    // built in host memory, then one streaming copy into the slot (a VRAM
+    // slot is write-combined: no reads of it, and the stores are fenced
+    // before any launch or copy can read them)
+    thread_local std::vector<uint32_t> build;
+    build.assign(bytes / 4, 0u);
+    uint32_t* host = build.data();
     for (int c = 0; c < cols; ++c)
         for (int r = 0; r < rows; ++r) {
             uint32_t t[5];
@@ -243,6 +266,8 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
                 w[8 + h] = t[4];
             }
         }
+    std::memcpy(st.host, host, bytes);
+    if (st.vram) _mm_sfence();
     if (inplace && st.dev_host) {
         *inplace_slot = static_cast<int>(&st - rs->tab_stage);
         *out = reinterpret_cast<const uint32_t*>(st.dev_host);
@@ -258,7 +283,8 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     rs_t::TableEntry te;
     te.dev = dptr;
     te.stream = stream;
-    hipError_t e = hipMemcpyAsync(dptr, host, bytes, hipMemcpyHostToDevice, stream);
+    hipError_t e = hipMemcpyAsync(dptr, st.host, bytes, st.vram ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                  stream);
     if (e == hipSuccess) e = hipEventRecord(st.done, stream);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&te.ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(te.ready, stream);
@@ -881,6 +907,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "bind_numa") g_bind_numa = value;
         else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
         else if (n == "table_inplace_max") g_tab_inplace_max = value < 0 ? 0 : static_cast<size_t>(value);
+        else if (n == "table_stage_vram") g_tab_stage_vram = value ? 1 : 0;
         else if (n == "host_coalesce_linger_us") g_coalesce_linger_us = value < 0 ? 0 : value;
         else if (n == "host_engine_direct") g_engine_direct = value ? 1 : 0;
         else if (n == "host_coalesce_running") g_co_running = value < 1 ? 1 : value > 2 ? 2 : value;

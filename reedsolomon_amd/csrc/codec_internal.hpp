@@ -40,6 +40,7 @@ constexpr int kMaxVects = 256;                              // rs.go:47
 constexpr uint64_t kMaxInverseCacheBytes = 16ull << 20;     // rs.go:50
 extern size_t g_registry_max;  // coefficient-table registry cap (distinct matrices per handle)
 extern size_t g_tab_inplace_max;  // launches up to this many input bytes read a new matrix's tables in place
+extern int g_tab_stage_vram;      // table staging slots in host-writable device memory when the platform maps it
 
 // Record which HIP call failed (thread-local, read by rs_last_device_error)
 // and return RS_ERR_DEVICE.
@@ -115,7 +116,8 @@ struct rs_codec {
     // once the copy enqueued from it kRing uploads earlier has finished.
     struct TabStage {
         uint8_t* host = nullptr;
-        const uint8_t* dev_host = nullptr;  // its device address (coherent, mapped: read in place)
+        const uint8_t* dev_host = nullptr;  // its device address (a first-sight launch reads it in place)
+        bool vram = false;                  // host-writable device memory (else coherent pinned host memory)
         size_t cap = 0;
         hipEvent_t done = nullptr;
         bool pending = false;
@@ -338,7 +340,8 @@ inline void rs_codec::release_device() {
             if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
         }
         for (TabStage& t : tab_stage) {
-            if (t.host) (void)hipHostFree(t.host);
+            if (t.host && t.vram) rsamd::detail::host_writable_vram_put(device, t.host, t.cap);
+            else if (t.host) (void)hipHostFree(t.host);
             if (t.done) (void)hipEventDestroy(t.done);
         }
         for (UploadSlot& u : up) {

@@ -159,7 +159,7 @@ def first_small(g):
     ref = buf.clone()
     seen = set()
     fresh = []
-    while len(fresh) < 101:
+    while len(fresh) < 303:
         pt = tuple(sorted(int(x) for x in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False)))
         if pt not in seen:
             seen.add(pt)
@@ -174,10 +174,25 @@ def first_small(g):
             ts.append(time.perf_counter() - t0)
         return sorted(ts)[len(ts) // 2]
     r.reconst_batch(buf, [], fresh[0])
-    t_new = per_call(fresh[1:])
+    up0, ip0 = r.coef_table_stats()
+    t_new = per_call(fresh[1:101])  # default: a new matrix's tables read in place (table_inplace_max)
+    up1, ip1 = r.coef_table_stats()
     t_rep = per_call([fresh[1]] * 100)
+    L.rs_tune(b"table_inplace_max", 0)  # the same with the upload at first sight (round 5's path)
+    t_up = per_call(fresh[101:201])
+    L.rs_tune(b"table_inplace_max", 2 << 20)
+    # in place from coherent pinned host memory (staging slots not in VRAM: a new handle)
+    L.rs_tune(b"table_stage_vram", 0)
+    r_main, r = r, rs.New(k, m)
+    r.reconst_batch(buf, [], fresh[0])
+    t_pin = per_call(fresh[201:301])
+    r = r_main
+    L.rs_tune(b"table_stage_vram", 1)
     assert torch.equal(buf, ref), "small first-sight reconst changed the stripes"
-    for label, t in (("first call of a new pattern", t_new), ("a pattern already seen", t_rep)):
+    print(f"first sights read in place: {ip1 - ip0}, uploads: {up1 - up0}", flush=True)
+    for label, t in (("first call of a new pattern", t_new), ("a pattern already seen", t_rep),
+                     ("first call of a new pattern, upload at first sight", t_up),
+                     ("first call of a new pattern, tables in pinned host memory", t_pin)):
         rec(f"reconst 10+4 8KiB x{S}, synchronous, {label}", S * (k + 2) * vec, t)
     L.rs_tune(b"jit", 2)
 
