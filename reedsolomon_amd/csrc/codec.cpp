@@ -200,7 +200,9 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     bool inplace = false;
     if (inplace_slot && g_tab_inplace_max && launch_in_bytes <= g_tab_inplace_max) {
         if (rs->tab_seen.size() >= 4096) rs->tab_seen.clear();
-        inplace = rs->tab_seen.emplace(key, 0u).second;  // first sight: in place; a second one uploads
+        uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a over the key (rows, cols, matrix bytes)
+        for (unsigned char ch : key) h = (h ^ ch) * 0x100000001b3ull;
+        inplace = rs->tab_seen.insert(h).second;  // first sight: in place; a second one uploads
     }
     const size_t main_dw = static_cast<size_t>(cols) * rows_pad * 5;
     const size_t img_dw = rows <= 4 ? rup(cols, 4) * 20 : 0;

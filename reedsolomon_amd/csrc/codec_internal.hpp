@@ -20,6 +20,7 @@
 #include <new>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/rs_amd.h"
@@ -126,9 +127,10 @@ struct rs_codec {
     TabStage tab_stage[kTabStages];
     int tab_stage_next = 0;
     // Matrices a small launch has used once with its tables read in place
-    // from a staging slot (get_tables): the second sight uploads them.
-    // Bounded (cleared when full).
-    std::unordered_map<std::string, uint32_t> tab_seen;
+    // from a staging slot (get_tables), by a 64-bit hash of the registry key
+    // (a collision only makes a first sight upload): the second sight
+    // uploads them.  Bounded (cleared when full).
+    std::unordered_set<uint64_t> tab_seen;
     uint64_t tab_uploads = 0, tab_inplace = 0;  // (rs_coef_table_stats)
 
     std::mutex stage_mu;  // staging for the host-memory entry points

@@ -125,14 +125,15 @@ int flag_sync(hipStream_t st, rs_codec::DoneFlag& f, const char* where) {
     for (uint32_t spins = 1; __atomic_load_n(f.host, __ATOMIC_ACQUIRE) != v; ++spins) {
         _mm_pause();
         if ((spins & 4095) != 0) continue;
+        const auto waited = std::chrono::steady_clock::now() - t0;
+        if (waited < std::chrono::microseconds(200)) continue;  // (a call's kernel is done within ~30 us)
         // A faulted kernel or queue never writes the flag: the stream's error
         // comes back now instead of after the 10 s bound (advisor r05).
-        // (~100 us between queries: a call's kernel usually finishes before
-        // the first; this stream holds no resident kernel.)
+        // (This stream holds no resident kernel.)
         const hipError_t q = hipStreamQuery(st);
         if (q != hipSuccess && q != hipErrorNotReady) return hip_ok(q, where);
         if (q == hipErrorNotReady) (void)hipGetLastError();
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return hip_ok(hipStreamSynchronize(st), where);
+        if (waited > std::chrono::seconds(10)) return hip_ok(hipStreamSynchronize(st), where);
     }
     return RS_OK;
 }
