@@ -42,11 +42,89 @@ std::vector<uint8_t> make_encode_matrix(int d, int p) {
     return m;
 }
 
+// Gauss-Jordan of invert() below on the augmented rows [left | inv], the
+// row operations as split-nibble products on 32-byte vectors (what the
+// reference's gmu_amd64.s does for vectors, here for matrix rows): the same
+// pivot order and the same field arithmetic, so the same bytes.
+namespace {
+struct NibTables {  // per v: v * i (i = 0..15), then v * (i << 4)
+    alignas(32) uint8_t t[256][32];
+    NibTables() {
+        const auto& T = gf();
+        for (int v = 0; v < 256; ++v)
+            for (int i = 0; i < 16; ++i) {
+                t[v][i] = T.mul[v][i];
+                t[v][16 + i] = T.mul[v][i << 4];
+            }
+    }
+};
+const NibTables& nib() {
+    static const NibTables n;
+    return n;
+}
+
+__attribute__((target("avx2"))) inline __m256i nib_mul(__m256i x, const uint8_t* tv) {
+    const __m256i lo_t = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i*>(tv)));
+    const __m256i hi_t = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i*>(tv + 16)));
+    const __m256i m = _mm256_set1_epi8(0x0f);
+    const __m256i lo = _mm256_shuffle_epi8(lo_t, _mm256_and_si256(x, m));
+    const __m256i hi = _mm256_shuffle_epi8(hi_t, _mm256_and_si256(_mm256_srli_epi16(x, 4), m));
+    return _mm256_xor_si256(lo, hi);
+}
+
+__attribute__((target("avx2"))) int invert_avx2(const uint8_t* src, int n, uint8_t* out) {
+    const int w = (2 * n + 31) & ~31;  // augmented row bytes, whole vectors
+    std::vector<uint8_t> aug(static_cast<size_t>(n) * w + 32, 0);
+    uint8_t* a = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(aug.data()) + 31) & ~uintptr_t{31});
+    for (int i = 0; i < n; ++i) {
+        std::memcpy(a + static_cast<size_t>(i) * w, src + static_cast<size_t>(i) * n, n);
+        a[static_cast<size_t>(i) * w + n + i] = 1;
+    }
+    const auto& T = gf();
+    const auto& N = nib();
+    const int nv = w / 32;
+    for (int i = 0; i < n; ++i) {
+        uint8_t* ri = a + static_cast<size_t>(i) * w;
+        if (ri[i] == 0) {
+            int j = i + 1;
+            while (j < n && a[static_cast<size_t>(j) * w + i] == 0) ++j;
+            if (j == n) return RS_ERR_SINGULAR_MATRIX;
+            std::swap_ranges(ri, ri + w, a + static_cast<size_t>(j) * w);
+        }
+        if (ri[i] != 1) {
+            const uint8_t* tv = N.t[T.inv[ri[i]]];
+            for (int k = 0; k < nv; ++k) {
+                __m256i* p = reinterpret_cast<__m256i*>(ri) + k;
+                _mm256_store_si256(p, nib_mul(_mm256_load_si256(p), tv));
+            }
+        }
+        for (int j = 0; j < n; ++j) {
+            uint8_t* rj = a + static_cast<size_t>(j) * w;
+            if (j == i || !rj[i]) continue;
+            const uint8_t* tv = N.t[rj[i]];
+            for (int k = 0; k < nv; ++k) {
+                __m256i* p = reinterpret_cast<__m256i*>(rj) + k;
+                const __m256i src_v = _mm256_load_si256(reinterpret_cast<const __m256i*>(ri) + k);
+                _mm256_store_si256(p, _mm256_xor_si256(_mm256_load_si256(p), nib_mul(src_v, tv)));
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i) std::memcpy(out + static_cast<size_t>(i) * n, a + static_cast<size_t>(i) * w + n, n);
+    return RS_OK;
+}
+
+// (env RSAMD_INVERT_SCALAR=1: the byte-table row operations, for A/B and for
+// testing that path on an AVX2 host)
+const bool g_has_avx2 = __builtin_cpu_supports("avx2") && !std::getenv("RSAMD_INVERT_SCALAR");
+}  // namespace
+
 // invert matrix.go:85-147 (Gauss-Jordan; a zero pivot swaps with the first
 // lower row that has a non-zero entry in the pivot column; the result is
-// bit-identical to the reference's).
+// bit-identical to the reference's).  AVX2 row operations where the host
+// has them (invert_avx2, same steps), else byte-table ones.
 int invert(const uint8_t* src, size_t len, int n, uint8_t* out) {
     if (static_cast<size_t>(n) * n != len) return RS_ERR_NOT_SQUARE;
+    if (g_has_avx2 && n > 0) return invert_avx2(src, n, out);
     std::vector<uint8_t> left(src, src + len), inv(len, 0);
     for (int i = 0; i < n; ++i) inv[i * n + i] = 1;
     auto swap_rows = [n](std::vector<uint8_t>& m, int a, int b) {
@@ -128,6 +206,8 @@ size_t g_tab_inplace_max = size_t{2} << 20;
 // no device memory for the CPU keep coherent pinned host memory.  Taken by
 // slots allocated after a change; rs_tune("table_stage_vram", 1 default | 0).
 int g_tab_stage_vram = 1;
+// The first-sight arena per handle (get_tables): ~400 new 10+4 matrices.
+constexpr size_t kTabArenaBytes = size_t{1} << 20;
 
 thread_local char g_last_dev_err[192] = {0};
 
@@ -152,15 +232,22 @@ int dev_fail(hipError_t e, const char* where) {
 // table may be handed out and launched across a recycle.
 //
 // First sight in a small launch (launch_in_bytes <= table_inplace_max, and
-// the caller passes inplace_slot): the tables are built into a coherent,
-// mapped staging slot and the launch reads them there in place (a few KiB
-// over PCIe per workgroup); *inplace_slot names the slot, and the caller
-// records the slot's `done` event behind its launch (the slot is reused only
-// after that).  No registry entry is made: the matrix's next use uploads.  A
-// small synchronous Reconst of a pattern new to the process spent ~12 of its
-// 33 us in the upload's host calls (hipMalloc, hipMemcpyAsync, event create
-// and two records; profiles/r05/first_sight_api_trace/), and a rebuild storm
-// of one-off patterns never reuses its tables.
+// the caller passes inplace_slot), no host call on the caller's path beyond
+// the launch itself: a small synchronous Reconst of a pattern new to the
+// process spent ~12 of its 33 us in the upload's host calls (hipMalloc,
+// hipMemcpyAsync, event create and two records;
+// profiles/r05/first_sight_api_trace/), and a rebuild storm of one-off
+// patterns never reuses its tables.
+//  * the first-sight arena (host-writable device memory, table_stage_vram):
+//    the host writes the tables there through the BAR and the registry entry
+//    points at them; the launch reads them from HBM.  The matrix's next use
+//    copies them to ordinary (cached) device memory.  Arena space comes back
+//    only with the registry, after its device drain; a full arena falls
+//    through to
+//  * a staging slot read in place (pinned or VRAM): *inplace_slot names the
+//    slot, and the caller records the slot's `done` event behind its launch
+//    (the slot is reused only after that).  No registry entry is made: the
+//    matrix's next use uploads.
 int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t stream, const uint32_t** out,
                int* rows_pad_out, uint64_t launch_in_bytes, int* inplace_slot) {
     if (inplace_slot) *inplace_slot = -1;
@@ -169,6 +256,37 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     key.append(reinterpret_cast<const char*>(&cols), sizeof cols);
     key.append(reinterpret_cast<const char*>(mat), static_cast<size_t>(rows) * cols);
     auto it = rs->tables.find(key);
+    if (it != rs->tables.end() && it->second.arena) {
+        // second use of a matrix whose tables sit in the first-sight arena:
+        // to ordinary device memory (a device-to-device copy on this stream;
+        // the arena copy stays valid for launches still reading it)
+        rs_t::TableEntry& te = it->second;
+        uint32_t* dptr = nullptr;
+        hipEvent_t ev = nullptr;
+        if (hipMalloc(&dptr, te.bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            *out = te.dev;  // (no memory: keep reading the arena copy)
+            *rows_pad_out = rows_pad;
+            return RS_OK;
+        }
+        hipError_t e = hipMemcpyAsync(dptr, te.dev, te.bytes, hipMemcpyDeviceToDevice, stream);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ev, stream);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(stream);
+            if (ev) (void)hipEventDestroy(ev);
+            (void)hipFree(dptr);
+            return dev_fail(e, "table move out of the first-sight arena");
+        }
+        te.dev = dptr;
+        te.arena = false;
+        te.ready = ev;
+        te.stream = stream;
+        ++rs->tab_uploads;
+        *out = dptr;
+        *rows_pad_out = rows_pad;
+        return RS_OK;
+    }
     if (it != rs->tables.end()) {
         rs_t::TableEntry& te = it->second;
         if (te.ready) {
@@ -192,13 +310,15 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
         engines_quiesce();  // other handles' instances on this device would hold the sync for their idle window
         RS_TRY(hip_ok(hipDeviceSynchronize(), "table registry drain"));
         for (auto& kv : rs->tables) {
-            (void)hipFree(kv.second.dev);
+            if (!kv.second.arena) (void)hipFree(kv.second.dev);
             if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
         }
         rs->tables.clear();
+        rs->tab_arena_off = 0;  // (drained above: no launch reads the arena)
     }
+    const bool small = inplace_slot && g_tab_inplace_max && launch_in_bytes <= g_tab_inplace_max;
     bool inplace = false;
-    if (inplace_slot && g_tab_inplace_max && launch_in_bytes <= g_tab_inplace_max) {
+    if (small) {
         if (rs->tab_seen.size() >= 4096) rs->tab_seen.clear();
         uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a over the key (rows, cols, matrix bytes)
         for (unsigned char ch : key) h = (h ^ ch) * 0x100000001b3ull;
@@ -212,6 +332,52 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     // partner has zero tables
     const size_t wide_dw = rows > 8 ? static_cast<size_t>((cols + 1) / 2) * rows_pad * 12 : 0;
     const size_t bytes = (main_dw + img_dw + wide_dw) * 4;
+    // built in host memory, then one streaming copy into its place (arena or
+    // staging slot; VRAM is write-combined: no reads of it, and the stores
+    // are fenced before any launch or copy can read them)
+    thread_local std::vector<uint32_t> build;
+    build.assign(bytes / 4, 0u);
+    uint32_t* host = build.data();
+    for (int c = 0; c < cols; ++c)
+        for (int r = 0; r < rows; ++r) {
+            uint32_t t[5];
+            perm_table(mat[static_cast<size_t>(r) * cols + c], t);
+            std::memcpy(&host[(static_cast<size_t>(c) * rows_pad + r) * 5], t, sizeof t);
+            if (img_dw) std::memcpy(&host[main_dw + static_cast<size_t>(c) * 20 + r * 5], t, sizeof t);
+            if (wide_dw) {
+                uint32_t* w = &host[main_dw + img_dw + (static_cast<size_t>(c / 2) * rows_pad + r) * 12];
+                const int h = c & 1;
+                w[2 * h] = t[0];
+                w[2 * h + 1] = t[2];
+                w[4 + 2 * h] = t[1];
+                w[5 + 2 * h] = t[3];
+                w[8 + h] = t[4];
+            }
+        }
+    if (small && g_tab_stage_vram) {
+        if (!rs->tab_arena) {
+            size_t cap = 0;
+            rs->tab_arena = host_writable_vram_get(rs->device, kTabArenaBytes, &cap);
+            rs->tab_arena_cap = rs->tab_arena ? cap : 0;
+            rs->tab_arena_off = 0;
+        }
+        const size_t at = rup(rs->tab_arena_off, size_t{256});
+        if (rs->tab_arena && at + bytes <= rs->tab_arena_cap) {
+            uint8_t* dst = rs->tab_arena + at;
+            std::memcpy(dst, host, bytes);
+            _mm_sfence();
+            rs->tab_arena_off = at + bytes;
+            rs_t::TableEntry te;
+            te.dev = reinterpret_cast<uint32_t*>(dst);
+            te.arena = true;
+            te.bytes = bytes;
+            rs->tables.emplace(std::move(key), te);
+            ++rs->tab_inplace;
+            *out = te.dev;
+            *rows_pad_out = rows_pad;
+            return RS_OK;
+        }
+    }
     rs_t::TabStage& st = rs->tab_stage[rs->tab_stage_next];
     rs->tab_stage_next = (rs->tab_stage_next + 1) % rs_t::kTabStages;
     if (st.pending) {  // the copy enqueued from this slot kTabStages uploads ago
@@ -246,28 +412,6 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
             st.vram = false;
         }
     }
-    // built in host memory, then one streaming copy into the slot (a VRAM
-    // slot is write-combined: no reads of it, and the stores are fenced
-    // before any launch or copy can read them)
-    thread_local std::vector<uint32_t> build;
-    build.assign(bytes / 4, 0u);
-    uint32_t* host = build.data();
-    for (int c = 0; c < cols; ++c)
-        for (int r = 0; r < rows; ++r) {
-            uint32_t t[5];
-            perm_table(mat[static_cast<size_t>(r) * cols + c], t);
-            std::memcpy(&host[(static_cast<size_t>(c) * rows_pad + r) * 5], t, sizeof t);
-            if (img_dw) std::memcpy(&host[main_dw + static_cast<size_t>(c) * 20 + r * 5], t, sizeof t);
-            if (wide_dw) {
-                uint32_t* w = &host[main_dw + img_dw + (static_cast<size_t>(c / 2) * rows_pad + r) * 12];
-                const int h = c & 1;
-                w[2 * h] = t[0];
-                w[2 * h + 1] = t[2];
-                w[4 + 2 * h] = t[1];
-                w[5 + 2 * h] = t[3];
-                w[8 + h] = t[4];
-            }
-        }
     std::memcpy(st.host, host, bytes);
     if (st.vram) _mm_sfence();
     if (inplace && st.dev_host) {

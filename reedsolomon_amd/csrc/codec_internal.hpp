@@ -110,6 +110,8 @@ struct rs_codec {
         uint32_t* dev = nullptr;
         hipEvent_t ready = nullptr;      // its upload's completion (nullptr once seen complete)
         hipStream_t stream = nullptr;    // ... enqueued on this stream
+        bool arena = false;              // written by the host into the first-sight arena (uncached VRAM)
+        size_t bytes = 0;
     };
     std::map<std::string, TableEntry> tables;
     // Pinned staging of table uploads (async on the launching stream, so a new
@@ -131,6 +133,13 @@ struct rs_codec {
     // (a collision only makes a first sight upload): the second sight
     // uploads them.  Bounded (cleared when full).
     std::unordered_set<uint64_t> tab_seen;
+    // First-sight arena (get_tables): host-writable device memory the host
+    // writes new matrices' tables into for small launches; registry entries
+    // point into it until the matrix's next use moves them to ordinary
+    // device memory.  Space is reclaimed only with the registry (after a
+    // device drain).
+    uint8_t* tab_arena = nullptr;
+    size_t tab_arena_cap = 0, tab_arena_off = 0;
     uint64_t tab_uploads = 0, tab_inplace = 0;  // (rs_coef_table_stats)
 
     std::mutex stage_mu;  // staging for the host-memory entry points
@@ -338,9 +347,10 @@ inline void rs_codec::release_device() {
         (void)hipDeviceSynchronize();
         step("frees");
         for (auto& kv : tables) {
-            (void)hipFree(kv.second.dev);
+            if (!kv.second.arena) (void)hipFree(kv.second.dev);
             if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
         }
+        if (tab_arena) rsamd::detail::host_writable_vram_put(device, tab_arena, tab_arena_cap);
         for (TabStage& t : tab_stage) {
             if (t.host && t.vram) rsamd::detail::host_writable_vram_put(device, t.host, t.cap);
             else if (t.host) (void)hipHostFree(t.host);

@@ -112,6 +112,36 @@ def test_invert_kats_and_random(rslib, orc):
                 assert np.array_equal(rslib.invert(m, n), exp)
 
 
+def test_invert_scalar_path_equals_vector_path(rslib, orc):
+    """invert() takes AVX2 row operations where the host has them and the
+    byte-table ones otherwise (RSAMD_INVERT_SCALAR=1 forces them): both give
+    the oracle's bytes (matrix.go:85-147) on random and singular matrices up
+    to 64 x 64, including zero pivots that swap rows."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r);"
+        "import reedsolomon_amd as rs; from oracle import oracle as orc; orc.build();"
+        "rng = np.random.default_rng(31); bad = 0\n"
+        "for n in (1, 2, 5, 10, 17, 32, 33, 64):\n"
+        "  for k in range(6):\n"
+        "    m = rng.integers(0, 256, n * n, dtype=np.uint8)\n"
+        "    if k == 0 and n > 1: m[0] = 0\n"
+        "    if k == 1 and n > 2: m[n:2 * n] = m[:n]\n"
+        "    rc, exp = orc.invert(m, n)\n"
+        "    try:\n"
+        "      got = rs.invert(m, n); bad += int(rc != 0 or not np.array_equal(got, exp))\n"
+        "    except rs.RSError:\n"
+        "      bad += int(rc == 0)\n"
+        "print('bad', bad)" % ROOT)
+    for env in ({}, {"RSAMD_INVERT_SCALAR": "1"}):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                           env=dict(os.environ, **env), timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert r.stdout.strip().endswith("bad 0"), (env, r.stdout)
+
+
 def test_inverse_cache_key(rslib, orc):
     rng = np.random.default_rng(12)
     for _ in range(200):
