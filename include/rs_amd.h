@@ -594,12 +594,13 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "table_inplace_max" (bytes of input vectors up to which a launch reads a
  * matrix it sees for the first time with its tables in place from a mapped
  * staging slot, the matrix's second use uploading them; default 2 MiB, 0 =
- * upload at first sight; see rs_coef_table_stats), "table_stage_vram" (1:
- * first-sight tables written by the host through the BAR into device memory
- * (a 1 MiB arena per handle, then the staging slots), where the platform maps
- * it, so the launch reads them from HBM and no upload call or event is made;
- * 0: coherent pinned host memory slots, read across PCIe, with an event per
- * launch; slots allocated after the change).  Returns
+ * upload at first sight; see rs_coef_table_stats), "table_stage_vram" (0,
+ * the default: coherent pinned host memory slots, read across PCIe, with an
+ * event per launch; 1: first-sight tables written by the host through the
+ * BAR into device memory (a 1 MiB arena per handle, then the staging slots),
+ * where the platform maps it, so the launch reads them from HBM and no
+ * upload call or event is made; slots allocated after the change; env
+ * RSAMD_TAB_VRAM).  Returns
  * RS_OK, or RS_ERR_INVAL for an unknown name.  The code-shape experiments of
  * earlier rounds (the knob named var, env RSAMD_VAR; some are XOR-only
  * diagnostics) exist only in the separate experiments build librsamd_exp.so:

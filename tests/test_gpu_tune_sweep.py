@@ -81,7 +81,7 @@ SWEEP = {
     "jit_share_cols": [2, -1, 1],
     "table_registry_max": [1, 1 << 14],
     "table_inplace_max": [0, 1 << 30, 2 << 20],
-    "table_stage_vram": [0, 1],
+    "table_stage_vram": [1, 0],
     "multi_gpu_plan": [1, 0, 8, -1],
 }
 

@@ -181,18 +181,18 @@ def first_small(g):
     L.rs_tune(b"table_inplace_max", 0)  # the same with the upload at first sight (round 5's path)
     t_up = per_call(fresh[101:201])
     L.rs_tune(b"table_inplace_max", 2 << 20)
-    # in place from coherent pinned host memory (staging slots not in VRAM: a new handle)
-    L.rs_tune(b"table_stage_vram", 0)
+    # in place from host-writable VRAM (the opt-in table_stage_vram 1: a new handle)
+    L.rs_tune(b"table_stage_vram", 1)
     r_main, r = r, rs.New(k, m)
     r.reconst_batch(buf, [], fresh[0])
-    t_pin = per_call(fresh[201:301])
+    t_vram = per_call(fresh[201:301])
     r = r_main
-    L.rs_tune(b"table_stage_vram", 1)
+    L.rs_tune(b"table_stage_vram", 0)
     assert torch.equal(buf, ref), "small first-sight reconst changed the stripes"
     print(f"first sights read in place: {ip1 - ip0}, uploads: {up1 - up0}", flush=True)
     for label, t in (("first call of a new pattern", t_new), ("a pattern already seen", t_rep),
                      ("first call of a new pattern, upload at first sight", t_up),
-                     ("first call of a new pattern, tables in pinned host memory", t_pin)):
+                     ("first call of a new pattern, tables in VRAM (table_stage_vram 1)", t_vram)):
         rec(f"reconst 10+4 8KiB x{S}, synchronous, {label}", S * (k + 2) * vec, t)
     L.rs_tune(b"jit", 2)
 
