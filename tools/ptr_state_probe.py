@@ -31,8 +31,35 @@ def main():
     hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
     hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
 
+    hsa = ctypes.CDLL("libhsa-runtime64.so.1")
+    CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p)
+    gpus = []
+
+    def on_agent(agent, _data):
+        kind = ctypes.c_uint32(0)
+        hsa.hsa_agent_get_info(ctypes.c_uint64(agent), 17, ctypes.byref(kind))  # HSA_AGENT_INFO_DEVICE
+        if kind.value == 1:  # HSA_DEVICE_TYPE_GPU
+            gpus.append(agent)
+        return 0
+
+    cb = CB(on_agent)
+    hsa.hsa_iterate_agents(cb, None)
+
+    class Pair(ctypes.Structure):
+        _fields_ = [("attribute", ctypes.c_uint64), ("value", ctypes.c_uint64)]
+
+    hsa.hsa_amd_svm_attributes_get.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(Pair), ctypes.c_size_t]
+
+    def svm(addr):
+        """KFD's SVM view of one page: (status, global flag, GPU access, preferred location)."""
+        ps = (Pair * 3)((0, 0), (0x203, gpus[0] if gpus else 0), (4, 0))
+        rc = hsa.hsa_amd_svm_attributes_get(ctypes.c_void_p(addr), 4096, ps, 3)
+        acc = {0x200: "accessible", 0x201: "in-place", 0x202: "no-access"}.get(ps[1].attribute, hex(ps[1].attribute))
+        return rc, ps[0].value, acc, ps[2].value
+
     def show(label, addr):
-        print(f"{label:<48} rocr type/base/size + hip type: {hip_ptr.page_state(addr)}", flush=True)
+        print(f"{label:<48} rocr type/base/size + hip type: {hip_ptr.page_state(addr)}  svm: {svm(addr)}",
+              flush=True)
 
     a = np.zeros(16 * 4096, np.uint8)
     base = a.ctypes.data + (-a.ctypes.data) % 4096
@@ -52,6 +79,30 @@ def main():
     show(f"hipHostMalloc'ed (rc {rc})", h.value + 4096)
     blk = rs.host_alloc(1 << 16)
     show("rs_host_alloc pool block", blk.ctypes.data + 4096)
+    # registered, unregistered, freed, the range handed out again
+    import mmap as _mm
+    m = _mm.mmap(-1, 16 * 4096)
+    mb = np.frombuffer(m, dtype=np.uint8)
+    mbase = mb.ctypes.data
+    show("fresh mapping, never registered", mbase + 4096)
+    rs.host_register(mbase, 8 * 4096)
+    show("  registered", mbase + 4096)
+    rs.host_unregister(mbase)
+    show("  unregistered (still mapped)", mbase + 4096)
+    del mb
+    m.close()
+    c = ctypes.CDLL(None)
+    c.mmap.restype = ctypes.c_void_p
+    c.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    again = c.mmap(ctypes.c_void_p(mbase), 16 * 4096, 3, 0x22 | 0x10, -1, 0)  # MAP_FIXED at the same address
+    show(f"  unmapped, mapped again at the same address ({again == mbase})", mbase + 4096)
+    x = np.full(2 << 20, 7, np.uint8)
+    show("pageable 2 MiB array before any copy", x.ctypes.data + 8192)
+    tx = torch.from_numpy(x).cuda()
+    torch.cuda.synchronize()
+    show("  after a pageable H2D copy of it", x.ctypes.data + 8192)
+    y = tx.cpu()
+    show("  after a pageable D2H copy into a new tensor (dst)", y.data_ptr() + 8192)
     t = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
     show("device memory (torch)", t.data_ptr() + 4096)
     p = torch.empty(1 << 20, dtype=torch.uint8).pin_memory()
