@@ -282,11 +282,14 @@ RS_API int rs_group_encode_host_batch(rs_group_t* g, uint8_t* base, int64_t stri
  * rs_host_unregister(ptr) takes the address given to rs_host_register
  * (RS_ERR_INVAL for any other); a page leaves the runtime when the last
  * registration holding it goes, after every device this process launched on
- * has been drained.  The library then holds nothing of the range, and the
- * runtime reports no page of it registered any more (hipPointerGetAttributes,
- * checked after every unregister of the GPU tests): the
- * caller may free the memory and the allocator may reuse the addresses (the
- * reference retains nothing after a call: rs.go:101-111).
+ * has been drained.  The library then holds nothing of the range, the
+ * runtime reports no page of it registered any more (hipPointerGetAttributes),
+ * and the GPUs' in-place mapping of the caller's whole pages, which the
+ * runtime's own unregister leaves in KFD's shared-virtual-memory ranges, is
+ * revoked (rs_tune("host_unregister_revoke"); checked after every unregister
+ * of the GPU tests): the caller may free the memory and the
+ * allocator may reuse the addresses (the reference retains nothing after a
+ * call: rs.go:101-111).
  * No rs_host_register equivalent exists in the reference; it replaces the
  * pinning a cgo caller would otherwise do per call. */
 RS_API int rs_host_register(void* ptr, size_t bytes);
@@ -530,6 +533,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * batches in flight at once: 1 | 2 default),
  * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
  * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
+ * "host_unregister_revoke" (1 default: rs_host_unregister takes back the
+ * GPUs' in-place mapping of the caller's whole pages | 0: leave the
+ * runtime's state; env RSAMD_UNREGISTER_REVOKE),
  * "jit" (run-time bit-sliced kernels for 5-16 output rows: 1 default = compile
  * in the background on first sight, perm-table kernels until ready | 2 =
  * compile on the launching thread | 0 = off), "jit_min_launches" (background

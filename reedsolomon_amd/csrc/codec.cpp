@@ -1057,6 +1057,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_pinned_max") g_pinned_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_zc_max") g_zc_max = value < 0 ? SIZE_MAX : static_cast<size_t>(value);
         else if (n == "host_batch_zc") g_host_batch_zc = value;
+        else if (n == "host_unregister_revoke") g_unregister_revoke = value ? 1 : 0;
         else if (n == "host_dma_1d") g_host_dma_1d = value;
         else if (n == "host_pageable_stage") g_host_pageable_stage = value;
         else if (n == "bind_numa") g_bind_numa = value;

@@ -1,6 +1,7 @@
 // host_batches.cpp — host-resident batches of stripes: zero-copy kernels
 // over pinned / registered memory, the H2D / kernel / D2H pipeline for
 // pageable memory, and device groups (one process, several GPUs).
+#include <dlfcn.h>
 #include <pthread.h>
 #include <sched.h>
 #include <sys/mman.h>
@@ -143,6 +144,66 @@ std::vector<std::pair<uintptr_t, uintptr_t>> spans_release(const std::vector<uin
     return dead;
 }
 
+// hipHostRegister on this system grants the GPUs in-place access to the
+// range through KFD's shared-virtual-memory ranges, and hipHostUnregister
+// does not take it back: HIP forgets the registration, but the pages stay
+// GPU-mapped (HSA_AMD_SVM_ATTRIB_ACCESS_QUERY reports AGENT_ACCESSIBLE_IN_PLACE)
+// until they leave the process (tools/ptr_state_probe.py,
+// profiles/r06/ptr_state_probe_svm.log).  The caller then frees the memory;
+// every later trim or discard of those pages by the allocator (Go's
+// scavenger, glibc's trim) has the kernel tear down a GPU mapping nobody
+// uses, which with XNACK off means evicting and restoring the process's GPU
+// queues.  So after the runtime's unregister the library returns the pages
+// that belonged to the caller's range alone (whole pages inside
+// [ptr, ptr + bytes); a partial edge page may hold a neighbour the runtime
+// is copying) to their never-registered state: AGENT_NO_ACCESS for every GPU.
+// rs_tune("host_unregister_revoke", 1 default | 0); best effort (no ROCr
+// SVM API: nothing is done).
+struct SvmApi {
+    typedef struct { uint64_t attribute, value; } Pair;
+    int (*set)(void*, size_t, Pair*, size_t) = nullptr;
+    std::vector<uint64_t> gpus;  // agent handles
+    SvmApi() {
+        void* h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) return;
+        auto iterate = reinterpret_cast<int (*)(int (*)(uint64_t, void*), void*)>(dlsym(h, "hsa_iterate_agents"));
+        auto info = reinterpret_cast<int (*)(uint64_t, int, void*)>(dlsym(h, "hsa_agent_get_info"));
+        set = reinterpret_cast<int (*)(void*, size_t, Pair*, size_t)>(dlsym(h, "hsa_amd_svm_attributes_set"));
+        if (!iterate || !info || !set) {
+            set = nullptr;
+            return;
+        }
+        struct Ctx {
+            decltype(info) get;
+            std::vector<uint64_t>* out;
+        } ctx{info, &gpus};
+        iterate(
+            [](uint64_t agent, void* c) -> int {
+                Ctx* x = static_cast<Ctx*>(c);
+                uint32_t kind = 0;
+                if (x->get(agent, 17 /* HSA_AGENT_INFO_DEVICE */, &kind) == 0 && kind == 1 /* GPU */)
+                    x->out->push_back(agent);
+                return 0;
+            },
+            &ctx);
+        if (gpus.empty()) set = nullptr;
+    }
+};
+const SvmApi& svm_api() {
+    static const SvmApi a;
+    return a;
+}
+
+// [lo, hi): whole pages of one caller's range, just unregistered (see above).
+void svm_revoke(uintptr_t lo, uintptr_t hi) {
+    if (!g_unregister_revoke || lo >= hi) return;
+    const SvmApi& a = svm_api();
+    if (!a.set) return;
+    std::vector<SvmApi::Pair> attrs;
+    for (uint64_t g : a.gpus) attrs.push_back({0x202 /* HSA_AMD_SVM_ATTRIB_AGENT_NO_ACCESS */, g});
+    (void)a.set(reinterpret_cast<void*>(lo), hi - lo, attrs.data(), attrs.size());
+}
+
 bool overlaps_dying(uintptr_t lo, uintptr_t hi) {  // caller holds g_reg_mu
     auto it = g_dying.upper_bound(lo);
     if (it != g_dying.begin() && std::prev(it)->second > lo) return true;
@@ -150,6 +211,10 @@ bool overlaps_dying(uintptr_t lo, uintptr_t hi) {  // caller holds g_reg_mu
 }
 }  // namespace
 std::atomic<int> g_reg_count{0};
+int g_unregister_revoke = [] {  // (svm_revoke above)
+    const char* e = std::getenv("RSAMD_UNREGISTER_REVOKE");
+    return e ? (std::atoi(e) ? 1 : 0) : 1;
+}();
 
 // [p, p + bytes) inside one span AND inside a live registration or a pool
 // block: pages a span keeps for another registration (a shared page's whole
@@ -459,6 +524,8 @@ int rs_host_unregister(void* ptr) {
         auto it = g_user.find(reinterpret_cast<uintptr_t>(ptr));
         if (it == g_user.end()) return RS_ERR_INVAL;
         const std::vector<std::pair<uintptr_t, uintptr_t>> dead = spans_release(it->second.spans);
+        const uintptr_t ps = page_bytes(), ua = it->first;
+        const uintptr_t in_lo = (ua + ps - 1) & ~(ps - 1), in_hi = (ua + it->second.bytes) & ~(ps - 1);
         g_user.erase(it);
         if (dead.empty()) return RS_OK;  // every page still held by another registration or the pool
         // No longer found by the lookup; whatever the caller queued over the
@@ -473,6 +540,8 @@ int rs_host_unregister(void* ptr) {
         for (auto& d : dead) {
             const int r = hip_ok(hipHostUnregister(reinterpret_cast<void*>(d.first)), "hipHostUnregister");
             if (rc == RS_OK) rc = r;
+            // the caller's own whole pages of this span: GPU access revoked (above)
+            if (r == RS_OK) svm_revoke(std::max(d.first, in_lo), std::min(d.second, in_hi));
         }
         lk.lock();
         for (auto& d : dead) g_dying.erase(d.first);

@@ -84,3 +84,51 @@ def known_pages(lo: int, hi: int, skip=()):
 
 def registered(addr: int) -> bool:
     return page_state(addr)[3] == HIP_HOST
+
+
+_GPUS = []
+
+
+def _gpu_agents():
+    if not _GPUS:
+        hsa = _libs()[1]
+        cb_t = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p)
+
+        def on_agent(agent, _data):
+            kind = ctypes.c_uint32(0)
+            hsa.hsa_agent_get_info(ctypes.c_uint64(agent), 17, ctypes.byref(kind))  # HSA_AGENT_INFO_DEVICE
+            if kind.value == 1:  # HSA_DEVICE_TYPE_GPU
+                _GPUS.append(agent)
+            return 0
+
+        cb = cb_t(on_agent)
+        hsa.hsa_iterate_agents(cb, None)
+    return _GPUS
+
+
+class _SvmPair(ctypes.Structure):
+    _fields_ = [("attribute", ctypes.c_uint64), ("value", ctypes.c_uint64)]
+
+
+def gpu_access(addr: int) -> str:
+    """KFD's shared-virtual-memory view of the page holding addr for the first
+    GPU (hsa_amd_svm_attributes_get, HSA_AMD_SVM_ATTRIB_ACCESS_QUERY):
+    "in-place" (GPU-mapped, what hipHostRegister sets), "accessible",
+    "no-access" (a never-registered page) or "unknown" (no SVM API / error)."""
+    hsa = _libs()[1]
+    gpus = _gpu_agents()
+    if not gpus:
+        return "unknown"
+    hsa.hsa_amd_svm_attributes_get.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_SvmPair),
+                                               ctypes.c_size_t]
+    pr = (_SvmPair * 1)((0x203, gpus[0]))
+    if hsa.hsa_amd_svm_attributes_get(ctypes.c_void_p(addr & ~(PAGE - 1)), PAGE, pr, 1) != 0:
+        return "unknown"
+    return {0x200: "accessible", 0x201: "in-place", 0x202: "no-access"}.get(pr[0].attribute, "unknown")
+
+
+def gpu_mapped_pages(lo: int, hi: int):
+    """Whole pages inside [lo, hi) that KFD still maps for the GPU in place."""
+    first = (lo + PAGE - 1) & ~(PAGE - 1)
+    return [hex(pg) for pg in range(first, hi - PAGE + 1, PAGE) if gpu_access(pg) == "in-place"]
+

@@ -278,6 +278,8 @@ def test_unregister_does_not_wait_out_engine_idle(rslib, orc, torch_dev):
             rslib.host_unregister(buf[off:].ctypes.data)
             times.append(time.perf_counter() - t0)
             assert hip_ptr.known_pages(buf.ctypes.data, buf.ctypes.data + buf.nbytes) == [], it
+            # the caller's whole pages are no longer GPU-mapped (KFD SVM, the revoke)
+            assert hip_ptr.gpu_mapped_pages(buf[off:].ctypes.data, buf[off:].ctypes.data + (d + p) * size) == [], it
             assert _encode_ok(orc, r, d, p, v, rng), it  # pageable now
         print("unregister ms", [round(x * 1e3, 3) for x in times])
         assert sorted(times)[2] < 0.02, times
@@ -328,6 +330,7 @@ def test_host_calls_proceed_during_unregister_drain(rslib, orc, torch_dev):
     assert not errs, errs[:3]
     lo, hi = churn.ctypes.data, churn.ctypes.data + churn.nbytes
     assert hip_ptr.known_pages(lo, hi) == []
+    assert hip_ptr.gpu_mapped_pages(lo, hi) == []  # (KFD SVM: the caller's whole pages revoked)
     del churn
     rng = np.random.default_rng(510)
     for shape in [(3, 10, 16), (2, 10, 2064), (3, 10, 4112), (2, 10, 65632), (2, 5, 65632), (2, 10, (1 << 20) + 16),
@@ -337,3 +340,39 @@ def test_host_calls_proceed_during_unregister_drain(rslib, orc, torch_dev):
         dev = torch.from_numpy(host).cuda()
         torch.cuda.synchronize()
         assert np.array_equal(dev.cpu().numpy(), host), shape
+
+
+def test_unregister_revokes_gpu_mapping(rslib, torch_dev):
+    """hipHostRegister grants the GPU in-place access to the range through
+    KFD's shared-virtual-memory ranges and hipHostUnregister leaves it
+    (tools/ptr_state_probe.py): rs_host_unregister takes it back for the
+    caller's whole pages, so memory the caller frees is not left GPU-mapped
+    (each later trim of it by the allocator would have the kernel tear down a
+    GPU mapping, evicting the process's queues).  A partial edge page keeps
+    the runtime's state (a neighbour may be in a runtime copy); with
+    host_unregister_revoke 0 the runtime's own behaviour shows."""
+    L = rslib.lib()
+    a = np.zeros(40 * 4096 + 123, np.uint8)  # an ordinary heap array, unaligned
+    lo, hi = a.ctypes.data, a.ctypes.data + a.nbytes
+    inner = ((lo + 4095) & ~4095) + 4096
+    if hip_ptr.gpu_access(inner) == "unknown":
+        pytest.skip("no ROCr SVM attribute API")
+    assert hip_ptr.gpu_access(inner) == "no-access"
+    rslib.host_register(lo, a.nbytes)
+    assert hip_ptr.registered(inner) and hip_ptr.gpu_access(inner) == "in-place"
+    rslib.host_unregister(lo)
+    assert not hip_ptr.registered(inner)
+    assert hip_ptr.gpu_mapped_pages(lo, hi) == []
+    try:
+        assert L.rs_tune(b"host_unregister_revoke", 0) == 0
+        rslib.host_register(lo, a.nbytes)
+        rslib.host_unregister(lo)
+        assert not hip_ptr.registered(inner)
+        assert hip_ptr.gpu_access(inner) == "in-place"  # the runtime's own unregister leaves the mapping
+    finally:
+        L.rs_tune(b"host_unregister_revoke", 1)
+    rslib.host_register(lo, a.nbytes)  # registering again after a revoke works, and revokes again
+    assert hip_ptr.gpu_access(inner) == "in-place"
+    rslib.host_unregister(lo)
+    assert hip_ptr.gpu_mapped_pages(lo, hi) == []
+

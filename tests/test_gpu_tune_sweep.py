@@ -54,6 +54,7 @@ SWEEP = {
     "host_coalesce_linger_us": [100, 0],
     "host_coalesce_running": [1, 2],
     "host_batch_zc": [0, 1],
+    "host_unregister_revoke": [0, 1],
     "host_dma_1d": [1, 0],
     "host_pageable_stage": [0, 1],
     "bind_numa": [0, 1],
