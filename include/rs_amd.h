@@ -534,8 +534,8 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
  * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
  * "host_unregister_revoke" (1 default: rs_host_unregister takes back the
- * GPUs' in-place mapping of the caller's whole pages | 0: leave the
- * runtime's state; env RSAMD_UNREGISTER_REVOKE),
+ * GPUs' in-place mapping of the caller's whole pages, ~0.18 ms per call on
+ * MI355X | 0: leave the runtime's state; env RSAMD_UNREGISTER_REVOKE),
  * "jit" (run-time bit-sliced kernels for 5-16 output rows: 1 default = compile
  * in the background on first sight, perm-table kernels until ready | 2 =
  * compile on the launching thread | 0 = off), "jit_min_launches" (background
