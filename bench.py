@@ -114,6 +114,15 @@ def timing_backend(env=None) -> str:
     return b
 
 
+def gloo_env(env=None) -> None:
+    """The timing group is single-node by the bench's contract (N GPUs of one
+    node, MASTER_ADDR 127.0.0.1): gloo on the loopback interface, so the run
+    does not depend on the host name resolving (gloo picks its interface from
+    it otherwise).  An explicit GLOO_SOCKET_IFNAME wins."""
+    env = os.environ if env is None else env
+    env.setdefault("GLOO_SOCKET_IFNAME", "lo")
+
+
 def rank_devices(pg, me: dict) -> list:
     """Every rank's device record, in rank order (all_gather_object over the
     timing group; [me] without one)."""
@@ -503,6 +512,7 @@ def rehearse_cpu(args, world: int, rank: int) -> dict | None:
     if world > 1:
         if backend != "gloo":
             raise SystemExit("bench: --rehearse-cpu runs on gloo only (no GPU)")
+        gloo_env()
         dist.init_process_group("gloo")
         pg = dist
     ranks_seen = count_ranks(pg, torch.device("cpu"))
@@ -742,6 +752,7 @@ def main(argv=None):
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
+            gloo_env()
             dist.init_process_group(backend)
         pg = dist
 

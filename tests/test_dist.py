@@ -251,6 +251,20 @@ def test_bench_eight_ranks_rehearsal():
     assert len({d["pid"] for d in line["rank_devices"]}) == 8, line
 
 
+def test_gloo_env_defaults_to_loopback():
+    """Single-node timing group: gloo on the loopback interface unless the
+    caller names one (the host name need not resolve)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    env = {}
+    bench.gloo_env(env)
+    assert env["GLOO_SOCKET_IFNAME"] == "lo"
+    env = {"GLOO_SOCKET_IFNAME": "eth0"}
+    bench.gloo_env(env)
+    assert env["GLOO_SOCKET_IFNAME"] == "eth0"
+
+
 def test_timing_backend_default_is_gloo():
     """the driver's first 8-GPU run must not depend on an RCCL
     init that never ran on hardware; the timing collectives default to gloo,
