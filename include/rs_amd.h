@@ -233,10 +233,11 @@ RS_API int rs_replace_batch(rs_t* rs, const uint8_t* data_base, int64_t data_str
  * Host-resident batches (the path storage callers see: stripes arrive in
  * host memory from disk or the network).  Layout as for rs_encode_batch but
  * `base` is a HOST pointer.  Pinned / registered memory: one zero-copy launch
- * straight over it.  Pageable memory with stripes up to 16 MiB: staged
- * through a pinned mirror by host copy threads, zero-copy kernels on the
- * mirror.  Otherwise (or with rs_tune("host_batch_zc" / "host_pageable_stage",
- * 0)): H2D copies of the data vectors, the device encode and D2H copies of the
+ * straight over it.  Pageable memory: staged through a pinned mirror by host
+ * copy threads, zero-copy kernels on the mirror (stripes above 16 MiB in byte
+ * windows of every vector), so no pageable byte reaches the runtime's own
+ * pageable copies.  With rs_tune("host_batch_zc" / "host_pageable_stage",
+ * 0): H2D copies of the data vectors, the device encode and D2H copies of the
  * parity vectors pipelined over `streams` HIP streams with
  * `stripes_per_chunk` stripes per step.  Returns when every parity byte is
  * back in host memory.  Strides are non-negative (RS_ERR_INVAL otherwise).
@@ -323,9 +324,10 @@ RS_API int rs_host_device_pointer(const void* host_ptr, size_t bytes, void** dev
  * (need_masks as in rs_reconst_batch_multi): stripe s, vector v at
  * base + s*stripe_stride + v*vect_stride (data 0..d-1, then parity).
  * Pinned / registered memory is processed in place (zero-copy); pageable
- * memory with stripes up to 16 MiB is staged through a pinned mirror (the
- * first d survivors in, the rebuilt vectors out); larger pageable stripes,
- * or rs_tune("host_pageable_stage", 0), give RS_ERR_INVAL.  Every mask is
+ * memory is staged through a pinned mirror (the first d survivors in, the
+ * rebuilt vectors out; stripes above 16 MiB in byte windows of every
+ * vector); with rs_tune("host_pageable_stage", 0) pageable memory gives
+ * RS_ERR_INVAL.  Every mask is
  * validated before anything is copied or launched.  Synchronous. */
 RS_API int rs_reconst_host_batch_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t vect_stride,
                                        int nstripes, size_t len, const uint64_t* need_masks);

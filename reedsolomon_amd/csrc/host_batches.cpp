@@ -296,8 +296,10 @@ int g_host_batch_zc = 1;
 int g_host_dma_1d = 0;
 // Group worker threads bind to their GPU's local CPUs (bind_thread_to_device).
 int g_bind_numa = 1;
-// Pageable host batches with stripes up to 4 MiB are staged through the
-// pinned mirror (encode_pageable_batch); 0 = the DMA pipeline's 1-D copies.
+// Pageable host batches are staged through the pinned mirror (stripes above
+// kPageableStripeMax in byte windows: encode_pageable_batch,
+// reconst_pageable_batch); 0 = Encode takes the DMA pipeline's 1-D runtime
+// copies and a pageable multi-pattern Reconst is refused (RS_ERR_INVAL).
 int g_host_pageable_stage = 1;
 
 }  // namespace detail
@@ -315,6 +317,16 @@ int g_host_pageable_stage = 1;
 // bytes, pitch) enqueues the kernel on rs->stream.  Caller holds stage_mu.
 constexpr size_t kPageableStripeMax = size_t{16} << 20;
 constexpr size_t kPageableSlot = size_t{8} << 20;
+// Larger pageable stripes go through the same mirror in byte windows of
+// every vector (Encode and Reconst are byte-wise: a window of all d+p
+// vectors is a stripe of its own), so no pageable byte is handed to the
+// runtime's pageable copies, which leave the caller's pages GPU-mapped in
+// place after the copy (~200 us of driver work when that memory is freed,
+// DESIGN.md §5.8).  Window: the largest 256-byte multiple that keeps a
+// stripe within kPageableStripeMax.
+static size_t pageable_window(int nvec) {
+    return std::max<size_t>(256, (kPageableStripeMax / static_cast<size_t>(nvec)) & ~size_t{255});
+}
 
 template <class RowsIn, class RowsOut, class Launch>
 static int pageable_pipeline(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, int nstripes, size_t len,
@@ -647,9 +659,15 @@ int rs_encode_host_batch(rs_t* rs, uint8_t* base, int64_t stripe_stride, int64_t
             const int sync_rc = hip_ok(hipStreamSynchronize(rs->stream), "host-batch sync");
             return rc ? rc : sync_rc;
         }
-        if (!pinned && g_host_pageable_stage && rup(len, 256) * static_cast<size_t>(d + p) <= kPageableStripeMax) {
+        if (!pinned && g_host_pageable_stage) {
             std::lock_guard<std::mutex> lk(rs->stage_mu);
-            return encode_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len);
+            if (rup(len, 256) * static_cast<size_t>(d + p) <= kPageableStripeMax)
+                return encode_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len);
+            const size_t w = pageable_window(d + p);  // large stripes: byte windows of every vector
+            for (size_t off = 0; off < len; off += w)
+                RS_TRY(encode_pageable_batch(rs, base + off, stripe_stride, vect_stride, nstripes,
+                                             std::min(w, len - off)));
+            return RS_OK;
         }
         // [S][d+p][len] with 256-B-multiple len: data and parity of a stripe are contiguous rows
         const bool dense = vect_stride == static_cast<int64_t>(len) && len % 256 == 0;
@@ -871,11 +889,17 @@ static int reconst_host_multi(rs_t* rs, uint8_t* base, int64_t stripe_stride, in
     DeviceGuard g(rs->device);
     uint8_t* zc = nullptr;
     if (host_device_range(base, batch_extent(stripe_stride, vect_stride, nstripes, d + p, len), &zc) != RS_OK) {
-        // pageable memory: staged through the pinned mirror
-        if (!g_host_pageable_stage || rup(len, 256) * static_cast<size_t>(d + p) > kPageableStripeMax)
-            return RS_ERR_INVAL;
+        // pageable memory: staged through the pinned mirror (large stripes in
+        // byte windows of every vector)
+        if (!g_host_pageable_stage) return RS_ERR_INVAL;
         std::lock_guard<std::mutex> lk(rs->stage_mu);
-        return reconst_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len, masks);
+        if (rup(len, 256) * static_cast<size_t>(d + p) <= kPageableStripeMax)
+            return reconst_pageable_batch(rs, base, stripe_stride, vect_stride, nstripes, len, masks);
+        const size_t w = pageable_window(d + p);
+        for (size_t off = 0; off < len; off += w)
+            RS_TRY(reconst_pageable_batch(rs, base + off, stripe_stride, vect_stride, nstripes, std::min(w, len - off),
+                                          masks));
+        return RS_OK;
     }
     rs_layout_t L{zc, stripe_stride, vect_stride, zc + static_cast<int64_t>(d) * vect_stride, stripe_stride,
                   vect_stride};

@@ -854,6 +854,45 @@ def test_host_batch_zero_copy(rslib, orc, torch_dev):
     assert np.array_equal(pageable, broken)
 
 
+def test_host_batch_large_pageable_stripes(rslib, orc, torch_dev):
+    """Pageable host batches whose stripes exceed one mirror slot (16 MiB):
+    10+4 with 2 MiB + 40 byte vectors (a 28 MiB stripe) and 4+2 with 3 MiB +
+    3 bytes, interleaved [S][d+p][len] and with a gap between vectors, are
+    staged through the pinned mirror in byte windows of every vector (Encode
+    and multi-pattern Reconst, rs.go:104-203 / 221-380): bytes equal the
+    oracle's, and no page of the caller's buffer was ever GPU-mapped (KFD
+    SVM access stays no-access: the runtime's pageable copies, which map the
+    source in place, were not used)."""
+    rng = np.random.default_rng(2048)
+    for d, p, S, n, gap in ((10, 4, 2, (2 << 20) + 40, 0), (4, 2, 3, (3 << 20) + 3, 4096 + 5)):
+        r = rslib.New(d, p)
+        vs = n + gap
+        buf = np.zeros(S * (d + p) * vs + 64, np.uint8)  # an ordinary heap array
+        view = np.lib.stride_tricks.as_strided(buf[64:], shape=(S, d + p, n), strides=((d + p) * vs, vs, 1))
+        host = rng.integers(0, 256, (S, d + p, n), dtype=np.uint8)
+        view[:] = host
+        view[:, d:] = 0xA5
+        lo, hi = buf.ctypes.data, buf.ctypes.data + buf.nbytes
+        probe = ((lo + 4095) & ~4095) + 4096
+        before = hip_ptr.gpu_access(probe)
+        r.encode_host_batch(view)
+        exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
+        assert np.array_equal(view[:, d:], exp), (d, p, n, _first_diff(view[:, d:], exp))
+        assert np.array_equal(view[:, :d], host[:, :d])
+        full = np.concatenate([host[:, :d], exp], axis=1)
+        masks = np.zeros(S, np.uint64)
+        for s_ in range(S):
+            for v in rng.choice(d + p, int(rng.integers(1, p + 1)), replace=False):
+                masks[s_] |= np.uint64(1) << np.uint64(int(v))
+                view[s_, int(v)] = 0xEE
+        r.reconst_host_batch_multi(view, masks)
+        assert np.array_equal(view, full), (d, p, n, _first_diff(view, full))
+        if before != "unknown":  # (the SVM query exists on the box)
+            assert before == "no-access"
+            assert hip_ptr.gpu_mapped_pages(lo, hi) == [], "pageable buffer was handed to the runtime"
+        del view, buf
+
+
 def test_split_layout_encode_reconst(rslib, orc, torch_dev):
     """Data and parity in separate buffers (rs_layout_t)."""
     torch = torch_dev
