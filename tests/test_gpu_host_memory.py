@@ -357,7 +357,9 @@ def test_unregister_revokes_gpu_mapping(rslib, torch_dev):
     inner = ((lo + 4095) & ~4095) + 4096
     if hip_ptr.gpu_access(inner) == "unknown":
         pytest.skip("no ROCr SVM attribute API")
-    assert hip_ptr.gpu_access(inner) == "no-access"
+    # (no precondition on the pages: in a full run an earlier test's pageable
+    # torch copy may have left this reused heap range GPU-mapped already; the
+    # revoke below covers that case as well)
     rslib.host_register(lo, a.nbytes)
     assert hip_ptr.registered(inner) and hip_ptr.gpu_access(inner) == "in-place"
     rslib.host_unregister(lo)
