@@ -132,3 +132,19 @@ def gpu_mapped_pages(lo: int, hi: int):
     first = (lo + PAGE - 1) & ~(PAGE - 1)
     return [hex(pg) for pg in range(first, hi - PAGE + 1, PAGE) if gpu_access(pg) == "in-place"]
 
+
+
+def gpu_revoke(lo: int, hi: int) -> bool:
+    """Set KFD's SVM access of the whole pages inside [lo, hi) to no-access
+    for every GPU (hsa_amd_svm_attributes_set, what rs_host_unregister's
+    revoke does), so a test can start from pages no earlier copy left
+    GPU-mapped.  False when the SVM API is missing or refuses."""
+    hsa = _libs()[1]
+    gpus = _gpu_agents()
+    first, last = (lo + PAGE - 1) & ~(PAGE - 1), hi & ~(PAGE - 1)
+    if not gpus or last <= first:
+        return False
+    hsa.hsa_amd_svm_attributes_set.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_SvmPair),
+                                               ctypes.c_size_t]
+    prs = (_SvmPair * len(gpus))(*[(0x202, g) for g in gpus])
+    return hsa.hsa_amd_svm_attributes_set(ctypes.c_void_p(first), last - first, prs, len(gpus)) == 0

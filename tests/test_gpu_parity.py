@@ -874,7 +874,11 @@ def test_host_batch_large_pageable_stripes(rslib, orc, torch_dev):
         view[:, d:] = 0xA5
         lo, hi = buf.ctypes.data, buf.ctypes.data + buf.nbytes
         probe = ((lo + 4095) & ~4095) + 4096
-        before = hip_ptr.gpu_access(probe)
+        # (a fresh mapping at an address an earlier test's pageable copy used
+        # can report in-place already: start from no-access explicitly)
+        svm = hip_ptr.gpu_access(probe) != "unknown"  # (the SVM API exists on the box)
+        if svm:
+            assert hip_ptr.gpu_revoke(lo, hi) and hip_ptr.gpu_access(probe) == "no-access"
         r.encode_host_batch(view)
         exp = orc.encode_numpy(orc.gen_matrix(d, p).reshape(p, d), host[:, :d])
         assert np.array_equal(view[:, d:], exp), (d, p, n, _first_diff(view[:, d:], exp))
@@ -887,8 +891,7 @@ def test_host_batch_large_pageable_stripes(rslib, orc, torch_dev):
                 view[s_, int(v)] = 0xEE
         r.reconst_host_batch_multi(view, masks)
         assert np.array_equal(view, full), (d, p, n, _first_diff(view, full))
-        if before != "unknown":  # (the SVM query exists on the box)
-            assert before == "no-access"
+        if svm:
             assert hip_ptr.gpu_mapped_pages(lo, hi) == [], "pageable buffer was handed to the runtime"
         del view, buf
 
