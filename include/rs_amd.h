@@ -297,8 +297,9 @@ RS_API int rs_host_register(void* ptr, size_t bytes);
 /* Library-owned page-locked buffers (mmap + hipHostRegister), for callers
  * that allocate and release stripe buffers continually (a Go server's
  * per-request buffers): rs_host_alloc hands out a block of at least `bytes`
- * (page-aligned; size classes of powers of two from 64 KiB), device-mapped
- * like registered memory; rs_host_free returns it to the library, which keeps
+ * (page-aligned; size classes of powers of two from 64 KiB, carved from
+ * 2 MiB-aligned slabs of whole 2 MiB granules that no other mapping shares),
+ * device-mapped like registered memory; rs_host_free returns it to the library, which keeps
  * it registered and mapped for reuse and never gives the pages back while the
  * process runs (no per-buffer register / unregister cost).  A reused block holds its
  * previous bytes.  rs_host_free(NULL) is a no-op; any other pointer that is

@@ -85,9 +85,21 @@ struct UserReg {
     std::vector<uintptr_t> spans;  // the spans it holds a reference on
 };
 std::map<uintptr_t, UserReg> g_user;                    // rs_host_register'ed ranges, by address
-std::map<uintptr_t, PoolBlock> g_pool;                  // every pool block ever mapped
+std::map<uintptr_t, PoolBlock> g_pool;                  // every pool block ever handed out
 std::multimap<size_t, uintptr_t> g_pool_free;           // size class -> free pool block
 size_t g_pool_mapped = 0, g_pool_in_use = 0;
+// Pool memory comes in slabs the pool owns whole: 2 MiB-aligned runs of whole
+// 2 MiB granules (KFD's SVM granularity here, amdgpu svm_default_granularity
+// 9), registered once, never sharing a granule with another mapping (a
+// caller's buffer mapped next to a 128 KiB block used to share one; DESIGN.md
+// §5.8), never backed by transparent huge pages (no collapse or split
+// invalidates them).  Classes below 2 MiB are carved from a slab of their own
+// class as blocks are first handed out.
+constexpr size_t kPoolGranule = size_t{2} << 20;
+struct Slab {
+    uintptr_t next = 0, end = 0;
+};
+std::map<size_t, Slab> g_slab;  // size class -> the slab its next new block comes from
 
 uintptr_t page_bytes() {
     static const uintptr_t ps = [] {
@@ -580,19 +592,30 @@ int rs_host_alloc(size_t bytes, void** out) {
             *out = reinterpret_cast<void*>(b);
             return RS_OK;
         }
-        void* m = mmap(nullptr, cls, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-        if (m == MAP_FAILED) return RS_ERR_NOMEM;
-        const uintptr_t b = reinterpret_cast<uintptr_t>(m);
-        const int rc = span_register(b, b + cls);  // the pool's own reference: never released
-        if (rc != RS_OK) {
-            munmap(m, cls);
-            return rc;
+        Slab& sl = g_slab[cls];
+        if (sl.end - sl.next < cls) {  // a new slab: whole granules, 2 MiB-aligned
+            const size_t sb = std::max(cls, kPoolGranule);
+            void* m = mmap(nullptr, sb + kPoolGranule, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (m == MAP_FAILED) return RS_ERR_NOMEM;
+            const uintptr_t a = reinterpret_cast<uintptr_t>(m), lo = (a + kPoolGranule - 1) & ~(kPoolGranule - 1);
+            if (lo > a) munmap(m, lo - a);
+            if (a + kPoolGranule > lo) munmap(reinterpret_cast<void*>(lo + sb), a + kPoolGranule - lo);
+            (void)madvise(reinterpret_cast<void*>(lo), sb, MADV_NOHUGEPAGE);
+            const int rc = span_register(lo, lo + sb);  // the pool's own reference: never released
+            if (rc != RS_OK) {
+                munmap(reinterpret_cast<void*>(lo), sb);
+                return rc;
+            }
+            g_reg_count.store(static_cast<int>(g_spans.size()));
+            g_pool_mapped += sb;
+            sl.next = lo;
+            sl.end = lo + sb;
         }
-        g_reg_count.store(static_cast<int>(g_spans.size()));
+        const uintptr_t b = sl.next;
+        sl.next += cls;
         g_pool.emplace(b, PoolBlock{cls, false});
-        g_pool_mapped += cls;
         g_pool_in_use += cls;
-        *out = m;
+        *out = reinterpret_cast<void*>(b);
         return RS_OK;
     });
 }

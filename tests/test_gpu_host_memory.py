@@ -154,6 +154,8 @@ def _pool_rounds(rslib, orc, torch, r, d, p, size, rng):
         with pytest.raises(rslib.ErrInvalidArgument):
             rslib.host_free(addr)
         x = np.full(20 << 20, it, np.uint8)
+        print(f"round {it}: pool block {addr:#x}, fresh array {x.ctypes.data:#x}-{x.ctypes.data + x.nbytes:#x}",
+              flush=True)
         t = torch.from_numpy(x).cuda()
         torch.cuda.synchronize()
         assert int(t[-1].item()) == it
