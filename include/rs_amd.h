@@ -535,7 +535,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * callers before it launches; default 0), "host_coalesce_running" (shared
  * batches in flight at once: 1 | 2 default),
  * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
- * pageable host batches staged through a pinned mirror), "bind_numa" (0/1),
+ * pageable host batches staged through a pinned mirror), "host_copy_nt" (1
+ * default: the host threads' staging copies of large batches store
+ * non-temporally | 0: memcpy), "bind_numa" (0/1),
  * "host_unregister_revoke" (1 default: rs_host_unregister takes back the
  * GPUs' in-place mapping of the caller's whole pages, ~0.18 ms per call on
  * MI355X | 0: leave the runtime's state; env RSAMD_UNREGISTER_REVOKE),

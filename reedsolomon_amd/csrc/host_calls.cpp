@@ -226,6 +226,37 @@ size_t g_chunk = 128 * 1024;
 // over the host copy pool.
 constexpr size_t kParallelCopyMin = 512 * 1024;
 
+// Staging copies of large batches store with non-temporal stores
+// (rs_tune("host_copy_nt"), default 1): the pinned mirror is read by the GPU
+// over PCIe and the caller's outputs are not read back at once, so the
+// copies skip the read-for-ownership of every destination line and leave the
+// caches to the source.  Pieces below 4 KiB, and CPUs without AVX2, use memcpy.
+int g_copy_nt = 1;
+static const bool g_copy_avx2 = __builtin_cpu_supports("avx2");
+
+__attribute__((target("avx2"))) static void copy_nt(uint8_t* dst, const uint8_t* src, size_t b) {
+    const size_t head = (32 - (reinterpret_cast<uintptr_t>(dst) & 31)) & 31;
+    std::memcpy(dst, src, head);
+    size_t i = head;
+    for (; i + 128 <= b; i += 128) {
+        const __m256i a0 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+        const __m256i a1 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+        const __m256i a2 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+        const __m256i a3 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a0);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), a1);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), a2);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), a3);
+    }
+    std::memcpy(dst + i, src + i, b - i);
+    _mm_sfence();  // the streamed lines are globally visible before the copier reports the piece done
+}
+
+static void copy_piece(uint8_t* dst, const uint8_t* src, size_t b) {
+    if (g_copy_nt && g_copy_avx2 && b >= 4096) copy_nt(dst, src, b);
+    else std::memcpy(dst, src, b);
+}
+
 // dst[i] <- src[i] (n vectors, len bytes each) on the copy pool, in
 // 64 KiB pieces so every thread gets work; on the calling thread alone when
 // the pool is busy with another caller's copies.
@@ -240,7 +271,7 @@ void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t
     CopyPool::get().run_or_inline(total, [&](size_t k) {
         const size_t v = k / per, off = (k % per) * piece;
         const size_t b = std::min(piece, len - off);
-        std::memcpy(dst[v] + off, src[v] + off, b);
+        copy_piece(dst[v] + off, src[v] + off, b);
     });
 }
 

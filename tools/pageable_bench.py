@@ -2,8 +2,9 @@
 """Pageable host batches (rs_encode_host_batch / rs_reconst_host_batch_multi
 on ordinary numpy memory): the staged pipeline's rate per size, with the
 copy pool size taken from RSAMD_HOST_THREADS (read once per process, so run
-this once per setting).  Every result is checked against the device-resident
-Encode of the same stripes.
+this once per setting), with the staging copies' non-temporal stores on and
+off (rs_tune "host_copy_nt"), alternating in one process.  Every result is
+checked against the device-resident Encode of the same stripes.
 
 Usage: RSAMD_HOST_THREADS=8 python tools/pageable_bench.py
 """
@@ -26,12 +27,16 @@ def main():
     r = rs.New(d, p)
     threads = os.environ.get("RSAMD_HOST_THREADS", "4 (default)")
     rng = np.random.default_rng(5)
-    for vec, S in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64), ((2 << 20) + 40, 24)):
+    for vec, S, nt in [(v, s_, nt) for v, s_ in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64), ((2 << 20) + 40, 24))
+                       for nt in (1, 0, 1, 0)]:
+        rs.lib().rs_tune(b"host_copy_nt", nt)
         host = rng.integers(0, 256, (S, d + p, vec), dtype=np.uint8)
-        dev = torch.from_numpy(host).cuda()
+        pin = torch.from_numpy(host).pin_memory()  # (the reference through pinned memory: no runtime pageable copy)
+        dev = pin.cuda()
         r.encode_batch(dev)
-        ref = dev.cpu().numpy()
-        del dev
+        pin.copy_(dev)
+        ref = pin.numpy().copy()
+        del dev, pin
         host[:, d:] = 0
         r.encode_host_batch(host)  # warm (mirror allocation)
         assert np.array_equal(host, ref), "encode mismatch"
@@ -59,7 +64,7 @@ def main():
         tr /= reps
         assert np.array_equal(work, ref), "reconst mismatch"
         gib = S * (d + p) * vec / 2**30
-        print(f"threads {threads:>12}  10+4 {vec:>8} B x{S:<5} pageable: encode {gib / te:6.1f} GiB/s "
+        print(f"threads {threads:>12} nt {nt}  10+4 {vec:>8} B x{S:<5} pageable: encode {gib / te:6.1f} GiB/s "
               f"({te * 1e3:7.2f} ms), reconst 4 lost {gib / tr:6.1f} GiB/s ({tr * 1e3:7.2f} ms)", flush=True)
         del host, lost, work, ref
 
