@@ -529,7 +529,10 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * the change),
  * "host_pinned_max", "host_zc_max" (bytes, -1 = no limit, the default since
  * round 4: every synchronous host call takes the chunked zero-copy pipeline),
- * "host_chunk" (bytes; host-memory call staging), "host_coalesce_max" (bytes per vector up to which
+ * "host_chunk" (bytes per vector per chunk of the host-memory call pipeline,
+ * at least; default 128 KiB), "host_chunk_split" (n: chunks of at least 1/n
+ * of the vectors, within 8 MiB per chunk of all vectors; default 4, 0 =
+ * host_chunk alone), "host_coalesce_max" (bytes per vector up to which
  * concurrent host calls of one shape share a launch; 0 = off),
  * "host_coalesce_linger_us" (a ready shared batch waits this long for more
  * callers before it launches; default 0), "host_coalesce_running" (shared

@@ -1070,6 +1070,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_coalesce_running") g_co_running = value < 1 ? 1 : value > 2 ? 2 : value;
         else if (n == "host_coalesce_max") g_coalesce_max = value < 0 ? 0 : static_cast<size_t>(value);
         else if (n == "host_chunk") g_chunk = value < 4096 ? 4096 : static_cast<size_t>(value) & ~size_t{4095};
+        else if (n == "host_chunk_split") g_chunk_split = value < 0 ? 0 : static_cast<size_t>(value);
         else return RS_ERR_INVAL;
         return RS_OK;
     });

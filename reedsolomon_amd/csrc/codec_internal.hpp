@@ -607,7 +607,7 @@ struct ReconstPlan {
 int check_reconst_passes(const rs_t* rs, const ReconstPlan& pl, const size_t* lens, int n, int* parity_rc);
 
 // ---------------------------------------------------------------- host calls (host_calls.cpp)
-extern size_t g_pinned_max, g_zc_max, g_chunk, g_coalesce_max;
+extern size_t g_pinned_max, g_zc_max, g_chunk, g_chunk_split, g_coalesce_max;
 extern int g_coalesce_linger_us, g_co_running, g_engine_direct;
 int host_product(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t* const* src, uint8_t* const* dst,
                  size_t size, bool accumulate);

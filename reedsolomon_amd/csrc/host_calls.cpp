@@ -220,8 +220,16 @@ int stage_out(rs_t* rs, uint8_t* const* dst, int n, size_t size, size_t pitch, i
 }
 
 
-// Column-chunk size of the host-call pipeline (bytes per vector per chunk).
+// Column-chunk size of the host-call pipeline (bytes per vector per chunk):
+// at least g_chunk, and at least 1/g_chunk_split of the vectors (0 = g_chunk
+// alone), within 8 MiB per slot.  Each chunk costs a launch, an event wait
+// and two pool dispatches (~20 us), so large vectors take a few large chunks:
+// 10+4 pageable Encode at 1 / 2 MiB 397-408 / 780-881 us with 128 KiB
+// chunks, 337-353 / 601-666 with host_chunk_split 4 (alternating in one
+// process, profiles/r06/host_chunk_split_ab_1m.log); 4 / 16 MiB 1.6-2.4 /
+// 6.6-6.8 ms -> 1.1-1.4 / 4.1-4.4 ms (host_chunk_split_sweep.log).
 size_t g_chunk = 128 * 1024;
+size_t g_chunk_split = 4;
 // Total copy bytes of one chunk above which the staging copies are split
 // over the host copy pool.
 constexpr size_t kParallelCopyMin = 512 * 1024;
@@ -286,9 +294,10 @@ int host_matmul(rs_t* rs, const uint8_t* mat, int rows, int cols, const uint8_t*
                 size_t size, bool accumulate) {
     const int nvec = rows + cols;
     if (!rs->stream) RS_TRY(hip_ok(hipStreamCreateWithFlags(&rs->stream, hipStreamNonBlocking), "stream create"));
-    // chunk: <= g_chunk per vector and <= 8 MiB per slot, 4 KiB multiple
+    // chunk: max(g_chunk, size / g_chunk_split) per vector, <= 8 MiB per slot, 4 KiB multiple
     size_t C = rup(size, 256);
-    const size_t cap = std::max<size_t>(4096, std::min(g_chunk, (size_t{8} << 20) / nvec) & ~size_t{4095});
+    const size_t want = g_chunk_split ? std::max(g_chunk, rup(size / g_chunk_split, 4096)) : g_chunk;
+    const size_t cap = std::max<size_t>(4096, std::min(want, (size_t{8} << 20) / nvec) & ~size_t{4095});
     if (C > cap) C = cap;
     const size_t nch = (size + C - 1) / C;
     const int ns = nch > 1 ? 3 : 1;

@@ -50,6 +50,7 @@ SWEEP = {
     "host_pinned_max": [0, 4 << 20, 256 << 10],
     "host_zc_max": [0, 2 << 20, -1],
     "host_chunk": [4096, 128 << 10],
+    "host_chunk_split": [0, 1, 4],
     "host_coalesce_max": [0, 128 << 10],
     "host_coalesce_linger_us": [100, 0],
     "host_coalesce_running": [1, 2],
