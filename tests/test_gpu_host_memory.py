@@ -161,6 +161,38 @@ def _pool_rounds(rslib, orc, torch, r, d, p, size, rng):
         assert int(t[-1].item()) == it
 
 
+def _mapping_of(addr):
+    """(start, end) of the /proc/self/maps entry holding addr."""
+    with open("/proc/self/maps") as f:
+        for line in f:
+            lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
+            if lo <= addr < hi:
+                return lo, hi
+    return None
+
+
+def test_pool_slabs_own_their_granules(rslib, torch_dev):
+    """Pool blocks come from slabs of whole 2 MiB granules (KFD's SVM unit on
+    MI355X): the mapping holding any block starts and ends on
+    a 2 MiB boundary, so no other mapping (a caller's array the runtime maps
+    in place for a pageable copy) shares a granule with registered pool
+    memory; a small class's blocks are carved side by side from one slab."""
+    g = 2 << 20
+    blocks = [rslib.host_alloc(n) for n in (64 << 10, 64 << 10, 300 << 10, (3 << 20) + 1)]
+    try:
+        for b in blocks:
+            m = _mapping_of(b.ctypes.data)
+            assert m is not None and m[0] % g == 0 and m[1] % g == 0, (hex(b.ctypes.data), m)
+        assert blocks[3].ctypes.data % g == 0  # a class of 4 MiB: a slab of its own
+        x = np.full(20 << 20, 3, np.uint8)  # a fresh multi-MiB array mapped next to the pool
+        t = torch_dev.from_numpy(x).cuda()
+        torch_dev.cuda.synchronize()
+        assert int(t[-1].item()) == 3
+    finally:
+        for b in blocks:
+            rslib.host_free(b)
+
+
 def test_concurrent_register_unregister_shared_pages(rslib, torch_dev):
     """Two threads register and unregister buffers that share pages (one
     mapping, the threads' ranges overlapping by half a page) 200 times each:
