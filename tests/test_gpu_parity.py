@@ -1204,14 +1204,17 @@ def test_reconst_batch_multi_parity_rows_bitsliced(rslib, orc, torch_dev, d, p):
 
 # ---------------------------------------------------------------- host-call staging paths
 
-@pytest.mark.parametrize("mode", ["chunked", "small_chunks", "staged_pinned", "staged_pageable"])
+@pytest.mark.parametrize("mode", ["chunked", "fixed_chunks", "small_chunks", "staged_pinned", "staged_pageable"])
 def test_host_calls_staging_paths(rslib, orc, torch_dev, mode):
     """The synchronous host-memory calls through every staging path:
-    the chunked zero-copy pipeline (default; 1 MiB + 5 B = 5 ragged chunks),
-    4 KiB chunks (many trips around the 3-slot ring), and the older staged
-    paths (device staging with pinned DMA / pageable copies)."""
+    the chunked zero-copy pipeline (default: chunks of a quarter of the
+    vectors, 1 MiB + 5 B = 4 ragged chunks, 3 MiB + 48 B = 6 chunks capped at
+    8 MiB per slot, around the 3-slot ring twice), fixed 128 KiB chunks
+    (host_chunk_split 0), 4 KiB chunks (many trips around the ring), and the
+    older staged paths (device staging with pinned DMA / pageable copies)."""
     L = rslib.lib()
-    knobs = {"chunked": {}, "small_chunks": {"host_chunk": 4096},
+    knobs = {"chunked": {}, "fixed_chunks": {"host_chunk_split": 0},
+             "small_chunks": {"host_chunk": 4096, "host_chunk_split": 0},
              "staged_pinned": {"host_zc_max": 0, "host_pinned_max": 4 << 20},
              "staged_pageable": {"host_zc_max": 0, "host_pinned_max": 0}}[mode]
     try:
@@ -1220,7 +1223,7 @@ def test_host_calls_staging_paths(rslib, orc, torch_dev, mode):
         d, p = 10, 4
         r = rslib.New(d, p)
         rng = np.random.default_rng(120)
-        for size in (1, 4099, 65536 * 3 + 7, (1 << 20) + 5):
+        for size in (1, 4099, 65536 * 3 + 7, (1 << 20) + 5) + (((3 << 20) + 48,) if mode == "chunked" else ()):
             data = [_rand(rng, size) for _ in range(d)]
             exp = _oracle_encode(orc, d, p, data)
             act = [x.copy() for x in data] + [np.full(size, 0xA5, np.uint8) for _ in range(p)]
@@ -1248,7 +1251,8 @@ def test_host_calls_staging_paths(rslib, orc, torch_dev, mode):
             for j in range(p):
                 assert np.array_equal(par[j], ora[j]), (size, j)
     finally:
-        for k, v in {"host_chunk": 128 << 10, "host_zc_max": -1, "host_pinned_max": 256 << 10}.items():
+        for k, v in {"host_chunk": 128 << 10, "host_chunk_split": 4, "host_zc_max": -1,
+                     "host_pinned_max": 256 << 10}.items():
             L.rs_tune(k.encode(), v)
 
 
