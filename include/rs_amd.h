@@ -538,7 +538,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * callers before it launches; default 0), "host_coalesce_running" (shared
  * batches in flight at once: 1 | 2 default),
  * "host_batch_zc" (0/1), "host_dma_1d" (0/1), "host_pageable_stage" (0/1:
- * pageable host batches staged through a pinned mirror), "host_copy_nt" (1
+ * pageable host batches staged through a pinned mirror), "host_pageable_slot"
+ * (bytes of stripes per chunk of that staging, at least one stripe; default
+ * 8 MiB), "host_copy_nt" (1
  * default: the host threads' staging copies of large batches store
  * non-temporally | 0: memcpy), "bind_numa" (0/1),
  * "host_unregister_revoke" (1 default: rs_host_unregister takes back the

@@ -328,7 +328,8 @@ int g_host_pageable_stage = 1;
 // / out (add(v) per vector index); launch(first, count, dev_slot, stripe
 // bytes, pitch) enqueues the kernel on rs->stream.  Caller holds stage_mu.
 constexpr size_t kPageableStripeMax = size_t{16} << 20;
-constexpr size_t kPageableSlot = size_t{8} << 20;
+// Bytes of stripes per chunk (at least one stripe); rs_tune("host_pageable_slot").
+size_t rsamd::detail::g_pageable_slot = size_t{8} << 20;
 // Larger pageable stripes go through the same mirror in byte windows of
 // every vector (Encode and Reconst are byte-wise: a window of all d+p
 // vectors is a stripe of its own), so no pageable byte is handed to the
@@ -348,7 +349,7 @@ static int pageable_pipeline(rs_t* rs, uint8_t* base, int64_t ss, int64_t vs, in
     if (rs->zc_pending) RS_TRY(hip_ok(hipStreamSynchronize(rs->stream), "host-call stream sync"));
     const size_t pitch = rup(len, 256);
     const size_t sbytes = pitch * static_cast<size_t>(nvec);
-    const int cs = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, kPageableSlot / sbytes)));
+    const int cs = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, g_pageable_slot / sbytes)));
     const int nch = (nstripes + cs - 1) / cs;
     const int ns = nch > 1 ? 3 : 1;
     const size_t slot = sbytes * static_cast<size_t>(cs);

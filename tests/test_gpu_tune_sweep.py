@@ -58,6 +58,7 @@ SWEEP = {
     "host_unregister_revoke": [0, 1],
     "host_dma_1d": [1, 0],
     "host_pageable_stage": [0, 1],
+    "host_pageable_slot": [4096, 32 << 20, 8 << 20],
     "host_copy_nt": [0, 1],
     "bind_numa": [0, 1],
     "jit": [0, 2, 1],

@@ -30,6 +30,10 @@ def main():
     for vec, S, nt in [(v, s_, nt) for v, s_ in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64), ((2 << 20) + 40, 24))
                        for nt in (1, 0, 1, 0)]:
         rs.lib().rs_tune(b"host_copy_nt", nt)
+        slot = int(os.environ.get("RSAMD_BENCH_SLOTS", "0"))  # alternate the chunk size instead of nt
+        if slot:
+            rs.lib().rs_tune(b"host_copy_nt", 1)
+            rs.lib().rs_tune(b"host_pageable_slot", (8 << 20) if nt else (slot << 20))
         host = rng.integers(0, 256, (S, d + p, vec), dtype=np.uint8)
         pin = torch.from_numpy(host).pin_memory()  # (the reference through pinned memory: no runtime pageable copy)
         dev = pin.cuda()
@@ -64,7 +68,8 @@ def main():
         tr /= reps
         assert np.array_equal(work, ref), "reconst mismatch"
         gib = S * (d + p) * vec / 2**30
-        print(f"threads {threads:>12} nt {nt}  10+4 {vec:>8} B x{S:<5} pageable: encode {gib / te:6.1f} GiB/s "
+        tag = f"slot {(8 if nt else slot):>2} MiB" if slot else f"nt {nt}"
+        print(f"threads {threads:>12} {tag}  10+4 {vec:>8} B x{S:<5} pageable: encode {gib / te:6.1f} GiB/s "
               f"({te * 1e3:7.2f} ms), reconst 4 lost {gib / tr:6.1f} GiB/s ({tr * 1e3:7.2f} ms)", flush=True)
         del host, lost, work, ref
 
