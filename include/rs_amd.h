@@ -542,7 +542,9 @@ RS_API int64_t rs_jit_asm_source(const uint8_t* mat, int rows, int cols, int acc
  * (bytes of stripes per chunk of that staging, at least one stripe; default
  * 8 MiB), "host_copy_nt" (1
  * default: the host threads' staging copies of large batches store
- * non-temporally | 0: memcpy), "bind_numa" (0/1),
+ * non-temporally | 0: memcpy), "host_copy_coalesce" (1 default: vectors back
+ * to back in both source and destination are copied as one run | 0: one
+ * piece per vector at least), "bind_numa" (0/1),
  * "host_unregister_revoke" (1 default: rs_host_unregister takes back the
  * GPUs' in-place mapping of the caller's whole pages, ~0.18 ms per call on
  * MI355X | 0: leave the runtime's state; env RSAMD_UNREGISTER_REVOKE),

@@ -1062,6 +1062,7 @@ int rs_tune(const char* name, int value) {
         else if (n == "host_pageable_stage") g_host_pageable_stage = value;
         else if (n == "host_pageable_slot") g_pageable_slot = value < 4096 ? 4096 : static_cast<size_t>(value);
         else if (n == "host_copy_nt") g_copy_nt = value ? 1 : 0;
+        else if (n == "host_copy_coalesce") g_copy_coalesce = value ? 1 : 0;
         else if (n == "bind_numa") g_bind_numa = value;
         else if (n == "table_registry_max") g_registry_max = value < 1 ? 1 : static_cast<size_t>(value);
         else if (n == "table_inplace_max") g_tab_inplace_max = value < 0 ? 0 : static_cast<size_t>(value);

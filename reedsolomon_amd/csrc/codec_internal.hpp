@@ -620,7 +620,7 @@ int flag_sync(hipStream_t st, rs_codec::DoneFlag& f, const char* where);
 extern int g_host_flag_sync;
 
 // ---------------------------------------------------------------- host batches (host_batches.cpp)
-extern int g_host_batch_zc, g_host_dma_1d, g_bind_numa, g_host_pageable_stage, g_copy_nt;
+extern int g_host_batch_zc, g_host_dma_1d, g_bind_numa, g_host_pageable_stage, g_copy_nt, g_copy_coalesce;
 extern size_t g_pageable_slot;  // pageable host batches: stripe bytes per chunk (host_batches.cpp)
 extern int g_unregister_revoke;  // rs_host_unregister returns the caller's pages to no GPU access (host_batches.cpp)
 // dst[i] <- src[i] (n vectors, len bytes each) on the host copy pool (host_calls.cpp).

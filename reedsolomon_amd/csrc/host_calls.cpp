@@ -265,22 +265,40 @@ static void copy_piece(uint8_t* dst, const uint8_t* src, size_t b) {
     else std::memcpy(dst, src, b);
 }
 
+// Vectors that lie back to back in both source and destination (the data
+// rows of a dense [S][d+p][len] batch and its mirror stripe) are copied as
+// one run, in 64 KiB pieces, instead of one piece per vector: 8 KiB vectors
+// otherwise cost a pool hand-out per 8 KiB.  rs_tune("host_copy_coalesce").
+int g_copy_coalesce = 1;
+
 // dst[i] <- src[i] (n vectors, len bytes each) on the copy pool, in
 // 64 KiB pieces so every thread gets work; on the calling thread alone when
 // the pool is busy with another caller's copies.
 void parallel_copy(uint8_t* const* dst, const uint8_t* const* src, int n, size_t len) {
     const size_t piece = 64 * 1024;
-    const size_t per = (len + piece - 1) / piece;
-    const size_t total = per * static_cast<size_t>(n);
-    if (len * static_cast<size_t>(n) < kParallelCopyMin || total <= 1) {
+    if (len * static_cast<size_t>(n) < kParallelCopyMin || (n <= 1 && len <= piece)) {
         for (int i = 0; i < n; ++i) std::memcpy(dst[i], src[i], len);
         return;
     }
-    CopyPool::get().run_or_inline(total, [&](size_t k) {
-        const size_t v = k / per, off = (k % per) * piece;
-        const size_t b = std::min(piece, len - off);
-        copy_piece(dst[v] + off, src[v] + off, b);
-    });
+    struct Run {
+        uint8_t* d;
+        const uint8_t* s;
+        size_t bytes;
+    };
+    std::vector<Run> runs;
+    runs.reserve(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) {
+        if (g_copy_coalesce && !runs.empty() && runs.back().d + runs.back().bytes == dst[i] &&
+            runs.back().s + runs.back().bytes == src[i])
+            runs.back().bytes += len;
+        else
+            runs.push_back(Run{dst[i], src[i], len});
+    }
+    std::vector<Run> pieces;
+    for (const Run& r : runs)
+        for (size_t off = 0; off < r.bytes; off += piece)
+            pieces.push_back(Run{r.d + off, r.s + off, std::min(piece, r.bytes - off)});
+    CopyPool::get().run_or_inline(pieces.size(), [&](size_t k) { copy_piece(pieces[k].d, pieces[k].s, pieces[k].bytes); });
 }
 
 // The synchronous host-memory product behind rs_encode / rs_reconst /

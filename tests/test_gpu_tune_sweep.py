@@ -60,6 +60,7 @@ SWEEP = {
     "host_pageable_stage": [0, 1],
     "host_pageable_slot": [4096, 32 << 20, 8 << 20],
     "host_copy_nt": [0, 1],
+    "host_copy_coalesce": [0, 1],
     "bind_numa": [0, 1],
     "jit": [0, 2, 1],
     "jit_min_launches": [1, 2],

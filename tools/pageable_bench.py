@@ -30,6 +30,9 @@ def main():
     for vec, S, nt in [(v, s_, nt) for v, s_ in ((8 << 10, 2048), (64 << 10, 512), (1 << 20, 64), ((2 << 20) + 40, 24))
                        for nt in (1, 0, 1, 0)]:
         rs.lib().rs_tune(b"host_copy_nt", nt)
+        if os.environ.get("RSAMD_BENCH_COALESCE"):  # alternate run coalescing instead of nt
+            rs.lib().rs_tune(b"host_copy_nt", 1)
+            rs.lib().rs_tune(b"host_copy_coalesce", nt)
         slot = int(os.environ.get("RSAMD_BENCH_SLOTS", "0"))  # alternate the chunk size instead of nt
         if slot:
             rs.lib().rs_tune(b"host_copy_nt", 1)
@@ -68,7 +71,8 @@ def main():
         tr /= reps
         assert np.array_equal(work, ref), "reconst mismatch"
         gib = S * (d + p) * vec / 2**30
-        tag = f"slot {(8 if nt else slot):>2} MiB" if slot else f"nt {nt}"
+        tag = f"slot {(8 if nt else slot):>2} MiB" if slot else \
+            f"coalesce {nt}" if os.environ.get("RSAMD_BENCH_COALESCE") else f"nt {nt}"
         print(f"threads {threads:>12} {tag}  10+4 {vec:>8} B x{S:<5} pageable: encode {gib / te:6.1f} GiB/s "
               f"({te * 1e3:7.2f} ms), reconst 4 lost {gib / tr:6.1f} GiB/s ({tr * 1e3:7.2f} ms)", flush=True)
         del host, lost, work, ref
