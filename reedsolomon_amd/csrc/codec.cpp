@@ -396,7 +396,7 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
     if (!st.done) RS_TRY(hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "table staging event"));
     if (st.cap < bytes) {
         if (st.host && st.vram) host_writable_vram_put(rs->device, st.host, st.cap);
-        else if (st.host) (void)hipHostFree(st.host);
+        else if (st.host) coherent_put(st.host, st.cap);
         st.host = nullptr;
         st.dev_host = nullptr;
         st.cap = 0;
@@ -408,16 +408,13 @@ int get_tables(rs_t* rs, const uint8_t* mat, int rows, int cols, hipStream_t str
             st.dev_host = v;
             st.cap = vcap;
             st.vram = true;
-        } else {  // coherent and mapped pinned host memory: read in place over PCIe
-            if (hipHostMalloc(reinterpret_cast<void**>(&st.host), cap,
-                              hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
-                (void)hipGetLastError();
-                return RS_ERR_NOMEM;
-            }
+        } else {  // coherent and mapped pinned host memory (recycled blocks): read in place over PCIe
+            size_t ccap = 0;
             void* hd = nullptr;
-            if (hipHostGetDevicePointer(&hd, st.host, 0) == hipSuccess) st.dev_host = static_cast<const uint8_t*>(hd);
-            (void)hipGetLastError();
-            st.cap = cap;
+            st.host = coherent_get(cap, &ccap, &hd);
+            if (!st.host) return RS_ERR_NOMEM;
+            st.dev_host = static_cast<const uint8_t*>(hd);
+            st.cap = ccap;
             st.vram = false;
         }
     }

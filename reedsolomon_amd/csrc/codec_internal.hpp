@@ -304,6 +304,13 @@ extern int g_engine, g_engine_waves, g_engine_group_waves, g_engine_idle_us, g_e
 // platform maps no such memory for the CPU (engine.cpp).  Blocks are pooled
 // per device and never freed while the process runs.
 uint8_t* host_writable_vram_get(int device, size_t bytes, size_t* cap);
+// Coherent, mapped pinned host blocks (table staging slots, completion
+// flags) recycled process-wide instead of freed with their handle, as the
+// engine's rings are: no allocate / free churn of coherent mappings while
+// other work runs.  Size classes: powers of two from 4 KiB.
+// *dev receives the block's device address.  nullptr when out of memory.
+uint8_t* coherent_get(size_t bytes, size_t* cap, void** dev);
+void coherent_put(uint8_t* p, size_t cap);
 void host_writable_vram_put(int device, uint8_t* p, size_t cap);
 extern size_t g_engine_max_bytes;
 
@@ -353,11 +360,11 @@ inline void rs_codec::release_device() {
         if (tab_arena) rsamd::detail::host_writable_vram_put(device, tab_arena, tab_arena_cap);
         for (TabStage& t : tab_stage) {
             if (t.host && t.vram) rsamd::detail::host_writable_vram_put(device, t.host, t.cap);
-            else if (t.host) (void)hipHostFree(t.host);
+            else if (t.host) rsamd::detail::coherent_put(t.host, t.cap);
             if (t.done) (void)hipEventDestroy(t.done);
         }
         for (UploadSlot& u : up) {
-            if (u.host) (void)hipHostFree(u.host);
+            if (u.host) rsamd::detail::coherent_put(u.host, u.cap);
             if (u.dev) (void)hipFree(u.dev);
             if (u.copied) (void)hipEventDestroy(u.copied);
             if (u.done) (void)hipEventDestroy(u.done);
@@ -380,7 +387,7 @@ inline void rs_codec::release_device() {
             if (s) (void)hipStreamDestroy(s);
         if (co_stream) (void)hipStreamDestroy(co_stream);
         for (DoneFlag* f : {&stream_flag, &co_flag})
-            if (f->host) (void)hipHostFree(f->host);
+            if (f->host) rsamd::detail::coherent_put(reinterpret_cast<uint8_t*>(f->host), 4096);
         for (hipEvent_t e : chunk_ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -443,19 +450,16 @@ public:
             }
         auto round = [](size_t b) { return (b + (size_t{64} << 10) - 1) & ~((size_t{64} << 10) - 1); };
         if (u.cap < bytes) {
-            if (u.host) (void)hipHostFree(u.host);
+            if (u.host) rsamd::detail::coherent_put(u.host, u.cap);
             u.host = nullptr;
             u.host_dev = nullptr;
             u.cap = 0;
-            const size_t cap = round(bytes);
-            // coherent and mapped: a kernel may read it in place (map() below)
-            if (hipHostMalloc(reinterpret_cast<void**>(&u.host), cap,
-                              hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
-                u.host = nullptr;
-                return RS_ERR_NOMEM;
-            }
+            // coherent and mapped (a recycled block): a kernel may read it in place (map() below)
+            size_t cap = 0;
             void* hd = nullptr;
-            if (hipHostGetDevicePointer(&hd, u.host, 0) == hipSuccess) u.host_dev = static_cast<const uint8_t*>(hd);
+            u.host = rsamd::detail::coherent_get(round(bytes), &cap, &hd);
+            if (!u.host) return RS_ERR_NOMEM;
+            u.host_dev = static_cast<const uint8_t*>(hd);
             u.cap = cap;
         }
         const size_t dneed = dev_bytes > bytes ? dev_bytes : bytes;

@@ -165,6 +165,52 @@ static void ring_put(int device, EngineRing* r) {
     g_ring_pool.emplace_back(device, r);
 }
 
+// ---- coherent pinned blocks, recycled (codec_internal.hpp)
+namespace {
+std::mutex g_coh_mu;
+std::multimap<size_t, std::pair<uint8_t*, void*>> g_coh_free;  // size class -> (host, device) of idle blocks
+}  // namespace
+
+uint8_t* coherent_get(size_t bytes, size_t* cap, void** dev) {
+    size_t cls = 4096;
+    while (cls < bytes) cls <<= 1;
+    {
+        std::lock_guard<std::mutex> lk(g_coh_mu);
+        auto it = g_coh_free.find(cls);
+        if (it != g_coh_free.end()) {
+            uint8_t* p = it->second.first;
+            *dev = it->second.second;
+            g_coh_free.erase(it);
+            *cap = cls;
+            return p;
+        }
+    }
+    void* h = nullptr;
+    if (hipHostMalloc(&h, cls, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        d = nullptr;
+    }
+    *dev = d;
+    *cap = cls;
+    return static_cast<uint8_t*>(h);
+}
+
+void coherent_put(uint8_t* p, size_t cap) {
+    if (!p) return;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        d = nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_coh_mu);
+    g_coh_free.emplace(cap, std::make_pair(p, d));
+}
+
 // ---- device memory the host writes through the BAR
 namespace {
 std::mutex g_vram_mu;

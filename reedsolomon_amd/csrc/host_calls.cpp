@@ -101,19 +101,18 @@ int sync(rs_t* rs) {
 int g_host_flag_sync = 1;
 
 int flag_sync(hipStream_t st, rs_codec::DoneFlag& f, const char* where) {
-    if (g_host_flag_sync && !f.host) {
-        void* h = nullptr;
-        if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) == hipSuccess) {
-            void* d = nullptr;
-            if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess && d) {
-                f.host = static_cast<uint32_t*>(h);
+    if (g_host_flag_sync && !f.host) {  // (a recycled coherent block: its word starts at this handle's seq)
+        size_t cap = 0;
+        void* d = nullptr;
+        if (uint8_t* h = coherent_get(64, &cap, &d)) {
+            if (d) {
+                f.host = reinterpret_cast<uint32_t*>(h);
                 f.dev = d;
                 __atomic_store_n(f.host, f.seq, __ATOMIC_RELEASE);
             } else {
-                (void)hipHostFree(h);
+                coherent_put(h, cap);
             }
         }
-        (void)hipGetLastError();
     }
     if (!g_host_flag_sync || !f.host) return hip_ok(hipStreamSynchronize(st), where);
     const uint32_t v = ++f.seq;
